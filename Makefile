@@ -1,0 +1,114 @@
+# p2p_matrix for MI355X (gfx950): RCCL over xGMI, MPI or TCP control plane.
+#
+#   make              build/p2p_matrix (HIP + RCCL + MPI) and the Python extension
+#   make host         build/p2p_matrix_host + build/p2p_host_tests (g++ only, no GPU code)
+#   make test         host unit tests + CPU pytest tier
+#   make test-gpu     pytest -m gpu (run on an MI355X, e.g. via gpurun)
+#   make asan         host unit tests under AddressSanitizer/UBSan (host code only)
+#   make clean        removes build/ and the extension (the reference's clean
+#                     target removes the misspelled "p2pmatrix", Makefile:5)
+#
+# Reference build (Makefile:1-2): `nvcc -lmpi -lnccl p2p_matrix.cc`.
+
+ROCM      ?= /opt/rocm
+ARCH      ?= gfx950
+MPI_HOME  ?= /opt/conda
+PYTHON    ?= python3
+HIPCC     := $(ROCM)/bin/hipcc
+CXX_HOST  ?= g++
+BUILD     := build
+
+CXXSTD    := -std=c++17
+WARN      := -Wall -Wextra -Wno-unused-parameter
+OPT       ?= -O3
+HIPFLAGS  := $(CXXSTD) $(OPT) $(WARN) -fPIC --offload-arch=$(ARCH) -Icsrc
+HOSTFLAGS := $(CXXSTD) $(OPT) $(WARN) -fPIC -Icsrc -pthread
+
+CORE      := common units stats schedule bootstrap transport_host runner report app
+GPU_OBJS  := $(addprefix $(BUILD)/gpu/,$(addsuffix .o,$(CORE) transport_rccl) kernels.o)
+HOST_OBJS := $(addprefix $(BUILD)/host/,$(addsuffix .o,$(CORE) transport_rccl_stub))
+
+# MPICH lives in /opt/conda; putting /opt/conda/lib on the rpath would pull in
+# conda's old libstdc++ (GLIBCXX_3.4.29 missing for libamdhip64), so only the
+# three MPI libraries are symlinked into build/mpilib.
+MPILIB    := $(BUILD)/mpilib
+MPI_LINK  := -L$(MPILIB) -lmpi -Wl,-rpath,'$$ORIGIN/mpilib'
+MPI_INC   := -I$(MPI_HOME)/include
+
+PY_EXT    := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
+PY_INC    := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_paths()['include'])")
+PYBIND    := $(shell $(PYTHON) -c "import pybind11;print(pybind11.get_include())")
+EXT       := test_nccl_p2p_amd/_p2pcore$(PY_EXT)
+
+.PHONY: all gpu host ext test test-host test-gpu asan clean
+
+all: gpu host ext
+
+gpu: $(BUILD)/p2p_matrix
+host: $(BUILD)/p2p_matrix_host $(BUILD)/p2p_host_tests
+ext: $(EXT)
+
+$(BUILD)/gpu $(BUILD)/host $(BUILD)/asan:
+	mkdir -p $@
+
+$(MPILIB)/.stamp:
+	mkdir -p $(MPILIB)
+	for l in libmpi.so.12 libgfortran.so.4 libquadmath.so.0; do ln -sf $(MPI_HOME)/lib/$$l $(MPILIB)/$$l; done
+	ln -sf libmpi.so.12 $(MPILIB)/libmpi.so
+	touch $@
+
+HEADERS := $(wildcard csrc/*.hpp)
+
+$(BUILD)/gpu/%.o: csrc/%.cpp $(HEADERS) | $(BUILD)/gpu
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/gpu/kernels.o: csrc/kernels.hip $(HEADERS) | $(BUILD)/gpu
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/gpu/bootstrap_mpi.o: csrc/bootstrap_mpi.cpp $(HEADERS) | $(BUILD)/gpu
+	$(HIPCC) $(HIPFLAGS) $(MPI_INC) -c $< -o $@
+
+$(BUILD)/gpu/main.o: csrc/main.cpp $(HEADERS) | $(BUILD)/gpu
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/host/%.o: csrc/%.cpp $(HEADERS) | $(BUILD)/host
+	$(CXX_HOST) $(HOSTFLAGS) -c $< -o $@
+
+$(BUILD)/host/bootstrap_mpi.o: csrc/bootstrap_mpi.cpp $(HEADERS) | $(BUILD)/host
+	$(CXX_HOST) $(HOSTFLAGS) $(MPI_INC) -c $< -o $@
+
+$(BUILD)/p2p_matrix: $(GPU_OBJS) $(BUILD)/gpu/bootstrap_mpi.o $(BUILD)/gpu/main.o $(MPILIB)/.stamp
+	$(HIPCC) --offload-arch=$(ARCH) $(GPU_OBJS) $(BUILD)/gpu/bootstrap_mpi.o $(BUILD)/gpu/main.o -o $@ \
+	    -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib $(MPI_LINK) -pthread
+
+$(BUILD)/p2p_matrix_host: $(HOST_OBJS) $(BUILD)/host/bootstrap_mpi.o $(BUILD)/host/main.o $(MPILIB)/.stamp
+	$(CXX_HOST) $(HOST_OBJS) $(BUILD)/host/bootstrap_mpi.o $(BUILD)/host/main.o -o $@ $(MPI_LINK) -pthread
+
+$(BUILD)/p2p_host_tests: $(HOST_OBJS) tests/host/test_main.cpp $(HEADERS)
+	$(CXX_HOST) $(HOSTFLAGS) $(HOST_OBJS) tests/host/test_main.cpp -o $@
+
+$(BUILD)/gpu/pymodule.o: csrc/pymodule.cpp $(HEADERS) | $(BUILD)/gpu
+	$(HIPCC) $(HIPFLAGS) -fvisibility=hidden -I$(PY_INC) -I$(PYBIND) -c $< -o $@
+
+$(EXT): $(GPU_OBJS) $(BUILD)/gpu/pymodule.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared $(GPU_OBJS) $(BUILD)/gpu/pymodule.o -o $@ \
+	    -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib -pthread
+
+# AddressSanitizer / UBSan on host code only (GPU sanitizers are not available).
+ASAN := -fsanitize=address,undefined -fno-omit-frame-pointer -g -O1
+asan: | $(BUILD)/asan
+	$(CXX_HOST) $(CXXSTD) $(WARN) $(ASAN) -Icsrc -pthread $(addprefix csrc/,$(addsuffix .cpp,$(CORE) transport_rccl_stub)) \
+	    tests/host/test_main.cpp -o $(BUILD)/asan/p2p_host_tests
+	ASAN_OPTIONS=detect_leaks=1 $(BUILD)/asan/p2p_host_tests
+
+test-host: $(BUILD)/p2p_host_tests
+	$(BUILD)/p2p_host_tests
+
+test: test-host
+	$(PYTHON) -m pytest tests -x -q -m "not gpu"
+
+test-gpu: all
+	$(PYTHON) -m pytest tests -x -q -m gpu
+
+clean:
+	rm -rf $(BUILD) test_nccl_p2p_amd/_p2pcore*.so

@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Headline benchmark: pairwise P2P GB/s matrix (min/mean) + p50 latency.
+
+Metric and configs come from BASELINE.json ("pairwise P2P GB/s matrix
+(min/mean) + p50 latency at 1/2/4/8 MI355X").  The reference
+(/root/reference/p2p_matrix.cc) measures an N x N matrix of NCCL send/recv
+bandwidth at 32 MiB per message; this bench measures the same matrix on
+MI355X through the native engine (RCCL ncclSend/ncclRecv over xGMI, hipEvent
+timing, gfx950 fill/verify kernels).
+
+One step = one round of the round-robin "tournament" schedule: the N ranks
+form N/2 disjoint pairs (xGMI is fully connected point-to-point, so pairs never
+share a link) and every pair exchanges --msgs messages of --size bytes in both
+directions, posted back to back inside ncclGroupStart/End.  Consecutive steps
+walk through the N-1 rounds, so after N-1 steps every cell of the matrix has
+been measured; per-GPU work per step is constant as N grows (weak scaling).
+With one GPU the step is a self send/recv (the reference prints only the
+diagonal 0.00 there).
+
+value = bytes sent by all ranks during the K timed steps / the slowest rank's
+wall time between two barrier + torch.cuda.synchronize() brackets, in GB/s
+(1e9 B/s).  Payloads are PRNG-filled on the device and the last step's receive
+buffers are verified on the device after the timed region.
+
+Usage (driver contract):
+  python bench.py --gpus 1 --steps K --warmup W
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+      --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+METRIC = "pairwise P2P GB/s matrix (min/mean) + p50 latency at 1/2/4/8 MI355X"
+BASELINE_VALUE = None  # the reference publishes no numbers
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=28)
+    ap.add_argument("--warmup", type=int, default=7)
+    ap.add_argument("--size", default="32M", help="message size (reference: 32 MiB, p2p_matrix.cc:124)")
+    ap.add_argument("--msgs", type=int, default=8, help="messages per direction per step")
+    ap.add_argument("--mode", default="tournament", choices=["tournament", "ring", "allpairs", "pair", "self"])
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "host"], help="host = CPU sockets (testing)")
+    ap.add_argument("--latency-iters", type=int, default=300)
+    ap.add_argument("--latency-size", default="8")
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--json-out", default=None, help="also write the result line to this file")
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    from test_nccl_p2p_amd import require_native
+    from test_nccl_p2p_amd.parallel.session import create_session, init_control_plane
+
+    nat = require_native()
+    env = init_control_plane("gloo")
+    if args.gpus != env.world:
+        log("bench: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, env.world))
+    n = env.world
+    use_gpu = args.transport == "rccl"
+    if use_gpu:
+        torch.cuda.set_device(env.local_rank)
+
+    def barrier():
+        if n > 1:
+            dist.barrier()
+
+    def gpu_sync():
+        if use_gpu:
+            torch.cuda.synchronize()
+
+    size = nat.parse_size(args.size)
+    sess = create_session(args.transport, device=env.local_rank)
+    if env.rank == 0:
+        log("bench: %d rank(s), %s, %s" % (n, sess.transport, sess.device_desc))
+    mode = "self" if n == 1 else args.mode
+    drv = nat.StepDriver(sess, mode, "bi", size, args.msgs, not args.no_verify)
+    drv.connect()
+
+    # Warmup (untimed): also walks every round once when W >= phases.
+    if args.warmup > 0:
+        drv.run_steps(0, args.warmup)
+        drv.sync()
+    drv.reset()
+
+    barrier()
+    gpu_sync()
+    barrier()
+    t0 = time.perf_counter()
+    drv.run_steps(args.warmup, args.steps)
+    drv.sync()
+    gpu_sync()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = sess.allreduce_max(t1 - t0)
+
+    job_bytes = sum(drv.job_bytes_per_step(args.warmup + k) for k in range(args.steps))
+    value = job_bytes / elapsed / 1e9
+
+    # Per-step GPU durations of every rank -> per-flow bandwidth.  The later
+    # arriving endpoint of a pair sees only the transfer (the earlier one also
+    # waits), so a flow's time is the min of its two endpoints' step times.
+    my_ms = drv.step_ms()
+    all_ms = [None] * n
+    if n > 1:
+        dist.all_gather_object(all_ms, my_ms)
+    else:
+        all_ms = [my_ms]
+    cells = {}
+    for k in range(args.steps):
+        step = args.warmup + k
+        for (src, dst) in drv.phase_flows(step):
+            ms = min(all_ms[src][k], all_ms[dst][k]) if src != dst else all_ms[src][k]
+            if ms > 0:
+                cells.setdefault((src, dst), []).append(size * args.msgs / (ms * 1e-3) / 1e9)
+    matrix = [[0.0] * n for _ in range(n)]
+    for (s, d), v in cells.items():
+        matrix[s][d] = statistics.median(v)
+    offdiag = [v for (s, d), vs in cells.items() for v in [statistics.median(vs)] if s != d or n == 1]
+    covered = len(cells)
+    expected = n * (n - 1) if n > 1 else 1
+
+    mismatches = drv.verify_last() if not args.no_verify else -1
+
+    lat = json.loads(sess.latency(nat.parse_size(args.latency_size), args.latency_iters, min(50, args.latency_iters)))
+    p50s = [p["one_way_us"]["p50"] for p in lat["pairs"]]
+    p50 = statistics.median(p50s) if p50s else None
+
+    step_ms_med = statistics.median(my_ms) if my_ms else 0.0
+    result = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GB/s",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
+        "dtype": "uint8",
+        "data": "synthetic (device PRNG-filled payloads, verified after timing)",
+        "config": {
+            "model": "p2p_matrix: RCCL ncclSend/ncclRecv %s-bidirectional, %s x %d msgs/step"
+                     % (mode, nat.format_size(size), args.msgs),
+            "global_batch": args.msgs * n,
+            "seq_len": size,
+            "parallelism": "p2p%d" % n,
+        },
+        "matrix_gbs_min": round(min(offdiag), 3) if offdiag else None,
+        "matrix_gbs_mean": round(statistics.mean(offdiag), 3) if offdiag else None,
+        "matrix_cells": "%d/%d" % (covered, expected),
+        "p50_latency_us": round(p50, 3) if p50 is not None else None,
+        "latency_bytes": nat.parse_size(args.latency_size),
+        "per_gpu_gbs": round(value / n, 3),
+        "rank0_step_ms_p50": round(step_ms_med, 4),
+        "verify_mismatches": mismatches,
+        "transport": sess.transport,
+    }
+    if env.rank == 0:
+        log("bench: GB/s matrix (row=src, col=dst), median over steps:")
+        for r in range(n):
+            log("  " + " ".join("%8.2f" % matrix[r][c] for c in range(n)))
+        line = json.dumps(result)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    barrier()
+    del drv
+    del sess
+    if n > 1 and dist.is_initialized():
+        dist.destroy_process_group()
+    return 0 if mismatches in (0, -1) else 3
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,326 @@
+#include "app.hpp"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <memory>
+
+#include "bootstrap.hpp"
+#include "common.hpp"
+#include "report.hpp"
+#include "transport.hpp"
+#include "units.hpp"
+
+namespace p2p {
+
+std::string usage_text() {
+  return R"(p2p_matrix — MI355X inter-GPU point-to-point bandwidth / latency matrix (RCCL over xGMI)
+
+usage: mpirun -n N ./p2p_matrix [options]          (reference-compatible launch)
+       torchrun --nproc-per-node N ... ./p2p_matrix   (RANK/WORLD_SIZE/MASTER_ADDR bootstrap)
+       ./p2p_matrix [options]                         (single rank: self path)
+
+With no options: serial pair schedule, uni then bi, 32 MiB x 128 per cell, printed
+exactly like the reference, followed by GB/s and per-message latency tables.
+
+schedule
+  -m, --mode LIST        pair | ring | allpairs | tournament | self | all   [pair]
+                           pair       ordered pairs one at a time (reference schedule)
+                           ring       r -> r+1 concurrently (PP hop pattern)
+                           allpairs   every rank to every peer in one group (EP all-to-all)
+                           tournament N-1 rounds of disjoint pairs (whole matrix, concurrent)
+                           self       every rank to itself (1-GPU path)
+  -d, --dir uni|bi|both  direction(s)                                         [both]
+  -b, --size SIZE        message size, e.g. 4K 32M 1G                         [32M]
+      --sizes LIST       sweep: 4K:4G (x2 steps), 4K:1G:4 (x4), 4K,1M,... ; overrides --size
+timing
+  -n, --iters N|auto     iterations per cell (auto: ~4 GiB per cell, 8..1000) [128]
+  -w, --warmup N         untimed iterations per cell                          [8]
+      --timing MODE      events    hipEvents, back-to-back messages, 1 sync  [events]
+                         wallclock reference semantics: host clock, sync per message
+      --reference        = --timing wallclock --warmup 0 --no-warm (the reference's methodology)
+      --no-warm          do not pre-establish connections before timing
+  -l, --latency          add a ping-pong latency matrix
+      --latency-size S   [8]      --latency-iters N   [1000]
+data
+  -c, --verify           random-fill sends, verify every received buffer on the device
+      --verify-impl I    auto | reg | lds  (register- or LDS-DMA-staged verify kernel)
+transport / launch
+      --transport T      rccl (MI355X + RCCL) | host (CPU sockets, no GPU)      [rccl]
+      --bootstrap B      auto | mpi | env | local                              [auto]
+      --device N         GPU index (default: local rank from block placement)
+      --timeout S        watchdog for init / waits, seconds                    [300]
+output
+      --json FILE        JSON lines (one object per run)
+      --csv FILE         per-flow CSV
+      --compat-only      only the reference matrices
+      --no-compat        only the extended tables
+      --dry-run          print the schedules and exit
+  -v, --verbose          -h, --help      --version
+)";
+}
+
+int auto_iters(size_t bytes, size_t target_bytes) {
+  size_t it = target_bytes / std::max<size_t>(bytes, 1);
+  return static_cast<int>(std::clamp<size_t>(it, 8, 1000));
+}
+
+namespace {
+
+std::vector<Mode> parse_modes(const std::string& s) {
+  if (s == "all") return {Mode::Pair, Mode::Tournament, Mode::Ring, Mode::AllPairs};
+  std::vector<Mode> out;
+  size_t pos = 0;
+  while (pos <= s.size()) {
+    size_t c = s.find(',', pos);
+    std::string item = s.substr(pos, c == std::string::npos ? std::string::npos : c - pos);
+    if (!item.empty()) out.push_back(parse_mode(item));
+    if (c == std::string::npos) break;
+    pos = c + 1;
+  }
+  return out;
+}
+
+}  // namespace
+
+bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out) {
+  *exit_code = 0;
+  bool size_given = false;
+  for (int i = 0; i < argc; ++i) {
+    std::string a = argv[i];
+    std::string val;
+    auto eq = a.find('=');
+    bool has_eq = a.rfind("--", 0) == 0 && eq != std::string::npos;
+    if (has_eq) {
+      val = a.substr(eq + 1);
+      a = a.substr(0, eq);
+    }
+    auto next = [&]() -> std::string {
+      if (has_eq) return val;
+      if (i + 1 >= argc) {
+        std::fprintf(stderr, "p2p_matrix: option %s needs a value\n", a.c_str());
+        std::exit(1);
+      }
+      return argv[++i];
+    };
+    if (a == "-h" || a == "--help") {
+      std::fprintf(out, "%s", usage_text().c_str());
+      return false;
+    } else if (a == "--version") {
+      std::fprintf(out, "p2p_matrix (MI355X / gfx950, RCCL) 1.0\n");
+      return false;
+    } else if (a == "-m" || a == "--mode") {
+      cfg->modes = parse_modes(next());
+    } else if (a == "-d" || a == "--dir") {
+      std::string d = next();
+      if (d == "both")
+        cfg->dirs = {Direction::Uni, Direction::Bi};
+      else
+        cfg->dirs = {parse_direction(d)};
+    } else if (a == "-b" || a == "--size") {
+      if (!size_given) cfg->sizes = {parse_size(next())};
+      else next();
+    } else if (a == "--sizes") {
+      cfg->sizes = parse_size_list(next());
+      size_given = true;
+    } else if (a == "-n" || a == "--iters") {
+      std::string v = next();
+      if (v == "auto") {
+        cfg->iters_auto = true;
+      } else {
+        cfg->run.iters = std::atoi(v.c_str());
+        cfg->iters_auto = false;
+      }
+    } else if (a == "-w" || a == "--warmup") {
+      cfg->run.warmup = std::atoi(next().c_str());
+    } else if (a == "--timing") {
+      cfg->run.timing = parse_timing(next());
+    } else if (a == "--reference") {
+      cfg->run.timing = Timing::Wallclock;
+      cfg->run.warmup = 0;
+      cfg->warm_connections = false;
+    } else if (a == "--no-warm") {
+      cfg->warm_connections = false;
+    } else if (a == "-l" || a == "--latency") {
+      cfg->latency = true;
+    } else if (a == "--latency-size") {
+      cfg->latency_bytes = parse_size(next());
+      cfg->latency = true;
+    } else if (a == "--latency-iters") {
+      cfg->latency_iters = std::atoi(next().c_str());
+      cfg->latency = true;
+    } else if (a == "-c" || a == "--verify") {
+      cfg->run.verify = true;
+    } else if (a == "--no-verify") {
+      cfg->run.verify = false;
+    } else if (a == "--verify-impl") {
+      std::string v = next();
+      cfg->verify_impl = v == "reg" || v == "register" ? 1 : v == "lds" ? 2 : 0;
+    } else if (a == "--transport") {
+      cfg->transport = next();
+    } else if (a == "--bootstrap") {
+      cfg->bootstrap = next();
+    } else if (a == "--device") {
+      cfg->device = std::atoi(next().c_str());
+    } else if (a == "--timeout") {
+      cfg->timeout_s = std::atof(next().c_str());
+    } else if (a == "--json") {
+      cfg->json_path = next();
+    } else if (a == "--csv") {
+      cfg->csv_path = next();
+    } else if (a == "--compat-only") {
+      cfg->extended = false;
+      cfg->compat = true;
+    } else if (a == "--no-compat") {
+      cfg->compat = false;
+    } else if (a == "--dry-run") {
+      cfg->dry_run = true;
+    } else if (a == "-v" || a == "--verbose") {
+      cfg->verbose++;
+    } else {
+      std::fprintf(stderr, "p2p_matrix: unknown option '%s' (see --help)\n", argv[i]);
+      *exit_code = 1;
+      return false;
+    }
+  }
+  if (cfg->run.iters < 1 && !cfg->iters_auto) {
+    std::fprintf(stderr, "p2p_matrix: --iters must be >= 1\n");
+    *exit_code = 1;
+    return false;
+  }
+  if (cfg->run.warmup < 0) cfg->run.warmup = 0;
+  if (cfg->transport != "rccl" && cfg->transport != "host") {
+    std::fprintf(stderr, "p2p_matrix: --transport must be rccl or host\n");
+    *exit_code = 1;
+    return false;
+  }
+  return true;
+}
+
+namespace {
+
+void print_schedule(FILE* out, const Schedule& s) {
+  std::fprintf(out, "schedule %s, %d ranks, %zu phases\n", s.name().c_str(), s.nranks, s.phases.size());
+  for (const auto& p : s.phases) {
+    std::fprintf(out, "  [%s]%s", p.label.c_str(), p.idle ? " idle" : "");
+    for (const auto& f : p.flows) std::fprintf(out, " %d->%d", f.src, f.dst);
+    std::fprintf(out, "\n");
+  }
+}
+
+}  // namespace
+
+int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result) {
+  if (cfg.verbose) set_log_level(cfg.verbose);
+  const int n = boot.size(), me = boot.rank();
+  const bool root = me == 0;
+
+  // Schedules: (mode, dir) pairs; Self and the concurrent all-pairs exchange
+  // have no meaningful uni/bi split, so they run once.
+  std::vector<Schedule> scheds;
+  for (Mode m : cfg.modes) {
+    if (m == Mode::Self || m == Mode::AllPairs) {
+      scheds.push_back(make_schedule(m, m == Mode::Self ? Direction::Uni : Direction::Bi, n));
+      continue;
+    }
+    for (Direction d : cfg.dirs) scheds.push_back(make_schedule(m, d, n));
+  }
+  for (const auto& s : scheds) {
+    std::string bad = validate(s);
+    P2P_CHECK(bad.empty(), "invalid schedule " + s.name() + ": " + bad);
+  }
+  if (cfg.dry_run) {
+    if (root)
+      for (const auto& s : scheds) print_schedule(out, s);
+    return 0;
+  }
+
+  Placement pl = check_placement(boot);
+  if (!pl.ok) P2P_FATAL("process placement check failed: " + pl.error);
+
+  TransportOptions topt;
+  topt.device = cfg.device >= 0 ? cfg.device : pl.local_rank;
+  topt.timeout_s = cfg.timeout_s;
+  topt.verify_impl = cfg.verify_impl;
+  std::unique_ptr<Transport> t =
+      cfg.transport == "host" ? make_host_transport(boot, topt) : make_rccl_transport(boot, topt);
+
+  size_t max_bytes = *std::max_element(cfg.sizes.begin(), cfg.sizes.end());
+  if (cfg.latency) max_bytes = std::max(max_bytes, cfg.latency_bytes);
+  int slots = 1;
+  for (const auto& s : scheds) slots = std::max(slots, s.max_recv_slots());
+  Buffers bufs(*t, max_bytes, slots);
+
+  // Connection warm-up outside any timed cell (the reference pays lazy p2p
+  // connection setup inside its first cells; --reference keeps that).
+  if (cfg.warm_connections)
+    for (const auto& s : scheds) warm_connections(*t, boot, s, bufs);
+
+  AppResult local;
+  AppResult& res = result ? *result : local;
+  bool printed_compat = false;
+  for (const auto& s : scheds) {
+    for (size_t si = 0; si < cfg.sizes.size(); ++si) {
+      RunRecord rec;
+      rec.mode = s.mode;
+      rec.dir = s.dir;
+      rec.bytes = cfg.sizes[si];
+      rec.cfg = cfg.run;
+      rec.cfg.bytes = rec.bytes;
+      rec.cfg.salt = static_cast<uint64_t>(res.runs.size());
+      if (cfg.iters_auto) rec.cfg.iters = auto_iters(rec.bytes, cfg.target_bytes);
+      const bool compat = cfg.compat && s.mode == Mode::Pair && root;
+      CompatPrinter cp(out, n);
+      if (compat) {
+        if (cfg.sizes.size() > 1)
+          std::fprintf(out, "%s# message size %s\n", printed_compat ? "\n" : "", format_size(rec.bytes).c_str());
+        cp.begin(s.dir, printed_compat && s.dir == Direction::Uni && cfg.sizes.size() == 1);
+        printed_compat = true;
+      }
+      rec.phases = run_schedule(*t, boot, s, rec.cfg, bufs, [&](const PhaseResult& r) {
+        if (compat) cp.on_phase(r);
+      });
+      for (const auto& ph : rec.phases) res.mismatches += ph.total_mismatches;
+      res.runs.push_back(std::move(rec));
+    }
+  }
+  if (cfg.latency) res.latency = run_latency(*t, boot, cfg.latency_bytes, cfg.latency_iters, std::min(cfg.latency_iters, 100), bufs);
+
+  // Device descriptions of every rank, for the banner.
+  char mine[256] = {0};
+  std::snprintf(mine, sizeof(mine), "%s", t->device_desc().c_str());
+  std::vector<char> all_desc(static_cast<size_t>(n) * sizeof(mine));
+  boot.allgather(mine, all_desc.data(), sizeof(mine));
+
+  if (root) {
+    if (cfg.extended) {
+      std::fprintf(out, "\n== p2p_matrix: %d rank(s), transport %s, bootstrap %s, %d host(s) ==\n", n, t->name().c_str(),
+                   boot.name().c_str(), pl.num_hosts);
+      for (int r = 0; r < n; ++r) std::fprintf(out, "  rank %d: %s\n", r, &all_desc[static_cast<size_t>(r) * sizeof(mine)]);
+      for (const auto& rec : res.runs) print_extended(out, rec, n);
+      print_latency(out, res.latency, n);
+    }
+    if (!cfg.json_path.empty()) {
+      std::ofstream js(cfg.json_path);
+      P2P_CHECK(js.good(), "cannot write " + cfg.json_path);
+      for (const auto& rec : res.runs) js << run_to_json(rec, n) << "\n";
+      if (!res.latency.empty()) js << latency_to_json(res.latency, n) << "\n";
+    }
+    if (!cfg.csv_path.empty()) {
+      std::ofstream cs(cfg.csv_path);
+      P2P_CHECK(cs.good(), "cannot write " + cfg.csv_path);
+      cs << csv_header();
+      for (const auto& rec : res.runs) cs << run_to_csv(rec);
+    }
+    std::fflush(out);
+  }
+  boot.barrier();
+  if (res.mismatches) {
+    if (root) std::fprintf(stderr, "p2p_matrix: VERIFICATION FAILED: %llu mismatching words\n", static_cast<unsigned long long>(res.mismatches));
+    return 2;
+  }
+  return 0;
+}
+
+}  // namespace p2p

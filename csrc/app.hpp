@@ -1,0 +1,66 @@
+// Top-level application: CLI -> bootstrap -> placement -> transport ->
+// schedules -> reports.  Shared by the p2p_matrix executable (main.cpp) and
+// the Python extension (pymodule.cpp).
+//
+// The reference has no CLI at all (argv only reaches MPI_Init_thread,
+// p2p_matrix.cc:105; message size and iteration count are compile-time
+// constants, :124 and :132).  Defaults here reproduce it: with no flags,
+// `mpirun -n N ./p2p_matrix` runs the serial pair schedule, uni then bi, at
+// 32 MiB x 128 and prints the same two matrices first.
+#pragma once
+
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "report.hpp"
+#include "runner.hpp"
+#include "schedule.hpp"
+
+namespace p2p {
+
+class Bootstrap;
+
+struct AppConfig {
+  std::vector<Mode> modes{Mode::Pair};
+  std::vector<Direction> dirs{Direction::Uni, Direction::Bi};
+  std::vector<size_t> sizes{32u << 20};
+  RunConfig run;                 // iters / warmup / timing / verify
+  bool iters_auto = false;       // scale iterations per size (target_bytes per cell)
+  size_t target_bytes = 4ull << 30;
+  bool latency = false;
+  size_t latency_bytes = 8;
+  int latency_iters = 1000;
+  std::string transport = "rccl";  // rccl | host
+  std::string bootstrap = "auto";  // auto | mpi | env | local
+  int device = -1;
+  std::string json_path;
+  std::string csv_path;
+  bool compat = true;      // reference matrices for pair mode
+  bool extended = true;    // GB/s / latency tables after the compat section
+  double timeout_s = 300;
+  int verify_impl = 0;
+  bool dry_run = false;    // print the schedules and exit (no transport)
+  bool warm_connections = true;
+  int verbose = 0;
+};
+
+// Parses argv (after the program name).  Sets *exit_code and returns false
+// when the program should exit immediately (--help, --version, bad flag).
+bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out = stdout);
+std::string usage_text();
+
+// Iterations for a message size under --iters auto.
+int auto_iters(size_t bytes, size_t target_bytes);
+
+struct AppResult {
+  std::vector<RunRecord> runs;
+  std::vector<LatencyResult> latency;
+  uint64_t mismatches = 0;
+};
+
+// Runs everything collectively; rank 0 prints to `out`.  Returns 0 on success,
+// 2 if verification found corrupted data.
+int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result = nullptr);
+
+}  // namespace p2p

@@ -1,0 +1,100 @@
+#include "common.hpp"
+
+#include <chrono>
+#include <cstdarg>
+#include <cstdlib>
+#include <mutex>
+#include <stdexcept>
+#include <vector>
+
+namespace p2p {
+
+namespace {
+std::mutex g_hook_mu;
+std::vector<std::pair<int, AbortHook>>& hooks() {
+  static std::vector<std::pair<int, AbortHook>> h;
+  return h;
+}
+int g_next_hook = 1;
+bool g_throw = false;
+int g_log_level = -1;
+}  // namespace
+
+int push_abort_hook(AbortHook hook) {
+  std::lock_guard<std::mutex> lk(g_hook_mu);
+  int id = g_next_hook++;
+  hooks().emplace_back(id, std::move(hook));
+  return id;
+}
+
+void remove_abort_hook(int handle) {
+  std::lock_guard<std::mutex> lk(g_hook_mu);
+  auto& h = hooks();
+  for (auto it = h.begin(); it != h.end(); ++it)
+    if (it->first == handle) {
+      h.erase(it);
+      return;
+    }
+}
+
+void clear_abort_hooks() {
+  std::lock_guard<std::mutex> lk(g_hook_mu);
+  hooks().clear();
+}
+
+void set_throw_on_fatal(bool enable) { g_throw = enable; }
+
+void fatal(const char* file, int line, const std::string& what) {
+  std::string msg = strfmt("p2p fatal error at %s:%d: %s", file, line, what.c_str());
+  if (g_throw) throw Error(msg);
+  std::fprintf(stderr, "%s\n", msg.c_str());
+  std::fflush(stderr);
+  std::vector<std::pair<int, AbortHook>> hs;
+  {
+    std::lock_guard<std::mutex> lk(g_hook_mu);
+    hs.swap(hooks());
+  }
+  // Innermost (most recently installed) first: transport before bootstrap.
+  for (auto it = hs.rbegin(); it != hs.rend(); ++it) it->second(EXIT_FAILURE);
+  std::exit(EXIT_FAILURE);
+}
+
+std::string strfmt(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  va_list ap2;
+  va_copy(ap2, ap);
+  int n = std::vsnprintf(nullptr, 0, fmt, ap);
+  va_end(ap);
+  std::string out(n > 0 ? static_cast<size_t>(n) : 0, '\0');
+  if (n > 0) std::vsnprintf(&out[0], static_cast<size_t>(n) + 1, fmt, ap2);
+  va_end(ap2);
+  return out;
+}
+
+int log_level() {
+  if (g_log_level < 0) {
+    const char* e = std::getenv("P2P_LOG");
+    g_log_level = e ? std::atoi(e) : 0;
+  }
+  return g_log_level;
+}
+
+void set_log_level(int level) { g_log_level = level; }
+
+void logf(int level, const char* fmt, ...) {
+  if (log_level() < level) return;
+  va_list ap;
+  va_start(ap, fmt);
+  std::fprintf(stderr, "[p2p] ");
+  std::vfprintf(stderr, fmt, ap);
+  std::fprintf(stderr, "\n");
+  va_end(ap);
+}
+
+double now_seconds() {
+  using clk = std::chrono::steady_clock;
+  return std::chrono::duration<double>(clk::now().time_since_epoch()).count();
+}
+
+}  // namespace p2p

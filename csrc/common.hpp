@@ -1,0 +1,56 @@
+// Error policy, logging and small shared helpers for the p2p framework.
+//
+// Reference parity: the reference's MPICHECK / CUDACHECK / NCCLCHECK macros
+// (/root/reference/p2p_matrix.cc:15-42) print to *stdout* and call exit()
+// without telling the peers, so a failing rank leaves every other rank blocked
+// in a barrier or a stream sync forever.  Here every check
+// routes through p2p::fatal(), which prints to stderr and then runs the
+// registered abort hook (MPI_Abort / ncclCommAbort / closing the TCP mesh) so
+// the whole job goes down together.
+#pragma once
+
+#include <cstdint>
+#include <cstdio>
+#include <functional>
+#include <stdexcept>
+#include <string>
+
+namespace p2p {
+
+// Called once by fatal() before the process exits.  Bootstraps and transports
+// install hooks so that an error on one rank aborts the job instead of hanging.
+using AbortHook = std::function<void(int code)>;
+int push_abort_hook(AbortHook hook);  // returns a handle for remove_abort_hook
+void remove_abort_hook(int handle);
+void clear_abort_hooks();
+
+[[noreturn]] void fatal(const char* file, int line, const std::string& what);
+
+// When set (Python bindings), fatal() throws p2p::Error instead of exiting.
+void set_throw_on_fatal(bool enable);
+
+struct Error : public std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+// printf-style std::string formatting.
+std::string strfmt(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+
+// Verbosity: 0 quiet, 1 info, 2 debug.  Set from P2P_LOG / --verbose.
+int log_level();
+void set_log_level(int level);
+void logf(int level, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+
+double now_seconds();  // monotonic (steady_clock), unlike the reference's system_clock
+
+}  // namespace p2p
+
+#define P2P_FATAL(msg) ::p2p::fatal(__FILE__, __LINE__, (msg))
+
+#define P2P_CHECK(cond, msg)                                             \
+  do {                                                                   \
+    if (!(cond)) ::p2p::fatal(__FILE__, __LINE__, std::string("check failed: " #cond ": ") + (msg)); \
+  } while (0)
+
+#define P2P_INFO(...) ::p2p::logf(1, __VA_ARGS__)
+#define P2P_DEBUG(...) ::p2p::logf(2, __VA_ARGS__)

@@ -1,0 +1,283 @@
+// Python bindings (`test_nccl_p2p_amd._p2pcore`), pybind11.
+//
+// Exposes the native engine to bench.py / the Python package: a Session owns
+// a Bootstrap (TCP star, or local) and a Transport (RCCL on the MI355X, or
+// host sockets).  Everything long-running releases the GIL.  Results cross
+// the boundary as JSON text produced by report.cpp, so the Python side and
+// the p2p_matrix executable share one result schema.
+//
+// The fill / verify kernels are also exposed on raw device pointers so they
+// can be driven on torch tensors and checked against a PyTorch reference.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "app.hpp"
+#include "bootstrap.hpp"
+#include "common.hpp"
+#include "kernels.hpp"
+#include "report.hpp"
+#include "runner.hpp"
+#include "schedule.hpp"
+#include "transport.hpp"
+#include "units.hpp"
+
+namespace py = pybind11;
+using namespace p2p;
+
+namespace {
+
+class Session {
+ public:
+  Session(int rank, int world, const std::string& host, int port, int device, const std::string& transport,
+          double timeout_s, TcpListener* listener)
+      : transport_kind_(transport) {
+    if (world == 1)
+      boot_ = make_local_bootstrap();
+    else
+      boot_ = make_tcp_bootstrap(rank, world, host, port, timeout_s, listener);
+    TransportOptions opt;
+    opt.device = device;
+    opt.timeout_s = timeout_s;
+    if (transport == "rccl")
+      t_ = make_rccl_transport(*boot_, opt);
+    else if (transport == "host")
+      t_ = make_host_transport(*boot_, opt);
+    else
+      P2P_FATAL("transport must be 'rccl' or 'host'");
+  }
+
+  int rank() const { return boot_->rank(); }
+  int world() const { return boot_->size(); }
+  std::string transport() const { return t_->name(); }
+  std::string device_desc() const { return t_->device_desc(); }
+  Bootstrap& boot() { return *boot_; }
+  Transport& t() { return *t_; }
+
+  void barrier() { boot_->barrier(); }
+  double allreduce_max(double v) { return boot_->allreduce_max(v); }
+  double allreduce_sum(double v) { return boot_->allreduce_sum(v); }
+
+  // One (mode, dir, size) run; returns the run JSON (report.cpp schema).
+  std::string run(const std::string& mode, const std::string& dir, size_t bytes, int iters, int warmup,
+                  const std::string& timing, bool verify, bool warm) {
+    Schedule s = make_schedule(parse_mode(mode), parse_direction(dir), world());
+    RunConfig cfg;
+    cfg.bytes = bytes;
+    cfg.iters = iters;
+    cfg.warmup = warmup;
+    cfg.timing = parse_timing(timing);
+    cfg.verify = verify;
+    cfg.salt = ++salt_;
+    Buffers bufs(*t_, bytes, std::max(1, s.max_recv_slots()));
+    if (warm) warm_connections(*t_, *boot_, s, bufs);
+    RunRecord rec;
+    rec.mode = s.mode;
+    rec.dir = s.dir;
+    rec.bytes = bytes;
+    rec.cfg = cfg;
+    rec.phases = run_schedule(*t_, *boot_, s, cfg, bufs);
+    return run_to_json(rec, world());
+  }
+
+  std::string latency(size_t bytes, int iters, int warmup) {
+    Buffers bufs(*t_, std::max<size_t>(bytes, 16), 1);
+    auto lat = run_latency(*t_, *boot_, bytes, iters, warmup, bufs);
+    return latency_to_json(lat, world());
+  }
+
+ private:
+  std::unique_ptr<Bootstrap> boot_;
+  std::unique_ptr<Transport> t_;
+  std::string transport_kind_;
+  uint64_t salt_ = 1000;
+};
+
+class PyStepDriver {
+ public:
+  PyStepDriver(std::shared_ptr<Session> s, const std::string& mode, const std::string& dir, size_t bytes, int msgs,
+               bool verify)
+      : session_(std::move(s)),
+        d_(session_->t(), session_->boot(), make_schedule(parse_mode(mode), parse_direction(dir), session_->world()),
+           bytes, msgs, verify) {}
+  StepDriver& d() { return d_; }
+
+ private:
+  std::shared_ptr<Session> session_;  // keeps transport alive
+  StepDriver d_;
+};
+
+hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Kernel entry points on raw device pointers (torch tensors' data_ptr()).
+struct KernelScratch {
+  dev::VerifyAccum* d = nullptr;
+  dev::VerifyAccum* h = nullptr;
+  int device = -1;
+};
+KernelScratch& scratch() {
+  static KernelScratch s;
+  int dv = 0;
+  if (hipGetDevice(&dv) != hipSuccess) P2P_FATAL("no HIP device");
+  if (s.device != dv) {
+    if (s.d) (void)hipFree(s.d);
+    if (s.h) (void)hipHostFree(s.h);
+    if (hipMalloc(&s.d, sizeof(dev::VerifyAccum)) != hipSuccess) P2P_FATAL("hipMalloc failed");
+    if (hipHostMalloc(&s.h, sizeof(dev::VerifyAccum), hipHostMallocDefault) != hipSuccess) P2P_FATAL("hipHostMalloc failed");
+    s.device = dv;
+  }
+  return s;
+}
+
+py::tuple device_verify(uintptr_t ptr, size_t bytes, uint64_t seed, int impl, bool check, uintptr_t stream) {
+  KernelScratch& ks = scratch();
+  hipStream_t st = as_stream(stream);
+  {
+    py::gil_scoped_release nogil;
+    dev::launch_verify_reset(ks.d, st);
+    dev::launch_verify(reinterpret_cast<const void*>(ptr), bytes, seed, ks.d, static_cast<dev::VerifyImpl>(impl), check, st);
+    if (hipMemcpyAsync(ks.h, ks.d, sizeof(dev::VerifyAccum), hipMemcpyDeviceToHost, st) != hipSuccess)
+      P2P_FATAL("hipMemcpyAsync failed");
+    if (hipStreamSynchronize(st) != hipSuccess) P2P_FATAL("hipStreamSynchronize failed");
+  }
+  return py::make_tuple(ks.h->mismatches, ks.h->checksum, ks.h->first_bad);
+}
+
+py::list schedule_py(const std::string& mode, const std::string& dir, int n) {
+  Schedule s = make_schedule(parse_mode(mode), parse_direction(dir), n);
+  py::list phases;
+  for (const auto& p : s.phases) {
+    py::dict d;
+    d["label"] = p.label;
+    d["row"] = p.row;
+    d["col"] = p.col;
+    d["idle"] = p.idle;
+    py::list flows;
+    for (const auto& f : p.flows) flows.append(py::make_tuple(f.src, f.dst));
+    d["flows"] = flows;
+    py::list ranks;
+    for (const auto& r : p.ranks) ranks.append(py::make_tuple(r.send_to, r.recv_from));
+    d["ranks"] = ranks;
+    phases.append(d);
+  }
+  return phases;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_p2pcore, m) {
+  m.doc() = "MI355X-native P2P benchmark engine (RCCL over xGMI, gfx950 kernels)";
+  set_throw_on_fatal(true);
+
+  py::class_<TcpListener>(m, "TcpListener")
+      .def(py::init<int, const std::string&>(), py::arg("port") = 0, py::arg("bind_addr") = "0.0.0.0")
+      .def_property_readonly("port", &TcpListener::port);
+
+  py::class_<Session, std::shared_ptr<Session>>(m, "Session")
+      .def(py::init<int, int, const std::string&, int, int, const std::string&, double, TcpListener*>(), py::arg("rank"),
+           py::arg("world"), py::arg("host") = "127.0.0.1", py::arg("port") = 0, py::arg("device") = 0,
+           py::arg("transport") = "rccl", py::arg("timeout_s") = 300.0, py::arg("listener") = nullptr,
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("rank", &Session::rank)
+      .def_property_readonly("world", &Session::world)
+      .def_property_readonly("transport", &Session::transport)
+      .def_property_readonly("device_desc", &Session::device_desc)
+      .def("barrier", &Session::barrier, py::call_guard<py::gil_scoped_release>())
+      .def("allreduce_max", &Session::allreduce_max, py::call_guard<py::gil_scoped_release>())
+      .def("allreduce_sum", &Session::allreduce_sum, py::call_guard<py::gil_scoped_release>())
+      .def("run", &Session::run, py::arg("mode") = "pair", py::arg("dir") = "uni", py::arg("bytes") = 32u << 20,
+           py::arg("iters") = 128, py::arg("warmup") = 8, py::arg("timing") = "events", py::arg("verify") = false,
+           py::arg("warm") = true, py::call_guard<py::gil_scoped_release>())
+      .def("latency", &Session::latency, py::arg("bytes") = 8, py::arg("iters") = 1000, py::arg("warmup") = 100,
+           py::call_guard<py::gil_scoped_release>());
+
+  py::class_<PyStepDriver>(m, "StepDriver")
+      .def(py::init<std::shared_ptr<Session>, const std::string&, const std::string&, size_t, int, bool>(),
+           py::arg("session"), py::arg("mode") = "tournament", py::arg("dir") = "bi", py::arg("bytes") = 32u << 20,
+           py::arg("msgs") = 8, py::arg("verify") = false, py::call_guard<py::gil_scoped_release>())
+      .def("connect", [](PyStepDriver& s) { s.d().connect(); }, py::call_guard<py::gil_scoped_release>())
+      .def("step", [](PyStepDriver& s, long k) { s.d().step(k); }, py::call_guard<py::gil_scoped_release>())
+      .def("run_steps", [](PyStepDriver& s, long first, long count) {
+            for (long k = first; k < first + count; ++k) s.d().step(k);
+          }, py::call_guard<py::gil_scoped_release>())
+      .def("sync", [](PyStepDriver& s) { s.d().sync(); }, py::call_guard<py::gil_scoped_release>())
+      .def("step_ms", [](PyStepDriver& s) { return s.d().step_ms(); })
+      .def("reset", [](PyStepDriver& s) { s.d().reset(); })
+      .def("verify_last", [](PyStepDriver& s) { return s.d().verify_last(); }, py::call_guard<py::gil_scoped_release>())
+      .def("bytes_sent_per_step", [](PyStepDriver& s, long k) { return s.d().bytes_sent_per_step(k); })
+      .def("job_bytes_per_step", [](PyStepDriver& s, long k) { return s.d().job_bytes_per_step(k); })
+      .def_property_readonly("phases", [](PyStepDriver& s) { return s.d().phases(); })
+      .def("phase_flows", [](PyStepDriver& s, long k) {
+        const auto& p = s.d().schedule().phases[static_cast<size_t>(k % s.d().phases())];
+        std::vector<std::pair<int, int>> f;
+        for (auto& x : p.flows) f.emplace_back(x.src, x.dst);
+        return f;
+      });
+
+  // ---- kernels on raw pointers ----
+  m.def("fill", [](uintptr_t ptr, size_t bytes, uint64_t seed, uintptr_t stream) {
+        dev::launch_fill(reinterpret_cast<void*>(ptr), bytes, seed, as_stream(stream));
+      }, py::arg("ptr"), py::arg("bytes"), py::arg("seed"), py::arg("stream") = 0);
+  m.def("verify", &device_verify, py::arg("ptr"), py::arg("bytes"), py::arg("seed"), py::arg("impl") = 0,
+        py::arg("check") = true, py::arg("stream") = 0,
+        "Returns (mismatching words, checksum, first bad byte offset or 2**64-1).");
+  m.def("fill_geometry", [](size_t bytes) {
+    auto g = dev::fill_geometry(bytes);
+    return py::make_tuple(g.grid, g.block, g.lds_bytes);
+  });
+  m.def("verify_geometry", [](size_t bytes, int impl) {
+    auto g = dev::verify_geometry(bytes, static_cast<dev::VerifyImpl>(impl));
+    return py::make_tuple(g.grid, g.block, g.lds_bytes);
+  });
+  m.def("rccl_available", &rccl_transport_available);
+
+  // ---- host reference (bit-compatible with the kernels) ----
+  m.def("host_fill", [](size_t bytes, uint64_t seed) {
+    std::string out(bytes, '\0');
+    host_fill(&out[0], bytes, seed);
+    return py::bytes(out);
+  });
+  m.def("host_verify", [](py::bytes data, uint64_t seed) {
+    std::string s = data;
+    VerifyResult r = host_verify(s.data(), s.size(), seed);
+    return py::make_tuple(r.mismatches, r.checksum, r.first_bad);
+  });
+  m.def("prng_word", &prng_word);
+  m.def("payload_seed", &payload_seed);
+
+  // ---- pure host helpers ----
+  m.def("schedule", &schedule_py, py::arg("mode"), py::arg("dir"), py::arg("n"));
+  m.def("round_robin_rounds", &round_robin_rounds);
+  m.def("parse_size", &parse_size);
+  m.def("parse_size_list", &parse_size_list);
+  m.def("format_size", &format_size);
+  m.def("host_hash", &host_hash);
+  m.def("compute_placement", [](const std::vector<uint64_t>& h, int rank) {
+    Placement p = compute_placement(h, rank);
+    py::dict d;
+    d["ok"] = p.ok;
+    d["error"] = p.error;
+    d["num_hosts"] = p.num_hosts;
+    d["ranks_per_host"] = p.ranks_per_host;
+    d["local_rank"] = p.local_rank;
+    return d;
+  });
+  m.def("usage", &usage_text);
+  // The full p2p_matrix application in-process (TCP/env or local bootstrap),
+  // e.g. `torchrun --nproc-per-node 8 -m test_nccl_p2p_amd --mode all`.
+  m.def("run_cli", [](std::vector<std::string> args) {
+    std::vector<char*> argv;
+    for (auto& a : args) argv.push_back(&a[0]);
+    AppConfig cfg;
+    int code = 0;
+    if (!parse_cli(static_cast<int>(argv.size()), argv.data(), &cfg, &code)) return code;
+    py::gil_scoped_release nogil;
+    std::string kind = cfg.bootstrap == "mpi" ? "env" : cfg.bootstrap;
+    auto boot = make_bootstrap(kind, nullptr, nullptr);
+    return run_app(cfg, *boot, stdout);
+  }, py::arg("args"));
+}

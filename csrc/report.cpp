@@ -1,0 +1,228 @@
+#include "report.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <sstream>
+
+#include "common.hpp"
+#include "stats.hpp"
+#include "units.hpp"
+
+namespace p2p {
+
+// -------------------------------------------------------------- compat ----
+
+void CompatPrinter::begin(Direction dir, bool leading_blank_line) {
+  if (dir == Direction::Uni) {
+    std::fprintf(out_, "%sEvaluating the Uni-Directional NCCL P2P Bandwidth (Gbps)\n", leading_blank_line ? "\n" : "");
+  } else {
+    // The reference's bi title always starts with "\n" (p2p_matrix.cc:189).
+    std::fprintf(out_, "\nEvaluating the Bi-Directional NCCL P2P Bandwidth (Gbps)\n");
+  }
+  std::fprintf(out_, "   D\\D");
+  for (int i = 0; i < n_; ++i) std::fprintf(out_, "%6d ", i);
+  std::fprintf(out_, "\n");
+  std::fflush(out_);
+}
+
+double compat_cell_gbps(const PhaseResult& r) {
+  if (r.idle) return 0.0;
+  return gbps(r.bytes_per_iter, r.seconds_per_iter);
+}
+
+void CompatPrinter::on_phase(const PhaseResult& r) {
+  if (r.row < 0) return;
+  if (r.col == 0) std::fprintf(out_, "%6d ", r.row);
+  std::fprintf(out_, "%6.02f ", compat_cell_gbps(r));
+  std::fflush(out_);  // p2p_matrix.cc:180: partial results survive a kill
+  if (r.col == n_ - 1) std::fprintf(out_, "\n");
+}
+
+// -------------------------------------------------------------- matrices --
+
+std::vector<double> flow_matrix_gbs(const RunRecord& rec, int n) {
+  std::vector<double> m(static_cast<size_t>(n) * n, 0.0);
+  for (const auto& ph : rec.phases)
+    for (const auto& f : ph.flows) m[static_cast<size_t>(f.flow.src) * n + f.flow.dst] = f.gbs;
+  return m;
+}
+
+std::vector<double> flow_matrix_p50_us(const RunRecord& rec, int n) {
+  std::vector<double> m(static_cast<size_t>(n) * n, 0.0);
+  for (const auto& ph : rec.phases)
+    for (const auto& f : ph.flows) m[static_cast<size_t>(f.flow.src) * n + f.flow.dst] = f.iter_us.p50;
+  return m;
+}
+
+void print_matrix(FILE* out, const std::string& title, const std::vector<double>& m, int n, const char* fmt,
+                  bool blank_diag) {
+  std::fprintf(out, "%s\n", title.c_str());
+  std::fprintf(out, "  src\\dst");
+  for (int j = 0; j < n; ++j) std::fprintf(out, " %9d", j);
+  std::fprintf(out, "\n");
+  for (int i = 0; i < n; ++i) {
+    std::fprintf(out, "  %7d", i);
+    for (int j = 0; j < n; ++j) {
+      double v = m[static_cast<size_t>(i) * n + j];
+      if ((blank_diag && i == j && n > 1) || v == 0.0) {
+        std::fprintf(out, " %9s", "-");
+      } else {
+        std::fprintf(out, " ");
+        std::fprintf(out, fmt, v);
+      }
+    }
+    std::fprintf(out, "\n");
+  }
+}
+
+void print_extended(FILE* out, const RunRecord& rec, int n) {
+  std::string head = strfmt("[%s %s | %s x %d | timing=%s warmup=%d%s]", mode_name(rec.mode), direction_name(rec.dir),
+                            format_size(rec.bytes).c_str(), rec.cfg.iters, timing_name(rec.cfg.timing), rec.cfg.warmup,
+                            rec.cfg.verify ? " verify" : "");
+  std::fprintf(out, "\n== %s ==\n", head.c_str());
+  bool blank_diag = rec.mode != Mode::Self && n > 1;
+  auto gbs = flow_matrix_gbs(rec, n);
+  print_matrix(out, "GB/s per direction (1 GB = 1e9 B; row = sender, col = receiver)", gbs, n, "%9.2f", blank_diag);
+  MatrixSummary ms = summarize_offdiag(gbs, n);
+  std::fprintf(out, "  flow GB/s: min %.2f  mean %.2f  max %.2f  (%zu cells)\n", ms.min, ms.mean, ms.max, ms.cells);
+  auto p50 = flow_matrix_p50_us(rec, n);
+  print_matrix(out, "p50 per-message time (us, receiver GPU timeline)", p50, n, "%9.1f", blank_diag);
+
+  // Concurrent modes: per-phase aggregate (bisection / ring throughput).
+  if (rec.mode != Mode::Pair) {
+    for (const auto& ph : rec.phases) {
+      std::fprintf(out, "  phase '%s': %zu flows, %.2f GB/s aggregate, %.1f us per iteration\n", ph.label.c_str(),
+                   ph.flows.size(), ph.agg_gbs, ph.seconds_per_iter * 1e6);
+    }
+    if (rec.mode == Mode::AllPairs || rec.mode == Mode::Ring) {
+      std::vector<double> egress(static_cast<size_t>(n), 0.0), ingress(static_cast<size_t>(n), 0.0);
+      for (const auto& ph : rec.phases)
+        for (const auto& f : ph.flows) {
+          egress[static_cast<size_t>(f.flow.src)] += static_cast<double>(rec.bytes) / ph.seconds_per_iter / 1e9;
+          ingress[static_cast<size_t>(f.flow.dst)] += static_cast<double>(rec.bytes) / ph.seconds_per_iter / 1e9;
+        }
+      std::fprintf(out, "  per-rank egress/ingress GB/s:");
+      for (int r = 0; r < n; ++r) std::fprintf(out, " [%d] %.1f/%.1f", r, egress[static_cast<size_t>(r)], ingress[static_cast<size_t>(r)]);
+      std::fprintf(out, "\n");
+    }
+  }
+  uint64_t bad = 0;
+  bool verified = false;
+  for (const auto& ph : rec.phases) {
+    bad += ph.total_mismatches;
+    for (const auto& f : ph.flows) verified |= f.verified;
+  }
+  if (verified) std::fprintf(out, "  verification: %s (%llu mismatching words)\n", bad ? "FAILED" : "OK", static_cast<unsigned long long>(bad));
+  std::fflush(out);
+}
+
+void print_latency(FILE* out, const std::vector<LatencyResult>& lat, int n) {
+  if (lat.empty()) return;
+  std::vector<double> m(static_cast<size_t>(n) * n, 0.0);
+  std::vector<double> p50s;
+  for (const auto& l : lat) {
+    m[static_cast<size_t>(l.a) * n + l.b] = l.one_way_us.p50;
+    m[static_cast<size_t>(l.b) * n + l.a] = l.one_way_us.p50;
+    p50s.push_back(l.one_way_us.p50);
+  }
+  std::fprintf(out, "\n== latency: %s messages, ping-pong ==\n", format_size(lat[0].bytes).c_str());
+  print_matrix(out, "p50 one-way latency (us)", m, n, "%9.2f", n > 1);
+  Summary s = summarize(p50s);
+  std::fprintf(out, "  p50 over pairs: min %.2f  median %.2f  max %.2f us\n", s.min, s.p50, s.max);
+  std::fflush(out);
+}
+
+// ---------------------------------------------------------------- json ----
+
+std::string json_escape(const std::string& s) {
+  std::string o;
+  for (char c : s) {
+    switch (c) {
+      case '"': o += "\\\""; break;
+      case '\\': o += "\\\\"; break;
+      case '\n': o += "\\n"; break;
+      case '\t': o += "\\t"; break;
+      default:
+        if (static_cast<unsigned char>(c) < 0x20)
+          o += strfmt("\\u%04x", c);
+        else
+          o += c;
+    }
+  }
+  return o;
+}
+
+namespace {
+std::string num(double v) {
+  if (!std::isfinite(v)) return "null";
+  return strfmt("%.6g", v);
+}
+std::string summary_json(const Summary& s) {
+  return strfmt("{\"n\":%zu,\"min\":%s,\"p50\":%s,\"p90\":%s,\"p99\":%s,\"max\":%s,\"mean\":%s}", s.n, num(s.min).c_str(),
+                num(s.p50).c_str(), num(s.p90).c_str(), num(s.p99).c_str(), num(s.max).c_str(), num(s.mean).c_str());
+}
+std::string matrix_json(const std::vector<double>& m, int n) {
+  std::string o = "[";
+  for (int i = 0; i < n; ++i) {
+    o += i ? ",[" : "[";
+    for (int j = 0; j < n; ++j) o += (j ? "," : "") + num(m[static_cast<size_t>(i) * n + j]);
+    o += "]";
+  }
+  return o + "]";
+}
+}  // namespace
+
+std::string run_to_json(const RunRecord& rec, int n) {
+  auto gbs = flow_matrix_gbs(rec, n);
+  MatrixSummary ms = summarize_offdiag(gbs, n);
+  std::ostringstream o;
+  o << "{\"type\":\"run\",\"mode\":\"" << mode_name(rec.mode) << "\",\"dir\":\"" << direction_name(rec.dir)
+    << "\",\"bytes\":" << rec.bytes << ",\"iters\":" << rec.cfg.iters << ",\"warmup\":" << rec.cfg.warmup
+    << ",\"timing\":\"" << timing_name(rec.cfg.timing) << "\",\"nranks\":" << n
+    << ",\"gbs_matrix\":" << matrix_json(gbs, n) << ",\"p50_us_matrix\":" << matrix_json(flow_matrix_p50_us(rec, n), n)
+    << ",\"gbs_min\":" << num(ms.min) << ",\"gbs_mean\":" << num(ms.mean) << ",\"gbs_max\":" << num(ms.max)
+    << ",\"phases\":[";
+  bool first = true;
+  for (const auto& ph : rec.phases) {
+    if (ph.idle) continue;
+    o << (first ? "" : ",") << "{\"label\":\"" << json_escape(ph.label) << "\",\"row\":" << ph.row << ",\"col\":" << ph.col
+      << ",\"seconds_per_iter\":" << num(ph.seconds_per_iter) << ",\"agg_gbs\":" << num(ph.agg_gbs)
+      << ",\"compat_gbps\":" << num(compat_cell_gbps(ph)) << ",\"wall_seconds\":" << num(ph.wall_seconds)
+      << ",\"mismatches\":" << ph.total_mismatches << ",\"flows\":[";
+    for (size_t i = 0; i < ph.flows.size(); ++i) {
+      const auto& f = ph.flows[i];
+      o << (i ? "," : "") << "{\"src\":" << f.flow.src << ",\"dst\":" << f.flow.dst << ",\"seconds\":" << num(f.seconds)
+        << ",\"gbps\":" << num(f.gbps) << ",\"gbs\":" << num(f.gbs) << ",\"iter_us\":" << summary_json(f.iter_us);
+      if (f.verified) o << ",\"mismatches\":" << f.mismatches << ",\"checksum\":" << f.checksum;
+      o << "}";
+    }
+    o << "]}";
+    first = false;
+  }
+  o << "]}";
+  return o.str();
+}
+
+std::string latency_to_json(const std::vector<LatencyResult>& lat, int n) {
+  std::ostringstream o;
+  o << "{\"type\":\"latency\",\"nranks\":" << n << ",\"bytes\":" << (lat.empty() ? 0 : lat[0].bytes) << ",\"pairs\":[";
+  for (size_t i = 0; i < lat.size(); ++i)
+    o << (i ? "," : "") << "{\"a\":" << lat[i].a << ",\"b\":" << lat[i].b << ",\"one_way_us\":" << summary_json(lat[i].one_way_us) << "}";
+  o << "]}";
+  return o.str();
+}
+
+std::string csv_header() { return "mode,dir,bytes,iters,timing,phase,src,dst,seconds,gbps,gbs,p50_us,p99_us,mismatches\n"; }
+
+std::string run_to_csv(const RunRecord& rec) {
+  std::ostringstream o;
+  for (const auto& ph : rec.phases)
+    for (const auto& f : ph.flows)
+      o << mode_name(rec.mode) << ',' << direction_name(rec.dir) << ',' << rec.bytes << ',' << rec.cfg.iters << ','
+        << timing_name(rec.cfg.timing) << ",\"" << ph.label << "\"," << f.flow.src << ',' << f.flow.dst << ','
+        << num(f.seconds) << ',' << num(f.gbps) << ',' << num(f.gbs) << ',' << num(f.iter_us.p50) << ','
+        << num(f.iter_us.p99) << ',' << f.mismatches << '\n';
+  return o.str();
+}
+
+}  // namespace p2p

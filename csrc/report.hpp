@@ -1,0 +1,67 @@
+// Reporting: the reference-compatible text matrices, extended tables, JSON.
+//
+// Compat format (byte-exact with /root/reference/p2p_matrix.cc):
+//   title   "Evaluating the Uni-Directional NCCL P2P Bandwidth (Gbps)\n"   :134
+//           "\nEvaluating the Bi-Directional NCCL P2P Bandwidth (Gbps)\n"  :189
+//   corner  "   D\\D"                                                     :135/:190
+//   col id  "%6d "                                                        :137/:192
+//   row id  "%6d "                                                        :143/:198
+//   cell    "%6.02f " (diagonal 0.00), fflush after each cell             :149,179/:204,260
+//   row end "\n"                                                          :184/:265
+// Values >= 1000 Gbps overflow the 6-char field exactly as the reference's
+// printf would; aligned GB/s tables follow after.
+#pragma once
+
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "runner.hpp"
+#include "schedule.hpp"
+
+namespace p2p {
+
+class CompatPrinter {
+ public:
+  CompatPrinter(FILE* out, int nranks) : out_(out), n_(nranks) {}
+  void begin(Direction dir, bool leading_blank_line);
+  void on_phase(const PhaseResult& r);  // pair-mode phases, in row-major order
+ private:
+  FILE* out_;
+  int n_;
+};
+
+// Gbps value the reference would print for a pair-mode cell: uni = the one
+// flow; bi = sum of both directions (p2p_matrix.cc:258 "* 2").
+double compat_cell_gbps(const PhaseResult& r);
+
+struct RunRecord {
+  Mode mode;
+  Direction dir;
+  size_t bytes;
+  RunConfig cfg;
+  std::vector<PhaseResult> phases;
+};
+
+// N x N (row = src, col = dst) matrices built from all flows of a run.
+std::vector<double> flow_matrix_gbs(const RunRecord& rec, int n);
+std::vector<double> flow_matrix_p50_us(const RunRecord& rec, int n);
+
+// Human-readable tables appended after the compat section.
+void print_extended(FILE* out, const RunRecord& rec, int n);
+void print_latency(FILE* out, const std::vector<LatencyResult>& lat, int n);
+void print_matrix(FILE* out, const std::string& title, const std::vector<double>& m, int n, const char* fmt,
+                  bool blank_diag);
+
+// Machine-readable JSON (one object per run / latency set).
+std::string run_to_json(const RunRecord& rec, int n);
+std::string latency_to_json(const std::vector<LatencyResult>& lat, int n);
+
+// CSV rows: mode,dir,bytes,iters,timing,phase,src,dst,seconds,gbps,gbs,p50_us,p99_us,mismatches
+std::string csv_header();
+std::string run_to_csv(const RunRecord& rec);
+
+// Minimal JSON string escaping.
+std::string json_escape(const std::string& s);
+
+}  // namespace p2p

@@ -1,0 +1,427 @@
+#include "runner.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+
+#include "bootstrap.hpp"
+#include "common.hpp"
+#include "units.hpp"
+
+namespace p2p {
+
+const char* timing_name(Timing t) { return t == Timing::Events ? "events" : "wallclock"; }
+
+Timing parse_timing(const std::string& s) {
+  if (s == "events" || s == "event" || s == "hipevents") return Timing::Events;
+  if (s == "wallclock" || s == "wall" || s == "reference") return Timing::Wallclock;
+  P2P_FATAL("unknown timing '" + s + "' (events|wallclock)");
+}
+
+// ------------------------------------------------------------- Buffers ----
+
+Buffers::Buffers(Transport& t, size_t max_bytes, int recv_slots) : t_(t), cap_(std::max<size_t>(max_bytes, 16)) {
+  send_ = t_.alloc(cap_);
+  for (int i = 0; i < recv_slots; ++i) recv_.push_back(t_.alloc(cap_));
+}
+
+Buffers::~Buffers() {
+  for (void* p : recv_) t_.release(p);
+  if (send_) t_.release(send_);
+}
+
+// -------------------------------------------------------------- helpers ----
+
+void post_phase_iteration(Transport& t, const Phase& phase, size_t bytes, Buffers& bufs) {
+  const RankOps& ops = phase.ranks[static_cast<size_t>(t.rank())];
+  t.group_begin();
+  for (int peer : ops.send_to) t.send(bufs.send_buf(), bytes, peer);
+  for (size_t i = 0; i < ops.recv_from.size(); ++i) t.recv(bufs.recv_buf(static_cast<int>(i)), bytes, ops.recv_from[i]);
+  t.group_end();
+}
+
+namespace {
+
+// Slot on the receiver of each flow: flows were appended in the same order as
+// the receiver's recv_from list (schedule.cpp add_flow).
+std::vector<int> flow_slots(const Phase& phase) {
+  std::vector<int> slots;
+  std::vector<int> seen(phase.ranks.size(), 0);
+  for (const auto& f : phase.flows) slots.push_back(seen[static_cast<size_t>(f.dst)]++);
+  return slots;
+}
+
+void prepare_payload(Transport& t, const Phase& phase, const RunConfig& cfg, Buffers& bufs) {
+  const RankOps& ops = phase.ranks[static_cast<size_t>(t.rank())];
+  P2P_CHECK(cfg.bytes <= bufs.capacity(), "message larger than buffers");
+  P2P_CHECK(static_cast<int>(ops.recv_from.size()) <= bufs.slots(), "not enough receive slots");
+  if (!ops.send_to.empty()) t.fill(bufs.send_buf(), cfg.bytes, payload_seed(t.rank(), cfg.bytes, cfg.salt));
+  if (cfg.verify)
+    for (size_t i = 0; i < ops.recv_from.size(); ++i) t.zero(bufs.recv_buf(static_cast<int>(i)), cfg.bytes);
+}
+
+// Fault injection for the failure-detection tests: P2P_INJECT_FAULT =
+// "<kind>@<rank>[:<phase>]" with kind one of
+//   corrupt — zero the first 64 B of receive slot 0 after the timed loop
+//             (verification must report it, exit code 2),
+//   exit    — the rank dies abruptly (peers must fail, not hang),
+//   hang    — the rank stops responding (peers' watchdogs must fire).
+struct FaultSpec {
+  std::string kind;
+  int rank = -1;
+  long phase = -1;
+};
+
+const FaultSpec& fault_spec() {
+  static FaultSpec spec = [] {
+    FaultSpec s;
+    const char* e = std::getenv("P2P_INJECT_FAULT");
+    if (!e || !*e) return s;
+    std::string v(e);
+    auto at = v.find('@');
+    if (at == std::string::npos) return s;
+    s.kind = v.substr(0, at);
+    std::string rest = v.substr(at + 1);
+    auto colon = rest.find(':');
+    s.rank = std::atoi(rest.substr(0, colon).c_str());
+    if (colon != std::string::npos) s.phase = std::atol(rest.substr(colon + 1).c_str());
+    return s;
+  }();
+  return spec;
+}
+
+void maybe_inject_fault(Transport& t, Buffers& bufs, int rank, size_t phase_index, size_t bytes) {
+  const FaultSpec& f = fault_spec();
+  if (f.kind.empty() || f.rank != rank) return;
+  if (f.phase >= 0 && static_cast<size_t>(f.phase) != phase_index) return;
+  if (f.kind == "corrupt") {
+    if (bufs.slots() > 0) {
+      t.zero(bufs.recv_buf(0), std::min<size_t>(bytes, 64));
+      t.sync();
+    }
+  } else if (f.kind == "exit") {
+    std::fprintf(stderr, "[p2p] injected fault: rank %d exits\n", rank);
+    std::fflush(stderr);
+    std::_Exit(17);
+  } else if (f.kind == "hang") {
+    std::fprintf(stderr, "[p2p] injected fault: rank %d hangs\n", rank);
+    std::fflush(stderr);
+    for (;;) std::this_thread::sleep_for(std::chrono::seconds(1));
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------ run_phase ----
+
+PhaseResult run_phase(Transport& t, Bootstrap& boot, const Phase& phase, size_t phase_index, const RunConfig& cfg,
+                      Buffers& bufs) {
+  const int n = boot.size();
+  const int me = boot.rank();
+  PhaseResult res;
+  res.index = phase_index;
+  res.label = phase.label;
+  res.row = phase.row;
+  res.col = phase.col;
+  res.idle = phase.idle;
+  res.bytes = cfg.bytes;
+  res.iters = cfg.iters;
+  res.rank_seconds.assign(static_cast<size_t>(n), 0.0);
+
+  if (phase.idle) {
+    // p2p_matrix.cc:146-152: every rank takes the barrier, then the diagonal
+    // is reported as 0.00 without moving data.
+    boot.barrier();
+    return res;
+  }
+  P2P_CHECK(cfg.iters >= 1, "iters must be >= 1");
+  const bool active = phase.participates(me);
+
+  if (active) {
+    prepare_payload(t, phase, cfg, bufs);
+    for (int i = 0; i < cfg.warmup; ++i) post_phase_iteration(t, phase, cfg.bytes, bufs);
+    t.sync();
+  }
+
+  double my_seconds = 0;
+  std::vector<double> iter_samples;
+  boot.barrier();
+  const double w0 = now_seconds();
+  if (cfg.timing == Timing::Wallclock) {
+    // Reference semantics: a host stream-sync after every message
+    // (p2p_matrix.cc:162, :170, :229-230, :250-251) and a barrier-bracketed
+    // host clock (:153, :173-176).
+    if (active) {
+      iter_samples.reserve(static_cast<size_t>(cfg.iters));
+      for (int i = 0; i < cfg.iters; ++i) {
+        double a = now_seconds();
+        post_phase_iteration(t, phase, cfg.bytes, bufs);
+        t.sync();
+        iter_samples.push_back((now_seconds() - a) * 1e6);
+      }
+    }
+    boot.barrier();
+    my_seconds = now_seconds() - w0;
+  } else {
+    if (active) {
+      t.clear_marks();
+      int m0 = t.mark();
+      std::vector<int> marks;
+      marks.reserve(static_cast<size_t>(cfg.iters));
+      for (int i = 0; i < cfg.iters; ++i) {
+        post_phase_iteration(t, phase, cfg.bytes, bufs);
+        if (cfg.samples || i + 1 == cfg.iters) marks.push_back(t.mark());
+      }
+      t.sync();
+      my_seconds = t.elapsed_ms(m0, marks.back()) / 1e3;
+      if (cfg.samples) {
+        int prev = m0;
+        for (int m : marks) {
+          iter_samples.push_back(t.elapsed_ms(prev, m) * 1e3);
+          prev = m;
+        }
+      }
+    }
+    boot.barrier();
+  }
+  res.wall_seconds = now_seconds() - w0;
+
+  if (active) maybe_inject_fault(t, bufs, me, phase_index, cfg.bytes);
+
+  std::string err = t.async_error();
+  if (!err.empty()) P2P_FATAL("transport reported an asynchronous error: " + err);
+
+  // Verification of every receive slot on this rank.
+  const int maxslots = std::max(1, phase.max_recv_slots());
+  std::vector<uint64_t> vr(static_cast<size_t>(maxslots) * 2, 0);
+  if (active && cfg.verify) {
+    const RankOps& ops = phase.ranks[static_cast<size_t>(me)];
+    for (size_t i = 0; i < ops.recv_from.size(); ++i) {
+      VerifyResult v = t.verify(bufs.recv_buf(static_cast<int>(i)), cfg.bytes, payload_seed(ops.recv_from[i], cfg.bytes, cfg.salt));
+      vr[2 * i] = v.mismatches;
+      vr[2 * i + 1] = v.checksum;
+    }
+  }
+
+  res.rank_seconds = boot.allgather_value(my_seconds);
+  Summary mine = summarize(iter_samples);
+  auto summaries = boot.allgather_value(mine);
+  auto all_vr = boot.allgather_vector(vr);
+
+  double phase_s = 0;
+  for (int r = 0; r < n; ++r)
+    if (cfg.timing == Timing::Wallclock || phase.participates(r)) phase_s = std::max(phase_s, res.rank_seconds[static_cast<size_t>(r)]);
+  res.seconds_per_iter = phase_s / cfg.iters;
+  res.bytes_per_iter = static_cast<double>(cfg.bytes) * static_cast<double>(phase.flows.size());
+  res.agg_gbs = gbytes_per_s(res.bytes_per_iter, res.seconds_per_iter);
+
+  auto slots = flow_slots(phase);
+  for (size_t fi = 0; fi < phase.flows.size(); ++fi) {
+    const Flow& f = phase.flows[fi];
+    FlowResult fr;
+    fr.flow = f;
+    double s = cfg.timing == Timing::Wallclock
+                   ? phase_s
+                   : std::max(res.rank_seconds[static_cast<size_t>(f.src)], res.rank_seconds[static_cast<size_t>(f.dst)]);
+    fr.seconds = s / cfg.iters;
+    fr.gbps = gbps(static_cast<double>(cfg.bytes), fr.seconds);
+    fr.gbs = gbytes_per_s(static_cast<double>(cfg.bytes), fr.seconds);
+    fr.iter_us = summaries[static_cast<size_t>(f.dst)];
+    if (cfg.verify) {
+      size_t base = static_cast<size_t>(f.dst) * vr.size() + 2 * static_cast<size_t>(slots[fi]);
+      fr.verified = true;
+      fr.mismatches = all_vr[base];
+      fr.checksum = all_vr[base + 1];
+      res.total_mismatches += fr.mismatches;
+    }
+    res.flows.push_back(fr);
+  }
+  return res;
+}
+
+std::vector<PhaseResult> run_schedule(Transport& t, Bootstrap& boot, const Schedule& s, const RunConfig& cfg, Buffers& bufs,
+                                      const PhaseCallback& on_phase) {
+  std::string bad = validate(s);
+  P2P_CHECK(bad.empty(), "invalid schedule: " + bad);
+  std::vector<PhaseResult> out;
+  out.reserve(s.phases.size());
+  for (size_t i = 0; i < s.phases.size(); ++i) {
+    out.push_back(run_phase(t, boot, s.phases[i], i, cfg, bufs));
+    if (on_phase) on_phase(out.back());
+  }
+  return out;
+}
+
+void warm_connections(Transport& t, Bootstrap& boot, const Schedule& s, Buffers& bufs, size_t bytes) {
+  bytes = std::min(bytes, bufs.capacity());
+  for (const Phase& p : s.phases) {
+    if (p.idle || !p.participates(t.rank())) continue;
+    post_phase_iteration(t, p, bytes, bufs);
+    t.sync();
+  }
+  boot.barrier();
+}
+
+// -------------------------------------------------------------- latency ----
+
+std::vector<LatencyResult> run_latency(Transport& t, Bootstrap& boot, size_t bytes, int iters, int warmup, Buffers& bufs) {
+  const int n = boot.size(), me = boot.rank();
+  P2P_CHECK(bytes <= bufs.capacity() && bufs.slots() >= 1, "latency buffers too small");
+  P2P_CHECK(iters >= 1, "latency iters must be >= 1");
+  std::vector<LatencyResult> out;
+
+  auto run_round = [&](int partner) -> Summary {
+    const bool self = (partner == me);
+    const bool lead = self || (partner >= 0 && me < partner);
+    auto exchange = [&]() {
+      if (self) {
+        t.group_begin();
+        t.send(bufs.send_buf(), bytes, me);
+        t.recv(bufs.recv_buf(0), bytes, me);
+        t.group_end();
+      } else if (lead) {
+        t.group_begin(); t.send(bufs.send_buf(), bytes, partner); t.group_end();
+        t.group_begin(); t.recv(bufs.recv_buf(0), bytes, partner); t.group_end();
+      } else {
+        t.group_begin(); t.recv(bufs.recv_buf(0), bytes, partner); t.group_end();
+        t.group_begin(); t.send(bufs.send_buf(), bytes, partner); t.group_end();
+      }
+    };
+    if (partner >= 0) {
+      for (int i = 0; i < warmup; ++i) exchange();
+      t.sync();
+    }
+    boot.barrier();
+    std::vector<double> samples;
+    if (partner >= 0) {
+      t.clear_marks();
+      std::vector<int> marks;
+      marks.push_back(t.mark());
+      for (int i = 0; i < iters; ++i) {
+        exchange();
+        marks.push_back(t.mark());
+      }
+      t.sync();
+      if (lead)
+        for (size_t i = 1; i < marks.size(); ++i) {
+          double us = t.elapsed_ms(marks[i - 1], marks[i]) * 1e3;
+          samples.push_back(self ? us : us / 2.0);
+        }
+    }
+    boot.barrier();
+    return summarize(samples);
+  };
+
+  if (n == 1) {
+    Summary s = run_round(0);
+    LatencyResult r;
+    r.a = r.b = 0;
+    r.bytes = bytes;
+    r.one_way_us = s;
+    out.push_back(r);
+    return out;
+  }
+  for (const auto& round : round_robin_rounds(n)) {
+    int partner = -1;
+    for (auto& pr : round) {
+      if (pr.first == me) partner = pr.second;
+      if (pr.second == me) partner = pr.first;
+    }
+    Summary s = run_round(partner);
+    auto all = boot.allgather_value(s);
+    for (auto& pr : round) {
+      LatencyResult r;
+      r.a = pr.first;
+      r.b = pr.second;
+      r.bytes = bytes;
+      r.one_way_us = all[static_cast<size_t>(pr.first)];
+      out.push_back(r);
+    }
+  }
+  std::sort(out.begin(), out.end(), [](const LatencyResult& x, const LatencyResult& y) {
+    return x.a != y.a ? x.a < y.a : x.b < y.b;
+  });
+  return out;
+}
+
+// ---------------------------------------------------------- StepDriver ----
+
+StepDriver::StepDriver(Transport& t, Bootstrap& boot, Schedule sched, size_t bytes, int msgs, bool verify, uint64_t salt)
+    : t_(t), boot_(boot), sched_(std::move(sched)), bytes_(bytes), msgs_(msgs), verify_(verify), salt_(salt),
+      bufs_(t, bytes, std::max(1, sched_.max_recv_slots())) {
+  std::string bad = validate(sched_);
+  P2P_CHECK(bad.empty(), "invalid schedule: " + bad);
+  P2P_CHECK(!sched_.phases.empty(), "empty schedule");
+  P2P_CHECK(msgs_ >= 1, "msgs per step must be >= 1");
+  t_.fill(bufs_.send_buf(), bytes_, payload_seed(t_.rank(), bytes_, salt_));
+  if (verify_)
+    for (int i = 0; i < bufs_.slots(); ++i) t_.zero(bufs_.recv_buf(i), bytes_);
+  t_.sync();
+}
+
+StepDriver::~StepDriver() = default;
+
+void StepDriver::connect() {
+  warm_connections(t_, boot_, sched_, bufs_, std::min<size_t>(bytes_, 4096));
+  // Restore the payload the tiny warm-up may have overwritten on receivers.
+  if (verify_)
+    for (int i = 0; i < bufs_.slots(); ++i) t_.zero(bufs_.recv_buf(i), bytes_);
+  t_.sync();
+}
+
+void StepDriver::step(long k) {
+  const Phase& p = sched_.phases[static_cast<size_t>(k % phases())];
+  if (!p.participates(t_.rank())) {
+    marks_.emplace_back(-1, -1);
+  } else {
+    int a = t_.mark();
+    for (int m = 0; m < msgs_; ++m) post_phase_iteration(t_, p, bytes_, bufs_);
+    int b = t_.mark();
+    marks_.emplace_back(a, b);
+  }
+  last_step_ = k;
+}
+
+void StepDriver::sync() {
+  t_.sync();
+  std::string err = t_.async_error();
+  if (!err.empty()) P2P_FATAL("transport reported an asynchronous error: " + err);
+}
+
+std::vector<double> StepDriver::step_ms() {
+  std::vector<double> out;
+  out.reserve(marks_.size());
+  for (auto& m : marks_) out.push_back(m.first < 0 ? 0.0 : t_.elapsed_ms(m.first, m.second));
+  return out;
+}
+
+void StepDriver::reset() {
+  marks_.clear();
+  t_.clear_marks();
+}
+
+uint64_t StepDriver::verify_last() {
+  uint64_t bad = 0;
+  if (last_step_ >= 0 && verify_) {
+    const Phase& p = sched_.phases[static_cast<size_t>(last_step_ % phases())];
+    const RankOps& ops = p.ranks[static_cast<size_t>(t_.rank())];
+    for (size_t i = 0; i < ops.recv_from.size(); ++i)
+      bad += t_.verify(bufs_.recv_buf(static_cast<int>(i)), bytes_, payload_seed(ops.recv_from[i], bytes_, salt_)).mismatches;
+  }
+  return boot_.allreduce_sum_u64(bad);
+}
+
+double StepDriver::bytes_sent_per_step(long k) const {
+  const Phase& p = sched_.phases[static_cast<size_t>(k % static_cast<long>(sched_.phases.size()))];
+  return static_cast<double>(p.ranks[static_cast<size_t>(t_.rank())].send_to.size()) * static_cast<double>(bytes_) * msgs_;
+}
+
+double StepDriver::job_bytes_per_step(long k) const {
+  const Phase& p = sched_.phases[static_cast<size_t>(k % static_cast<long>(sched_.phases.size()))];
+  return static_cast<double>(p.flows.size()) * static_cast<double>(bytes_) * msgs_;
+}
+
+}  // namespace p2p

@@ -1,0 +1,155 @@
+// Measurement engine: executes schedules on a Transport and times them.
+//
+// Reference: the cell loops at /root/reference/p2p_matrix.cc:141-186 (uni) and
+// :196-267 (bi).  Two timing methodologies:
+//   * Timing::Wallclock — reference semantics: barrier, steady clock, one
+//     group + host stream-sync per message, barrier, clock; no warmup unless
+//     asked, so first-use connection setup lands inside the cell, exactly like
+//     the reference (which also used the non-monotonic system_clock; we use
+//     steady_clock).
+//   * Timing::Events (default) — barrier, `warmup` untimed iterations (which
+//     also establish the lazy RCCL p2p connections), barrier, then all `iters`
+//     groups are posted back to back on the stream with a hipEvent between
+//     iterations, one sync at the end; per-rank durations are all-gathered and
+//     each flow is charged the max of its two endpoints.  The per-iteration
+//     event deltas give the per-message time distribution (p50/p99).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "schedule.hpp"
+#include "stats.hpp"
+#include "transport.hpp"
+
+namespace p2p {
+
+class Bootstrap;
+
+enum class Timing { Events, Wallclock };
+const char* timing_name(Timing t);
+Timing parse_timing(const std::string& s);
+
+struct RunConfig {
+  size_t bytes = 32u << 20;  // reference: msg_size = 32 MiB (p2p_matrix.cc:124)
+  int iters = 128;           // reference: count = 128 (p2p_matrix.cc:132)
+  int warmup = 8;            // reference: none (p2p_matrix.cc:153-172)
+  Timing timing = Timing::Events;
+  bool verify = false;
+  bool samples = true;       // record an event per iteration for the distribution
+  uint64_t salt = 0;
+};
+
+struct FlowResult {
+  Flow flow;
+  double seconds = 0;     // per message
+  double gbps = 0;        // reference unit: bytes*8/s/1e9
+  double gbs = 0;         // GB/s (1e9 B/s)
+  Summary iter_us;        // per-iteration time seen by the receiver, microseconds
+  bool verified = false;
+  uint64_t mismatches = 0;
+  uint64_t checksum = 0;
+};
+
+struct PhaseResult {
+  size_t index = 0;
+  std::string label;
+  int row = -1, col = -1;
+  bool idle = false;
+  size_t bytes = 0;
+  int iters = 0;
+  double seconds_per_iter = 0;  // phase time per iteration (max over participants)
+  double wall_seconds = 0;      // host barrier-to-barrier time of the timed region
+  double bytes_per_iter = 0;    // all flows of the phase
+  double agg_gbs = 0;           // bytes_per_iter / seconds_per_iter
+  std::vector<double> rank_seconds;  // each rank's own timed duration (0 = not participating)
+  std::vector<FlowResult> flows;
+  uint64_t total_mismatches = 0;
+};
+
+// Send buffer + receive slots for one rank, sized for the largest message.
+class Buffers {
+ public:
+  Buffers(Transport& t, size_t max_bytes, int recv_slots);
+  ~Buffers();
+  Buffers(const Buffers&) = delete;
+  Buffers& operator=(const Buffers&) = delete;
+  void* send_buf() const { return send_; }
+  void* recv_buf(int slot) const { return recv_.at(static_cast<size_t>(slot)); }
+  size_t capacity() const { return cap_; }
+  int slots() const { return static_cast<int>(recv_.size()); }
+
+ private:
+  Transport& t_;
+  size_t cap_;
+  void* send_ = nullptr;
+  std::vector<void*> recv_;
+};
+
+// Posts one iteration (one group) of `phase` for this rank.
+void post_phase_iteration(Transport& t, const Phase& phase, size_t bytes, Buffers& bufs);
+
+// Runs one phase on every rank (collective over `boot`).
+PhaseResult run_phase(Transport& t, Bootstrap& boot, const Phase& phase, size_t phase_index, const RunConfig& cfg,
+                      Buffers& bufs);
+
+using PhaseCallback = std::function<void(const PhaseResult&)>;
+
+// Runs every phase of a schedule (collective).  `on_phase` fires on every rank
+// after each phase, so reports can stream like the reference's fflush'd rows.
+std::vector<PhaseResult> run_schedule(Transport& t, Bootstrap& boot, const Schedule& s, const RunConfig& cfg,
+                                      Buffers& bufs, const PhaseCallback& on_phase = nullptr);
+
+// Establish every lazy connection a schedule will use (one tiny untimed
+// iteration per phase), so no timed cell pays connection setup.
+void warm_connections(Transport& t, Bootstrap& boot, const Schedule& s, Buffers& bufs, size_t bytes = 4096);
+
+// ---- latency: ping-pong between disjoint pairs, concurrently per round ----
+struct LatencyResult {
+  int a = -1, b = -1;   // a < b; a == b for the self path
+  size_t bytes = 0;
+  Summary one_way_us;   // half round trip, microseconds
+};
+
+// Ping-pong over round-robin rounds (every unordered pair once; each round's
+// pairs run concurrently on disjoint xGMI links).  n == 1 measures the self
+// path (one grouped self send/recv per sample).
+std::vector<LatencyResult> run_latency(Transport& t, Bootstrap& boot, size_t bytes, int iters, int warmup,
+                                       Buffers& bufs);
+
+// ---- step driver (used by bench.py): one phase per step, no host syncs ----
+// Step k posts `msgs` iterations of phase (k mod phases) with a timestamp
+// around them; nothing blocks until sync().  Per-step durations are read
+// after sync().
+class StepDriver {
+ public:
+  StepDriver(Transport& t, Bootstrap& boot, Schedule sched, size_t bytes, int msgs, bool verify, uint64_t salt = 0);
+  ~StepDriver();
+  void connect();               // warm every phase once (collective, blocking)
+  void step(long k);            // enqueue step k
+  void sync();                  // wait for everything posted
+  std::vector<double> step_ms();       // this rank's per-step durations since the last reset
+  void reset();                 // forget recorded steps
+  uint64_t verify_last();       // mismatches in the receive slots of the last step's phase (collective)
+  double bytes_sent_per_step(long k) const;  // by THIS rank
+  double job_bytes_per_step(long k) const;   // by all ranks
+  const Schedule& schedule() const { return sched_; }
+  int phases() const { return static_cast<int>(sched_.phases.size()); }
+
+ private:
+  Transport& t_;
+  Bootstrap& boot_;
+  Schedule sched_;
+  size_t bytes_;
+  int msgs_;
+  bool verify_;
+  uint64_t salt_;
+  Buffers bufs_;
+  std::vector<std::pair<int, int>> marks_;
+  long last_step_ = -1;
+};
+
+}  // namespace p2p

@@ -1,0 +1,83 @@
+// Data plane abstraction: buffers, grouped point-to-point ops, timestamps.
+//
+// The measurement engine (runner.cpp) is written against this interface only.
+// Two implementations:
+//   * RcclTransport (transport_rccl.cpp, HIP + RCCL): MI355X device buffers in
+//     HBM3E, ncclSend/ncclRecv over xGMI inside ncclGroupStart/End (reference
+//     call sites p2p_matrix.cc:156-169, 211-249), hipEvent timestamps on the
+//     comm stream, hand-written gfx950 fill/verify kernels.
+//   * HostTransport (transport_host.cpp): host memory over a TCP mesh, steady
+//     clock timestamps.  Same schedule, same runner, same report — it is the
+//     CPU plumbing path (BASELINE.json config 1) and what the CPU test tier
+//     drives, so the whole engine is exercised without a GPU.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <string>
+
+#include "prng.hpp"
+
+namespace p2p {
+
+class Bootstrap;
+
+class Transport {
+ public:
+  virtual ~Transport() = default;
+  virtual std::string name() const = 0;
+  virtual int rank() const = 0;
+  virtual int nranks() const = 0;
+  virtual std::string device_desc() const { return ""; }
+
+  // ---- memory ----
+  virtual void* alloc(size_t bytes) = 0;
+  virtual void release(void* p) = 0;
+  // Stream-ordered fill of `bytes` with the PRNG stream `seed`.
+  virtual void fill(void* p, size_t bytes, uint64_t seed) = 0;
+  // Stream-ordered zeroing (used to poison receive buffers before a cell).
+  virtual void zero(void* p, size_t bytes) = 0;
+  // Blocking: compares `bytes` at p against the PRNG stream `seed`.
+  virtual VerifyResult verify(const void* p, size_t bytes, uint64_t seed) = 0;
+
+  // ---- data plane: one group == one fused launch ----
+  virtual void group_begin() = 0;
+  virtual void send(const void* p, size_t bytes, int peer) = 0;
+  virtual void recv(void* p, size_t bytes, int peer) = 0;
+  virtual void group_end() = 0;
+
+  // ---- timing ----
+  // Enqueue a timestamp behind all work posted so far; returns its id.
+  virtual int mark() = 0;
+  // Milliseconds between two marks; only valid after sync().
+  virtual double elapsed_ms(int from, int to) = 0;
+  virtual void clear_marks() = 0;
+  // Wait for all posted work (bounded by the transport's watchdog timeout).
+  virtual void sync() = 0;
+
+  // ---- health ----
+  // Non-empty when the transport saw an asynchronous error (e.g. a peer died).
+  virtual std::string async_error() { return ""; }
+};
+
+struct TransportOptions {
+  int device = -1;                 // -1: local rank from placement
+  double timeout_s = 300.0;        // watchdog for init / sync
+  bool nonblocking_init = true;    // RCCL: ncclCommInitRankConfig(blocking=0) + polling
+  int verify_impl = 0;             // 0 = auto, 1 = register-staged, 2 = LDS-staged (global_load_lds)
+};
+
+// HIP + RCCL on the local MI355X.  Defined in transport_rccl.cpp (hipcc).
+std::unique_ptr<Transport> make_rccl_transport(Bootstrap& boot, const TransportOptions& opt);
+bool rccl_transport_available();
+
+// Host memory over TCP sockets.  Defined in transport_host.cpp.
+std::unique_ptr<Transport> make_host_transport(Bootstrap& boot, const TransportOptions& opt);
+
+// CPU reference of the verify kernel, bit-compatible with it (tests and the
+// host transport use it).
+VerifyResult host_verify(const void* p, size_t bytes, uint64_t seed);
+void host_fill(void* p, size_t bytes, uint64_t seed);
+
+}  // namespace p2p

@@ -1,0 +1,252 @@
+// RcclTransport: MI355X device buffers + RCCL point-to-point over xGMI.
+//
+// Reference call sites replaced here (/root/reference/p2p_matrix.cc):
+//   ncclGetUniqueId + MPI_Bcast + cudaSetDevice + ncclCommInitRank  :111-120
+//   cudaStreamCreateWithFlags(cudaStreamNonBlocking) x2               :121-122
+//   cudaMalloc + cudaMemset                                           :124-130
+//   ncclGroupStart / ncclSend / ncclRecv / ncclGroupEnd               :156-169, 211-249
+//   cudaStreamSynchronize                                             :162, :170, :229-251
+//   ncclCommDestroy                                                   :270
+// Differences by design:
+//   * ncclGetUniqueId and every RCCL call are checked (the reference leaves
+//     :116 and :270 unchecked); the unique id travels over the Bootstrap.
+//   * The communicator is created non-blocking (ncclCommInitRankConfig with
+//     blocking = 0) and polled with a deadline, and every sync is a bounded
+//     poll of hipStreamQuery + ncclCommGetAsyncError: a dead peer becomes
+//     ncclCommAbort + a fatal error on every rank instead of a silent hang.
+//   * One non-blocking stream: the reference's second stream for the bi
+//     direction is joined by the group anyway.
+//   * hipEvents on the stream give GPU-timeline timestamps.
+//   * Payloads are written / checked by the gfx950 kernels in kernels.hip.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "bootstrap.hpp"
+#include "common.hpp"
+#include "kernels.hpp"
+#include "transport.hpp"
+
+namespace p2p {
+namespace {
+
+#define HIPCHECK(cmd)                                                                          \
+  do {                                                                                         \
+    hipError_t e_ = (cmd);                                                                     \
+    if (e_ != hipSuccess) P2P_FATAL(strfmt("HIP error in %s: %s", #cmd, hipGetErrorString(e_))); \
+  } while (0)
+
+class RcclTransport final : public Transport {
+ public:
+  RcclTransport(Bootstrap& boot, const TransportOptions& opt)
+      : rank_(boot.rank()), n_(boot.size()), timeout_(opt.timeout_s) {
+    verify_impl_ = static_cast<dev::VerifyImpl>(opt.verify_impl);
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0)
+      P2P_FATAL(strfmt("rank %d: no HIP device visible (%s)", rank_, e == hipSuccess ? "0 devices" : hipGetErrorString(e)));
+    device_ = opt.device >= 0 ? opt.device : 0;
+    // The reference never checks this and lets cudaSetDevice fail.
+    if (device_ >= ndev)
+      P2P_FATAL(strfmt("rank %d wants GPU %d but only %d are visible: more ranks per host than GPUs", rank_, device_, ndev));
+    HIPCHECK(hipSetDevice(device_));
+    HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    HIPCHECK(hipMalloc(&acc_, sizeof(dev::VerifyAccum)));
+    HIPCHECK(hipHostMalloc(&acc_host_, sizeof(dev::VerifyAccum), hipHostMallocDefault));
+
+    ncclUniqueId id;
+    std::memset(&id, 0, sizeof(id));
+    if (rank_ == 0) nccl_ok(ncclGetUniqueId(&id), "ncclGetUniqueId");
+    boot.bcast(&id, sizeof(id), 0);
+
+    const char* blk = std::getenv("P2P_RCCL_BLOCKING");
+    nonblocking_ = opt.nonblocking_init && !(blk && std::atoi(blk));
+    if (nonblocking_) {
+      ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+      cfg.blocking = 0;
+      ncclResult_t r = ncclCommInitRankConfig(&comm_, n_, id, rank_, &cfg);
+      wait_ready(r, "ncclCommInitRankConfig");
+    } else {
+      nccl_ok(ncclCommInitRank(&comm_, n_, id, rank_), "ncclCommInitRank");
+    }
+    hook_ = push_abort_hook([this](int) {
+      if (comm_) ncclCommAbort(comm_);
+      comm_ = nullptr;
+    });
+    hipDeviceProp_t prop;
+    HIPCHECK(hipGetDeviceProperties(&prop, device_));
+    char pci[64] = {0};
+    if (hipDeviceGetPCIBusId(pci, sizeof(pci), device_) != hipSuccess) pci[0] = 0;
+    int ver = 0;
+    ncclGetVersion(&ver);
+    desc_ = strfmt("hip:%d %s (%s, %d CUs, %.0f GiB, pci %s) rccl %d", device_, prop.name, prop.gcnArchName,
+                   prop.multiProcessorCount, static_cast<double>(prop.totalGlobalMem) / (1ull << 30), pci, ver);
+  }
+
+  ~RcclTransport() override {
+    remove_abort_hook(hook_);
+    if (comm_) {
+      // Drain, then destroy (checked, unlike p2p_matrix.cc:270).
+      (void)hipStreamSynchronize(stream_);
+      ncclCommDestroy(comm_);
+      comm_ = nullptr;
+    }
+    for (auto ev : events_) (void)hipEventDestroy(ev);
+    if (acc_) (void)hipFree(acc_);
+    if (acc_host_) (void)hipHostFree(acc_host_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+  }
+
+  std::string name() const override { return "rccl"; }
+  int rank() const override { return rank_; }
+  int nranks() const override { return n_; }
+  std::string device_desc() const override { return desc_; }
+
+  void* alloc(size_t bytes) override {
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, std::max<size_t>(bytes, 256));
+    if (e != hipSuccess) P2P_FATAL(strfmt("hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e)));
+    return p;
+  }
+  void release(void* p) override {
+    if (p) HIPCHECK(hipFree(p));
+  }
+  void fill(void* p, size_t bytes, uint64_t seed) override { dev::launch_fill(p, bytes, seed, stream_); }
+  void zero(void* p, size_t bytes) override { HIPCHECK(hipMemsetAsync(p, 0, bytes, stream_)); }
+
+  VerifyResult verify(const void* p, size_t bytes, uint64_t seed) override {
+    dev::launch_verify_reset(acc_, stream_);
+    dev::launch_verify(p, bytes, seed, acc_, verify_impl_, true, stream_);
+    HIPCHECK(hipMemcpyAsync(acc_host_, acc_, sizeof(dev::VerifyAccum), hipMemcpyDeviceToHost, stream_));
+    sync();
+    VerifyResult r;
+    r.mismatches = acc_host_->mismatches;
+    r.checksum = acc_host_->checksum;
+    r.first_bad = acc_host_->first_bad;
+    return r;
+  }
+
+  void group_begin() override { nccl_ok(ncclGroupStart(), "ncclGroupStart"); }
+  void send(const void* p, size_t bytes, int peer) override {
+    nccl_ok(ncclSend(p, bytes, ncclUint8, peer, comm_, stream_), "ncclSend");
+  }
+  void recv(void* p, size_t bytes, int peer) override {
+    nccl_ok(ncclRecv(p, bytes, ncclUint8, peer, comm_, stream_), "ncclRecv");
+  }
+  void group_end() override {
+    ncclResult_t r = ncclGroupEnd();
+    // Non-blocking comm: the ops are only enqueued once the comm leaves
+    // ncclInProgress, so wait before any event is recorded behind them.
+    wait_ready(r, "ncclGroupEnd");
+  }
+
+  int mark() override {
+    if (next_event_ == static_cast<int>(events_.size())) {
+      hipEvent_t ev;
+      HIPCHECK(hipEventCreate(&ev));
+      events_.push_back(ev);
+    }
+    HIPCHECK(hipEventRecord(events_[static_cast<size_t>(next_event_)], stream_));
+    return next_event_++;
+  }
+  double elapsed_ms(int a, int b) override {
+    float ms = 0;
+    HIPCHECK(hipEventElapsedTime(&ms, events_.at(static_cast<size_t>(a)), events_.at(static_cast<size_t>(b))));
+    return ms;
+  }
+  void clear_marks() override { next_event_ = 0; }
+
+  void sync() override {
+    // Bounded poll instead of hipStreamSynchronize: spins for the first 2 ms
+    // (so per-message syncs in wallclock mode are not inflated by sleeps),
+    // then backs off; checks RCCL's async error so a failed peer aborts.
+    double t0 = now_seconds();
+    double deadline = t0 + timeout_;
+    for (long it = 0;; ++it) {
+      hipError_t e = hipStreamQuery(stream_);
+      if (e == hipSuccess) return;
+      if (e != hipErrorNotReady) P2P_FATAL(strfmt("stream error: %s", hipGetErrorString(e)));
+      if ((it & 255) == 0) {
+        std::string err = async_error();
+        if (!err.empty()) P2P_FATAL("RCCL asynchronous error while waiting: " + err);
+        double now = now_seconds();
+        if (now > deadline)
+          P2P_FATAL(strfmt("rank %d: stream did not finish within %.0f s (peer hung or dead?); aborting", rank_, timeout_));
+        if (now - t0 > 2e-3) std::this_thread::sleep_for(std::chrono::microseconds(50));
+      }
+    }
+  }
+
+  std::string async_error() override {
+    if (!comm_) return "communicator aborted";
+    ncclResult_t st = ncclSuccess;
+    ncclResult_t r = ncclCommGetAsyncError(comm_, &st);
+    if (r != ncclSuccess) return ncclGetErrorString(r);
+    if (st != ncclSuccess && st != ncclInProgress) return ncclGetErrorString(st);
+    return "";
+  }
+
+ private:
+  void nccl_ok(ncclResult_t r, const char* what) {
+    if (r == ncclSuccess) return;
+    if (r == ncclInProgress && nonblocking_ && comm_) {
+      wait_ready(r, what);
+      return;
+    }
+    P2P_FATAL(strfmt("rank %d: %s failed: %s (%s)", rank_, what, ncclGetErrorString(r),
+                     comm_ ? ncclGetLastError(comm_) : ""));
+  }
+
+  void wait_ready(ncclResult_t r, const char* what) {
+    double deadline = now_seconds() + timeout_;
+    while (r == ncclInProgress) {
+      if (now_seconds() > deadline) {
+        if (comm_) ncclCommAbort(comm_);
+        comm_ = nullptr;
+        P2P_FATAL(strfmt("rank %d: %s did not complete within %.0f s (peer missing?)", rank_, what, timeout_));
+      }
+      std::this_thread::yield();
+      ncclResult_t st = ncclSuccess;
+      ncclResult_t q = ncclCommGetAsyncError(comm_, &st);
+      if (q != ncclSuccess) {
+        r = q;
+        break;
+      }
+      r = st;
+    }
+    if (r != ncclSuccess)
+      P2P_FATAL(strfmt("rank %d: %s failed: %s", rank_, what, ncclGetErrorString(r)));
+  }
+
+  int rank_, n_;
+  double timeout_;
+  int device_ = 0;
+  bool nonblocking_ = true;
+  hipStream_t stream_ = nullptr;
+  ncclComm_t comm_ = nullptr;
+  std::vector<hipEvent_t> events_;
+  int next_event_ = 0;
+  dev::VerifyAccum* acc_ = nullptr;
+  dev::VerifyAccum* acc_host_ = nullptr;
+  dev::VerifyImpl verify_impl_ = dev::VerifyImpl::Auto;
+  std::string desc_;
+  int hook_ = 0;
+};
+
+}  // namespace
+
+std::unique_ptr<Transport> make_rccl_transport(Bootstrap& boot, const TransportOptions& opt) {
+  return std::make_unique<RcclTransport>(boot, opt);
+}
+
+bool rccl_transport_available() {
+  int n = 0;
+  return hipGetDeviceCount(&n) == hipSuccess && n > 0;
+}
+
+}  // namespace p2p

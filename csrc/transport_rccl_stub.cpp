@@ -1,0 +1,14 @@
+// Host-only builds (CPU test binaries) link this instead of
+// transport_rccl.cpp + kernels.hip: the RCCL transport is unavailable.
+#include "common.hpp"
+#include "transport.hpp"
+
+namespace p2p {
+
+std::unique_ptr<Transport> make_rccl_transport(Bootstrap&, const TransportOptions&) {
+  P2P_FATAL("this binary was built without HIP/RCCL; use --transport host");
+}
+
+bool rccl_transport_available() { return false; }
+
+}  // namespace p2p

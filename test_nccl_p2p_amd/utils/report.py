@@ -1,0 +1,96 @@
+"""Reference-compatible matrix text, its parser, and scaling tables.
+
+``compat_matrix_text`` reproduces /root/reference/p2p_matrix.cc's printf
+sequence byte for byte (title :134/:189, corner "   D\\D" :135/:190, column
+ids "%6d " :137/:192, row ids "%6d " :143/:198, cells "%6.02f " with 0.00 on
+the diagonal :149/:179/:204/:260, newline per row :184/:265).
+``parse_compat`` reads such output back (also the native binary's), which is
+how the test-suite and scaling scripts consume ``mpirun ... > result.txt``
+files (the reference's .gitignore lists result.txt).
+"""
+
+from __future__ import annotations
+
+import json
+import re
+from typing import Dict, Iterable, List, Optional
+
+UNI_TITLE = "Evaluating the Uni-Directional NCCL P2P Bandwidth (Gbps)"
+BI_TITLE = "Evaluating the Bi-Directional NCCL P2P Bandwidth (Gbps)"
+
+
+def compat_matrix_text(m: List[List[float]], direction: str, leading_newline: Optional[bool] = None) -> str:
+    n = len(m)
+    lead = (direction == "bi") if leading_newline is None else leading_newline
+    title = UNI_TITLE if direction == "uni" else BI_TITLE
+    out = ["\n" if lead else "", title, "\n", "   D\\D"]
+    out += ["%6d " % i for i in range(n)]
+    out.append("\n")
+    for r in range(n):
+        out.append("%6d " % r)
+        for c in range(n):
+            out.append("%6.02f " % (0.0 if r == c else m[r][c]))
+        out.append("\n")
+    return "".join(out)
+
+
+_CELL = re.compile(r"-?\d+\.\d\d")
+
+
+def parse_compat(text: str) -> Dict[str, List[List[float]]]:
+    """Returns {"uni": matrix, "bi": matrix} (Gbps) found in reference-format text.
+
+    Cells are split by the fixed "%6.02f " layout when it holds and by
+    whitespace otherwise (values >= 1000 overflow the 6-char field, exactly as
+    the reference's printf does)."""
+    res: Dict[str, List[List[float]]] = {}
+    lines = text.splitlines()
+    i = 0
+    while i < len(lines):
+        line = lines[i]
+        key = "uni" if line.strip() == UNI_TITLE else "bi" if line.strip() == BI_TITLE else None
+        if key is None:
+            i += 1
+            continue
+        header = lines[i + 1]
+        n = len(header.replace("   D\\D", "").split())
+        rows = []
+        for r in range(n):
+            toks = lines[i + 2 + r].split()
+            assert int(toks[0]) == r, "row label mismatch"
+            rows.append([float(t) for t in toks[1:1 + n]])
+        res[key] = rows
+        i += 2 + n
+    return res
+
+
+def gbps_to_gbs(m: List[List[float]]) -> List[List[float]]:
+    return [[v / 8.0 for v in row] for row in m]
+
+
+def read_json_lines(path: str) -> List[dict]:
+    out = []
+    with open(path) as f:
+        for line in f:
+            line = line.strip()
+            if line.startswith("{"):
+                out.append(json.loads(line))
+    return out
+
+
+def scaling_table(results: Iterable[dict]) -> str:
+    """Markdown table of bench.py lines (one per GPU count): aggregate GB/s,
+    per-GPU GB/s, matrix min/mean, p50 latency, and efficiency vs N=2 (the
+    first point where xGMI links are involved; N=1 is the self path)."""
+    rows = sorted(results, key=lambda r: r["n_gpus"])
+    base = next((r for r in rows if r["n_gpus"] == 2), None)
+    out = ["| GPUs | aggregate GB/s | per-GPU GB/s | matrix min / mean GB/s | p50 latency us | eff. vs 2 GPUs |",
+           "|---|---|---|---|---|---|"]
+    for r in rows:
+        eff = ""
+        if base and r["n_gpus"] >= 2:
+            eff = "%.1f%%" % (100.0 * r["value"] / r["n_gpus"] / (base["value"] / 2))
+        out.append("| %d | %.1f | %.1f | %s / %s | %s | %s |" % (
+            r["n_gpus"], r["value"], r["value"] / r["n_gpus"], r.get("matrix_gbs_min"), r.get("matrix_gbs_mean"),
+            r.get("p50_latency_us"), eff))
+    return "\n".join(out)

@@ -1,0 +1,53 @@
+import os
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+MPIRUN = os.environ.get("P2P_MPIRUN", "/opt/conda/bin/mpirun")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an AMD MI355X (gfx950) GPU")
+    config.addinivalue_line("markers", "mpi: needs the MPICH mpirun launcher")
+
+
+def ensure_built(target: str) -> None:
+    """Builds a Makefile target in-tree if its artefact is missing."""
+    subprocess.run(["make", "-C", ROOT, "-j8", target], check=True, capture_output=True)
+
+
+@pytest.fixture(scope="session")
+def host_build():
+    ensure_built("host")
+    return os.path.join(ROOT, "build")
+
+
+@pytest.fixture(scope="session")
+def native():
+    ensure_built("ext")
+    import test_nccl_p2p_amd
+
+    return test_nccl_p2p_amd.require_native()
+
+
+@pytest.fixture(scope="session")
+def mpirun():
+    if not (os.path.exists(MPIRUN) or shutil.which("mpirun")):
+        pytest.skip("mpirun not available")
+    return MPIRUN if os.path.exists(MPIRUN) else shutil.which("mpirun")
+
+
+def free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p

@@ -1,0 +1,457 @@
+// Host-only unit tests (tier T0 in SURVEY.md §4): no GPU, no MPI launcher.
+// Built with g++ by `make host`; run directly or through tests/test_host_unit.py.
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <set>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "app.hpp"
+#include "bootstrap.hpp"
+#include "common.hpp"
+#include "prng.hpp"
+#include "report.hpp"
+#include "runner.hpp"
+#include "schedule.hpp"
+#include "stats.hpp"
+#include "transport.hpp"
+#include "units.hpp"
+
+using namespace p2p;
+
+static std::atomic<int> g_failures{0};
+static std::atomic<int> g_checks{0};
+
+#define EXPECT(cond)                                                       \
+  do {                                                                     \
+    ++g_checks;                                                            \
+    if (!(cond)) {                                                         \
+      ++g_failures;                                                        \
+      std::fprintf(stderr, "  FAIL %s:%d: %s\n", __FILE__, __LINE__, #cond); \
+    }                                                                      \
+  } while (0)
+
+#define EXPECT_NEAR(a, b, tol) EXPECT(std::fabs((a) - (b)) <= (tol))
+
+struct TestCase {
+  const char* name;
+  std::function<void()> fn;
+};
+static std::vector<TestCase>& registry() {
+  static std::vector<TestCase> r;
+  return r;
+}
+#define TEST(name)                                              \
+  static void name();                                           \
+  static bool name##_reg = (registry().push_back({#name, name}), true); \
+  static void name()
+
+// --------------------------------------------------------------- units ----
+
+TEST(test_parse_size) {
+  EXPECT(parse_size("4096") == 4096);
+  EXPECT(parse_size("4K") == 4096);
+  EXPECT(parse_size("4KiB") == 4096);
+  EXPECT(parse_size("32M") == 32u << 20);
+  EXPECT(parse_size("32mb") == 32u << 20);
+  EXPECT(parse_size("1G") == 1ull << 30);
+  EXPECT(parse_size("4G") == 4ull << 30);  // > INT_MAX: the reference's int msg_size could not
+  EXPECT(parse_size("1.5K") == 1536);
+  EXPECT(format_size(32u << 20) == "32M");
+  EXPECT(format_size(4096) == "4K");
+  EXPECT(format_size(1000) == "1000");
+  EXPECT(format_size(4ull << 30) == "4G");
+}
+
+TEST(test_parse_size_list) {
+  auto v = parse_size_list("4K:64K");
+  EXPECT(v.size() == 5);
+  EXPECT(v.front() == 4096 && v.back() == 65536);
+  auto w = parse_size_list("4K:1M:4");
+  EXPECT(w.size() == 5);  // 4K 16K 64K 256K 1M
+  EXPECT(w.back() == 1u << 20);
+  auto x = parse_size_list("4K,1M,3M");
+  EXPECT(x.size() == 3 && x[2] == 3u << 20);
+  auto big = parse_size_list("4K:4G");
+  EXPECT(big.size() == 21);
+}
+
+TEST(test_gbps_units) {
+  // Reference: throughput = msg_size * 8. / time / 1e9 (p2p_matrix.cc:177)
+  EXPECT_NEAR(gbps(33554432.0, 1e-3), 268.435456, 1e-9);
+  EXPECT_NEAR(gbytes_per_s(33554432.0, 1e-3), 33.554432, 1e-12);
+}
+
+// --------------------------------------------------------------- stats ----
+
+TEST(test_stats) {
+  std::vector<double> s{5, 1, 4, 2, 3};
+  EXPECT_NEAR(percentile(s, 50), 3.0, 1e-12);
+  EXPECT_NEAR(percentile(s, 0), 1.0, 1e-12);
+  EXPECT_NEAR(percentile(s, 100), 5.0, 1e-12);
+  EXPECT_NEAR(percentile({1, 2, 3, 4}, 50), 2.5, 1e-12);
+  EXPECT_NEAR(percentile({1, 2, 3, 4}, 90), 3.7, 1e-12);
+  Summary m = summarize(s);
+  EXPECT(m.n == 5);
+  EXPECT_NEAR(m.mean, 3.0, 1e-12);
+  EXPECT_NEAR(m.stdev, std::sqrt(2.5), 1e-12);
+  EXPECT(summarize({}).n == 0);
+  std::vector<double> mat{0, 10, 20, 30, 0, 40, 50, 60, 0};
+  MatrixSummary ms = summarize_offdiag(mat, 3);
+  EXPECT(ms.cells == 6);
+  EXPECT_NEAR(ms.min, 10, 1e-12);
+  EXPECT_NEAR(ms.mean, 35, 1e-12);
+  EXPECT_NEAR(ms.max, 60, 1e-12);
+}
+
+// ------------------------------------------------------------ schedules ----
+
+static std::multiset<std::pair<int, int>> all_flows(const Schedule& s) {
+  std::multiset<std::pair<int, int>> m;
+  for (const auto& p : s.phases)
+    for (const auto& f : p.flows) m.insert({f.src, f.dst});
+  return m;
+}
+
+TEST(test_schedules_valid) {
+  for (int n = 1; n <= 9; ++n) {
+    for (Mode m : {Mode::Pair, Mode::Ring, Mode::AllPairs, Mode::Tournament, Mode::Self})
+      for (Direction d : {Direction::Uni, Direction::Bi}) {
+        Schedule s = make_schedule(m, d, n);
+        EXPECT(validate(s).empty());
+        EXPECT(s.nranks == n);
+      }
+  }
+}
+
+TEST(test_pair_schedule_reference_order) {
+  // p2p_matrix.cc:141-145: for src { for dst { barrier; ... } }, diagonal idle.
+  Schedule s = make_pair_schedule(3, Direction::Uni);
+  EXPECT(s.phases.size() == 9);
+  int k = 0;
+  for (int src = 0; src < 3; ++src)
+    for (int dst = 0; dst < 3; ++dst, ++k) {
+      const Phase& p = s.phases[k];
+      EXPECT(p.row == src && p.col == dst);
+      EXPECT(p.idle == (src == dst));
+      if (src != dst) {
+        EXPECT(p.flows.size() == 1);
+        EXPECT(p.ranks[src].send_to == std::vector<int>{dst});
+        EXPECT(p.ranks[dst].recv_from == std::vector<int>{src});
+        for (int r = 0; r < 3; ++r)
+          if (r != src && r != dst) EXPECT(!p.participates(r));
+      }
+    }
+  Schedule b = make_pair_schedule(2, Direction::Bi);
+  EXPECT(b.phases[1].flows.size() == 2);  // both endpoints send and receive (:211-249)
+  EXPECT(b.phases[1].ranks[0].send_to == std::vector<int>{1});
+  EXPECT(b.phases[1].ranks[0].recv_from == std::vector<int>{1});
+}
+
+TEST(test_round_robin_rounds) {
+  for (int n = 2; n <= 12; ++n) {
+    auto rounds = round_robin_rounds(n);
+    EXPECT(static_cast<int>(rounds.size()) == (n % 2 == 0 ? n - 1 : n));
+    std::set<std::pair<int, int>> seen;
+    for (auto& r : rounds) {
+      std::set<int> busy;
+      for (auto& pr : r) {
+        EXPECT(pr.first < pr.second);
+        EXPECT(busy.insert(pr.first).second);  // disjoint within a round
+        EXPECT(busy.insert(pr.second).second);
+        EXPECT(seen.insert(pr).second);        // each pair once overall
+      }
+      EXPECT(static_cast<int>(r.size()) == n / 2);
+    }
+    EXPECT(static_cast<int>(seen.size()) == n * (n - 1) / 2);
+  }
+}
+
+TEST(test_tournament_covers_matrix) {
+  for (int n = 2; n <= 9; ++n) {
+    std::multiset<std::pair<int, int>> want;
+    for (int a = 0; a < n; ++a)
+      for (int b = 0; b < n; ++b)
+        if (a != b) want.insert({a, b});
+    EXPECT(all_flows(make_tournament_schedule(n, Direction::Uni)) == want);
+    EXPECT(all_flows(make_tournament_schedule(n, Direction::Bi)) == want);
+    // Uni: no rank is both sender and receiver in one phase -> one link per pair.
+    for (const auto& p : make_tournament_schedule(n, Direction::Uni).phases)
+      for (const auto& ro : p.ranks) EXPECT(ro.send_to.size() + ro.recv_from.size() <= 1);
+  }
+}
+
+TEST(test_ring_and_allpairs) {
+  Schedule r = make_ring_schedule(4, Direction::Uni);
+  EXPECT(r.phases.size() == 1);
+  std::multiset<std::pair<int, int>> ring{{0, 1}, {1, 2}, {2, 3}, {3, 0}};
+  EXPECT(all_flows(r) == ring);
+  Schedule rb = make_ring_schedule(4, Direction::Bi);
+  EXPECT(rb.phases[0].flows.size() == 8);
+  Schedule r2 = make_ring_schedule(2, Direction::Bi);
+  EXPECT(r2.phases[0].flows.size() == 2);  // next == prev: no duplicate hop
+  Schedule a = make_allpairs_schedule(8, Direction::Bi);
+  EXPECT(a.phases.size() == 1);
+  EXPECT(a.phases[0].flows.size() == 56);
+  EXPECT(a.max_recv_slots() == 7);
+  Schedule s1 = make_ring_schedule(1, Direction::Uni);
+  EXPECT(all_flows(s1) == (std::multiset<std::pair<int, int>>{{0, 0}}));
+  EXPECT(parse_mode("a2a") == Mode::AllPairs);
+}
+
+// ----------------------------------------------------------- placement ----
+
+TEST(test_host_hash_matches_reference) {
+  // getHostHash (p2p_matrix.cc:44-51) computed by hand for "ab":
+  // h0 = 5381; h1 = (5381*33) ^ 'a'; h2 = (h1*33) ^ 'b'
+  uint64_t h = 5381;
+  h = (h * 33) ^ 'a';
+  h = (h * 33) ^ 'b';
+  EXPECT(host_hash("ab") == h);
+  EXPECT(host_hash("") == 5381);
+  EXPECT(host_hash("node-1") != host_hash("node-2"));
+}
+
+TEST(test_placement) {
+  std::vector<uint64_t> one(4, 7);
+  Placement p = compute_placement(one, 3);
+  EXPECT(p.ok && p.num_hosts == 1 && p.ranks_per_host == 4 && p.local_rank == 3);
+  std::vector<uint64_t> blocks{1, 1, 2, 2};
+  p = compute_placement(blocks, 3);
+  EXPECT(p.ok && p.num_hosts == 2 && p.local_rank == 1 && p.host_index == 1);
+  std::vector<uint64_t> rr{1, 2, 1, 2};  // round-robin placement is rejected
+  p = compute_placement(rr, 0);
+  EXPECT(!p.ok);
+  EXPECT(p.error.find("block") != std::string::npos);
+  std::vector<uint64_t> uneven{1, 1, 2};
+  EXPECT(!compute_placement(uneven, 0).ok);
+}
+
+// ----------------------------------------------------------------- prng ----
+
+TEST(test_prng_fill_verify) {
+  for (size_t bytes : {size_t(1), size_t(3), size_t(4), size_t(15), size_t(16), size_t(17), size_t(4096), size_t(4099), size_t(1 << 20)}) {
+    std::vector<uint8_t> buf(bytes + 8, 0xEE);
+    host_fill(buf.data(), bytes, 42);
+    EXPECT(buf[bytes] == 0xEE);  // no overrun
+    VerifyResult r = host_verify(buf.data(), bytes, 42);
+    EXPECT(r.mismatches == 0);
+    EXPECT(r.first_bad == ~0ull);
+    VerifyResult w = host_verify(buf.data(), bytes, 43);
+    EXPECT(bytes < 4 ? w.mismatches <= 1 : w.mismatches > 0);
+    if (bytes >= 16) {
+      buf[bytes / 2] ^= 0x10;
+      VerifyResult c = host_verify(buf.data(), bytes, 42);
+      EXPECT(c.mismatches == 1);
+      EXPECT(c.first_bad == (bytes / 2) / 4 * 4);
+    }
+  }
+  // Words are a function of (seed, index) only.
+  EXPECT(prng_word(1, 0) != prng_word(2, 0));
+  EXPECT(prng_word(1, 5) == prng_word(1, 5));
+  EXPECT(prng_word(1, 1ull << 32) != prng_word(1, 0));
+  EXPECT(payload_seed(0, 4096, 0) != payload_seed(1, 4096, 0));
+  EXPECT(payload_seed(0, 4096, 0) != payload_seed(0, 8192, 0));
+  // Known-answer vector pinned for cross-language checks (tests/test_prng.py).
+  std::printf("    prng_word(0x1234, 0..3) = %08x %08x %08x %08x\n", prng_word(0x1234, 0), prng_word(0x1234, 1),
+              prng_word(0x1234, 2), prng_word(0x1234, 3));
+}
+
+TEST(test_checksum_convention) {
+  uint8_t b[6] = {1, 0, 0, 0, 2, 3};
+  VerifyResult r = host_verify(b, 6, 0);
+  EXPECT(r.checksum == 1u + (2u | (3u << 8)));
+}
+
+// --------------------------------------------------------------- report ----
+
+static std::string capture(const std::function<void(FILE*)>& fn) {
+  char* buf = nullptr;
+  size_t len = 0;
+  FILE* f = open_memstream(&buf, &len);
+  fn(f);
+  std::fclose(f);
+  std::string s(buf, len);
+  std::free(buf);
+  return s;
+}
+
+static PhaseResult fake_cell(int row, int col, double gbps_value) {
+  PhaseResult r;
+  r.row = row;
+  r.col = col;
+  r.idle = row == col;
+  r.seconds_per_iter = 1.0;
+  r.bytes_per_iter = gbps_value * 1e9 / 8.0;
+  return r;
+}
+
+TEST(test_compat_golden) {
+  // SURVEY.md Appendix B, generated from the reference's printf sequence.
+  const std::string golden =
+      "Evaluating the Uni-Directional NCCL P2P Bandwidth (Gbps)\n"
+      "   D\\D     0      1 \n"
+      "     0   0.00 391.53 \n"
+      "     1 1234.50   0.00 \n"
+      "\n"
+      "Evaluating the Bi-Directional NCCL P2P Bandwidth (Gbps)\n"
+      "   D\\D     0      1 \n"
+      "     0   0.00 391.53 \n"
+      "     1 1234.50   0.00 \n";
+  std::string got = capture([](FILE* f) {
+    CompatPrinter cp(f, 2);
+    for (Direction d : {Direction::Uni, Direction::Bi}) {
+      cp.begin(d, false);
+      cp.on_phase(fake_cell(0, 0, 0));
+      cp.on_phase(fake_cell(0, 1, 391.53));
+      cp.on_phase(fake_cell(1, 0, 1234.5));
+      cp.on_phase(fake_cell(1, 1, 0));
+    }
+  });
+  EXPECT(got == golden);
+  if (got != golden) std::fprintf(stderr, "got:\n%s\n", got.c_str());
+}
+
+TEST(test_json_escape) {
+  EXPECT(json_escape("a\"b\\c\n") == "a\\\"b\\\\c\\n");
+}
+
+TEST(test_cli_defaults_match_reference) {
+  AppConfig cfg;
+  int code = -1;
+  char prog_args[1][1] = {{0}};
+  (void)prog_args;
+  EXPECT(parse_cli(0, nullptr, &cfg, &code));
+  EXPECT(cfg.modes.size() == 1 && cfg.modes[0] == Mode::Pair);
+  EXPECT(cfg.dirs.size() == 2 && cfg.dirs[0] == Direction::Uni && cfg.dirs[1] == Direction::Bi);
+  EXPECT(cfg.sizes.size() == 1 && cfg.sizes[0] == (32u << 20));
+  EXPECT(cfg.run.iters == 128);
+  std::vector<std::string> args{"--mode", "ring,allpairs", "--sizes", "4K:16K", "-n", "auto", "--reference", "--dir=bi"};
+  std::vector<char*> argv;
+  for (auto& a : args) argv.push_back(&a[0]);
+  AppConfig c2;
+  EXPECT(parse_cli(static_cast<int>(argv.size()), argv.data(), &c2, &code));
+  EXPECT(c2.modes.size() == 2 && c2.modes[1] == Mode::AllPairs);
+  EXPECT(c2.sizes.size() == 3);
+  EXPECT(c2.iters_auto);
+  EXPECT(c2.run.timing == Timing::Wallclock && c2.run.warmup == 0 && !c2.warm_connections);
+  EXPECT(c2.dirs.size() == 1 && c2.dirs[0] == Direction::Bi);
+  EXPECT(auto_iters(32u << 20, 4ull << 30) == 128);  // the reference's 128 x 32 MiB
+  EXPECT(auto_iters(4096, 4ull << 30) == 1000);
+  EXPECT(auto_iters(4ull << 30, 4ull << 30) == 8);
+}
+
+// ------------------------------------------- multi-rank engine (threads) ----
+
+static void run_ranks(int n, const std::function<void(Bootstrap&, Transport&)>& body) {
+  TcpListener listener(0, "127.0.0.1");
+  int port = listener.port();
+  std::vector<std::thread> th;
+  for (int r = 0; r < n; ++r) {
+    th.emplace_back([&, r]() {
+      auto boot = make_tcp_bootstrap(r, n, "127.0.0.1", port, 60.0, r == 0 ? &listener : nullptr);
+      TransportOptions opt;
+      opt.timeout_s = 60;
+      auto t = make_host_transport(*boot, opt);
+      body(*boot, *t);
+    });
+  }
+  for (auto& t : th) t.join();
+}
+
+TEST(test_bootstrap_collectives) {
+  run_ranks(4, [](Bootstrap& b, Transport&) {
+    auto v = b.allgather_value(b.rank() * 10);
+    EXPECT(v.size() == 4 && v[3] == 30);
+    int x = b.rank() == 2 ? 77 : 0;
+    b.bcast(&x, sizeof(x), 2);
+    EXPECT(x == 77);
+    EXPECT(b.allreduce_max(static_cast<double>(b.rank())) == 3.0);
+    EXPECT(b.allreduce_sum_u64(1) == 4);
+    b.barrier();
+  });
+}
+
+TEST(test_engine_all_modes_host_transport) {
+  const int n = 4;
+  std::vector<uint64_t> mism(n, 1);
+  run_ranks(n, [&](Bootstrap& b, Transport& t) {
+    uint64_t bad = 0;
+    for (Mode m : {Mode::Pair, Mode::Ring, Mode::AllPairs, Mode::Tournament, Mode::Self}) {
+      for (Direction d : {Direction::Uni, Direction::Bi}) {
+        Schedule s = make_schedule(m, d, n);
+        RunConfig cfg;
+        cfg.bytes = 4099;  // odd size exercises the tail path
+        cfg.iters = 3;
+        cfg.warmup = 1;
+        cfg.verify = true;
+        Buffers bufs(t, cfg.bytes, std::max(1, s.max_recv_slots()));
+        auto res = run_schedule(t, b, s, cfg, bufs);
+        EXPECT(res.size() == s.phases.size());
+        for (auto& ph : res) {
+          bad += ph.total_mismatches;
+          if (!ph.idle) {
+            EXPECT(ph.seconds_per_iter > 0);
+            for (auto& f : ph.flows) EXPECT(f.verified && f.gbs > 0);
+          }
+        }
+      }
+    }
+    mism[b.rank()] = bad;
+  });
+  for (auto v : mism) EXPECT(v == 0);
+}
+
+TEST(test_wallclock_and_latency_host) {
+  run_ranks(3, [&](Bootstrap& b, Transport& t) {
+    Schedule s = make_pair_schedule(3, Direction::Bi);
+    RunConfig cfg;
+    cfg.bytes = 4096;
+    cfg.iters = 4;
+    cfg.warmup = 0;
+    cfg.timing = Timing::Wallclock;
+    Buffers bufs(t, 4096, 1);
+    auto res = run_schedule(t, b, s, cfg, bufs);
+    for (auto& ph : res)
+      if (!ph.idle) EXPECT(ph.seconds_per_iter > 0 && ph.flows.size() == 2);
+    auto lat = run_latency(t, b, 8, 20, 2, bufs);
+    EXPECT(lat.size() == 3);
+    for (auto& l : lat) EXPECT(l.one_way_us.n == 20 && l.one_way_us.p50 > 0);
+  });
+}
+
+TEST(test_step_driver_host) {
+  run_ranks(4, [&](Bootstrap& b, Transport& t) {
+    StepDriver d(t, b, make_tournament_schedule(4, Direction::Bi), 8192, 2, true);
+    d.connect();
+    for (long k = 0; k < 6; ++k) d.step(k);
+    d.sync();
+    auto ms = d.step_ms();
+    EXPECT(ms.size() == 6);
+    EXPECT(d.verify_last() == 0);
+    EXPECT(d.job_bytes_per_step(0) == 4.0 * 8192 * 2);
+    EXPECT(d.bytes_sent_per_step(0) == 8192.0 * 2);
+    b.barrier();
+  });
+}
+
+int main(int argc, char** argv) {
+  const char* only = argc > 1 ? argv[1] : nullptr;
+  int ran = 0;
+  for (auto& tc : registry()) {
+    if (only && !std::strstr(tc.name, only)) continue;
+    int before = g_failures;
+    std::printf("[ RUN  ] %s\n", tc.name);
+    std::fflush(stdout);
+    tc.fn();
+    std::printf("[ %s ] %s\n", g_failures == before ? " OK " : "FAIL", tc.name);
+    ++ran;
+  }
+  std::printf("%d tests, %d checks, %d failures\n", ran, g_checks.load(), g_failures.load());
+  return g_failures ? 1 : 0;
+}

@@ -1,0 +1,55 @@
+"""Tier T3: the p2p_matrix executable and bench.py on one MI355X."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import MPIRUN, ROOT, ensure_built
+from test_nccl_p2p_amd.utils.report import parse_compat
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def exe():
+    ensure_built("gpu")
+    return os.path.join(ROOT, "build", "p2p_matrix")
+
+
+def test_default_run_single_rank_compat(exe):
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    m = parse_compat(out.stdout)
+    assert m == {"uni": [[0.0]], "bi": [[0.0]]}
+    assert "gfx950" in out.stdout
+
+
+def test_self_sweep_verify(exe, tmp_path):
+    js = tmp_path / "r.json"
+    out = subprocess.run([exe, "--mode", "self", "--sizes", "4K:256M:4", "-n", "auto", "--verify", "--latency",
+                          "--json", str(js), "--verify-impl", "lds"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    runs = [json.loads(l) for l in js.read_text().splitlines()]
+    assert sum(1 for r in runs if r["type"] == "run") == 7
+    assert "verification: OK" in out.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
+def test_mpirun_one_rank(exe):
+    out = subprocess.run([MPIRUN, "-n", "1", exe, "--mode", "pair,self", "--size", "8M", "-n", "8", "--verify"],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert "bootstrap mpi" in out.stdout
+
+
+def test_bench_contract_single_gpu():
+    out = subprocess.run([sys.executable, "bench.py", "--steps", "6", "--warmup", "2", "--latency-iters", "50"],
+                         capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 1 and r["steps"] == 6 and r["value"] > 10
+    assert r["verify_mismatches"] == 0 and r["transport"] == "rccl"

@@ -1,0 +1,125 @@
+"""Tier T1: the p2p_matrix application under `mpirun -n N` on the CPU
+(host transport), exercising bootstrap, placement, schedules, reporting and
+failure handling end to end without a GPU."""
+import json
+import os
+import re
+import subprocess
+
+import pytest
+
+from test_nccl_p2p_amd.utils.report import parse_compat
+
+pytestmark = pytest.mark.mpi
+
+
+def run(mpirun, exe, n, args, env=None, timeout=120):
+    e = dict(os.environ)
+    e.update(env or {})
+    cmd = [mpirun, "-n", str(n), exe] + args
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=e)
+
+
+def test_compat_output_format(mpirun, host_build):
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    out = run(mpirun, exe, 3, ["--transport", "host", "--size", "64K", "-n", "4", "--compat-only"])
+    assert out.returncode == 0, out.stderr
+    txt = out.stdout
+    assert txt.startswith("Evaluating the Uni-Directional NCCL P2P Bandwidth (Gbps)\n   D\\D     0      1      2 \n")
+    assert "\n\nEvaluating the Bi-Directional NCCL P2P Bandwidth (Gbps)\n" in txt
+    m = parse_compat(txt)
+    for key in ("uni", "bi"):
+        mat = m[key]
+        assert len(mat) == 3
+        for i in range(3):
+            assert mat[i][i] == 0.0
+            assert all(mat[i][j] > 0 for j in range(3) if j != i)
+    # every row line: label "%6d " then 3 cells "%6.02f " (values < 1000 on CPU)
+    rows = [l for l in txt.splitlines() if re.match(r"^ {5}\d ", l)]
+    assert all(len(l) == 7 * 4 for l in rows)
+
+
+def test_all_modes_verify_json(mpirun, host_build, tmp_path):
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    js = tmp_path / "r.json"
+    csv = tmp_path / "r.csv"
+    out = run(mpirun, exe, 4, ["--transport", "host", "--mode", "all", "--sizes", "4K:16K", "-n", "3",
+                               "--verify", "--latency", "--latency-iters", "20", "--json", str(js), "--csv", str(csv)])
+    assert out.returncode == 0, out.stderr
+    recs = [json.loads(l) for l in js.read_text().splitlines()]
+    runs = [r for r in recs if r["type"] == "run"]
+    # pair/tournament/ring x {uni,bi} + allpairs once, x 3 sizes
+    assert len(runs) == (3 * 2 + 1) * 3
+    for r in runs:
+        for ph in r["phases"]:
+            assert ph["mismatches"] == 0
+    lat = [r for r in recs if r["type"] == "latency"][0]
+    assert len(lat["pairs"]) == 6
+    assert "verification: OK" in out.stdout
+    assert csv.read_text().startswith("mode,dir,bytes")
+
+
+def test_dry_run_and_help(host_build):
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    out = subprocess.run([exe, "--dry-run", "--mode", "tournament", "--dir", "bi"], capture_output=True, text=True,
+                         timeout=60)
+    assert out.returncode == 0 and "schedule tournament-bi, 1 ranks" in out.stdout
+    h = subprocess.run([exe, "--help"], capture_output=True, text=True, timeout=60)
+    assert h.returncode == 0 and "mpirun -n N ./p2p_matrix" in h.stdout
+    bad = subprocess.run([exe, "--bogus"], capture_output=True, text=True, timeout=60)
+    assert bad.returncode == 1
+
+
+def test_block_placement_enforced(mpirun, host_build):
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    base = ["--transport", "host", "--size", "4K", "-n", "2", "--compat-only"]
+    ok = subprocess.run([mpirun, "-n", "2", "-env", "P2P_HOSTNAME", "hostA", exe] + base +
+                        [":", "-n", "2", "-env", "P2P_HOSTNAME", "hostB", exe] + base,
+                        capture_output=True, text=True, timeout=120)
+    assert ok.returncode == 0, ok.stderr
+    bad = subprocess.run([mpirun, "-n", "1", "-env", "P2P_HOSTNAME", "hostA", exe] + base +
+                         [":", "-n", "1", "-env", "P2P_HOSTNAME", "hostB", exe] + base +
+                         [":", "-n", "1", "-env", "P2P_HOSTNAME", "hostA", exe] + base +
+                         [":", "-n", "1", "-env", "P2P_HOSTNAME", "hostB", exe] + base,
+                         capture_output=True, text=True, timeout=120)
+    assert bad.returncode != 0
+    assert "block placement" in bad.stderr
+
+
+def test_corruption_detected(mpirun, host_build):
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    out = run(mpirun, exe, 2, ["--transport", "host", "--size", "64K", "-n", "3", "--verify", "--compat-only"],
+              env={"P2P_INJECT_FAULT": "corrupt@1:1"})
+    assert out.returncode == 2
+    assert "VERIFICATION FAILED" in out.stderr
+
+
+def test_dead_rank_does_not_hang(mpirun, host_build):
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    out = run(mpirun, exe, 3, ["--transport", "host", "--size", "64K", "-n", "3"],
+              env={"P2P_INJECT_FAULT": "exit@2:2"}, timeout=120)
+    assert out.returncode != 0
+    assert "injected fault" in out.stderr
+
+
+def test_hung_rank_times_out_tcp(host_build):
+    """TCP bootstrap (torchrun-style env): a hung rank trips the others' watchdogs."""
+    from conftest import free_port
+
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    port = free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", P2P_BOOTSTRAP_PORT=str(port),
+                   P2P_BOOTSTRAP_TIMEOUT="5", P2P_INJECT_FAULT="hang@1:1")
+        procs.append(subprocess.Popen([exe, "--transport", "host", "--size", "4K", "-n", "2", "--timeout", "5"],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    try:
+        _, err0 = procs[0].communicate(timeout=90)
+        assert procs[0].returncode != 0
+        assert "timeout" in err0 or "closed" in err0
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()

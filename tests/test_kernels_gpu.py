@@ -1,0 +1,95 @@
+"""Tier T3: the gfx950 fill / verify / reduce kernels against the plain
+PyTorch reference of the same op (integer PRNG + word compare + checksum)."""
+import pytest
+import torch
+
+from test_nccl_p2p_amd.ops import checksum, fill_, reference_bytes, reference_verify, verify
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [16, 48, 1000, 4096, 4099, (1 << 20) + 13, 4 << 20, 64 << 20]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(native):
+    assert torch.cuda.is_available(), "GPU tier needs a GPU"
+    torch.cuda.set_device(0)
+
+
+def dev_bytes(n):
+    # Over-allocate so the tail path cannot write past the logical size unnoticed.
+    return torch.full((n + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+
+
+@pytest.mark.parametrize("nbytes", SIZES)
+def test_fill_matches_reference(nbytes):
+    buf = dev_bytes(nbytes)
+    fill_(buf[:nbytes], 0xC0FFEE)
+    torch.cuda.synchronize()
+    ref = reference_bytes(nbytes, 0xC0FFEE, device="cuda")
+    assert torch.equal(buf[:nbytes], ref)
+    assert torch.all(buf[nbytes:] == 0xAB), "fill wrote past the end"
+
+
+@pytest.mark.parametrize("impl", ["reg", "lds"])
+@pytest.mark.parametrize("nbytes", SIZES)
+def test_verify_clean_and_checksum(impl, nbytes):
+    buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    fill_(buf, 77)
+    r = verify(buf, 77, impl=impl)
+    ref = reference_verify(buf, 77)
+    assert r.mismatches == 0 and r.first_bad == 2**64 - 1
+    assert r.checksum == ref.checksum
+    assert checksum(buf, impl=impl) == ref.checksum
+    wrong = verify(buf, 78, impl=impl)
+    assert wrong.mismatches == reference_verify(buf, 78).mismatches > 0
+
+
+@pytest.mark.parametrize("impl", ["reg", "lds"])
+def test_verify_counts_exact_bitflips(impl):
+    nbytes = (8 << 20) + 5
+    buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    fill_(buf, 1234)
+    flips = [7, 4096, 123457, nbytes - 1, nbytes - 3, 5 << 20]
+    for off in flips:
+        buf[off] ^= 0x40
+    r = verify(buf, 1234, impl=impl)
+    ref = reference_verify(buf, 1234)
+    words = {(o // 4) for o in flips}
+    assert r.mismatches == ref.mismatches == len(words)
+    assert r.first_bad == ref.first_bad == 4
+    assert r.checksum == ref.checksum
+
+
+def test_lds_and_register_agree_on_random_data():
+    g = torch.Generator(device="cuda").manual_seed(0)
+    buf = torch.randint(0, 256, (3 << 20,), dtype=torch.uint8, device="cuda", generator=g)
+    a = verify(buf, 5, impl="reg")
+    b = verify(buf, 5, impl="lds")
+    assert a == b == reference_verify(buf, 5)
+
+
+def test_int32_tensor_and_alignment_checks():
+    t = torch.empty(1 << 16, dtype=torch.int32, device="cuda")
+    fill_(t, 9)
+    assert verify(t, 9).ok
+    with pytest.raises(ValueError):
+        verify(t.view(torch.uint8)[1:17], 9)
+
+
+def test_kernel_bandwidth_sanity():
+    """fill / verify at 1 GiB must run at a healthy fraction of the HBM roof."""
+    nbytes = 1 << 30
+    buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    fill_(buf, 1)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(5):
+        fill_(buf, 1)
+    e.record()
+    e.synchronize()
+    fill_tbs = 5 * nbytes / (s.elapsed_time(e) * 1e-3) / 1e12
+    assert verify(buf, 1, impl="reg").ok
+    print("fill %.2f TB/s" % fill_tbs)
+    assert fill_tbs > 2.0

@@ -1,0 +1,67 @@
+"""Tier T3: the RCCL transport on one MI355X (1-rank communicator: self
+send/recv through ncclGroupStart/End), through every engine entry point."""
+import json
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def session(native):
+    assert torch.cuda.is_available()
+    torch.cuda.set_device(0)
+    s = native.Session(0, 1, device=0, transport="rccl", timeout_s=120)
+    yield s
+    del s
+
+
+def test_device_desc(session):
+    assert "gfx950" in session.device_desc
+    assert session.transport == "rccl"
+
+
+@pytest.mark.parametrize("mode", ["self", "ring", "allpairs", "tournament"])
+def test_self_modes_verified(session, mode):
+    r = json.loads(session.run(mode=mode, dir="bi", bytes=(4 << 20) + 12, iters=6, warmup=2, verify=True))
+    (ph,) = r["phases"]
+    assert ph["mismatches"] == 0
+    (flow,) = ph["flows"]
+    assert flow["src"] == flow["dst"] == 0 and flow["gbs"] > 1.0
+
+
+def test_pair_mode_single_rank_is_idle_diagonal(session):
+    r = json.loads(session.run(mode="pair", dir="uni", bytes=1 << 20, iters=2, warmup=0))
+    assert r["phases"] == []  # diagonal only, like the reference's 1-rank run
+
+
+@pytest.mark.parametrize("timing", ["events", "wallclock"])
+def test_timings(session, timing):
+    r = json.loads(session.run(mode="self", dir="uni", bytes=32 << 20, iters=16, warmup=2, timing=timing, verify=True))
+    ph = r["phases"][0]
+    assert ph["mismatches"] == 0 and ph["seconds_per_iter"] > 0
+    assert ph["flows"][0]["iter_us"]["n"] == 16
+
+
+def test_sweep_up_to_1g(session):
+    for nbytes in [4096, 1 << 20, 64 << 20, 1 << 30]:
+        r = json.loads(session.run(mode="self", dir="uni", bytes=nbytes, iters=4, warmup=1, verify=True))
+        assert r["phases"][0]["mismatches"] == 0
+
+
+def test_latency(session):
+    lat = json.loads(session.latency(8, 200, 20))
+    (p,) = lat["pairs"]
+    assert p["one_way_us"]["n"] == 200 and 0 < p["one_way_us"]["p50"] < 1000
+
+
+def test_step_driver(native, session):
+    d = native.StepDriver(session, "self", "bi", 8 << 20, 4, True)
+    d.connect()
+    d.run_steps(0, 5)
+    d.sync()
+    ms = d.step_ms()
+    assert len(ms) == 5 and all(m > 0 for m in ms)
+    assert d.verify_last() == 0
+    assert d.job_bytes_per_step(0) == 4 * (8 << 20)

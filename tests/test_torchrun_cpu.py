@@ -1,0 +1,49 @@
+"""Multi-process paths over torch.distributed on the CPU: the gloo harness
+(BASELINE.json config 1: 2-rank CPU/gloo send/recv of a 4 KiB buffer), the
+native engine under torchrun (TCP bootstrap + host transport), and bench.py's
+full control flow with the host transport."""
+import json
+import os
+import subprocess
+import sys
+
+from conftest import ROOT, free_port
+
+
+def torchrun(nproc, args, timeout=240, env=None):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port())] + args
+    e = dict(os.environ, OMP_NUM_THREADS="1")
+    e.update(env or {})
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=e)
+
+
+def test_gloo_config1_4k():
+    out = torchrun(2, ["-m", "test_nccl_p2p_amd.parallel.gloo_harness", "--size", "4K", "--iters", "50"])
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "Evaluating the Uni-Directional NCCL P2P Bandwidth (Gbps)" in out.stdout
+    assert "mismatches 0" in out.stdout
+
+
+def test_native_module_under_torchrun(native):
+    out = torchrun(2, ["-m", "test_nccl_p2p_amd", "--transport", "host", "--mode", "pair,ring", "--size", "16K",
+                       "-n", "5", "--verify", "--latency", "--latency-iters", "20"])
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert out.stdout.count("Evaluating the") == 2
+    assert "verification: OK" in out.stdout
+    assert "bootstrap tcp" in out.stdout
+
+
+def test_bench_cpu_two_ranks(native):
+    out = torchrun(2, ["bench.py", "--gpus", "2", "--steps", "4", "--warmup", "2", "--transport", "host",
+                       "--size", "256K", "--msgs", "2", "--latency-iters", "20"])
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    r = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in r
+    assert r["n_gpus"] == 2 and r["steps"] == 4 and r["value"] > 0
+    assert r["verify_mismatches"] == 0
+    assert r["matrix_cells"] == "2/2"
