@@ -48,6 +48,23 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+class stdout_to_stderr:
+    """fd-level redirect: RCCL prints its version banner on stdout during
+    communicator init; the driver contract wants exactly one JSON line there."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -87,12 +104,13 @@ def main(argv=None) -> int:
             torch.cuda.synchronize()
 
     size = nat.parse_size(args.size)
-    sess = create_session(args.transport, device=env.local_rank)
-    if env.rank == 0:
-        log("bench: %d rank(s), %s, %s" % (n, sess.transport, sess.device_desc))
-    mode = "self" if n == 1 else args.mode
-    drv = nat.StepDriver(sess, mode, "bi", size, args.msgs, not args.no_verify)
-    drv.connect()
+    with stdout_to_stderr():
+        sess = create_session(args.transport, device=env.local_rank)
+        if env.rank == 0:
+            log("bench: %d rank(s), %s, %s" % (n, sess.transport, sess.device_desc))
+        mode = "self" if n == 1 else args.mode
+        drv = nat.StepDriver(sess, mode, "bi", size, args.msgs, not args.no_verify)
+        drv.connect()
 
     # Warmup (untimed): also walks every round once when W >= phases.
     if args.warmup > 0:

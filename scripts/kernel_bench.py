@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Bandwidth of the gfx950 buffer kernels (fill, verify-register, verify-LDS,
+checksum) vs the HBM3E roofline.  Used for the A/B that decides the default
+verify staging and as the workload for the rocprofv3
+runs in scripts/profile.sh.
+
+    python scripts/kernel_bench.py [--sizes 64M,1G,4G] [--reps 10] [--json out.json]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+import test_nccl_p2p_amd  # noqa: E402
+from test_nccl_p2p_amd.ops import buffers  # noqa: E402
+
+HBM_MEASURED_TBS = 6.29  # float4 copy, MI355X_MICROARCH.md
+
+
+def timed(fn, reps):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sizes", default="64M,256M,1G,4G")
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    nat = test_nccl_p2p_amd.require_native()
+    torch.cuda.set_device(0)
+    stream = torch.cuda.current_stream().cuda_stream
+    rows = []
+    for sz in [nat.parse_size(s) for s in a.sizes.split(",")]:
+        buf = torch.empty(sz, dtype=torch.uint8, device="cuda")
+        ptr = buf.data_ptr()
+        t_fill = timed(lambda: nat.fill(ptr, sz, 7, stream), a.reps)
+        res = {}
+        for name, impl, check in [("verify_reg", 1, True), ("verify_lds", 2, True), ("checksum_reg", 1, False),
+                                  ("checksum_lds", 2, False)]:
+            # verify() syncs (result readback); time with a host-side loop of
+            # launches through the same path and subtract nothing: the sync is
+            # part of what a caller pays.
+            t = timed(lambda: nat.verify(ptr, sz, 7, impl, check, stream), a.reps)
+            res[name] = t
+            assert nat.verify(ptr, sz, 7, impl, True, stream)[0] == 0
+        row = {"bytes": sz, "fill_tbs": sz / t_fill / 1e12}
+        for k, t in res.items():
+            row[k + "_tbs"] = sz / t / 1e12
+        row["fill_geom"] = nat.fill_geometry(sz)
+        row["verify_reg_geom"] = nat.verify_geometry(sz, 1)
+        row["verify_lds_geom"] = nat.verify_geometry(sz, 2)
+        rows.append(row)
+        print("%6s  fill %.2f  verify reg %.2f / lds %.2f  checksum reg %.2f / lds %.2f TB/s  (HBM measured roof %.2f)"
+              % (nat.format_size(sz), row["fill_tbs"], row["verify_reg_tbs"], row["verify_lds_tbs"],
+                 row["checksum_reg_tbs"], row["checksum_lds_tbs"], HBM_MEASURED_TBS), flush=True)
+        del buf
+        torch.cuda.empty_cache()
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(rows, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -32,7 +32,7 @@ def test_self_sweep_verify(exe, tmp_path):
                           "--json", str(js), "--verify-impl", "lds"], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr
     runs = [json.loads(l) for l in js.read_text().splitlines()]
-    assert sum(1 for r in runs if r["type"] == "run") == 7
+    assert sum(1 for r in runs if r["type"] == "run") == 9  # 4K,16K,...,256M
     assert "verification: OK" in out.stdout
 
 
