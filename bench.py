@@ -73,10 +73,14 @@ def parse_args(argv=None):
     ap.add_argument("--size", default="32M", help="message size (reference: 32 MiB, p2p_matrix.cc:124)")
     ap.add_argument("--msgs", type=int, default=8, help="messages per direction per step")
     ap.add_argument("--mode", default="tournament", choices=["tournament", "ring", "allpairs", "pair", "self"])
-    ap.add_argument("--transport", default="rccl", choices=["rccl", "host"], help="host = CPU sockets (testing)")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "ipc", "ipc:sdma", "host"],
+                    help="rccl (headline) | ipc = one-sided gfx950 copy kernel over hipIpc mappings | host = CPU (tests)")
+    ap.add_argument("--device", type=int, default=None, help="GPU index (default LOCAL_RANK)")
     ap.add_argument("--latency-iters", type=int, default=300)
     ap.add_argument("--latency-size", default="8")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--batch", type=int, default=1, help="1: all msgs of a step in one ncclGroup (one launch)")
+    ap.add_argument("--graph", type=int, default=0, help="1: replay each step as a captured hipGraph")
     ap.add_argument("--json-out", default=None, help="also write the result line to this file")
     return ap.parse_args(argv)
 
@@ -91,9 +95,10 @@ def main(argv=None) -> int:
     if args.gpus != env.world:
         log("bench: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, env.world))
     n = env.world
-    use_gpu = args.transport == "rccl"
+    use_gpu = args.transport != "host"
+    device = env.local_rank if args.device is None else args.device
     if use_gpu:
-        torch.cuda.set_device(env.local_rank)
+        torch.cuda.set_device(device)
 
     def barrier():
         if n > 1:
@@ -105,11 +110,11 @@ def main(argv=None) -> int:
 
     size = nat.parse_size(args.size)
     with stdout_to_stderr():
-        sess = create_session(args.transport, device=env.local_rank)
+        sess = create_session(args.transport, device=device)
         if env.rank == 0:
             log("bench: %d rank(s), %s, %s" % (n, sess.transport, sess.device_desc))
         mode = "self" if n == 1 else args.mode
-        drv = nat.StepDriver(sess, mode, "bi", size, args.msgs, not args.no_verify)
+        drv = nat.StepDriver(sess, mode, "bi", size, args.msgs, not args.no_verify, bool(args.batch), bool(args.graph))
         drv.connect()
 
     # Warmup (untimed): also walks every round once when W >= phases.
@@ -176,8 +181,9 @@ def main(argv=None) -> int:
         "dtype": "uint8",
         "data": "synthetic (device PRNG-filled payloads, verified after timing)",
         "config": {
-            "model": "p2p_matrix: RCCL ncclSend/ncclRecv %s-bidirectional, %s x %d msgs/step"
-                     % (mode, nat.format_size(size), args.msgs),
+            "model": "p2p_matrix: %s %s-bidirectional, %s x %d msgs/step"
+                     % ("RCCL ncclSend/ncclRecv" if sess.transport == "rccl" else sess.transport + " transport",
+                        mode, nat.format_size(size), args.msgs),
             "global_batch": args.msgs * n,
             "seq_len": size,
             "parallelism": "p2p%d" % n,
@@ -191,6 +197,7 @@ def main(argv=None) -> int:
         "rank0_step_ms_p50": round(step_ms_med, 4),
         "verify_mismatches": mismatches,
         "transport": sess.transport,
+        "posting": {"batch": bool(args.batch), "graph": bool(args.graph)},
     }
     if env.rank == 0:
         log("bench: GB/s matrix (row=src, col=dst), median over steps:")

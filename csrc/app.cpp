@@ -47,7 +47,11 @@ data
   -c, --verify           random-fill sends, verify every received buffer on the device
       --verify-impl I    auto | reg | lds  (register- or LDS-DMA-staged verify kernel)
 transport / launch
-      --transport T      rccl (MI355X + RCCL) | host (CPU sockets, no GPU)      [rccl]
+      --transport T      rccl  MI355X + RCCL ncclSend/ncclRecv over xGMI      [rccl]
+                         ipc   one-sided pulls from hipIpc-mapped peer buffers (gfx950 copy
+                               kernel or SDMA); ranks may share a GPU
+                         host  CPU sockets, no GPU
+      --ipc-engine E     kernel | sdma (for --transport ipc)                   [kernel]
       --bootstrap B      auto | mpi | env | local                              [auto]
       --device N         GPU index (default: local rank from block placement)
       --timeout S        watchdog for init / waits, seconds                    [300]
@@ -159,6 +163,8 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
       cfg->verify_impl = v == "reg" || v == "register" ? 1 : v == "lds" ? 2 : 0;
     } else if (a == "--transport") {
       cfg->transport = next();
+    } else if (a == "--ipc-engine") {
+      cfg->ipc_engine = next();
     } else if (a == "--bootstrap") {
       cfg->bootstrap = next();
     } else if (a == "--device") {
@@ -190,8 +196,8 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
     return false;
   }
   if (cfg->run.warmup < 0) cfg->run.warmup = 0;
-  if (cfg->transport != "rccl" && cfg->transport != "host") {
-    std::fprintf(stderr, "p2p_matrix: --transport must be rccl or host\n");
+  if (cfg->transport != "rccl" && cfg->transport != "host" && cfg->transport != "ipc") {
+    std::fprintf(stderr, "p2p_matrix: --transport must be rccl, ipc or host\n");
     *exit_code = 1;
     return false;
   }
@@ -243,8 +249,10 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
   topt.device = cfg.device >= 0 ? cfg.device : pl.local_rank;
   topt.timeout_s = cfg.timeout_s;
   topt.verify_impl = cfg.verify_impl;
-  std::unique_ptr<Transport> t =
-      cfg.transport == "host" ? make_host_transport(boot, topt) : make_rccl_transport(boot, topt);
+  topt.ipc_engine = cfg.ipc_engine;
+  std::unique_ptr<Transport> t = cfg.transport == "host"  ? make_host_transport(boot, topt)
+                                 : cfg.transport == "ipc" ? make_ipc_transport(boot, topt)
+                                                          : make_rccl_transport(boot, topt);
 
   size_t max_bytes = *std::max_element(cfg.sizes.begin(), cfg.sizes.end());
   if (cfg.latency) max_bytes = std::max(max_bytes, cfg.latency_bytes);

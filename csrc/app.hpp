@@ -31,7 +31,8 @@ struct AppConfig {
   bool latency = false;
   size_t latency_bytes = 8;
   int latency_iters = 1000;
-  std::string transport = "rccl";  // rccl | host
+  std::string transport = "rccl";  // rccl | ipc | host
+  std::string ipc_engine = "kernel";
   std::string bootstrap = "auto";  // auto | mpi | env | local
   int device = -1;
   std::string json_path;

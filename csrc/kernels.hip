@@ -30,8 +30,12 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
 constexpr int kFillUnroll = 4;
-constexpr int kVerifyUnroll = 4;
+constexpr int kVerifyUnroll = 4;   // register variant, default
+constexpr int kVerifyUnroll8 = 8;  // register variant with twice the loads in flight
 constexpr int kLdsStages = 4;  // 1 KiB pieces per wave per batch
+// Defaults picked from scripts/kernel_bench.py A/B runs (profiles/).
+constexpr FillImpl kDefaultFill = FillImpl::Plain;
+constexpr VerifyImpl kDefaultVerify = VerifyImpl::Register;
 
 #define HIP_OK(cmd)                                                                          \
   do {                                                                                       \
@@ -39,24 +43,36 @@ constexpr int kLdsStages = 4;  // 1 KiB pieces per wave per batch
     if (e_ != hipSuccess) P2P_FATAL(strfmt("HIP error %s: %s", #cmd, hipGetErrorString(e_))); \
   } while (0)
 
-__device__ __forceinline__ uint4 prng_vec(uint64_t seed, uint64_t vec_index) {
-  const uint64_t w = vec_index * 4;
-  const uint32_t key = prng_key(seed, w);
-  const uint32_t lo = static_cast<uint32_t>(w);
+// The key depends only on (seed, word_index >> 32).  Every tile below is a
+// multiple of 4096 words and starts on such a multiple, so it never straddles
+// a 2^32-word boundary: the key is computed once per tile from tile-uniform
+// values (scalar ALU) and only the 4 per-word mixes run on the vector ALU.
+__device__ __forceinline__ uint4 prng_vec_k(uint32_t key, uint64_t vec_index) {
+  const uint32_t lo = static_cast<uint32_t>(vec_index * 4);
   return make_uint4(prng_word_k(key, lo), prng_word_k(key, lo + 1), prng_word_k(key, lo + 2), prng_word_k(key, lo + 3));
 }
 
 // ------------------------------------------------------------------ fill ----
 
+template <bool NT>
 __global__ __launch_bounds__(kBlock) void fill_kernel(uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
                                                       uint8_t* __restrict__ tail, uint32_t tail_bytes,
                                                       uint64_t tail_offset) {
   const uint64_t tile = static_cast<uint64_t>(kBlock) * kFillUnroll;
   for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * tile; base < nvec; base += static_cast<uint64_t>(gridDim.x) * tile) {
+    const uint32_t key = prng_key(seed, base * 4);
 #pragma unroll
     for (int u = 0; u < kFillUnroll; ++u) {
       const uint64_t i = base + static_cast<uint64_t>(u) * kBlock + threadIdx.x;
-      if (i < nvec) p[i] = prng_vec(seed, i);
+      if (i < nvec) {
+        const uint4 v = prng_vec_k(key, i);
+        if (NT) {
+          u32x4 w = {v.x, v.y, v.z, v.w};
+          __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p) + i);
+        } else {
+          p[i] = v;
+        }
+      }
     }
   }
   if (blockIdx.x == 0 && threadIdx.x < tail_bytes) tail[threadIdx.x] = prng_byte(seed, tail_offset + threadIdx.x);
@@ -71,10 +87,10 @@ struct Partial {
 };
 
 template <bool CHECK>
-__device__ __forceinline__ void check_vec(const uint4 v, uint64_t seed, uint64_t vec_index, Partial& acc) {
+__device__ __forceinline__ void check_vec(const uint4 v, uint32_t key, uint64_t vec_index, Partial& acc) {
   acc.sum += static_cast<unsigned long long>(v.x) + v.y + static_cast<unsigned long long>(v.z) + v.w;
   if (CHECK) {
-    const uint4 e = prng_vec(seed, vec_index);
+    const uint4 e = prng_vec_k(key, vec_index);
     const unsigned bad = (v.x != e.x) + (v.y != e.y) + (v.z != e.z) + (v.w != e.w);
     if (bad) {
       acc.mism += bad;
@@ -133,16 +149,16 @@ __device__ __forceinline__ void block_commit(Partial acc, VerifyAccum* out) {
   }
 }
 
-template <bool CHECK>
+template <bool CHECK, int UNROLL>
 __global__ __launch_bounds__(kBlock) void verify_reg_kernel(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
                                                             const uint8_t* __restrict__ tail, uint32_t tail_bytes,
                                                             uint64_t tail_offset, VerifyAccum* __restrict__ out) {
   Partial acc{0, 0, ~0ull};
-  const uint64_t tile = static_cast<uint64_t>(kBlock) * kVerifyUnroll;
+  const uint64_t tile = static_cast<uint64_t>(kBlock) * UNROLL;
   for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * tile; base < nvec; base += static_cast<uint64_t>(gridDim.x) * tile) {
-    uint4 v[kVerifyUnroll];
+    uint4 v[UNROLL];
 #pragma unroll
-    for (int u = 0; u < kVerifyUnroll; ++u) {  // all loads issued before any compare
+    for (int u = 0; u < UNROLL; ++u) {  // all loads issued before any compare
       const uint64_t i = base + static_cast<uint64_t>(u) * kBlock + threadIdx.x;
       if (i < nvec) {
         const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p) + i);
@@ -151,10 +167,11 @@ __global__ __launch_bounds__(kBlock) void verify_reg_kernel(const uint4* __restr
         v[u] = make_uint4(0, 0, 0, 0);
       }
     }
+    const uint32_t key = prng_key(seed, base * 4);
 #pragma unroll
-    for (int u = 0; u < kVerifyUnroll; ++u) {
+    for (int u = 0; u < UNROLL; ++u) {
       const uint64_t i = base + static_cast<uint64_t>(u) * kBlock + threadIdx.x;
-      if (i < nvec) check_vec<CHECK>(v[u], seed, i, acc);
+      if (i < nvec) check_vec<CHECK>(v[u], key, i, acc);
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) check_tail<CHECK>(tail, tail_bytes, tail_offset, seed, acc);
@@ -223,10 +240,11 @@ __global__ __launch_bounds__(kBlock) void verify_lds_kernel(const uint4* __restr
         : "v"(lds_addr)
         : "memory");
     const u32x4 rv[kLdsStages] = {r0, r1, r2, r3};
+    const uint32_t key = prng_key(seed, sc * sc_vecs * 4);
 #pragma unroll
     for (int s = 0; s < kLdsStages; ++s) {
       const uint64_t i = sc * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
-      if (i < nvec) check_vec<CHECK>(make_uint4(rv[s].x, rv[s].y, rv[s].z, rv[s].w), seed, i, acc);
+      if (i < nvec) check_vec<CHECK>(make_uint4(rv[s].x, rv[s].y, rv[s].z, rv[s].w), key, i, acc);
     }
     buf ^= 1;
   }
@@ -288,21 +306,26 @@ LaunchGeom verify_geometry(size_t bytes, VerifyImpl impl) {
     const uint64_t cap = static_cast<uint64_t>(cu_count()) * std::min<uint64_t>(per_cu, 8);
     g.grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min(blocks, cap)));
   } else {
-    const uint64_t tiles = (nvec + kBlock * kVerifyUnroll - 1) / (kBlock * kVerifyUnroll);
+    const int unroll = impl == VerifyImpl::Register8 ? kVerifyUnroll8 : kVerifyUnroll;
+    const uint64_t tiles = (nvec + static_cast<uint64_t>(kBlock) * unroll - 1) / (static_cast<uint64_t>(kBlock) * unroll);
     const uint64_t cap = static_cast<uint64_t>(cu_count()) * 8;
     g.grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min(tiles, cap)));
   }
   return g;
 }
 
-void launch_fill(void* p, size_t bytes, uint64_t seed, hipStream_t stream) {
+void launch_fill(void* p, size_t bytes, uint64_t seed, hipStream_t stream, FillImpl impl) {
   if (!bytes) return;
   P2P_CHECK(reinterpret_cast<uintptr_t>(p) % 16 == 0, "fill: buffer must be 16-byte aligned");
+  if (impl == FillImpl::Auto) impl = kDefaultFill;
   const uint64_t nvec = bytes / 16;
   const uint32_t tail = static_cast<uint32_t>(bytes - nvec * 16);
   LaunchGeom g = fill_geometry(bytes);
   auto* base = static_cast<uint8_t*>(p);
-  fill_kernel<<<g.grid, kBlock, 0, stream>>>(reinterpret_cast<uint4*>(p), nvec, seed, base + nvec * 16, tail, nvec * 16);
+  if (impl == FillImpl::Nontemporal)
+    fill_kernel<true><<<g.grid, kBlock, 0, stream>>>(reinterpret_cast<uint4*>(p), nvec, seed, base + nvec * 16, tail, nvec * 16);
+  else
+    fill_kernel<false><<<g.grid, kBlock, 0, stream>>>(reinterpret_cast<uint4*>(p), nvec, seed, base + nvec * 16, tail, nvec * 16);
   HIP_OK(hipGetLastError());
 }
 
@@ -311,28 +334,120 @@ void launch_verify_reset(VerifyAccum* acc, hipStream_t stream) {
   HIP_OK(hipGetLastError());
 }
 
+namespace {
+template <bool CHECK>
+void launch_verify_t(const uint4* vp, uint64_t nvec, uint64_t seed, const uint8_t* tp, uint32_t tail, VerifyAccum* acc,
+                     VerifyImpl impl, const LaunchGeom& g, hipStream_t stream) {
+  switch (impl) {
+    case VerifyImpl::Lds:
+      verify_lds_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
+      break;
+    case VerifyImpl::Register8:
+      verify_reg_kernel<CHECK, kVerifyUnroll8><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
+      break;
+    default:
+      verify_reg_kernel<CHECK, kVerifyUnroll><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
+  }
+}
+}  // namespace
+
 void launch_verify(const void* p, size_t bytes, uint64_t seed, VerifyAccum* acc, VerifyImpl impl, bool check_prng,
                    hipStream_t stream) {
   if (!bytes) return;
   P2P_CHECK(reinterpret_cast<uintptr_t>(p) % 16 == 0, "verify: buffer must be 16-byte aligned");
-  if (impl == VerifyImpl::Auto) impl = VerifyImpl::Register;
+  if (impl == VerifyImpl::Auto) impl = kDefaultVerify;
   const uint64_t nvec = bytes / 16;
   const uint32_t tail = static_cast<uint32_t>(bytes - nvec * 16);
   const auto* vp = static_cast<const uint4*>(p);
   const auto* tp = static_cast<const uint8_t*>(p) + nvec * 16;
   LaunchGeom g = verify_geometry(bytes, impl);
-  if (impl == VerifyImpl::Lds) {
-    if (check_prng)
-      verify_lds_kernel<true><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
-    else
-      verify_lds_kernel<false><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
-  } else {
-    if (check_prng)
-      verify_reg_kernel<true><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
-    else
-      verify_reg_kernel<false><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
-  }
+  if (check_prng)
+    launch_verify_t<true>(vp, nvec, seed, tp, tail, acc, impl, g, stream);
+  else
+    launch_verify_t<false>(vp, nvec, seed, tp, tail, acc, impl, g, stream);
   HIP_OK(hipGetLastError());
+}
+
+// ------------------------------------------------------------ multi copy ----
+
+namespace {
+
+constexpr int kCopyUnroll = 4;
+
+// Passed by value in the kernarg segment: no device-side descriptor upload,
+// so a launch is a single stream operation (and graph-capturable).
+struct CopyArgs {
+  const uint4* src[kMaxCopyOps];
+  uint4* dst[kMaxCopyOps];
+  uint64_t nvec[kMaxCopyOps];
+  uint32_t tail[kMaxCopyOps];
+  uint32_t block_begin[kMaxCopyOps + 1];
+  int nops;
+};
+
+__global__ __launch_bounds__(kBlock) void multi_copy_kernel(const CopyArgs a) {
+  // Workgroup -> op: block ranges are contiguous per op; the scan is over at
+  // most kMaxCopyOps wave-uniform values.
+  int op = 0;
+  while (op + 1 < a.nops && blockIdx.x >= a.block_begin[op + 1]) ++op;
+  const uint32_t b = blockIdx.x - a.block_begin[op];
+  const uint32_t nb = a.block_begin[op + 1] - a.block_begin[op];
+  const uint4* __restrict__ s = a.src[op];
+  uint4* __restrict__ d = a.dst[op];
+  const uint64_t n = a.nvec[op];
+  const uint64_t tile = static_cast<uint64_t>(kBlock) * kCopyUnroll;
+  for (uint64_t base = static_cast<uint64_t>(b) * tile; base < n; base += static_cast<uint64_t>(nb) * tile) {
+    uint4 v[kCopyUnroll];
+#pragma unroll
+    for (int u = 0; u < kCopyUnroll; ++u) {  // all (remote) loads in flight before the stores
+      const uint64_t i = base + static_cast<uint64_t>(u) * kBlock + threadIdx.x;
+      if (i < n) v[u] = s[i];
+    }
+#pragma unroll
+    for (int u = 0; u < kCopyUnroll; ++u) {
+      const uint64_t i = base + static_cast<uint64_t>(u) * kBlock + threadIdx.x;
+      if (i < n) d[i] = v[u];
+    }
+  }
+  if (b == 0 && threadIdx.x < a.tail[op]) {
+    const uint8_t* st = reinterpret_cast<const uint8_t*>(s + n);
+    uint8_t* dt = reinterpret_cast<uint8_t*>(d + n);
+    dt[threadIdx.x] = st[threadIdx.x];
+  }
+}
+
+}  // namespace
+
+void launch_multi_copy(const CopyOp* ops, int nops, hipStream_t stream, int max_blocks) {
+  for (int first = 0; first < nops; first += kMaxCopyOps) {
+    const int cnt = std::min(kMaxCopyOps, nops - first);
+    CopyArgs a{};
+    a.nops = cnt;
+    uint64_t need[kMaxCopyOps] = {0};
+    uint64_t total_need = 0;
+    const uint64_t tile = static_cast<uint64_t>(kBlock) * kCopyUnroll;
+    for (int i = 0; i < cnt; ++i) {
+      const CopyOp& o = ops[first + i];
+      P2P_CHECK(reinterpret_cast<uintptr_t>(o.src) % 16 == 0 && reinterpret_cast<uintptr_t>(o.dst) % 16 == 0,
+                "multi_copy: 16-byte aligned buffers required");
+      a.src[i] = static_cast<const uint4*>(o.src);
+      a.dst[i] = static_cast<uint4*>(o.dst);
+      a.nvec[i] = o.bytes / 16;
+      a.tail[i] = static_cast<uint32_t>(o.bytes - a.nvec[i] * 16);
+      need[i] = std::max<uint64_t>(1, (a.nvec[i] + tile - 1) / tile);
+      total_need += need[i];
+    }
+    const uint64_t cap = max_blocks > 0 ? static_cast<uint64_t>(max_blocks) : static_cast<uint64_t>(cu_count()) * 8;
+    uint32_t acc = 0;
+    for (int i = 0; i < cnt; ++i) {
+      a.block_begin[i] = acc;
+      uint64_t share = total_need <= cap ? need[i] : std::max<uint64_t>(1, need[i] * cap / total_need);
+      acc += static_cast<uint32_t>(std::min(share, need[i]));
+    }
+    a.block_begin[cnt] = acc;
+    multi_copy_kernel<<<acc, kBlock, 0, stream>>>(a);
+    HIP_OK(hipGetLastError());
+  }
 }
 
 }  // namespace dev

@@ -33,7 +33,8 @@ struct VerifyAccum {
   unsigned long long first_bad;
 };
 
-enum class VerifyImpl : int { Auto = 0, Register = 1, Lds = 2 };
+enum class VerifyImpl : int { Auto = 0, Register = 1, Lds = 2, Register8 = 3 };
+enum class FillImpl : int { Auto = 0, Plain = 1, Nontemporal = 2 };
 
 // Geometry chosen for a launch (exposed for tests / profiling scripts).
 struct LaunchGeom {
@@ -45,7 +46,7 @@ struct LaunchGeom {
 LaunchGeom fill_geometry(size_t bytes);
 LaunchGeom verify_geometry(size_t bytes, VerifyImpl impl);
 
-void launch_fill(void* p, size_t bytes, uint64_t seed, hipStream_t stream);
+void launch_fill(void* p, size_t bytes, uint64_t seed, hipStream_t stream, FillImpl impl = FillImpl::Auto);
 void launch_verify_reset(VerifyAccum* acc, hipStream_t stream);
 // check_prng=false only sums the words (checksum of an arbitrary buffer).
 void launch_verify(const void* p, size_t bytes, uint64_t seed, VerifyAccum* acc, VerifyImpl impl, bool check_prng,
@@ -53,6 +54,20 @@ void launch_verify(const void* p, size_t bytes, uint64_t seed, VerifyAccum* acc,
 
 // Device attributes cached per device (CU count drives grid sizing).
 int cu_count();
+
+// ---- multi-source copy (IPC transport data plane) ----
+// One launch moves every receive of a group: op i copies ops[i].bytes from
+// src (typically a peer GPU's buffer mapped through hipIpcOpenMemHandle, so
+// the loads travel over xGMI) to dst.  Workgroups are split across ops in
+// proportion to their size; each lane keeps UNROLL x 16 B loads in flight to
+// cover the remote-read latency.
+struct CopyOp {
+  const void* src;
+  void* dst;
+  size_t bytes;
+};
+constexpr int kMaxCopyOps = 16;
+void launch_multi_copy(const CopyOp* ops, int nops, hipStream_t stream, int max_blocks = 0);
 
 }  // namespace dev
 }  // namespace p2p

@@ -43,12 +43,17 @@ class Session {
     TransportOptions opt;
     opt.device = device;
     opt.timeout_s = timeout_s;
-    if (transport == "rccl")
+    // "ipc" or "ipc:sdma" / "ipc:kernel"
+    std::string kind = transport.substr(0, transport.find(':'));
+    if (kind == "ipc" && transport.size() > 4) opt.ipc_engine = transport.substr(4);
+    if (kind == "rccl")
       t_ = make_rccl_transport(*boot_, opt);
-    else if (transport == "host")
+    else if (kind == "ipc")
+      t_ = make_ipc_transport(*boot_, opt);
+    else if (kind == "host")
       t_ = make_host_transport(*boot_, opt);
     else
-      P2P_FATAL("transport must be 'rccl' or 'host'");
+      P2P_FATAL("transport must be 'rccl', 'ipc[:kernel|:sdma]' or 'host'");
   }
 
   int rank() const { return boot_->rank(); }
@@ -100,10 +105,10 @@ class Session {
 class PyStepDriver {
  public:
   PyStepDriver(std::shared_ptr<Session> s, const std::string& mode, const std::string& dir, size_t bytes, int msgs,
-               bool verify)
+               bool verify, bool batch, bool graph)
       : session_(std::move(s)),
         d_(session_->t(), session_->boot(), make_schedule(parse_mode(mode), parse_direction(dir), session_->world()),
-           bytes, msgs, verify) {}
+           bytes, msgs, verify, 0, StepOptions{batch, graph}) {}
   StepDriver& d() { return d_; }
 
  private:
@@ -196,9 +201,10 @@ PYBIND11_MODULE(_p2pcore, m) {
            py::call_guard<py::gil_scoped_release>());
 
   py::class_<PyStepDriver>(m, "StepDriver")
-      .def(py::init<std::shared_ptr<Session>, const std::string&, const std::string&, size_t, int, bool>(),
+      .def(py::init<std::shared_ptr<Session>, const std::string&, const std::string&, size_t, int, bool, bool, bool>(),
            py::arg("session"), py::arg("mode") = "tournament", py::arg("dir") = "bi", py::arg("bytes") = 32u << 20,
-           py::arg("msgs") = 8, py::arg("verify") = false, py::call_guard<py::gil_scoped_release>())
+           py::arg("msgs") = 8, py::arg("verify") = false, py::arg("batch") = false, py::arg("graph") = false,
+           py::call_guard<py::gil_scoped_release>())
       .def("connect", [](PyStepDriver& s) { s.d().connect(); }, py::call_guard<py::gil_scoped_release>())
       .def("step", [](PyStepDriver& s, long k) { s.d().step(k); }, py::call_guard<py::gil_scoped_release>())
       .def("run_steps", [](PyStepDriver& s, long first, long count) {
@@ -219,9 +225,10 @@ PYBIND11_MODULE(_p2pcore, m) {
       });
 
   // ---- kernels on raw pointers ----
-  m.def("fill", [](uintptr_t ptr, size_t bytes, uint64_t seed, uintptr_t stream) {
-        dev::launch_fill(reinterpret_cast<void*>(ptr), bytes, seed, as_stream(stream));
-      }, py::arg("ptr"), py::arg("bytes"), py::arg("seed"), py::arg("stream") = 0);
+  m.def("fill", [](uintptr_t ptr, size_t bytes, uint64_t seed, uintptr_t stream, int impl) {
+        dev::launch_fill(reinterpret_cast<void*>(ptr), bytes, seed, as_stream(stream), static_cast<dev::FillImpl>(impl));
+      }, py::arg("ptr"), py::arg("bytes"), py::arg("seed"), py::arg("stream") = 0, py::arg("impl") = 0,
+      "impl: 0 auto, 1 plain stores, 2 non-temporal stores");
   m.def("verify", &device_verify, py::arg("ptr"), py::arg("bytes"), py::arg("seed"), py::arg("impl") = 0,
         py::arg("check") = true, py::arg("stream") = 0,
         "Returns (mismatching words, checksum, first bad byte offset or 2**64-1).");

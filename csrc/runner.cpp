@@ -26,9 +26,11 @@ Timing parse_timing(const std::string& s) {
 Buffers::Buffers(Transport& t, size_t max_bytes, int recv_slots) : t_(t), cap_(std::max<size_t>(max_bytes, 16)) {
   send_ = t_.alloc(cap_);
   for (int i = 0; i < recv_slots; ++i) recv_.push_back(t_.alloc(cap_));
+  t_.register_buffers(send_, recv_, cap_);
 }
 
 Buffers::~Buffers() {
+  t_.unregister_buffers(send_);
   for (void* p : recv_) t_.release(p);
   if (send_) t_.release(send_);
 }
@@ -349,9 +351,11 @@ std::vector<LatencyResult> run_latency(Transport& t, Bootstrap& boot, size_t byt
 
 // ---------------------------------------------------------- StepDriver ----
 
-StepDriver::StepDriver(Transport& t, Bootstrap& boot, Schedule sched, size_t bytes, int msgs, bool verify, uint64_t salt)
-    : t_(t), boot_(boot), sched_(std::move(sched)), bytes_(bytes), msgs_(msgs), verify_(verify), salt_(salt),
+StepDriver::StepDriver(Transport& t, Bootstrap& boot, Schedule sched, size_t bytes, int msgs, bool verify, uint64_t salt,
+                       StepOptions opt)
+    : t_(t), boot_(boot), sched_(std::move(sched)), bytes_(bytes), msgs_(msgs), verify_(verify), salt_(salt), opt_(opt),
       bufs_(t, bytes, std::max(1, sched_.max_recv_slots())) {
+  if (opt_.graph && !t_.supports_graphs()) opt_.graph = false;
   std::string bad = validate(sched_);
   P2P_CHECK(bad.empty(), "invalid schedule: " + bad);
   P2P_CHECK(!sched_.phases.empty(), "empty schedule");
@@ -370,15 +374,48 @@ void StepDriver::connect() {
   if (verify_)
     for (int i = 0; i < bufs_.slots(); ++i) t_.zero(bufs_.recv_buf(i), bytes_);
   t_.sync();
+  // Graph capture only records launches (no peer interaction), so it must
+  // follow the warm-up that established every lazy connection.
+  if (opt_.graph && graphs_.empty()) {
+    for (const Phase& p : sched_.phases) {
+      if (!p.participates(t_.rank())) {
+        graphs_.push_back(-1);
+        continue;
+      }
+      t_.capture_begin();
+      post_step_ops(p);
+      graphs_.push_back(t_.capture_end());
+    }
+    boot_.barrier();
+  }
+}
+
+void StepDriver::post_step_ops(const Phase& p) {
+  if (!opt_.batch) {
+    for (int m = 0; m < msgs_; ++m) post_phase_iteration(t_, p, bytes_, bufs_);
+    return;
+  }
+  // One group: every message of the step, fused into one launch by RCCL.
+  const RankOps& ops = p.ranks[static_cast<size_t>(t_.rank())];
+  t_.group_begin();
+  for (int m = 0; m < msgs_; ++m) {
+    for (int peer : ops.send_to) t_.send(bufs_.send_buf(), bytes_, peer);
+    for (size_t i = 0; i < ops.recv_from.size(); ++i) t_.recv(bufs_.recv_buf(static_cast<int>(i)), bytes_, ops.recv_from[i]);
+  }
+  t_.group_end();
 }
 
 void StepDriver::step(long k) {
-  const Phase& p = sched_.phases[static_cast<size_t>(k % phases())];
+  const size_t pi = static_cast<size_t>(k % phases());
+  const Phase& p = sched_.phases[pi];
   if (!p.participates(t_.rank())) {
     marks_.emplace_back(-1, -1);
   } else {
     int a = t_.mark();
-    for (int m = 0; m < msgs_; ++m) post_phase_iteration(t_, p, bytes_, bufs_);
+    if (opt_.graph && pi < graphs_.size() && graphs_[pi] >= 0)
+      t_.graph_launch(graphs_[pi]);
+    else
+      post_step_ops(p);
     int b = t_.mark();
     marks_.emplace_back(a, b);
   }

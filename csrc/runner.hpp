@@ -124,9 +124,15 @@ std::vector<LatencyResult> run_latency(Transport& t, Bootstrap& boot, size_t byt
 // Step k posts `msgs` iterations of phase (k mod phases) with a timestamp
 // around them; nothing blocks until sync().  Per-step durations are read
 // after sync().
+struct StepOptions {
+  bool batch = false;  // all msgs of a step in ONE group (one launch) instead of one group per message
+  bool graph = false;  // capture each phase's step into a hipGraph (transports that support it)
+};
+
 class StepDriver {
  public:
-  StepDriver(Transport& t, Bootstrap& boot, Schedule sched, size_t bytes, int msgs, bool verify, uint64_t salt = 0);
+  StepDriver(Transport& t, Bootstrap& boot, Schedule sched, size_t bytes, int msgs, bool verify, uint64_t salt = 0,
+             StepOptions opt = StepOptions());
   ~StepDriver();
   void connect();               // warm every phase once (collective, blocking)
   void step(long k);            // enqueue step k
@@ -147,9 +153,13 @@ class StepDriver {
   int msgs_;
   bool verify_;
   uint64_t salt_;
+  StepOptions opt_;
   Buffers bufs_;
   std::vector<std::pair<int, int>> marks_;
+  std::vector<int> graphs_;  // per phase, when opt_.graph
   long last_step_ = -1;
+
+  void post_step_ops(const Phase& p);
 };
 
 }  // namespace p2p

@@ -16,6 +16,7 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "prng.hpp"
 
@@ -56,6 +57,23 @@ class Transport {
   // Wait for all posted work (bounded by the transport's watchdog timeout).
   virtual void sync() = 0;
 
+  // Collective: called by every rank, in the same order, right after it
+  // allocated a buffer set (Buffers' constructor / destructor).  One-sided
+  // transports map the peers' send buffers here and route a receive into one
+  // of `recvs` to the same set's send buffer on the peer; two-sided ones
+  // (RCCL, host) ignore it.
+  virtual void register_buffers(void* /*send*/, const std::vector<void*>& /*recvs*/, size_t /*bytes*/) {}
+  virtual void unregister_buffers(void* /*send*/) {}
+
+  // ---- graphs: record posted work once, replay it with one launch ----
+  // Between capture_begin() and capture_end() nothing executes; the returned
+  // handle replays the recorded groups with graph_launch().  Transports that
+  // cannot capture return false from supports_graphs().
+  virtual bool supports_graphs() const { return false; }
+  virtual void capture_begin() {}
+  virtual int capture_end() { return -1; }
+  virtual void graph_launch(int /*handle*/) {}
+
   // ---- health ----
   // Non-empty when the transport saw an asynchronous error (e.g. a peer died).
   virtual std::string async_error() { return ""; }
@@ -66,11 +84,17 @@ struct TransportOptions {
   double timeout_s = 300.0;        // watchdog for init / sync
   bool nonblocking_init = true;    // RCCL: ncclCommInitRankConfig(blocking=0) + polling
   int verify_impl = 0;             // 0 = auto, 1 = register-staged, 2 = LDS-staged (global_load_lds)
+  std::string ipc_engine = "kernel";  // IPC transport copy engine: kernel (gfx950 pull kernel) | sdma
 };
 
 // HIP + RCCL on the local MI355X.  Defined in transport_rccl.cpp (hipcc).
 std::unique_ptr<Transport> make_rccl_transport(Bootstrap& boot, const TransportOptions& opt);
 bool rccl_transport_available();
+
+// One-sided pulls through hipIpc-mapped peer send buffers, moved by the
+// gfx950 multi-copy kernel (or the SDMA engines).  Defined in
+// transport_ipc.cpp.  Intra-node only; several ranks may share one GPU.
+std::unique_ptr<Transport> make_ipc_transport(Bootstrap& boot, const TransportOptions& opt);
 
 // Host memory over TCP sockets.  Defined in transport_host.cpp.
 std::unique_ptr<Transport> make_host_transport(Bootstrap& boot, const TransportOptions& opt);

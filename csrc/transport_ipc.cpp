@@ -1,0 +1,305 @@
+// IpcTransport: one-sided point-to-point over xGMI without RCCL.
+//
+// Every rank exports its send buffer with hipIpcGetMemHandle when the
+// buffers are created (register_send_buffer, collective); every peer maps it
+// with hipIpcOpenMemHandle.  A receive is then a *pull*: the receiver's GPU
+// reads the sender's send buffer directly over the xGMI link into its own
+// receive buffer.  A send moves nothing (the receiver does the work), which
+// is valid for this benchmark because a phase's payload is written once
+// (fill + sync + barrier) before any timed receive reads it.
+//
+// Data movers (TransportOptions::ipc_engine):
+//   kernel — one launch of the gfx950 multi-source copy kernel per group
+//            (kernels.hip: all receives of the group in one grid, workgroups
+//            split by size, 4 x 16 B remote loads in flight per lane);
+//   sdma   — hipMemcpyAsync per receive, forked onto one stream per receive
+//            slot so the copies of an all-pairs group run concurrently.
+//
+// Why it exists: it is the hand-written CDNA4 data plane to compare RCCL's
+// ncclSend/ncclRecv against on the same links, and, because IPC mappings
+// also work between processes on ONE GPU, it lets the complete multi-rank GPU
+// engine (events, kernels, verification, every schedule) run on a single
+// MI355X, where RCCL refuses duplicate-GPU ranks.
+#include <hip/hip_runtime.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "bootstrap.hpp"
+#include "common.hpp"
+#include "kernels.hpp"
+#include "transport.hpp"
+
+namespace p2p {
+namespace {
+
+#define HIPCHECK(cmd)                                                                          \
+  do {                                                                                         \
+    hipError_t e_ = (cmd);                                                                     \
+    if (e_ != hipSuccess) P2P_FATAL(strfmt("HIP error in %s: %s", #cmd, hipGetErrorString(e_))); \
+  } while (0)
+
+struct Export {
+  hipIpcMemHandle_t handle;
+  uint64_t bytes;
+  uint64_t host_hash;
+  int32_t device;
+  int32_t pid;
+};
+
+class IpcTransport final : public Transport {
+ public:
+  IpcTransport(Bootstrap& boot, const TransportOptions& opt)
+      : boot_(boot), rank_(boot.rank()), n_(boot.size()), timeout_(opt.timeout_s), engine_(opt.ipc_engine) {
+    P2P_CHECK(engine_ == "kernel" || engine_ == "sdma", "ipc engine must be 'kernel' or 'sdma'");
+    verify_impl_ = static_cast<dev::VerifyImpl>(opt.verify_impl);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) P2P_FATAL("ipc transport: no HIP device visible");
+    device_ = opt.device >= 0 ? opt.device : 0;
+    P2P_CHECK(device_ < ndev, strfmt("rank %d wants GPU %d but only %d are visible", rank_, device_, ndev));
+    HIPCHECK(hipSetDevice(device_));
+    HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    HIPCHECK(hipMalloc(&acc_, sizeof(dev::VerifyAccum)));
+    HIPCHECK(hipHostMalloc(&acc_host_, sizeof(dev::VerifyAccum), hipHostMallocDefault));
+    hipDeviceProp_t prop;
+    HIPCHECK(hipGetDeviceProperties(&prop, device_));
+    desc_ = strfmt("hip:%d %s (%s, %d CUs) ipc-%s", device_, prop.name, prop.gcnArchName, prop.multiProcessorCount,
+                   engine_.c_str());
+  }
+
+  ~IpcTransport() override {
+    (void)hipStreamSynchronize(stream_);
+    for (auto& r : regs_) close_registration(r);
+    regs_.clear();
+    for (auto ex : execs_) (void)hipGraphExecDestroy(ex);
+    for (auto s : side_) (void)hipStreamDestroy(s);
+    for (auto e : side_done_) (void)hipEventDestroy(e);
+    if (fork_) (void)hipEventDestroy(fork_);
+    for (auto ev : events_) (void)hipEventDestroy(ev);
+    if (acc_) (void)hipFree(acc_);
+    if (acc_host_) (void)hipHostFree(acc_host_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+  }
+
+  std::string name() const override { return "ipc"; }
+  int rank() const override { return rank_; }
+  int nranks() const override { return n_; }
+  std::string device_desc() const override { return desc_; }
+
+  void* alloc(size_t bytes) override {
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, std::max<size_t>(bytes, 256));
+    if (e != hipSuccess) P2P_FATAL(strfmt("hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e)));
+    return p;
+  }
+  void release(void* p) override {
+    if (p) HIPCHECK(hipFree(p));
+  }
+  void fill(void* p, size_t bytes, uint64_t seed) override { dev::launch_fill(p, bytes, seed, stream_); }
+  void zero(void* p, size_t bytes) override { HIPCHECK(hipMemsetAsync(p, 0, bytes, stream_)); }
+
+  VerifyResult verify(const void* p, size_t bytes, uint64_t seed) override {
+    dev::launch_verify_reset(acc_, stream_);
+    dev::launch_verify(p, bytes, seed, acc_, verify_impl_, true, stream_);
+    HIPCHECK(hipMemcpyAsync(acc_host_, acc_, sizeof(dev::VerifyAccum), hipMemcpyDeviceToHost, stream_));
+    sync();
+    VerifyResult r;
+    r.mismatches = acc_host_->mismatches;
+    r.checksum = acc_host_->checksum;
+    r.first_bad = acc_host_->first_bad;
+    return r;
+  }
+
+  // Buffer sets are registered collectively in the same order on every rank,
+  // so "the same set" on a peer is the one with the same position.  A receive
+  // into one of a set's receive slots pulls from that set's send buffer on the
+  // peer.
+  void register_buffers(void* send, const std::vector<void*>& recvs, size_t bytes) override {
+    Export me{};
+    HIPCHECK(hipIpcGetMemHandle(&me.handle, send));
+    me.bytes = bytes;
+    me.host_hash = host_hash(real_hostname());
+    me.device = device_;
+    me.pid = static_cast<int32_t>(getpid());
+    auto all = boot_.allgather_value(me);
+    Registration reg;
+    reg.send = send;
+    reg.bytes = bytes;
+    reg.recvs = recvs;
+    reg.peer_send.assign(static_cast<size_t>(n_), nullptr);
+    for (int r = 0; r < n_; ++r) {
+      if (r == rank_) {
+        reg.peer_send[static_cast<size_t>(r)] = send;
+        continue;
+      }
+      P2P_CHECK(all[static_cast<size_t>(r)].host_hash == me.host_hash,
+                strfmt("ipc transport is intra-node only: rank %d is on another host", r));
+      P2P_CHECK(all[static_cast<size_t>(r)].bytes == bytes, "ipc transport: buffer sets differ in size across ranks");
+      void* mapped = nullptr;
+      HIPCHECK(hipIpcOpenMemHandle(&mapped, all[static_cast<size_t>(r)].handle, hipIpcMemLazyEnablePeerAccess));
+      reg.peer_send[static_cast<size_t>(r)] = mapped;
+    }
+    regs_.push_back(std::move(reg));
+    boot_.barrier();
+  }
+
+  void unregister_buffers(void* send) override {
+    auto it = std::find_if(regs_.begin(), regs_.end(), [&](const Registration& r) { return r.send == send; });
+    if (it == regs_.end()) return;
+    sync();
+    // Every rank stops pulling before any rank frees the pages it exported.
+    boot_.barrier();
+    close_registration(*it);
+    regs_.erase(it);
+  }
+
+  void group_begin() override {
+    P2P_CHECK(!in_group_, "nested group");
+    in_group_ = true;
+    ops_.clear();
+  }
+  void send(const void* p, size_t bytes, int peer) override {
+    P2P_CHECK(peer >= 0 && peer < n_, "bad peer");
+    bool ok = std::any_of(regs_.begin(), regs_.end(), [&](const Registration& r) { return r.send == p && bytes <= r.bytes; });
+    P2P_CHECK(ok, "ipc transport sends only from a registered send buffer (one-sided pull)");
+    // Nothing to move: the receiver pulls.
+  }
+  void recv(void* p, size_t bytes, int peer) override {
+    P2P_CHECK(peer >= 0 && peer < n_, "bad peer");
+    const Registration* reg = nullptr;
+    for (const auto& r : regs_)
+      if (std::find(r.recvs.begin(), r.recvs.end(), p) != r.recvs.end()) reg = &r;
+    P2P_CHECK(reg && bytes <= reg->bytes, "ipc transport receives only into a registered receive slot");
+    ops_.push_back({reg->peer_send[static_cast<size_t>(peer)], p, bytes});
+    if (!in_group_) flush();
+  }
+  void group_end() override {
+    P2P_CHECK(in_group_, "group_end without group_begin");
+    in_group_ = false;
+    flush();
+  }
+
+  int mark() override {
+    if (next_event_ == static_cast<int>(events_.size())) {
+      hipEvent_t ev;
+      HIPCHECK(hipEventCreate(&ev));
+      events_.push_back(ev);
+    }
+    HIPCHECK(hipEventRecord(events_[static_cast<size_t>(next_event_)], stream_));
+    return next_event_++;
+  }
+  double elapsed_ms(int a, int b) override {
+    float ms = 0;
+    HIPCHECK(hipEventElapsedTime(&ms, events_.at(static_cast<size_t>(a)), events_.at(static_cast<size_t>(b))));
+    return ms;
+  }
+  void clear_marks() override { next_event_ = 0; }
+
+  bool supports_graphs() const override { return engine_ == "kernel"; }
+  void capture_begin() override { HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal)); }
+  int capture_end() override {
+    hipGraph_t g = nullptr;
+    HIPCHECK(hipStreamEndCapture(stream_, &g));
+    hipGraphExec_t ex = nullptr;
+    HIPCHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    HIPCHECK(hipGraphDestroy(g));
+    execs_.push_back(ex);
+    return static_cast<int>(execs_.size()) - 1;
+  }
+  void graph_launch(int h) override { HIPCHECK(hipGraphLaunch(execs_.at(static_cast<size_t>(h)), stream_)); }
+
+  void sync() override {
+    double deadline = now_seconds() + timeout_;
+    double t0 = now_seconds();
+    for (long it = 0;; ++it) {
+      hipError_t e = hipStreamQuery(stream_);
+      if (e == hipSuccess) return;
+      if (e != hipErrorNotReady) P2P_FATAL(strfmt("stream error: %s", hipGetErrorString(e)));
+      if ((it & 255) == 0) {
+        double now = now_seconds();
+        if (now > deadline) P2P_FATAL(strfmt("rank %d: ipc stream did not finish within %.0f s", rank_, timeout_));
+        if (now - t0 > 2e-3) std::this_thread::sleep_for(std::chrono::microseconds(50));
+      }
+    }
+  }
+
+ private:
+  struct Registration {
+    void* send = nullptr;
+    size_t bytes = 0;
+    std::vector<void*> recvs;
+    std::vector<void*> peer_send;  // mapped send buffer of every rank (own one for self)
+  };
+
+  void close_registration(Registration& reg) {
+    for (int r = 0; r < n_; ++r) {
+      void*& m = reg.peer_send[static_cast<size_t>(r)];
+      if (m && r != rank_) (void)hipIpcCloseMemHandle(m);
+      m = nullptr;
+    }
+  }
+
+  void flush() {
+    if (ops_.empty()) return;
+    if (engine_ == "kernel") {
+      dev::launch_multi_copy(ops_.data(), static_cast<int>(ops_.size()), stream_);
+    } else if (ops_.size() == 1) {
+      HIPCHECK(hipMemcpyAsync(ops_[0].dst, ops_[0].src, ops_[0].bytes, hipMemcpyDeviceToDevice, stream_));
+    } else {
+      // Fork: every receive on its own stream so the copy engines overlap,
+      // then join back into the main stream.
+      ensure_side_streams(ops_.size());
+      HIPCHECK(hipEventRecord(fork_, stream_));
+      for (size_t i = 0; i < ops_.size(); ++i) {
+        HIPCHECK(hipStreamWaitEvent(side_[i], fork_, 0));
+        HIPCHECK(hipMemcpyAsync(ops_[i].dst, ops_[i].src, ops_[i].bytes, hipMemcpyDeviceToDevice, side_[i]));
+        HIPCHECK(hipEventRecord(side_done_[i], side_[i]));
+        HIPCHECK(hipStreamWaitEvent(stream_, side_done_[i], 0));
+      }
+    }
+    ops_.clear();
+  }
+
+  void ensure_side_streams(size_t n) {
+    if (!fork_) HIPCHECK(hipEventCreateWithFlags(&fork_, hipEventDisableTiming));
+    while (side_.size() < n) {
+      hipStream_t s;
+      HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      side_.push_back(s);
+      hipEvent_t e;
+      HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      side_done_.push_back(e);
+    }
+  }
+
+  Bootstrap& boot_;
+  int rank_, n_;
+  double timeout_;
+  std::string engine_;
+  int device_ = 0;
+  hipStream_t stream_ = nullptr;
+  std::vector<hipEvent_t> events_;
+  int next_event_ = 0;
+  std::vector<hipGraphExec_t> execs_;
+  std::vector<hipStream_t> side_;
+  std::vector<hipEvent_t> side_done_;
+  hipEvent_t fork_ = nullptr;
+  dev::VerifyAccum* acc_ = nullptr;
+  dev::VerifyAccum* acc_host_ = nullptr;
+  dev::VerifyImpl verify_impl_ = dev::VerifyImpl::Auto;
+  std::string desc_;
+  std::vector<Registration> regs_;
+  bool in_group_ = false;
+  std::vector<dev::CopyOp> ops_;
+};
+
+}  // namespace
+
+std::unique_ptr<Transport> make_ipc_transport(Bootstrap& boot, const TransportOptions& opt) {
+  return std::make_unique<IpcTransport>(boot, opt);
+}
+
+}  // namespace p2p

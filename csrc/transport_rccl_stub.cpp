@@ -1,5 +1,6 @@
 // Host-only builds (CPU test binaries) link this instead of
-// transport_rccl.cpp + kernels.hip: the RCCL transport is unavailable.
+// transport_rccl.cpp + transport_ipc.cpp + kernels.hip: the GPU transports
+// are unavailable there.
 #include "common.hpp"
 #include "transport.hpp"
 
@@ -7,6 +8,10 @@ namespace p2p {
 
 std::unique_ptr<Transport> make_rccl_transport(Bootstrap&, const TransportOptions&) {
   P2P_FATAL("this binary was built without HIP/RCCL; use --transport host");
+}
+
+std::unique_ptr<Transport> make_ipc_transport(Bootstrap&, const TransportOptions&) {
+  P2P_FATAL("this binary was built without HIP; use --transport host");
 }
 
 bool rccl_transport_available() { return false; }

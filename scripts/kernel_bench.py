@@ -46,26 +46,28 @@ def main():
     for sz in [nat.parse_size(s) for s in a.sizes.split(",")]:
         buf = torch.empty(sz, dtype=torch.uint8, device="cuda")
         ptr = buf.data_ptr()
-        t_fill = timed(lambda: nat.fill(ptr, sz, 7, stream), a.reps)
+        t_fill = timed(lambda: nat.fill(ptr, sz, 7, stream, 1), a.reps)
+        t_fill_nt = timed(lambda: nat.fill(ptr, sz, 7, stream, 2), a.reps)
         res = {}
-        for name, impl, check in [("verify_reg", 1, True), ("verify_lds", 2, True), ("checksum_reg", 1, False),
-                                  ("checksum_lds", 2, False)]:
+        for name, impl, check in [("verify_reg", 1, True), ("verify_reg8", 3, True), ("verify_lds", 2, True),
+                                  ("checksum_reg", 1, False), ("checksum_lds", 2, False)]:
             # verify() syncs (result readback); time with a host-side loop of
             # launches through the same path and subtract nothing: the sync is
             # part of what a caller pays.
             t = timed(lambda: nat.verify(ptr, sz, 7, impl, check, stream), a.reps)
             res[name] = t
             assert nat.verify(ptr, sz, 7, impl, True, stream)[0] == 0
-        row = {"bytes": sz, "fill_tbs": sz / t_fill / 1e12}
+        row = {"bytes": sz, "fill_tbs": sz / t_fill / 1e12, "fill_nt_tbs": sz / t_fill_nt / 1e12}
         for k, t in res.items():
             row[k + "_tbs"] = sz / t / 1e12
         row["fill_geom"] = nat.fill_geometry(sz)
         row["verify_reg_geom"] = nat.verify_geometry(sz, 1)
         row["verify_lds_geom"] = nat.verify_geometry(sz, 2)
         rows.append(row)
-        print("%6s  fill %.2f  verify reg %.2f / lds %.2f  checksum reg %.2f / lds %.2f TB/s  (HBM measured roof %.2f)"
-              % (nat.format_size(sz), row["fill_tbs"], row["verify_reg_tbs"], row["verify_lds_tbs"],
-                 row["checksum_reg_tbs"], row["checksum_lds_tbs"], HBM_MEASURED_TBS), flush=True)
+        print("%6s  fill %.2f (nt %.2f)  verify reg %.2f / reg8 %.2f / lds %.2f  checksum reg %.2f / lds %.2f TB/s"
+              "  (HBM measured roof %.2f)"
+              % (nat.format_size(sz), row["fill_tbs"], row["fill_nt_tbs"], row["verify_reg_tbs"], row["verify_reg8_tbs"],
+                 row["verify_lds_tbs"], row["checksum_reg_tbs"], row["checksum_lds_tbs"], HBM_MEASURED_TBS), flush=True)
         del buf
         torch.cuda.empty_cache()
     if a.json:
