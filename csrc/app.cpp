@@ -56,7 +56,10 @@ transport / launch
       --device N         GPU index (default: local rank from block placement)
       --timeout S        watchdog for init / waits, seconds                    [300]
 output
-      --json FILE        JSON lines (one object per run)
+      --json FILE        JSON lines, one object per run, appended + flushed as each run ends
+      --resume           skip the runs already in the --json file (restart a killed sweep)
+      --trace FILE       Chrome/Perfetto trace of every rank's timed phases
+                         (P2P_ROCTX=1 also emits roctx ranges for rocprofv3 --marker-trace)
       --csv FILE         per-flow CSV
       --compat-only      only the reference matrices
       --no-compat        only the extended tables
@@ -175,6 +178,10 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
       cfg->json_path = next();
     } else if (a == "--csv") {
       cfg->csv_path = next();
+    } else if (a == "--trace") {
+      cfg->trace_path = next();
+    } else if (a == "--resume") {
+      cfg->resume = true;
     } else if (a == "--compat-only") {
       cfg->extended = false;
       cfg->compat = true;
@@ -267,9 +274,38 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
 
   AppResult local;
   AppResult& res = result ? *result : local;
+
+  // Checkpoint / resume: every finished run is appended to the JSON-lines
+  // file and flushed at once, so a killed sweep keeps what it measured;
+  // --resume skips the (mode, dir, size) runs already present in that file.
+  std::vector<uint8_t> skip(scheds.size() * cfg.sizes.size(), 0);
+  std::ofstream js;
+  if (root && !cfg.json_path.empty()) {
+    if (cfg.resume) {
+      std::ifstream in(cfg.json_path);
+      std::vector<std::string> done;
+      for (std::string line; std::getline(in, line);) {
+        std::string k = run_key_from_json(line);
+        if (!k.empty()) done.push_back(k);
+      }
+      for (size_t i = 0; i < scheds.size(); ++i)
+        for (size_t j = 0; j < cfg.sizes.size(); ++j)
+          skip[i * cfg.sizes.size() + j] = std::find(done.begin(), done.end(),
+                                                     run_key(scheds[i].mode, scheds[i].dir, cfg.sizes[j])) != done.end();
+    }
+    js.open(cfg.json_path, cfg.resume ? std::ios::app : std::ios::trunc);
+    P2P_CHECK(js.good(), "cannot write " + cfg.json_path);
+  }
+  if (!skip.empty()) boot.bcast(skip.data(), skip.size(), 0);
+
   bool printed_compat = false;
-  for (const auto& s : scheds) {
+  for (size_t sj = 0; sj < scheds.size(); ++sj) {
+    const Schedule& s = scheds[sj];
     for (size_t si = 0; si < cfg.sizes.size(); ++si) {
+      if (skip[sj * cfg.sizes.size() + si]) {
+        if (root) P2P_INFO("resume: skipping %s", run_key(s.mode, s.dir, cfg.sizes[si]).c_str());
+        continue;
+      }
       RunRecord rec;
       rec.mode = s.mode;
       rec.dir = s.dir;
@@ -290,6 +326,10 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
         if (compat) cp.on_phase(r);
       });
       for (const auto& ph : rec.phases) res.mismatches += ph.total_mismatches;
+      if (js.is_open()) {
+        js << run_to_json(rec, n) << "\n";
+        js.flush();
+      }
       res.runs.push_back(std::move(rec));
     }
   }
@@ -309,11 +349,11 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
       for (const auto& rec : res.runs) print_extended(out, rec, n);
       print_latency(out, res.latency, n);
     }
-    if (!cfg.json_path.empty()) {
-      std::ofstream js(cfg.json_path);
-      P2P_CHECK(js.good(), "cannot write " + cfg.json_path);
-      for (const auto& rec : res.runs) js << run_to_json(rec, n) << "\n";
-      if (!res.latency.empty()) js << latency_to_json(res.latency, n) << "\n";
+    if (js.is_open() && !res.latency.empty()) js << latency_to_json(res.latency, n) << "\n";
+    if (!cfg.trace_path.empty()) {
+      std::ofstream tr(cfg.trace_path);
+      P2P_CHECK(tr.good(), "cannot write " + cfg.trace_path);
+      tr << chrome_trace(res.runs, n) << "\n";
     }
     if (!cfg.csv_path.empty()) {
       std::ofstream cs(cfg.csv_path);

@@ -37,6 +37,8 @@ struct AppConfig {
   int device = -1;
   std::string json_path;
   std::string csv_path;
+  std::string trace_path;
+  bool resume = false;
   bool compat = true;      // reference matrices for pair mode
   bool extended = true;    // GB/s / latency tables after the compat section
   double timeout_s = 300;

@@ -1,5 +1,7 @@
 #include "common.hpp"
 
+#include <dlfcn.h>
+
 #include <chrono>
 #include <cstdarg>
 #include <cstdlib>
@@ -90,6 +92,52 @@ void logf(int level, const char* fmt, ...) {
   std::vfprintf(stderr, fmt, ap);
   std::fprintf(stderr, "\n");
   va_end(ap);
+}
+
+namespace {
+
+struct Roctx {
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+  void (*mark)(const char*) = nullptr;
+  bool enabled = false;
+};
+
+Roctx& roctx() {
+  static Roctx r = [] {
+    Roctx x;
+    const char* e = std::getenv("P2P_ROCTX");
+    if (!e || std::atoi(e) == 0) return x;
+    void* h = nullptr;
+    for (const char* lib : {"libroctx64.so", "libroctx64.so.4", "/opt/rocm/lib/libroctx64.so"}) {
+      h = dlopen(lib, RTLD_NOW | RTLD_GLOBAL);
+      if (h) break;
+    }
+    if (!h) {
+      std::fprintf(stderr, "[p2p] P2P_ROCTX=1 but libroctx64 could not be loaded; tracing disabled\n");
+      return x;
+    }
+    x.push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+    x.pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+    x.mark = reinterpret_cast<void (*)(const char*)>(dlsym(h, "roctxMarkA"));
+    x.enabled = x.push && x.pop;
+    return x;
+  }();
+  return r;
+}
+
+}  // namespace
+
+void trace_push(const char* name) {
+  if (roctx().enabled) roctx().push(name);
+}
+
+void trace_pop() {
+  if (roctx().enabled) roctx().pop();
+}
+
+void trace_mark(const char* name) {
+  if (roctx().enabled && roctx().mark) roctx().mark(name);
 }
 
 double now_seconds() {

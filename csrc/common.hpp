@@ -43,6 +43,19 @@ void logf(int level, const char* fmt, ...) __attribute__((format(printf, 2, 3)))
 
 double now_seconds();  // monotonic (steady_clock), unlike the reference's system_clock
 
+// roctx ranges (visible in rocprofv3 --marker-trace / roctracer timelines).
+// libroctx64 is dlopen'ed on first use and only when P2P_ROCTX=1, so nothing
+// links against it and untraced runs pay nothing.
+void trace_push(const char* name);
+void trace_pop();
+void trace_mark(const char* name);
+
+// RAII helper.
+struct TraceRange {
+  explicit TraceRange(const char* name) { trace_push(name); }
+  ~TraceRange() { trace_pop(); }
+};
+
 }  // namespace p2p
 
 #define P2P_FATAL(msg) ::p2p::fatal(__FILE__, __LINE__, (msg))

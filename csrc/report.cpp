@@ -212,6 +212,61 @@ std::string latency_to_json(const std::vector<LatencyResult>& lat, int n) {
   return o.str();
 }
 
+std::string chrome_trace(const std::vector<RunRecord>& runs, int n) {
+  double t0 = 0;
+  bool have = false;
+  for (const auto& rec : runs)
+    for (const auto& ph : rec.phases)
+      for (double b : ph.host_begin)
+        if (!have || b < t0) {
+          t0 = b;
+          have = true;
+        }
+  std::ostringstream o;
+  o << "{\"displayTimeUnit\":\"ms\",\"traceEvents\":[";
+  bool first = true;
+  for (size_t ri = 0; ri < runs.size(); ++ri) {
+    const RunRecord& rec = runs[ri];
+    std::string run_name = strfmt("%s-%s %s", mode_name(rec.mode), direction_name(rec.dir), format_size(rec.bytes).c_str());
+    o << (first ? "" : ",") << "{\"name\":\"process_name\",\"ph\":\"M\",\"pid\":" << ri
+      << ",\"args\":{\"name\":\"" << json_escape(run_name) << "\"}}";
+    first = false;
+    for (const auto& ph : rec.phases) {
+      for (int r = 0; r < n && r < static_cast<int>(ph.host_begin.size()); ++r) {
+        double b = (ph.host_begin[static_cast<size_t>(r)] - t0) * 1e6;
+        double d = (ph.host_end[static_cast<size_t>(r)] - ph.host_begin[static_cast<size_t>(r)]) * 1e6;
+        o << ",{\"name\":\"" << json_escape(ph.label) << "\",\"ph\":\"X\",\"pid\":" << ri << ",\"tid\":" << r
+          << ",\"ts\":" << num(b) << ",\"dur\":" << num(d) << ",\"args\":{\"gpu_ms\":"
+          << num(ph.rank_seconds.size() > static_cast<size_t>(r) ? ph.rank_seconds[static_cast<size_t>(r)] * 1e3 : 0)
+          << ",\"agg_gbs\":" << num(ph.agg_gbs) << "}}";
+      }
+    }
+  }
+  o << "]}";
+  return o.str();
+}
+
+std::string run_key(Mode m, Direction d, size_t bytes) {
+  return strfmt("%s/%s/%zu", mode_name(m), direction_name(d), bytes);
+}
+
+std::string run_key_from_json(const std::string& line) {
+  auto field = [&](const char* key) -> std::string {
+    std::string k = std::string("\"") + key + "\":";
+    auto p = line.find(k);
+    if (p == std::string::npos) return "";
+    p += k.size();
+    if (line[p] == '"') {
+      auto e = line.find('"', p + 1);
+      return line.substr(p + 1, e - p - 1);
+    }
+    auto e = line.find_first_of(",}", p);
+    return line.substr(p, e - p);
+  };
+  if (field("type") != "run") return "";
+  return field("mode") + "/" + field("dir") + "/" + field("bytes");
+}
+
 std::string csv_header() { return "mode,dir,bytes,iters,timing,phase,src,dst,seconds,gbps,gbs,p50_us,p99_us,mismatches\n"; }
 
 std::string run_to_csv(const RunRecord& rec) {

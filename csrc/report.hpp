@@ -61,6 +61,14 @@ std::string latency_to_json(const std::vector<LatencyResult>& lat, int n);
 std::string csv_header();
 std::string run_to_csv(const RunRecord& rec);
 
+// Chrome / Perfetto trace ("traceEvents" JSON): one complete event per rank
+// per timed phase (host steady clock), pid = run, tid = rank.
+std::string chrome_trace(const std::vector<RunRecord>& runs, int n);
+
+// Resume support: the (mode, dir, bytes) key of a run and of a JSON line.
+std::string run_key(Mode m, Direction d, size_t bytes);
+std::string run_key_from_json(const std::string& line);  // "" if not a run line
+
 // Minimal JSON string escaping.
 std::string json_escape(const std::string& s);
 

@@ -24,6 +24,16 @@ Timing parse_timing(const std::string& s) {
 // ------------------------------------------------------------- Buffers ----
 
 Buffers::Buffers(Transport& t, size_t max_bytes, int recv_slots) : t_(t), cap_(std::max<size_t>(max_bytes, 16)) {
+  // One send buffer + one receive slot per concurrent peer, all sized for the
+  // largest message: check against free HBM up front so a 288 GB sweep fails
+  // with an explanation instead of a hipMalloc error mid-run.
+  size_t free_b = 0, total_b = 0;
+  const double need = static_cast<double>(cap_) * (1.0 + recv_slots);
+  if (t_.mem_info(&free_b, &total_b) && need > 0.98 * static_cast<double>(free_b))
+    P2P_FATAL(strfmt("buffers need %.2f GiB (%d x %s) but only %.2f of %.2f GiB are free on this GPU; use a smaller "
+                     "--size/--sizes maximum or a mode with fewer concurrent peers",
+                     need / (1ull << 30), recv_slots + 1, format_size(cap_).c_str(),
+                     static_cast<double>(free_b) / (1ull << 30), static_cast<double>(total_b) / (1ull << 30)));
   send_ = t_.alloc(cap_);
   for (int i = 0; i < recv_slots; ++i) recv_.push_back(t_.alloc(cap_));
   t_.register_buffers(send_, recv_, cap_);
@@ -151,6 +161,7 @@ PhaseResult run_phase(Transport& t, Bootstrap& boot, const Phase& phase, size_t 
   double my_seconds = 0;
   std::vector<double> iter_samples;
   boot.barrier();
+  TraceRange trace_range(phase.label.c_str());
   const double w0 = now_seconds();
   if (cfg.timing == Timing::Wallclock) {
     // Reference semantics: a host stream-sync after every message
@@ -189,7 +200,8 @@ PhaseResult run_phase(Transport& t, Bootstrap& boot, const Phase& phase, size_t 
     }
     boot.barrier();
   }
-  res.wall_seconds = now_seconds() - w0;
+  const double w1 = now_seconds();
+  res.wall_seconds = w1 - w0;
 
   if (active) maybe_inject_fault(t, bufs, me, phase_index, cfg.bytes);
 
@@ -209,6 +221,13 @@ PhaseResult run_phase(Transport& t, Bootstrap& boot, const Phase& phase, size_t 
   }
 
   res.rank_seconds = boot.allgather_value(my_seconds);
+  const double span[2] = {w0, w1};
+  std::vector<double> spans(static_cast<size_t>(2 * n));
+  boot.allgather(span, spans.data(), sizeof(span));
+  for (int r = 0; r < n; ++r) {
+    res.host_begin.push_back(spans[static_cast<size_t>(2 * r)]);
+    res.host_end.push_back(spans[static_cast<size_t>(2 * r + 1)]);
+  }
   Summary mine = summarize(iter_samples);
   auto summaries = boot.allgather_value(mine);
   auto all_vr = boot.allgather_vector(vr);

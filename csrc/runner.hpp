@@ -66,6 +66,8 @@ struct PhaseResult {
   double bytes_per_iter = 0;    // all flows of the phase
   double agg_gbs = 0;           // bytes_per_iter / seconds_per_iter
   std::vector<double> rank_seconds;  // each rank's own timed duration (0 = not participating)
+  std::vector<double> host_begin;    // each rank's steady-clock time at the start / end of the
+  std::vector<double> host_end;      // timed region (seconds; one clock per host) -> --trace
   std::vector<FlowResult> flows;
   uint64_t total_mismatches = 0;
 };

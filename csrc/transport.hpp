@@ -33,6 +33,8 @@ class Transport {
   virtual std::string device_desc() const { return ""; }
 
   // ---- memory ----
+  // Free / total device memory, when the transport knows it (sizing checks).
+  virtual bool mem_info(size_t* /*free_bytes*/, size_t* /*total_bytes*/) { return false; }
   virtual void* alloc(size_t bytes) = 0;
   virtual void release(void* p) = 0;
   // Stream-ordered fill of `bytes` with the PRNG stream `seed`.

@@ -89,6 +89,7 @@ class IpcTransport final : public Transport {
   int nranks() const override { return n_; }
   std::string device_desc() const override { return desc_; }
 
+  bool mem_info(size_t* free_b, size_t* total_b) override { return hipMemGetInfo(free_b, total_b) == hipSuccess; }
   void* alloc(size_t bytes) override {
     void* p = nullptr;
     hipError_t e = hipMalloc(&p, std::max<size_t>(bytes, 256));

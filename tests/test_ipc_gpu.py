@@ -32,7 +32,7 @@ def test_two_ranks_all_modes(exe, tmp_path, engine):
     m = parse_compat(out.stdout)
     assert m["uni"][0][1] > 0 and m["bi"][1][0] > 0
     runs = [json.loads(l) for l in js.read_text().splitlines() if '"run"' in l]
-    assert len(runs) == 7 * 5
+    assert len(runs) == 7 * 7  # 7 runs (3 modes x 2 dirs + allpairs) x 7 sizes
     assert all(ph["mismatches"] == 0 for r in runs for ph in r["phases"])
 
 
