@@ -82,6 +82,8 @@ def parse_args(argv=None):
     ap.add_argument("--batch", type=int, default=1, help="1: all msgs of a step in one ncclGroup (one launch)")
     ap.add_argument("--graph", type=int, default=0, help="1: replay each step as a captured hipGraph")
     ap.add_argument("--json-out", default=None, help="also write the result line to this file")
+    ap.add_argument("--ref-iters", type=int, default=32,
+                    help="iterations per cell of the reference-methodology comparison (0 = skip)")
     return ap.parse_args(argv)
 
 
@@ -166,6 +168,18 @@ def main(argv=None) -> int:
     p50s = [p["one_way_us"]["p50"] for p in lat["pairs"]]
     p50 = statistics.median(p50s) if p50s else None
 
+    # The reference's own methodology on the same communicator, for comparison
+    # (serial ordered pairs, host clock, one stream sync per message,
+    # p2p_matrix.cc:141-186), at the same message size.  Untimed by the
+    # driver's bracket; skipped on one GPU where the reference measures nothing.
+    ref = None
+    if n > 1 and args.ref_iters > 0:
+        r = json.loads(sess.run(mode="pair", dir="uni", bytes=size, iters=args.ref_iters, warmup=0,
+                                timing="wallclock", verify=False, warm=False))
+        ref = {"cell_gbs_min": round(r["gbs_min"], 3), "cell_gbs_mean": round(r["gbs_mean"], 3),
+               "iters": args.ref_iters, "size": size,
+               "method": "reference semantics: serial ordered pairs, wall clock, stream sync per message"}
+
     step_ms_med = statistics.median(my_ms) if my_ms else 0.0
     result = {
         "metric": METRIC,
@@ -198,6 +212,7 @@ def main(argv=None) -> int:
         "verify_mismatches": mismatches,
         "transport": sess.transport,
         "posting": {"batch": bool(args.batch), "graph": bool(args.graph)},
+        "reference_semantics": ref,
     }
     if env.rank == 0:
         log("bench: GB/s matrix (row=src, col=dst), median over steps:")

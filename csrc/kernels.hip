@@ -1,15 +1,21 @@
-// gfx950 (MI355X, CDNA4) buffer kernels: fill / verify / reduce.
-// See kernels.hpp for the contract.  Design notes (numbers from
-// /opt/skills/guides/MI355X_MICROARCH.md):
-//   * Pure streaming, so the target is the HBM3E roofline (~6.3 TB/s
-//     measured).  Every access is 16 B/lane so one wave instruction moves a
-//     contiguous 1 KiB (Guideline 13).
-//   * Grids are sized to the chip (CU count x resident blocks) and grid-stride
-//     the rest (Guideline 11); 256-thread blocks = 4 wave64s.
-//   * ~50 KB must be in flight per CU to cover HBM latency under load: the
-//     register variant keeps UNROLL=4 x 16 B per lane outstanding at up to 8
-//     blocks/CU; the LDS variant keeps two STAGES-deep batches of 1 KiB
-//     LDS-DMA pieces per wave in flight.
+// gfx950 (MI355X, CDNA4) buffer kernels: fill / verify / reduce / copy.
+// See kernels.hpp for the contract.  Design notes:
+//   * Pure streaming: the target is the HBM3E roofline.  Every access is
+//     16 B per lane, so one wave instruction moves a contiguous 1 KiB
+//     (cdna_hip_programming.md Guideline 13).
+//   * Grid shape (measured, scripts/fill_probe.hip): one 16 B access per lane
+//     and one 4 KiB block per 256-thread workgroup, up to kMaxGrid = 2^20
+//     workgroups and grid-striding only beyond 4 GiB.  On MI355X this "full
+//     grid" streams stores at 6.9-7.0 TB/s (torch zero_: 6.87) and loads at
+//     6.7-6.8 TB/s, while the textbook grid-stride loop over a grid capped at
+//     4-32 blocks per CU tops out at 5.1-5.6 (stores) / 6.3 (loads) TB/s.
+//   * The PRNG key depends only on word_index >> 32; a block iteration covers
+//     1024 words starting at a multiple of 1024, so the key is computed once per
+//     iteration from block-uniform values on the scalar unit and the vector ALU
+//     only runs the 4 per-word mixes.
+//   * The verify epilogue never funnels into one hot address: each block
+//     commits with one atomic per field into shard (blockIdx % 64) of a
+//     64-line accumulator, and a one-wave finalize kernel folds the shards.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -29,13 +35,19 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
-constexpr int kFillUnroll = 4;
-constexpr int kVerifyUnroll = 4;   // register variant, default
-constexpr int kVerifyUnroll8 = 8;  // register variant with twice the loads in flight
-constexpr int kLdsStages = 4;  // 1 KiB pieces per wave per batch
-// Defaults picked from scripts/kernel_bench.py A/B runs (profiles/).
-constexpr FillImpl kDefaultFill = FillImpl::Plain;
-constexpr VerifyImpl kDefaultVerify = VerifyImpl::Register;
+constexpr uint64_t kBlockVecs = kBlock;     // 16 B vectors per block iteration (4 KiB)
+constexpr uint64_t kMaxGrid = 1ull << 20;   // 4 GiB per grid pass
+constexpr int kStrideUnroll = 4;            // legacy grid-stride variants
+constexpr int kStrideBlocksPerCu = 8;        // legacy fill stride grid
+constexpr int kLdsStages = 4;               // 1 KiB LDS-DMA pieces per wave (4 KiB per wave)
+// Verify grid caps per variant, from scripts/verify_grid_sweep.py on MI355X
+// (1 GiB / 4 GiB, TB/s): stride 16/CU 6.41 / 6.73; full-grid register 256/CU
+// 5.67 / 6.86 (uncapped: 2.25 / 2.44, epilogue-bound); LDS 4/CU 5.83 / 5.83.
+constexpr int kVerifyStridePerCu = 16;
+constexpr int kVerifyGridPerCu = 256;
+constexpr int kVerifyLdsPerCu = 4;
+constexpr FillImpl kDefaultFill = FillImpl::Grid;
+constexpr VerifyImpl kDefaultVerify = VerifyImpl::Stride;
 
 #define HIP_OK(cmd)                                                                          \
   do {                                                                                       \
@@ -43,39 +55,51 @@ constexpr VerifyImpl kDefaultVerify = VerifyImpl::Register;
     if (e_ != hipSuccess) P2P_FATAL(strfmt("HIP error %s: %s", #cmd, hipGetErrorString(e_))); \
   } while (0)
 
-// The key depends only on (seed, word_index >> 32).  Every tile below is a
-// multiple of 4096 words and starts on such a multiple, so it never straddles
-// a 2^32-word boundary: the key is computed once per tile from tile-uniform
-// values (scalar ALU) and only the 4 per-word mixes run on the vector ALU.
 __device__ __forceinline__ uint4 prng_vec_k(uint32_t key, uint64_t vec_index) {
   const uint32_t lo = static_cast<uint32_t>(vec_index * 4);
   return make_uint4(prng_word_k(key, lo), prng_word_k(key, lo + 1), prng_word_k(key, lo + 2), prng_word_k(key, lo + 3));
 }
 
+__device__ __forceinline__ void store_tail(uint8_t* tail, uint32_t tail_bytes, uint64_t tail_offset, uint64_t seed) {
+  if (blockIdx.x == 0 && threadIdx.x < tail_bytes) tail[threadIdx.x] = prng_byte(seed, tail_offset + threadIdx.x);
+}
+
 // ------------------------------------------------------------------ fill ----
 
 template <bool NT>
-__global__ __launch_bounds__(kBlock) void fill_kernel(uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
-                                                      uint8_t* __restrict__ tail, uint32_t tail_bytes,
-                                                      uint64_t tail_offset) {
-  const uint64_t tile = static_cast<uint64_t>(kBlock) * kFillUnroll;
-  for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * tile; base < nvec; base += static_cast<uint64_t>(gridDim.x) * tile) {
-    const uint32_t key = prng_key(seed, base * 4);
-#pragma unroll
-    for (int u = 0; u < kFillUnroll; ++u) {
-      const uint64_t i = base + static_cast<uint64_t>(u) * kBlock + threadIdx.x;
-      if (i < nvec) {
-        const uint4 v = prng_vec_k(key, i);
-        if (NT) {
-          u32x4 w = {v.x, v.y, v.z, v.w};
-          __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p) + i);
-        } else {
-          p[i] = v;
-        }
+__global__ __launch_bounds__(kBlock) void fill_grid_kernel(uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
+                                                           uint8_t* __restrict__ tail, uint32_t tail_bytes,
+                                                           uint64_t tail_offset) {
+  for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBlockVecs; base < nvec;
+       base += static_cast<uint64_t>(gridDim.x) * kBlockVecs) {
+    const uint32_t key = prng_key(seed, base * 4);  // block-uniform: scalar ALU
+    const uint64_t i = base + threadIdx.x;
+    if (i < nvec) {
+      const uint4 v = prng_vec_k(key, i);
+      if (NT) {
+        u32x4 w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p) + i);
+      } else {
+        p[i] = v;
       }
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x < tail_bytes) tail[threadIdx.x] = prng_byte(seed, tail_offset + threadIdx.x);
+  store_tail(tail, tail_bytes, tail_offset, seed);
+}
+
+__global__ __launch_bounds__(kBlock) void fill_stride_kernel(uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
+                                                             uint8_t* __restrict__ tail, uint32_t tail_bytes,
+                                                             uint64_t tail_offset) {
+  const uint64_t tile = static_cast<uint64_t>(kBlock) * kStrideUnroll;
+  for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * tile; base < nvec; base += static_cast<uint64_t>(gridDim.x) * tile) {
+    const uint32_t key = prng_key(seed, base * 4);
+#pragma unroll
+    for (int u = 0; u < kStrideUnroll; ++u) {
+      const uint64_t i = base + static_cast<uint64_t>(u) * kBlock + threadIdx.x;
+      if (i < nvec) p[i] = prng_vec_k(key, i);
+    }
+  }
+  store_tail(tail, tail_bytes, tail_offset, seed);
 }
 
 // ---------------------------------------------------------------- verify ----
@@ -120,8 +144,8 @@ __device__ void check_tail(const uint8_t* tail, uint32_t tail_bytes, uint64_t ta
   }
 }
 
-// Reduction epilogue: wave64 butterfly, then the 4 wave partials through LDS,
-// then one atomic per block and per field (skipped when zero).
+// Reduction epilogue: wave64 butterfly, the 4 wave partials through LDS, then
+// one atomic per non-zero field into this block's shard.
 __device__ __forceinline__ void block_commit(Partial acc, VerifyAccum* out) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -141,35 +165,51 @@ __device__ __forceinline__ void block_commit(Partial acc, VerifyAccum* out) {
       t.sum += red[w].sum;
       t.first = min(t.first, red[w].first);
     }
-    if (t.sum) atomicAdd(&out->checksum, t.sum);
+    VerifyAccum* s = out + (blockIdx.x % kVerifyShards);
+    if (t.sum) atomicAdd(&s->checksum, t.sum);
     if (t.mism) {
-      atomicAdd(&out->mismatches, t.mism);
-      atomicMin(&out->first_bad, t.first);
+      atomicAdd(&s->mismatches, t.mism);
+      atomicMin(&s->first_bad, t.first);
     }
   }
 }
 
-template <bool CHECK, int UNROLL>
-__global__ __launch_bounds__(kBlock) void verify_reg_kernel(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
-                                                            const uint8_t* __restrict__ tail, uint32_t tail_bytes,
-                                                            uint64_t tail_offset, VerifyAccum* __restrict__ out) {
+__device__ __forceinline__ uint4 load_nt(const uint4* p, uint64_t i) {
+  const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p) + i);
+  return make_uint4(t.x, t.y, t.z, t.w);
+}
+
+template <bool CHECK>
+__global__ __launch_bounds__(kBlock) void verify_grid_kernel(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
+                                                             const uint8_t* __restrict__ tail, uint32_t tail_bytes,
+                                                             uint64_t tail_offset, VerifyAccum* __restrict__ out) {
   Partial acc{0, 0, ~0ull};
-  const uint64_t tile = static_cast<uint64_t>(kBlock) * UNROLL;
+  for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBlockVecs; base < nvec;
+       base += static_cast<uint64_t>(gridDim.x) * kBlockVecs) {
+    const uint64_t i = base + threadIdx.x;
+    const uint32_t key = prng_key(seed, base * 4);
+    if (i < nvec) check_vec<CHECK>(load_nt(p, i), key, i, acc);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) check_tail<CHECK>(tail, tail_bytes, tail_offset, seed, acc);
+  block_commit(acc, out);
+}
+
+template <bool CHECK>
+__global__ __launch_bounds__(kBlock) void verify_stride_kernel(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
+                                                               const uint8_t* __restrict__ tail, uint32_t tail_bytes,
+                                                               uint64_t tail_offset, VerifyAccum* __restrict__ out) {
+  Partial acc{0, 0, ~0ull};
+  const uint64_t tile = static_cast<uint64_t>(kBlock) * kStrideUnroll;
   for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * tile; base < nvec; base += static_cast<uint64_t>(gridDim.x) * tile) {
-    uint4 v[UNROLL];
+    uint4 v[kStrideUnroll];
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {  // all loads issued before any compare
+    for (int u = 0; u < kStrideUnroll; ++u) {  // all loads issued before any compare
       const uint64_t i = base + static_cast<uint64_t>(u) * kBlock + threadIdx.x;
-      if (i < nvec) {
-        const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p) + i);
-        v[u] = make_uint4(t.x, t.y, t.z, t.w);
-      } else {
-        v[u] = make_uint4(0, 0, 0, 0);
-      }
+      v[u] = i < nvec ? load_nt(p, i) : make_uint4(0, 0, 0, 0);
     }
     const uint32_t key = prng_key(seed, base * 4);
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
+    for (int u = 0; u < kStrideUnroll; ++u) {
       const uint64_t i = base + static_cast<uint64_t>(u) * kBlock + threadIdx.x;
       if (i < nvec) check_vec<CHECK>(v[u], key, i, acc);
     }
@@ -178,57 +218,38 @@ __global__ __launch_bounds__(kBlock) void verify_reg_kernel(const uint4* __restr
   block_commit(acc, out);
 }
 
-// LDS-staged verify.  Each wave owns a private double-buffered ring of
-// 2 x kLdsStages x 1 KiB in LDS.  A "super-chunk" is kLdsStages consecutive
-// KiB; wave g of G handles super-chunks g, g+G, ...  While the compare loop
-// reads batch b from LDS (ds_read_b128, each lane its own 16 B: conflict
-// free), the LDS-DMA of batch b+1 is already in flight; the counted
-// s_waitcnt vmcnt(kLdsStages) waits only for the older batch.  No
-// workgroup barrier is needed: a wave only reads bytes its own DMAs wrote.
+// LDS-staged verify.  Wave g owns super-chunk g (kLdsStages consecutive KiB)
+// of each grid pass: it issues kLdsStages LDS-DMA pieces
+// (global_load_lds_dwordx4: the wave's 64 lanes x 16 B land contiguously at
+// the LDS address in M0), waits for its own DMAs (vmcnt(0)), reads each lane's
+// 16 B back with ds_read_b128 (contiguous per lane: bank-conflict free) and
+// compares.  No workgroup barrier: a wave only reads bytes its own DMAs
+// wrote.  The four ds_read_b128 live in one asm statement: hipcc cannot tell
+// which LDS-DMA a ds_read aliases and would put a vmcnt(0) in front of each
+// one; the asm drains its own reads (lgkmcnt(0)).
 template <bool CHECK>
 __global__ __launch_bounds__(kBlock) void verify_lds_kernel(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
                                                             const uint8_t* __restrict__ tail, uint32_t tail_bytes,
                                                             uint64_t tail_offset, VerifyAccum* __restrict__ out) {
-  __shared__ uint4 ring[kWaves][2][kLdsStages][64];
+  static_assert(kLdsStages == 4, "asm block reads exactly four stages");
+  __shared__ uint4 slot[kWaves][kLdsStages][64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x / 64;
-  const uint64_t waves_total = static_cast<uint64_t>(gridDim.x) * kWaves;
-  const uint64_t g = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
   const uint64_t sc_vecs = static_cast<uint64_t>(kLdsStages) * 64;
   const uint64_t n_sc = (nvec + sc_vecs - 1) / sc_vecs;
-
-  auto issue = [&](uint64_t sc, int buf) {
+  const uint32_t lds_addr = static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)(&slot[wave][0][lane])));
+  Partial acc{0, 0, ~0ull};
+  for (uint64_t sc = static_cast<uint64_t>(blockIdx.x) * kWaves + wave; sc < n_sc;
+       sc += static_cast<uint64_t>(gridDim.x) * kWaves) {
 #pragma unroll
     for (int s = 0; s < kLdsStages; ++s) {
       const uint64_t i = sc * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
       if (i < nvec)
         __builtin_amdgcn_global_load_lds(static_cast<const void*>(p + i),
-                                         (__attribute__((address_space(3))) void*)(&ring[wave][buf][s][0]),
-                                         16, 0, 0);
+                                         (__attribute__((address_space(3))) void*)(&slot[wave][s][0]), 16, 0, 0);
     }
-  };
-
-  Partial acc{0, 0, ~0ull};
-  uint64_t sc = g;
-  int buf = 0;
-  if (sc < n_sc) issue(sc, 0);
-  for (; sc < n_sc; sc += waves_total) {
-    const uint64_t next = sc + waves_total;
-    const bool next_full = (next + 1) * sc_vecs <= nvec;  // wave-uniform
-    if (next < n_sc) issue(next, buf ^ 1);
-    if (next_full) {
-      // Older batch done; the kLdsStages youngest (next batch) may still fly.
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kLdsStages) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    // The four ds_read_b128 live in one asm statement: hipcc cannot tell which
-    // LDS-DMA a ds_read aliases and would put a full vmcnt(0) in front of
-    // each one, serialising the ring; here the only VMEM wait is the counted
-    // one above and the asm drains its own reads (lgkmcnt(0)).
-    static_assert(kLdsStages == 4, "asm block reads exactly four stages");
-    const uint32_t lds_addr = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
-        (__attribute__((address_space(3))) void*)(&ring[wave][buf][0][lane])));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     u32x4 r0, r1, r2, r3;
     asm volatile(
         "ds_read_b128 %0, %4\n\t"
@@ -240,22 +261,41 @@ __global__ __launch_bounds__(kBlock) void verify_lds_kernel(const uint4* __restr
         : "v"(lds_addr)
         : "memory");
     const u32x4 rv[kLdsStages] = {r0, r1, r2, r3};
-    const uint32_t key = prng_key(seed, sc * sc_vecs * 4);
+    const uint32_t key = prng_key(seed, sc * sc_vecs * 4);  // wave-uniform
 #pragma unroll
     for (int s = 0; s < kLdsStages; ++s) {
       const uint64_t i = sc * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
       if (i < nvec) check_vec<CHECK>(make_uint4(rv[s].x, rv[s].y, rv[s].z, rv[s].w), key, i, acc);
     }
-    buf ^= 1;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) check_tail<CHECK>(tail, tail_bytes, tail_offset, seed, acc);
   block_commit(acc, out);
 }
 
 __global__ void verify_reset_kernel(VerifyAccum* acc) {
-  acc->mismatches = 0;
-  acc->checksum = 0;
-  acc->first_bad = ~0ull;
+  if (threadIdx.x < kVerifyShards) {
+    acc[threadIdx.x].mismatches = 0;
+    acc[threadIdx.x].checksum = 0;
+    acc[threadIdx.x].first_bad = ~0ull;
+  }
+}
+
+// One wave folds the 64 shards into shard 0.
+__global__ __launch_bounds__(64) void verify_finalize_kernel(VerifyAccum* acc) {
+  const int l = threadIdx.x;
+  unsigned long long m = acc[l].mismatches, s = acc[l].checksum, f = acc[l].first_bad;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    m += __shfl_xor(m, off, 64);
+    s += __shfl_xor(s, off, 64);
+    f = min(f, __shfl_xor(f, off, 64));
+  }
+  __syncthreads();  // every lane has read its shard before shard 0 is overwritten
+  if (l == 0) {
+    acc[0].mismatches = m;
+    acc[0].checksum = s;
+    acc[0].first_bad = f;
+  }
 }
 
 struct DevCache {
@@ -267,6 +307,8 @@ DevCache& dev_cache() {
   static DevCache c;
   return c;
 }
+
+unsigned grid_for(uint64_t units) { return static_cast<unsigned>(std::max<uint64_t>(1, std::min(units, kMaxGrid))); }
 
 }  // namespace
 
@@ -284,32 +326,41 @@ int cu_count() {
   return c.cus[static_cast<size_t>(d)];
 }
 
-LaunchGeom fill_geometry(size_t bytes) {
+LaunchGeom fill_geometry(size_t bytes, FillImpl impl) {
   LaunchGeom g;
   const uint64_t nvec = bytes / 16;
-  const uint64_t tiles = (nvec + kBlock * kFillUnroll - 1) / (kBlock * kFillUnroll);
-  const uint64_t cap = static_cast<uint64_t>(cu_count()) * 8;  // 8 resident 256-thread blocks per CU
-  g.grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min(tiles, cap)));
+  if (impl == FillImpl::Stride) {
+    const uint64_t tiles = (nvec + kBlock * kStrideUnroll - 1) / (kBlock * kStrideUnroll);
+    g.grid = static_cast<unsigned>(
+        std::max<uint64_t>(1, std::min(tiles, static_cast<uint64_t>(cu_count()) * kStrideBlocksPerCu)));
+  } else {
+    g.grid = grid_for((nvec + kBlockVecs - 1) / kBlockVecs);
+  }
   return g;
 }
 
-LaunchGeom verify_geometry(size_t bytes, VerifyImpl impl) {
+LaunchGeom verify_geometry(size_t bytes, VerifyImpl impl, unsigned max_grid) {
   LaunchGeom g;
   const uint64_t nvec = bytes / 16;
+  if (impl == VerifyImpl::Auto) impl = kDefaultVerify;
+  // Unlike fill/copy, verify ends every workgroup with a reduction and an
+  // atomic commit, so a full grid (one 4 KiB block per workgroup) pays that
+  // epilogue 256K times per GiB; the defaults below cap the grid so each
+  // workgroup streams tens of KiB per epilogue (kernel_bench A/B).
+  const uint64_t per_cu = impl == VerifyImpl::Lds ? kVerifyLdsPerCu
+                          : impl == VerifyImpl::Stride ? kVerifyStridePerCu
+                                                       : kVerifyGridPerCu;
+  const uint64_t cap = max_grid ? max_grid : static_cast<uint64_t>(cu_count()) * per_cu;
   if (impl == VerifyImpl::Lds) {
     const uint64_t sc_vecs = static_cast<uint64_t>(kLdsStages) * 64;
     const uint64_t waves = (nvec + sc_vecs - 1) / sc_vecs;
-    const uint64_t blocks = (waves + kWaves - 1) / kWaves;
-    g.lds_bytes = sizeof(uint4) * kWaves * 2 * kLdsStages * 64;
-    // 160 KiB LDS per CU / 32 KiB per block -> 5 resident blocks per CU.
-    const uint64_t per_cu = std::max<uint64_t>(1, (160u * 1024u) / (g.lds_bytes + 256));
-    const uint64_t cap = static_cast<uint64_t>(cu_count()) * std::min<uint64_t>(per_cu, 8);
-    g.grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min(blocks, cap)));
-  } else {
-    const int unroll = impl == VerifyImpl::Register8 ? kVerifyUnroll8 : kVerifyUnroll;
-    const uint64_t tiles = (nvec + static_cast<uint64_t>(kBlock) * unroll - 1) / (static_cast<uint64_t>(kBlock) * unroll);
-    const uint64_t cap = static_cast<uint64_t>(cu_count()) * 8;
+    g.grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min((waves + kWaves - 1) / kWaves, cap)));
+    g.lds_bytes = sizeof(uint4) * kWaves * kLdsStages * 64;
+  } else if (impl == VerifyImpl::Stride) {
+    const uint64_t tiles = (nvec + kBlock * kStrideUnroll - 1) / (kBlock * kStrideUnroll);
     g.grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min(tiles, cap)));
+  } else {
+    g.grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min((nvec + kBlockVecs - 1) / kBlockVecs, cap)));
   }
   return g;
 }
@@ -320,17 +371,24 @@ void launch_fill(void* p, size_t bytes, uint64_t seed, hipStream_t stream, FillI
   if (impl == FillImpl::Auto) impl = kDefaultFill;
   const uint64_t nvec = bytes / 16;
   const uint32_t tail = static_cast<uint32_t>(bytes - nvec * 16);
-  LaunchGeom g = fill_geometry(bytes);
-  auto* base = static_cast<uint8_t*>(p);
-  if (impl == FillImpl::Nontemporal)
-    fill_kernel<true><<<g.grid, kBlock, 0, stream>>>(reinterpret_cast<uint4*>(p), nvec, seed, base + nvec * 16, tail, nvec * 16);
-  else
-    fill_kernel<false><<<g.grid, kBlock, 0, stream>>>(reinterpret_cast<uint4*>(p), nvec, seed, base + nvec * 16, tail, nvec * 16);
+  LaunchGeom g = fill_geometry(bytes, impl);
+  auto* vp = reinterpret_cast<uint4*>(p);
+  auto* tp = static_cast<uint8_t*>(p) + nvec * 16;
+  switch (impl) {
+    case FillImpl::Nontemporal:
+      fill_grid_kernel<true><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16);
+      break;
+    case FillImpl::Stride:
+      fill_stride_kernel<<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16);
+      break;
+    default:
+      fill_grid_kernel<false><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16);
+  }
   HIP_OK(hipGetLastError());
 }
 
 void launch_verify_reset(VerifyAccum* acc, hipStream_t stream) {
-  verify_reset_kernel<<<1, 1, 0, stream>>>(acc);
+  verify_reset_kernel<<<1, 64, 0, stream>>>(acc);
   HIP_OK(hipGetLastError());
 }
 
@@ -342,37 +400,38 @@ void launch_verify_t(const uint4* vp, uint64_t nvec, uint64_t seed, const uint8_
     case VerifyImpl::Lds:
       verify_lds_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
       break;
-    case VerifyImpl::Register8:
-      verify_reg_kernel<CHECK, kVerifyUnroll8><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
+    case VerifyImpl::Stride:
+      verify_stride_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
       break;
     default:
-      verify_reg_kernel<CHECK, kVerifyUnroll><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
+      verify_grid_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
   }
 }
 }  // namespace
 
 void launch_verify(const void* p, size_t bytes, uint64_t seed, VerifyAccum* acc, VerifyImpl impl, bool check_prng,
-                   hipStream_t stream) {
-  if (!bytes) return;
-  P2P_CHECK(reinterpret_cast<uintptr_t>(p) % 16 == 0, "verify: buffer must be 16-byte aligned");
-  if (impl == VerifyImpl::Auto) impl = kDefaultVerify;
-  const uint64_t nvec = bytes / 16;
-  const uint32_t tail = static_cast<uint32_t>(bytes - nvec * 16);
-  const auto* vp = static_cast<const uint4*>(p);
-  const auto* tp = static_cast<const uint8_t*>(p) + nvec * 16;
-  LaunchGeom g = verify_geometry(bytes, impl);
-  if (check_prng)
-    launch_verify_t<true>(vp, nvec, seed, tp, tail, acc, impl, g, stream);
-  else
-    launch_verify_t<false>(vp, nvec, seed, tp, tail, acc, impl, g, stream);
+                   hipStream_t stream, unsigned max_grid) {
+  if (bytes) {
+    P2P_CHECK(reinterpret_cast<uintptr_t>(p) % 16 == 0, "verify: buffer must be 16-byte aligned");
+    if (impl == VerifyImpl::Auto) impl = kDefaultVerify;
+    const uint64_t nvec = bytes / 16;
+    const uint32_t tail = static_cast<uint32_t>(bytes - nvec * 16);
+    const auto* vp = static_cast<const uint4*>(p);
+    const auto* tp = static_cast<const uint8_t*>(p) + nvec * 16;
+    LaunchGeom g = verify_geometry(bytes, impl, max_grid);
+    if (check_prng)
+      launch_verify_t<true>(vp, nvec, seed, tp, tail, acc, impl, g, stream);
+    else
+      launch_verify_t<false>(vp, nvec, seed, tp, tail, acc, impl, g, stream);
+    HIP_OK(hipGetLastError());
+  }
+  verify_finalize_kernel<<<1, 64, 0, stream>>>(acc);
   HIP_OK(hipGetLastError());
 }
 
 // ------------------------------------------------------------ multi copy ----
 
 namespace {
-
-constexpr int kCopyUnroll = 4;
 
 // Passed by value in the kernarg segment: no device-side descriptor upload,
 // so a launch is a single stream operation (and graph-capturable).
@@ -395,20 +454,8 @@ __global__ __launch_bounds__(kBlock) void multi_copy_kernel(const CopyArgs a) {
   const uint4* __restrict__ s = a.src[op];
   uint4* __restrict__ d = a.dst[op];
   const uint64_t n = a.nvec[op];
-  const uint64_t tile = static_cast<uint64_t>(kBlock) * kCopyUnroll;
-  for (uint64_t base = static_cast<uint64_t>(b) * tile; base < n; base += static_cast<uint64_t>(nb) * tile) {
-    uint4 v[kCopyUnroll];
-#pragma unroll
-    for (int u = 0; u < kCopyUnroll; ++u) {  // all (remote) loads in flight before the stores
-      const uint64_t i = base + static_cast<uint64_t>(u) * kBlock + threadIdx.x;
-      if (i < n) v[u] = s[i];
-    }
-#pragma unroll
-    for (int u = 0; u < kCopyUnroll; ++u) {
-      const uint64_t i = base + static_cast<uint64_t>(u) * kBlock + threadIdx.x;
-      if (i < n) d[i] = v[u];
-    }
-  }
+  for (uint64_t i = static_cast<uint64_t>(b) * kBlockVecs + threadIdx.x; i < n; i += static_cast<uint64_t>(nb) * kBlockVecs)
+    d[i] = s[i];
   if (b == 0 && threadIdx.x < a.tail[op]) {
     const uint8_t* st = reinterpret_cast<const uint8_t*>(s + n);
     uint8_t* dt = reinterpret_cast<uint8_t*>(d + n);
@@ -425,7 +472,6 @@ void launch_multi_copy(const CopyOp* ops, int nops, hipStream_t stream, int max_
     a.nops = cnt;
     uint64_t need[kMaxCopyOps] = {0};
     uint64_t total_need = 0;
-    const uint64_t tile = static_cast<uint64_t>(kBlock) * kCopyUnroll;
     for (int i = 0; i < cnt; ++i) {
       const CopyOp& o = ops[first + i];
       P2P_CHECK(reinterpret_cast<uintptr_t>(o.src) % 16 == 0 && reinterpret_cast<uintptr_t>(o.dst) % 16 == 0,
@@ -434,10 +480,10 @@ void launch_multi_copy(const CopyOp* ops, int nops, hipStream_t stream, int max_
       a.dst[i] = static_cast<uint4*>(o.dst);
       a.nvec[i] = o.bytes / 16;
       a.tail[i] = static_cast<uint32_t>(o.bytes - a.nvec[i] * 16);
-      need[i] = std::max<uint64_t>(1, (a.nvec[i] + tile - 1) / tile);
+      need[i] = std::max<uint64_t>(1, (a.nvec[i] + kBlockVecs - 1) / kBlockVecs);
       total_need += need[i];
     }
-    const uint64_t cap = max_blocks > 0 ? static_cast<uint64_t>(max_blocks) : static_cast<uint64_t>(cu_count()) * 8;
+    const uint64_t cap = max_blocks > 0 ? static_cast<uint64_t>(max_blocks) : kMaxGrid;
     uint32_t acc = 0;
     for (int i = 0; i < cnt; ++i) {
       a.block_begin[i] = acc;

@@ -4,16 +4,30 @@
 // cudaMemset (p2p_matrix.cc:129-130) and never read back.
 // These kernels replace that with verifiable random payloads:
 //   fill    — counter-based PRNG, one 16-byte global_store_dwordx4 per lane
-//   verify  — regenerates the stream and compares; two staging variants:
-//               * register: global_load_dwordx4, UNROLL loads in flight/lane
+//   verify  — regenerates the stream and compares; staging variants:
+//               * stride (default): 4 x global_load_dwordx4 in flight per
+//                           lane, grid capped at 16 workgroups per CU so the
+//                           reduction epilogue is amortised over 64 KiB+
+//               * register: one global_load_dwordx4 per lane per iteration
+//                           (the full-grid shape of fill/copy, capped at
+//                           256 workgroups per CU)
 //               * LDS:      global_load_lds_dwordx4 (LDS-DMA, 1 KiB per wave
-//                           instruction) into a double-buffered per-wave LDS
-//                           ring, then ds_read_b128 — the LDS-staged form the
-//                           north star asks for, A/B-tested against register
-//                           staging
+//                           instruction) into a per-wave LDS slot, then
+//                           ds_read_b128 — the LDS-staged form the north star
+//                           asks for, A/B-tested against register staging
+//                           (SURVEY.md §7.5 item 6): ~13% slower, as the
+//                           extra LDS round trip predicts for pure streaming
 //   reduce  — fused epilogue of verify: wave64 __shfl_xor tree -> LDS across
-//             the 4 waves -> one atomic per block (mismatches, checksum,
-//             first bad offset)
+//             the 4 waves -> one atomic per block into one of kVerifyShards
+//             64-byte counters (no single hot address), then a one-wave
+//             finalize kernel folds the shards
+//   copy    — multi-source copy for the IPC transport (remote loads over xGMI)
+//
+// Measured on MI355X (profiles/, scripts/fill_probe.hip): streaming at one
+// 16 B access per lane with one block per 4 KiB (a "full grid", up to 2^20
+// blocks, then grid-stride) reaches 6.9-7.0 TB/s for stores and 6.7-6.8 TB/s
+// for loads, against 5.1-5.6 / 6.3 TB/s for grid-stride loops over a grid
+// capped at 4-32 blocks per CU.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -26,15 +40,19 @@
 namespace p2p {
 namespace dev {
 
-// Device-side accumulator; `first_bad` must start at ~0 (verify_reset does it).
-struct VerifyAccum {
+// One 64-byte shard of the device-side accumulator; `first_bad` starts at ~0
+// (launch_verify_reset).  Allocate verify_accum_bytes() for the whole array;
+// after launch_verify the totals are in shard 0.
+struct alignas(64) VerifyAccum {
   unsigned long long mismatches;
   unsigned long long checksum;
   unsigned long long first_bad;
 };
+constexpr int kVerifyShards = 64;
+constexpr size_t verify_accum_bytes() { return sizeof(VerifyAccum) * kVerifyShards; }
 
-enum class VerifyImpl : int { Auto = 0, Register = 1, Lds = 2, Register8 = 3 };
-enum class FillImpl : int { Auto = 0, Plain = 1, Nontemporal = 2 };
+enum class VerifyImpl : int { Auto = 0, Register = 1, Lds = 2, Stride = 3 };
+enum class FillImpl : int { Auto = 0, Grid = 1, Nontemporal = 2, Stride = 3 };
 
 // Geometry chosen for a launch (exposed for tests / profiling scripts).
 struct LaunchGeom {
@@ -43,14 +61,17 @@ struct LaunchGeom {
   size_t lds_bytes = 0;
 };
 
-LaunchGeom fill_geometry(size_t bytes);
-LaunchGeom verify_geometry(size_t bytes, VerifyImpl impl);
+LaunchGeom fill_geometry(size_t bytes, FillImpl impl = FillImpl::Auto);
+// max_grid > 0 caps the workgroup count (the kernels grid-stride beyond it);
+// 0 = the tuned default of the variant.
+LaunchGeom verify_geometry(size_t bytes, VerifyImpl impl, unsigned max_grid = 0);
 
 void launch_fill(void* p, size_t bytes, uint64_t seed, hipStream_t stream, FillImpl impl = FillImpl::Auto);
 void launch_verify_reset(VerifyAccum* acc, hipStream_t stream);
 // check_prng=false only sums the words (checksum of an arbitrary buffer).
+// Leaves the totals in acc[0] (stream-ordered).
 void launch_verify(const void* p, size_t bytes, uint64_t seed, VerifyAccum* acc, VerifyImpl impl, bool check_prng,
-                   hipStream_t stream);
+                   hipStream_t stream, unsigned max_grid = 0);
 
 // Device attributes cached per device (CU count drives grid sizing).
 int cu_count();
@@ -58,9 +79,8 @@ int cu_count();
 // ---- multi-source copy (IPC transport data plane) ----
 // One launch moves every receive of a group: op i copies ops[i].bytes from
 // src (typically a peer GPU's buffer mapped through hipIpcOpenMemHandle, so
-// the loads travel over xGMI) to dst.  Workgroups are split across ops in
-// proportion to their size; each lane keeps UNROLL x 16 B loads in flight to
-// cover the remote-read latency.
+// the loads travel over xGMI) to dst.  Full grid: one 16 B load + store per
+// lane, one 4 KiB block per workgroup, workgroups split across ops by size.
 struct CopyOp {
   const void* src;
   void* dst;

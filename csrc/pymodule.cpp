@@ -131,7 +131,7 @@ KernelScratch& scratch() {
   if (s.device != dv) {
     if (s.d) (void)hipFree(s.d);
     if (s.h) (void)hipHostFree(s.h);
-    if (hipMalloc(&s.d, sizeof(dev::VerifyAccum)) != hipSuccess) P2P_FATAL("hipMalloc failed");
+    if (hipMalloc(&s.d, dev::verify_accum_bytes()) != hipSuccess) P2P_FATAL("hipMalloc failed");
     if (hipHostMalloc(&s.h, sizeof(dev::VerifyAccum), hipHostMallocDefault) != hipSuccess) P2P_FATAL("hipHostMalloc failed");
     s.device = dv;
   }
@@ -232,6 +232,21 @@ PYBIND11_MODULE(_p2pcore, m) {
   m.def("verify", &device_verify, py::arg("ptr"), py::arg("bytes"), py::arg("seed"), py::arg("impl") = 0,
         py::arg("check") = true, py::arg("stream") = 0,
         "Returns (mismatching words, checksum, first bad byte offset or 2**64-1).");
+  m.def("verify_launch", [](uintptr_t ptr, size_t bytes, uint64_t seed, int impl, bool check, uintptr_t stream,
+                            unsigned max_grid) {
+        // Stream-ordered launch only (reset + verify + finalize), no readback:
+        // for timing the kernel with events.
+        KernelScratch& ks = scratch();
+        dev::launch_verify_reset(ks.d, as_stream(stream));
+        dev::launch_verify(reinterpret_cast<const void*>(ptr), bytes, seed, ks.d, static_cast<dev::VerifyImpl>(impl),
+                           check, as_stream(stream), max_grid);
+      }, py::arg("ptr"), py::arg("bytes"), py::arg("seed"), py::arg("impl") = 0, py::arg("check") = true,
+      py::arg("stream") = 0, py::arg("max_grid") = 0);
+  m.def("copy", [](uintptr_t dst, uintptr_t src, size_t bytes, uintptr_t stream, int max_blocks) {
+        dev::CopyOp op{reinterpret_cast<const void*>(src), reinterpret_cast<void*>(dst), bytes};
+        dev::launch_multi_copy(&op, 1, as_stream(stream), max_blocks);
+      }, py::arg("dst"), py::arg("src"), py::arg("bytes"), py::arg("stream") = 0, py::arg("max_blocks") = 0,
+      "The IPC transport's gfx950 copy kernel on one (dst, src) pair.");
   m.def("fill_geometry", [](size_t bytes) {
     auto g = dev::fill_geometry(bytes);
     return py::make_tuple(g.grid, g.block, g.lds_bytes);

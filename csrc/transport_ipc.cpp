@@ -62,7 +62,7 @@ class IpcTransport final : public Transport {
     P2P_CHECK(device_ < ndev, strfmt("rank %d wants GPU %d but only %d are visible", rank_, device_, ndev));
     HIPCHECK(hipSetDevice(device_));
     HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    HIPCHECK(hipMalloc(&acc_, sizeof(dev::VerifyAccum)));
+    HIPCHECK(hipMalloc(&acc_, dev::verify_accum_bytes()));
     HIPCHECK(hipHostMalloc(&acc_host_, sizeof(dev::VerifyAccum), hipHostMallocDefault));
     hipDeviceProp_t prop;
     HIPCHECK(hipGetDeviceProperties(&prop, device_));

@@ -56,7 +56,7 @@ class RcclTransport final : public Transport {
       P2P_FATAL(strfmt("rank %d wants GPU %d but only %d are visible: more ranks per host than GPUs", rank_, device_, ndev));
     HIPCHECK(hipSetDevice(device_));
     HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    HIPCHECK(hipMalloc(&acc_, sizeof(dev::VerifyAccum)));
+    HIPCHECK(hipMalloc(&acc_, dev::verify_accum_bytes()));
     HIPCHECK(hipHostMalloc(&acc_host_, sizeof(dev::VerifyAccum), hipHostMallocDefault));
 
     ncclUniqueId id;

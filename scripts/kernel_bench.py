@@ -48,26 +48,38 @@ def main():
         ptr = buf.data_ptr()
         t_fill = timed(lambda: nat.fill(ptr, sz, 7, stream, 1), a.reps)
         t_fill_nt = timed(lambda: nat.fill(ptr, sz, 7, stream, 2), a.reps)
+        t_fill_stride = timed(lambda: nat.fill(ptr, sz, 7, stream, 3), a.reps)
         res = {}
-        for name, impl, check in [("verify_reg", 1, True), ("verify_reg8", 3, True), ("verify_lds", 2, True),
+        for name, impl, check in [("verify_reg", 1, True), ("verify_stride", 3, True), ("verify_lds", 2, True),
                                   ("checksum_reg", 1, False), ("checksum_lds", 2, False)]:
-            # verify() syncs (result readback); time with a host-side loop of
-            # launches through the same path and subtract nothing: the sync is
-            # part of what a caller pays.
-            t = timed(lambda: nat.verify(ptr, sz, 7, impl, check, stream), a.reps)
+            # Kernel time only: reset + verify + finalize launches, no readback.
+            t = timed(lambda: nat.verify_launch(ptr, sz, 7, impl, check, stream), a.reps)
             res[name] = t
             assert nat.verify(ptr, sz, 7, impl, True, stream)[0] == 0
-        row = {"bytes": sz, "fill_tbs": sz / t_fill / 1e12, "fill_nt_tbs": sz / t_fill_nt / 1e12}
+        row = {"bytes": sz, "fill_tbs": sz / t_fill / 1e12, "fill_nt_tbs": sz / t_fill_nt / 1e12,
+               "fill_stride_tbs": sz / t_fill_stride / 1e12}
+        # Roofs measured the same way: torch zero_() (write-only) and copy_()
+        # (read + write, counted once like ours), and our IPC copy kernel.
+        dst = torch.empty_like(buf)
+        row["torch_zero_tbs"] = sz / timed(lambda: buf.zero_(), a.reps) / 1e12
+        row["torch_copy_tbs"] = sz / timed(lambda: dst.copy_(buf), a.reps) / 1e12
+        row["copy_kernel_tbs"] = sz / timed(lambda: nat.copy(dst.data_ptr(), ptr, sz, stream), a.reps) / 1e12
+        nat.fill(ptr, sz, 7, stream)
+        nat.copy(dst.data_ptr(), ptr, sz, stream)
+        assert nat.verify(dst.data_ptr(), sz, 7, 1, True, stream)[0] == 0
+        del dst
         for k, t in res.items():
             row[k + "_tbs"] = sz / t / 1e12
         row["fill_geom"] = nat.fill_geometry(sz)
         row["verify_reg_geom"] = nat.verify_geometry(sz, 1)
         row["verify_lds_geom"] = nat.verify_geometry(sz, 2)
         rows.append(row)
-        print("%6s  fill %.2f (nt %.2f)  verify reg %.2f / reg8 %.2f / lds %.2f  checksum reg %.2f / lds %.2f TB/s"
+        print("%6s  fill %.2f (nt %.2f, stride %.2f)  verify grid %.2f / stride %.2f / lds %.2f  checksum reg %.2f / lds %.2f TB/s"
               "  (HBM measured roof %.2f)"
-              % (nat.format_size(sz), row["fill_tbs"], row["fill_nt_tbs"], row["verify_reg_tbs"], row["verify_reg8_tbs"],
+              % (nat.format_size(sz), row["fill_tbs"], row["fill_nt_tbs"], row["fill_stride_tbs"], row["verify_reg_tbs"], row["verify_stride_tbs"],
                  row["verify_lds_tbs"], row["checksum_reg_tbs"], row["checksum_lds_tbs"], HBM_MEASURED_TBS), flush=True)
+        print("        roofs: torch zero_ %.2f  torch copy_ %.2f  ours copy %.2f TB/s (copy counts bytes once)"
+              % (row["torch_zero_tbs"], row["torch_copy_tbs"], row["copy_kernel_tbs"]), flush=True)
         del buf
         torch.cuda.empty_cache()
     if a.json:

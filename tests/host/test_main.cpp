@@ -437,6 +437,17 @@ TEST(test_step_driver_host) {
     EXPECT(d.job_bytes_per_step(0) == 4.0 * 8192 * 2);
     EXPECT(d.bytes_sent_per_step(0) == 8192.0 * 2);
     b.barrier();
+    // Batched posting (one group per step) and a graph request on a
+    // transport without graphs (ignored) must move the same data.
+    StepOptions so;
+    so.batch = true;
+    so.graph = true;
+    StepDriver bd(t, b, make_ring_schedule(4, Direction::Bi), 4099, 3, true, 7, so);
+    bd.connect();
+    for (long k = 0; k < 3; ++k) bd.step(k);
+    bd.sync();
+    EXPECT(bd.verify_last() == 0);
+    b.barrier();
   });
 }
 

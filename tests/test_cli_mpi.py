@@ -123,3 +123,20 @@ def test_hung_rank_times_out_tcp(host_build):
             if p.poll() is None:
                 p.kill()
                 p.wait()
+
+
+def test_resume_and_trace(mpirun, host_build, tmp_path):
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    js, tr = tmp_path / "r.json", tmp_path / "t.json"
+    base = ["--transport", "host", "--sizes", "4K,64K", "-n", "2", "--no-compat", "--json", str(js)]
+    first = run(mpirun, exe, 2, base + ["--mode", "pair,ring", "--trace", str(tr)])
+    assert first.returncode == 0, first.stderr
+    assert len(js.read_text().splitlines()) == 8  # (pair, ring) x (uni, bi) x 2 sizes
+    trace = json.loads(tr.read_text())
+    xs = [e for e in trace["traceEvents"] if e["ph"] == "X"]
+    assert {e["tid"] for e in xs} == {0, 1} and all(e["dur"] >= 0 for e in xs)
+    again = run(mpirun, exe, 2, base + ["--mode", "pair,ring,allpairs", "--resume", "-v"])
+    assert again.returncode == 0, again.stderr
+    lines = js.read_text().splitlines()
+    assert len(lines) == 10  # only the 2 allpairs runs were added
+    assert again.stderr.count("resume: skipping") == 8
