@@ -1,0 +1,70 @@
+"""Tier T4: the RCCL data plane across real GPUs.  Runs only
+where >= 2 MI355X are visible (skipped on the 1-GPU test boxes; the 8-GPU
+scaling runs happen through bench.py on a full node)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import MPIRUN, ROOT, ensure_built, free_port
+from test_nccl_p2p_amd.utils.report import parse_compat
+
+
+def _gpus() -> int:
+    try:
+        import torch
+
+        return torch.cuda.device_count()
+    except Exception:  # pragma: no cover
+        return 0
+
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(_gpus() < 2, reason="needs >= 2 GPUs")]
+
+
+@pytest.fixture(scope="module")
+def exe():
+    ensure_built("gpu")
+    return os.path.join(ROOT, "build", "p2p_matrix")
+
+
+def _n():
+    return min(_gpus(), 8)
+
+
+@pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
+def test_reference_matrix_all_gpus(exe, tmp_path):
+    n = _n()
+    js = tmp_path / "r.json"
+    out = subprocess.run([MPIRUN, "-n", str(n), exe, "--verify", "-n", "16", "--json", str(js)],
+                         capture_output=True, text=True, timeout=900)
+    assert out.returncode == 0, out.stderr[-3000:]
+    m = parse_compat(out.stdout)
+    for key in ("uni", "bi"):
+        for i in range(n):
+            for j in range(n):
+                assert (m[key][i][j] == 0.0) == (i == j)
+    assert "verification: OK" in out.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
+def test_concurrent_modes_all_gpus(exe):
+    n = _n()
+    out = subprocess.run([MPIRUN, "-n", str(n), exe, "--mode", "tournament,ring,allpairs", "--sizes", "1M,256M",
+                          "-n", "8", "--verify", "--latency", "--no-compat"], capture_output=True, text=True, timeout=900)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "verification: OK" in out.stdout and "FAILED" not in out.stdout
+
+
+def test_bench_all_gpus():
+    n = _n()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", str(n), "--steps", "14",
+           "--warmup", "7"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert r["n_gpus"] == n and r["verify_mismatches"] == 0
+    assert r["matrix_cells"] == "%d/%d" % (n * (n - 1), n * (n - 1))
