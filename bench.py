@@ -48,21 +48,15 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-class stdout_to_stderr:
-    """fd-level redirect: RCCL prints its version banner on stdout during
-    communicator init; the driver contract wants exactly one JSON line there."""
-
-    def __enter__(self):
-        sys.stdout.flush()
-        self.saved = os.dup(1)
-        os.dup2(2, 1)
-        return self
-
-    def __exit__(self, *exc):
-        sys.stdout.flush()
-        os.dup2(self.saved, 1)
-        os.close(self.saved)
-        return False
+def claim_stdout() -> int:
+    """Points fd 1 at stderr for the whole run and returns a private duplicate
+    of the real stdout.  RCCL (version banner) and gloo ("Rank i is connected
+    to ...") print on stdout from every rank; the driver contract wants exactly
+    one JSON line there, written by rank 0 through the returned fd."""
+    sys.stdout.flush()
+    real = os.dup(1)
+    os.dup2(2, 1)
+    return real
 
 
 def parse_args(argv=None):
@@ -82,6 +76,8 @@ def parse_args(argv=None):
     ap.add_argument("--batch", type=int, default=1, help="1: all msgs of a step in one ncclGroup (one launch)")
     ap.add_argument("--graph", type=int, default=0, help="1: replay each step as a captured hipGraph")
     ap.add_argument("--json-out", default=None, help="also write the result line to this file")
+    ap.add_argument("--extras", type=int, default=1,
+                    help="1: also measure all-pairs 1 GiB and ring 256 MiB after the timed region (N > 1)")
     ap.add_argument("--ref-iters", type=int, default=32,
                     help="iterations per cell of the reference-methodology comparison (0 = skip)")
     return ap.parse_args(argv)
@@ -89,6 +85,7 @@ def parse_args(argv=None):
 
 def main(argv=None) -> int:
     args = parse_args(argv)
+    real_stdout = claim_stdout()
     from test_nccl_p2p_amd import require_native
     from test_nccl_p2p_amd.parallel.session import create_session, init_control_plane
 
@@ -111,13 +108,12 @@ def main(argv=None) -> int:
             torch.cuda.synchronize()
 
     size = nat.parse_size(args.size)
-    with stdout_to_stderr():
-        sess = create_session(args.transport, device=device)
-        if env.rank == 0:
-            log("bench: %d rank(s), %s, %s" % (n, sess.transport, sess.device_desc))
-        mode = "self" if n == 1 else args.mode
-        drv = nat.StepDriver(sess, mode, "bi", size, args.msgs, not args.no_verify, bool(args.batch), bool(args.graph))
-        drv.connect()
+    sess = create_session(args.transport, device=device)
+    if env.rank == 0:
+        log("bench: %d rank(s), %s, %s" % (n, sess.transport, sess.device_desc))
+    mode = "self" if n == 1 else args.mode
+    drv = nat.StepDriver(sess, mode, "bi", size, args.msgs, not args.no_verify, bool(args.batch), bool(args.graph))
+    drv.connect()
 
     # Warmup (untimed): also walks every round once when W >= phases.
     if args.warmup > 0:
@@ -180,6 +176,25 @@ def main(argv=None) -> int:
                "iters": args.ref_iters, "size": size,
                "method": "reference semantics: serial ordered pairs, wall clock, stream sync per message"}
 
+    # The other BASELINE.json configs, measured after the timed region so one
+    # driver run records them too: all-pairs concurrent exchange at 1 GiB
+    # (bisection: every GPU drives all N-1 xGMI links at once) and the ring
+    # neighbour exchange at 256 MiB (pipeline-parallel hop).
+    extras = None
+    if n > 1 and args.extras:
+        extras = {}
+        for name, mode_x, dir_x, nbytes, iters in (("allpairs_1g", "allpairs", "bi", 1 << 30, 4),
+                                                   ("ring_256m", "ring", "uni", 256 << 20, 8)):
+            r = json.loads(sess.run(mode=mode_x, dir=dir_x, bytes=nbytes, iters=iters, warmup=1, timing="events",
+                                    verify=False, warm=True))
+            ph = r["phases"][0]
+            flows = [f["gbs"] for f in ph["flows"]]
+            p50s = [f["iter_us"]["p50"] for f in ph["flows"]]
+            extras[name] = {"aggregate_gbs": round(ph["agg_gbs"], 2),
+                            "per_gpu_egress_gbs": round(ph["agg_gbs"] / n, 2),
+                            "flow_gbs_min": round(min(flows), 2), "flow_gbs_mean": round(statistics.mean(flows), 2),
+                            "iter_us_p50": round(statistics.median(p50s), 1), "bytes": nbytes, "iters": iters}
+
     step_ms_med = statistics.median(my_ms) if my_ms else 0.0
     result = {
         "metric": METRIC,
@@ -213,13 +228,14 @@ def main(argv=None) -> int:
         "transport": sess.transport,
         "posting": {"batch": bool(args.batch), "graph": bool(args.graph)},
         "reference_semantics": ref,
+        "extras": extras,
     }
     if env.rank == 0:
         log("bench: GB/s matrix (row=src, col=dst), median over steps:")
         for r in range(n):
             log("  " + " ".join("%8.2f" % matrix[r][c] for c in range(n)))
         line = json.dumps(result)
-        print(line, flush=True)
+        os.write(real_stdout, (line + "\n").encode())
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
