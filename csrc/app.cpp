@@ -34,6 +34,7 @@ schedule
   -d, --dir uni|bi|both  direction(s)                                         [both]
   -b, --size SIZE        message size, e.g. 4K 32M 1G                         [32M]
       --sizes LIST       sweep: 4K:4G (x2 steps), 4K:1G:4 (x4), 4K,1M,... ; overrides --size
+      --cells LIST       pair mode: measure only these src-dst cells, e.g. 0-1,3-2 (others print 0.00)
 timing
   -n, --iters N|auto     iterations per cell (auto: ~4 GiB per cell, 8..1000) [128]
   -w, --warmup N         untimed iterations per cell                          [8]
@@ -180,6 +181,23 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
       cfg->csv_path = next();
     } else if (a == "--trace") {
       cfg->trace_path = next();
+    } else if (a == "--cells") {
+      // "0-1,2-3" (src-dst pairs, also "0:1")
+      std::string v = next();
+      size_t pos = 0;
+      while (pos < v.size()) {
+        size_t c = v.find(',', pos);
+        std::string item = v.substr(pos, c == std::string::npos ? std::string::npos : c - pos);
+        size_t sep = item.find_first_of("-:");
+        if (sep == std::string::npos) {
+          std::fprintf(stderr, "p2p_matrix: bad --cells item '%s' (want src-dst)\n", item.c_str());
+          *exit_code = 1;
+          return false;
+        }
+        cfg->cells.emplace_back(std::atoi(item.substr(0, sep).c_str()), std::atoi(item.substr(sep + 1).c_str()));
+        if (c == std::string::npos) break;
+        pos = c + 1;
+      }
     } else if (a == "--resume") {
       cfg->resume = true;
     } else if (a == "--compat-only") {
@@ -238,6 +256,22 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
       continue;
     }
     for (Direction d : cfg.dirs) scheds.push_back(make_schedule(m, d, n));
+  }
+  // --cells: re-measure only some (src, dst) cells of the pair schedule; the
+  // others stay in the schedule as idle cells (barrier, reported 0.00), so the
+  // printed matrices keep their shape.
+  if (!cfg.cells.empty()) {
+    for (auto& s : scheds) {
+      if (s.mode != Mode::Pair) continue;
+      for (auto& p : s.phases) {
+        bool keep = std::find(cfg.cells.begin(), cfg.cells.end(), std::make_pair(p.row, p.col)) != cfg.cells.end();
+        if (!keep && !p.idle) {
+          p.idle = true;
+          p.flows.clear();
+          for (auto& r : p.ranks) r = RankOps{};
+        }
+      }
+    }
   }
   for (const auto& s : scheds) {
     std::string bad = validate(s);

@@ -39,6 +39,7 @@ struct AppConfig {
   std::string csv_path;
   std::string trace_path;
   bool resume = false;
+  std::vector<std::pair<int, int>> cells;  // pair-mode cell filter (empty = all)
   bool compat = true;      // reference matrices for pair mode
   bool extended = true;    // GB/s / latency tables after the compat section
   double timeout_s = 300;

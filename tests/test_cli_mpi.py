@@ -140,3 +140,14 @@ def test_resume_and_trace(mpirun, host_build, tmp_path):
     lines = js.read_text().splitlines()
     assert len(lines) == 10  # only the 2 allpairs runs were added
     assert again.stderr.count("resume: skipping") == 8
+
+
+def test_cells_filter(mpirun, host_build):
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    out = run(mpirun, exe, 3, ["--transport", "host", "--size", "16K", "-n", "2", "--cells", "0-1,2:0",
+                               "--compat-only"])
+    assert out.returncode == 0, out.stderr
+    m = parse_compat(out.stdout)
+    for key in ("uni", "bi"):
+        nz = {(i, j) for i in range(3) for j in range(3) if m[key][i][j] > 0}
+        assert nz == {(0, 1), (2, 0)}
