@@ -9,6 +9,7 @@
 #include "bootstrap.hpp"
 #include "common.hpp"
 #include "report.hpp"
+#include "topology.hpp"
 #include "transport.hpp"
 #include "units.hpp"
 
@@ -65,6 +66,7 @@ output
       --compat-only      only the reference matrices
       --no-compat        only the extended tables
       --dry-run          print the schedules and exit
+      --topology         print the GPU link matrix (xGMI/PCIe, hops, peer access) and exit
   -v, --verbose          -h, --help      --version
 )";
 }
@@ -207,6 +209,8 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
       cfg->compat = false;
     } else if (a == "--dry-run") {
       cfg->dry_run = true;
+    } else if (a == "--topology") {
+      cfg->topology_only = true;
     } else if (a == "-v" || a == "--verbose") {
       cfg->verbose++;
     } else {
@@ -280,6 +284,10 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
   if (cfg.dry_run) {
     if (root)
       for (const auto& s : scheds) print_schedule(out, s);
+    return 0;
+  }
+  if (cfg.topology_only) {
+    if (root) std::fprintf(out, "%s", topology_report().c_str());
     return 0;
   }
 
@@ -380,6 +388,7 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
       std::fprintf(out, "\n== p2p_matrix: %d rank(s), transport %s, bootstrap %s, %d host(s) ==\n", n, t->name().c_str(),
                    boot.name().c_str(), pl.num_hosts);
       for (int r = 0; r < n; ++r) std::fprintf(out, "  rank %d: %s\n", r, &all_desc[static_cast<size_t>(r) * sizeof(mine)]);
+      if (t->name() != "host") std::fprintf(out, "%s", topology_report().c_str());
       for (const auto& rec : res.runs) print_extended(out, rec, n);
       print_latency(out, res.latency, n);
     }

@@ -45,6 +45,7 @@ struct AppConfig {
   double timeout_s = 300;
   int verify_impl = 0;
   bool dry_run = false;    // print the schedules and exit (no transport)
+  bool topology_only = false;  // print the GPU link matrix and exit
   bool warm_connections = true;
   int verbose = 0;
 };

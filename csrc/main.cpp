@@ -21,7 +21,7 @@ int main(int argc, char** argv) {
   bool dry = false;
   for (int i = 1; i < argc; ++i)
     if (!std::strcmp(argv[i], "--dry-run") || !std::strcmp(argv[i], "--help") || !std::strcmp(argv[i], "-h") ||
-        !std::strcmp(argv[i], "--version"))
+        !std::strcmp(argv[i], "--version") || !std::strcmp(argv[i], "--topology"))
       dry = true;
   if (dry && boot_kind == "auto" && !p2p::mpi_launch_detected()) boot_kind = "local";
 

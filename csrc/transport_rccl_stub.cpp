@@ -17,3 +17,14 @@ std::unique_ptr<Transport> make_ipc_transport(Bootstrap&, const TransportOptions
 bool rccl_transport_available() { return false; }
 
 }  // namespace p2p
+
+// Topology probe stubs for host-only builds.
+#include "topology.hpp"
+
+namespace p2p {
+std::vector<LinkInfo> probe_topology(int* ndev) {
+  *ndev = 0;
+  return {};
+}
+std::string topology_report() { return "GPU link topology: not available in this host-only build\n"; }
+}  // namespace p2p

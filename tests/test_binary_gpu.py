@@ -53,3 +53,9 @@ def test_bench_contract_single_gpu():
     r = json.loads(lines[0])
     assert r["n_gpus"] == 1 and r["steps"] == 6 and r["value"] > 10
     assert r["verify_mismatches"] == 0 and r["transport"] == "rccl"
+
+
+def test_topology_probe(exe):
+    out = subprocess.run([exe, "--topology"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "GPU link topology" in out.stdout and "visible" in out.stdout
