@@ -106,14 +106,31 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
       val = a.substr(eq + 1);
       a = a.substr(0, eq);
     }
+    bool missing = false;
     auto next = [&]() -> std::string {
       if (has_eq) return val;
       if (i + 1 >= argc) {
-        std::fprintf(stderr, "p2p_matrix: option %s needs a value\n", a.c_str());
-        std::exit(1);
+        missing = true;
+        return "";
       }
       return argv[++i];
     };
+    auto value_ok = [&]() {
+      if (!missing) return true;
+      std::fprintf(stderr, "p2p_matrix: option %s needs a value\n", a.c_str());
+      *exit_code = 1;
+      return false;
+    };
+    // Options taking a value check it before use.
+    static const char* kValued[] = {"-m", "--mode", "-d", "--dir", "-b", "--size", "--sizes", "-n", "--iters", "-w",
+                                    "--warmup", "--timing", "--latency-size", "--latency-iters", "--verify-impl",
+                                    "--transport", "--ipc-engine", "--bootstrap", "--device", "--timeout", "--json",
+                                    "--csv", "--trace", "--cells"};
+    for (const char* v : kValued)
+      if (a == v && !has_eq && i + 1 >= argc) {
+        missing = true;
+        return value_ok();
+      }
     if (a == "-h" || a == "--help") {
       std::fprintf(out, "%s", usage_text().c_str());
       return false;

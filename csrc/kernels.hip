@@ -227,15 +227,49 @@ __global__ __launch_bounds__(kBlock) void verify_stride_kernel(const uint4* __re
 // wrote.  The four ds_read_b128 live in one asm statement: hipcc cannot tell
 // which LDS-DMA a ds_read aliases and would put a vmcnt(0) in front of each
 // one; the asm drains its own reads (lgkmcnt(0)).
-template <bool CHECK>
+// Reads this lane's 16 B of each of STAGES consecutive 1 KiB LDS pieces in
+// one asm statement and drains them (lgkmcnt(0)) before returning.
+template <int STAGES>
+__device__ __forceinline__ void lds_read_stages(uint32_t addr, u32x4 (&r)[STAGES]);
+
+template <>
+__device__ __forceinline__ void lds_read_stages<4>(uint32_t addr, u32x4 (&r)[4]) {
+  asm volatile(
+      "ds_read_b128 %0, %4\n\t"
+      "ds_read_b128 %1, %4 offset:1024\n\t"
+      "ds_read_b128 %2, %4 offset:2048\n\t"
+      "ds_read_b128 %3, %4 offset:3072\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3])
+      : "v"(addr)
+      : "memory");
+}
+
+template <>
+__device__ __forceinline__ void lds_read_stages<8>(uint32_t addr, u32x4 (&r)[8]) {
+  asm volatile(
+      "ds_read_b128 %0, %8\n\t"
+      "ds_read_b128 %1, %8 offset:1024\n\t"
+      "ds_read_b128 %2, %8 offset:2048\n\t"
+      "ds_read_b128 %3, %8 offset:3072\n\t"
+      "ds_read_b128 %4, %8 offset:4096\n\t"
+      "ds_read_b128 %5, %8 offset:5120\n\t"
+      "ds_read_b128 %6, %8 offset:6144\n\t"
+      "ds_read_b128 %7, %8 offset:7168\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3]), "=v"(r[4]), "=v"(r[5]), "=v"(r[6]), "=v"(r[7])
+      : "v"(addr)
+      : "memory");
+}
+
+template <bool CHECK, int STAGES>
 __global__ __launch_bounds__(kBlock) void verify_lds_kernel(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
                                                             const uint8_t* __restrict__ tail, uint32_t tail_bytes,
                                                             uint64_t tail_offset, VerifyAccum* __restrict__ out) {
-  static_assert(kLdsStages == 4, "asm block reads exactly four stages");
-  __shared__ uint4 slot[kWaves][kLdsStages][64];
+  __shared__ uint4 slot[kWaves][STAGES][64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x / 64;
-  const uint64_t sc_vecs = static_cast<uint64_t>(kLdsStages) * 64;
+  const uint64_t sc_vecs = static_cast<uint64_t>(STAGES) * 64;
   const uint64_t n_sc = (nvec + sc_vecs - 1) / sc_vecs;
   const uint32_t lds_addr = static_cast<uint32_t>(
       reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)(&slot[wave][0][lane])));
@@ -243,27 +277,18 @@ __global__ __launch_bounds__(kBlock) void verify_lds_kernel(const uint4* __restr
   for (uint64_t sc = static_cast<uint64_t>(blockIdx.x) * kWaves + wave; sc < n_sc;
        sc += static_cast<uint64_t>(gridDim.x) * kWaves) {
 #pragma unroll
-    for (int s = 0; s < kLdsStages; ++s) {
+    for (int s = 0; s < STAGES; ++s) {
       const uint64_t i = sc * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
       if (i < nvec)
         __builtin_amdgcn_global_load_lds(static_cast<const void*>(p + i),
                                          (__attribute__((address_space(3))) void*)(&slot[wave][s][0]), 16, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    u32x4 r0, r1, r2, r3;
-    asm volatile(
-        "ds_read_b128 %0, %4\n\t"
-        "ds_read_b128 %1, %4 offset:1024\n\t"
-        "ds_read_b128 %2, %4 offset:2048\n\t"
-        "ds_read_b128 %3, %4 offset:3072\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=v"(r0), "=v"(r1), "=v"(r2), "=v"(r3)
-        : "v"(lds_addr)
-        : "memory");
-    const u32x4 rv[kLdsStages] = {r0, r1, r2, r3};
+    u32x4 rv[STAGES];
+    lds_read_stages<STAGES>(lds_addr, rv);
     const uint32_t key = prng_key(seed, sc * sc_vecs * 4);  // wave-uniform
 #pragma unroll
-    for (int s = 0; s < kLdsStages; ++s) {
+    for (int s = 0; s < STAGES; ++s) {
       const uint64_t i = sc * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
       if (i < nvec) check_vec<CHECK>(make_uint4(rv[s].x, rv[s].y, rv[s].z, rv[s].w), key, i, acc);
     }
@@ -347,15 +372,15 @@ LaunchGeom verify_geometry(size_t bytes, VerifyImpl impl, unsigned max_grid) {
   // atomic commit, so a full grid (one 4 KiB block per workgroup) pays that
   // epilogue 256K times per GiB; the defaults below cap the grid so each
   // workgroup streams tens of KiB per epilogue (kernel_bench A/B).
-  const uint64_t per_cu = impl == VerifyImpl::Lds ? kVerifyLdsPerCu
+  const uint64_t per_cu = (impl == VerifyImpl::Lds || impl == VerifyImpl::Lds8) ? kVerifyLdsPerCu
                           : impl == VerifyImpl::Stride ? kVerifyStridePerCu
                                                        : kVerifyGridPerCu;
   const uint64_t cap = max_grid ? max_grid : static_cast<uint64_t>(cu_count()) * per_cu;
-  if (impl == VerifyImpl::Lds) {
-    const uint64_t sc_vecs = static_cast<uint64_t>(kLdsStages) * 64;
+  if (impl == VerifyImpl::Lds || impl == VerifyImpl::Lds8) {
+    const uint64_t sc_vecs = static_cast<uint64_t>(impl == VerifyImpl::Lds8 ? 8 : kLdsStages) * 64;
     const uint64_t waves = (nvec + sc_vecs - 1) / sc_vecs;
     g.grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min((waves + kWaves - 1) / kWaves, cap)));
-    g.lds_bytes = sizeof(uint4) * kWaves * kLdsStages * 64;
+    g.lds_bytes = sizeof(uint4) * kWaves * (impl == VerifyImpl::Lds8 ? 8 : kLdsStages) * 64;
   } else if (impl == VerifyImpl::Stride) {
     const uint64_t tiles = (nvec + kBlock * kStrideUnroll - 1) / (kBlock * kStrideUnroll);
     g.grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min(tiles, cap)));
@@ -398,7 +423,10 @@ void launch_verify_t(const uint4* vp, uint64_t nvec, uint64_t seed, const uint8_
                      VerifyImpl impl, const LaunchGeom& g, hipStream_t stream) {
   switch (impl) {
     case VerifyImpl::Lds:
-      verify_lds_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
+      verify_lds_kernel<CHECK, kLdsStages><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
+      break;
+    case VerifyImpl::Lds8:
+      verify_lds_kernel<CHECK, 8><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
       break;
     case VerifyImpl::Stride:
       verify_stride_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
