@@ -47,7 +47,8 @@ timing
       --latency-size S   [8]      --latency-iters N   [1000]
 data
   -c, --verify           random-fill sends, verify every received buffer on the device
-      --verify-impl I    auto | reg | lds  (register- or LDS-DMA-staged verify kernel)
+      --verify-impl I    auto (= lds) | lds | lds8 | lds-cached | stride | reg
+                         (LDS-DMA- or register-staged verify kernel variants)
 transport / launch
       --transport T      rccl  MI355X + RCCL ncclSend/ncclRecv over xGMI      [rccl]
                          ipc   one-sided pulls from hipIpc-mapped peer buffers (gfx950 copy
@@ -183,7 +184,12 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
       cfg->run.verify = false;
     } else if (a == "--verify-impl") {
       std::string v = next();
-      cfg->verify_impl = v == "reg" || v == "register" ? 1 : v == "lds" ? 2 : 0;
+      cfg->verify_impl = v == "reg" || v == "register" ? 1
+                         : v == "lds"                  ? 2
+                         : v == "stride"               ? 3
+                         : v == "lds8"                 ? 4
+                         : v == "lds-cached"           ? 5
+                                                       : 0;
     } else if (a == "--transport") {
       cfg->transport = next();
     } else if (a == "--ipc-engine") {

@@ -41,13 +41,16 @@ constexpr int kStrideUnroll = 4;            // legacy grid-stride variants
 constexpr int kStrideBlocksPerCu = 8;        // legacy fill stride grid
 constexpr int kLdsStages = 4;               // 1 KiB LDS-DMA pieces per wave (4 KiB per wave)
 // Verify grid caps per variant, from scripts/verify_grid_sweep.py on MI355X
-// (1 GiB / 4 GiB, TB/s): stride 16/CU 6.41 / 6.73; full-grid register 256/CU
-// 5.67 / 6.86 (uncapped: 2.25 / 2.44, epilogue-bound); LDS 4/CU 5.83 / 5.83.
+// (1 GiB / 4 GiB, TB/s): LDS-DMA nt 16/CU 6.32 / 6.58; register stride 16/CU
+// 6.42 / 6.72; full-grid register 256/CU 5.61 / 6.71 (uncapped: 2.3 / 2.5,
+// epilogue-bound); LDS-DMA default cache policy 5.7 / 5.9 at any cap.
 constexpr int kVerifyStridePerCu = 16;
 constexpr int kVerifyGridPerCu = 256;
-constexpr int kVerifyLdsPerCu = 4;
+constexpr int kVerifyLdsPerCu = 16;
 constexpr FillImpl kDefaultFill = FillImpl::Grid;
-constexpr VerifyImpl kDefaultVerify = VerifyImpl::Stride;
+// LDS-staged verify is the default: with non-temporal LDS-DMA it runs within
+// 2-3% of register staging (profiles/r1_tuned/verify_grid_sweep.txt).
+constexpr VerifyImpl kDefaultVerify = VerifyImpl::Lds;
 
 #define HIP_OK(cmd)                                                                          \
   do {                                                                                       \
@@ -262,7 +265,7 @@ __device__ __forceinline__ void lds_read_stages<8>(uint32_t addr, u32x4 (&r)[8])
       : "memory");
 }
 
-template <bool CHECK, int STAGES>
+template <bool CHECK, int STAGES, int AUX>
 __global__ __launch_bounds__(kBlock) void verify_lds_kernel(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
                                                             const uint8_t* __restrict__ tail, uint32_t tail_bytes,
                                                             uint64_t tail_offset, VerifyAccum* __restrict__ out) {
@@ -281,7 +284,7 @@ __global__ __launch_bounds__(kBlock) void verify_lds_kernel(const uint4* __restr
       const uint64_t i = sc * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
       if (i < nvec)
         __builtin_amdgcn_global_load_lds(static_cast<const void*>(p + i),
-                                         (__attribute__((address_space(3))) void*)(&slot[wave][s][0]), 16, 0, 0);
+                                         (__attribute__((address_space(3))) void*)(&slot[wave][s][0]), 16, 0, AUX);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     u32x4 rv[STAGES];
@@ -372,11 +375,11 @@ LaunchGeom verify_geometry(size_t bytes, VerifyImpl impl, unsigned max_grid) {
   // atomic commit, so a full grid (one 4 KiB block per workgroup) pays that
   // epilogue 256K times per GiB; the defaults below cap the grid so each
   // workgroup streams tens of KiB per epilogue (kernel_bench A/B).
-  const uint64_t per_cu = (impl == VerifyImpl::Lds || impl == VerifyImpl::Lds8) ? kVerifyLdsPerCu
+  const uint64_t per_cu = (impl == VerifyImpl::Lds || impl == VerifyImpl::Lds8 || impl == VerifyImpl::LdsCached) ? kVerifyLdsPerCu
                           : impl == VerifyImpl::Stride ? kVerifyStridePerCu
                                                        : kVerifyGridPerCu;
   const uint64_t cap = max_grid ? max_grid : static_cast<uint64_t>(cu_count()) * per_cu;
-  if (impl == VerifyImpl::Lds || impl == VerifyImpl::Lds8) {
+  if (impl == VerifyImpl::Lds || impl == VerifyImpl::Lds8 || impl == VerifyImpl::LdsCached) {
     const uint64_t sc_vecs = static_cast<uint64_t>(impl == VerifyImpl::Lds8 ? 8 : kLdsStages) * 64;
     const uint64_t waves = (nvec + sc_vecs - 1) / sc_vecs;
     g.grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min((waves + kWaves - 1) / kWaves, cap)));
@@ -423,10 +426,15 @@ void launch_verify_t(const uint4* vp, uint64_t nvec, uint64_t seed, const uint8_
                      VerifyImpl impl, const LaunchGeom& g, hipStream_t stream) {
   switch (impl) {
     case VerifyImpl::Lds:
-      verify_lds_kernel<CHECK, kLdsStages><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
+      // aux = 2: non-temporal LDS-DMA (MI355X_MICROARCH.md ldsdma-fill row: 6.4 TB/s default
+      // policy vs 6.5-6.8 nt); measured here 6.3 / 6.6 TB/s nt vs 5.7 / 5.9 default policy.
+      verify_lds_kernel<CHECK, kLdsStages, 2><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
       break;
     case VerifyImpl::Lds8:
-      verify_lds_kernel<CHECK, 8><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
+      verify_lds_kernel<CHECK, 8, 2><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
+      break;
+    case VerifyImpl::LdsCached:
+      verify_lds_kernel<CHECK, kLdsStages, 0><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
       break;
     case VerifyImpl::Stride:
       verify_stride_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);

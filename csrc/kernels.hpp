@@ -5,18 +5,20 @@
 // These kernels replace that with verifiable random payloads:
 //   fill    — counter-based PRNG, one 16-byte global_store_dwordx4 per lane
 //   verify  — regenerates the stream and compares; staging variants:
-//               * stride (default): 4 x global_load_dwordx4 in flight per
-//                           lane, grid capped at 16 workgroups per CU so the
+//               * LDS (default): non-temporal global_load_lds_dwordx4
+//                           (LDS-DMA, 1 KiB per wave instruction) into a
+//                           per-wave LDS slot, then ds_read_b128 — the
+//                           LDS-staged form the north star asks for; 6.3 / 6.6
+//                           TB/s at 1 / 4 GiB, within 2-3% of register staging
+//                           (SURVEY.md §7.5 item 6 A/B).  Lds8 stages 8 KiB per
+//                           wave; LdsCached keeps the default cache policy
+//                           (5.7-5.9 TB/s, the A/B that chose nt)
+//               * stride:   register staging, 4 x global_load_dwordx4 in flight
+//                           per lane, grid capped at 16 workgroups per CU so the
 //                           reduction epilogue is amortised over 64 KiB+
 //               * register: one global_load_dwordx4 per lane per iteration
 //                           (the full-grid shape of fill/copy, capped at
 //                           256 workgroups per CU)
-//               * LDS:      global_load_lds_dwordx4 (LDS-DMA, 1 KiB per wave
-//                           instruction) into a per-wave LDS slot, then
-//                           ds_read_b128 — the LDS-staged form the north star
-//                           asks for, A/B-tested against register staging
-//                           (SURVEY.md §7.5 item 6): ~13% slower, as the
-//                           extra LDS round trip predicts for pure streaming
 //   reduce  — fused epilogue of verify: wave64 __shfl_xor tree -> LDS across
 //             the 4 waves -> one atomic per block into one of kVerifyShards
 //             64-byte counters (no single hot address), then a one-wave
@@ -51,7 +53,7 @@ struct alignas(64) VerifyAccum {
 constexpr int kVerifyShards = 64;
 constexpr size_t verify_accum_bytes() { return sizeof(VerifyAccum) * kVerifyShards; }
 
-enum class VerifyImpl : int { Auto = 0, Register = 1, Lds = 2, Stride = 3, Lds8 = 4 };
+enum class VerifyImpl : int { Auto = 0, Register = 1, Lds = 2, Stride = 3, Lds8 = 4, LdsCached = 5 };
 enum class FillImpl : int { Auto = 0, Grid = 1, Nontemporal = 2, Stride = 3 };
 
 // Geometry chosen for a launch (exposed for tests / profiling scripts).
