@@ -41,16 +41,18 @@ constexpr int kStrideUnroll = 4;            // legacy grid-stride variants
 constexpr int kStrideBlocksPerCu = 8;        // legacy fill stride grid
 constexpr int kLdsStages = 4;               // 1 KiB LDS-DMA pieces per wave (4 KiB per wave)
 // Verify grid caps per variant, from scripts/verify_grid_sweep.py on MI355X
-// (1 GiB / 4 GiB, TB/s): LDS-DMA nt 16/CU 6.32 / 6.58; register stride 16/CU
-// 6.42 / 6.72; full-grid register 256/CU 5.61 / 6.71 (uncapped: 2.3 / 2.5,
-// epilogue-bound); LDS-DMA default cache policy 5.7 / 5.9 at any cap.
+// (1 GiB / 4 GiB, TB/s, run-to-run noise ~5%): LDS-DMA nt 8 KiB/wave 16/CU
+// 6.44 / 6.64; 4 KiB/wave 5.5-6.3 / 6.4-6.6; register stride 16/CU 6.5 / 6.7;
+// full-grid register 256/CU 5.6-6.4 / 6.7 (uncapped: 2.3 / 2.5, epilogue-bound);
+// LDS-DMA default cache policy 5.7 / 5.9 at any cap.
 constexpr int kVerifyStridePerCu = 16;
 constexpr int kVerifyGridPerCu = 256;
 constexpr int kVerifyLdsPerCu = 16;
 constexpr FillImpl kDefaultFill = FillImpl::Grid;
-// LDS-staged verify is the default: with non-temporal LDS-DMA it runs within
-// 2-3% of register staging (profiles/r1_tuned/verify_grid_sweep.txt).
-constexpr VerifyImpl kDefaultVerify = VerifyImpl::Lds;
+// LDS-staged verify is the default: 8 KiB of non-temporal LDS-DMA per wave
+// runs within 1-2% of register staging (profiles/r1_tuned/verify_grid_sweep.txt:
+// 6.44 / 6.64 TB/s at 1 / 4 GiB vs 6.53 / 6.74).
+constexpr VerifyImpl kDefaultVerify = VerifyImpl::Lds8;
 
 #define HIP_OK(cmd)                                                                          \
   do {                                                                                       \

@@ -5,13 +5,13 @@
 // These kernels replace that with verifiable random payloads:
 //   fill    — counter-based PRNG, one 16-byte global_store_dwordx4 per lane
 //   verify  — regenerates the stream and compares; staging variants:
-//               * LDS (default): non-temporal global_load_lds_dwordx4
+//               * LDS (default Lds8): non-temporal global_load_lds_dwordx4
 //                           (LDS-DMA, 1 KiB per wave instruction) into a
-//                           per-wave LDS slot, then ds_read_b128 — the
-//                           LDS-staged form the north star asks for; 6.3 / 6.6
-//                           TB/s at 1 / 4 GiB, within 2-3% of register staging
-//                           (SURVEY.md §7.5 item 6 A/B).  Lds8 stages 8 KiB per
-//                           wave; LdsCached keeps the default cache policy
+//                           per-wave LDS slot of 8 KiB (Lds: 4 KiB), then
+//                           ds_read_b128 — the LDS-staged form the north star
+//                           asks for; 6.44 / 6.64 TB/s at 1 / 4 GiB, within
+//                           1-2% of register staging (SURVEY.md §7.5 item 6
+//                           A/B).  LdsCached keeps the default cache policy
 //                           (5.7-5.9 TB/s, the A/B that chose nt)
 //               * stride:   register staging, 4 x global_load_dwordx4 in flight
 //                           per lane, grid capped at 16 workgroups per CU so the

@@ -94,3 +94,55 @@ def scaling_table(results: Iterable[dict]) -> str:
             r["n_gpus"], r["value"], r["value"] / r["n_gpus"], r.get("matrix_gbs_min"), r.get("matrix_gbs_mean"),
             r.get("p50_latency_us"), eff))
     return "\n".join(out)
+
+
+def summarize_compat(text: str) -> str:
+    """GB/s min/mean/max (off-diagonal) of each reference-format matrix."""
+    from .stats import offdiag_summary
+
+    lines = []
+    for key, m in parse_compat(text).items():
+        s = offdiag_summary(gbps_to_gbs(m))
+        lines.append("%s: %d ranks, GB/s min %.2f mean %.2f max %.2f over %d cells"
+                     % (key, len(m), s["min"], s["mean"], s["max"], s["cells"]))
+    return "\n".join(lines)
+
+
+def main(argv=None) -> int:
+    """python -m test_nccl_p2p_amd.utils.report FILE...
+
+    Reference-format text (e.g. `mpirun ... > result.txt`) -> GB/s summary;
+    bench.py JSON lines -> scaling table; p2p_matrix --json lines -> per-run
+    min/mean GB/s."""
+    import argparse
+
+    ap = argparse.ArgumentParser(description=main.__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("files", nargs="+")
+    a = ap.parse_args(argv)
+    for path in a.files:
+        text = open(path).read()
+        print("== %s" % path)
+        recs = []
+        for line in text.splitlines():
+            line = line.strip()
+            if line.startswith("{"):
+                try:
+                    recs.append(json.loads(line))
+                except ValueError:
+                    pass
+        bench = [r for r in recs if "metric" in r and "n_gpus" in r]
+        runs = [r for r in recs if r.get("type") == "run"]
+        if bench:
+            print(scaling_table(bench))
+        for r in runs:
+            print("%-10s %-3s %10d B x %4d: GB/s min %.2f mean %.2f max %.2f"
+                  % (r["mode"], r["dir"], r["bytes"], r["iters"], r["gbs_min"], r["gbs_mean"], r["gbs_max"]))
+        if UNI_TITLE in text or BI_TITLE in text:
+            print(summarize_compat(text))
+    return 0
+
+
+if __name__ == "__main__":
+    import sys
+
+    sys.exit(main())
