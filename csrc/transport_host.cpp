@@ -69,9 +69,6 @@ namespace {
 void sockopts(int fd) {
   int one = 1;
   setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
-  int buf = 4 << 20;
-  setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &buf, sizeof(buf));
-  setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof(buf));
 }
 
 void blocking_io(int fd, void* buf, size_t n, bool is_send, double timeout_s) {
@@ -263,6 +260,10 @@ class HostTransport final : public Transport {
         if ((pf.revents & (POLLIN | POLLHUP)) && !recvq[peer].empty()) {
           Op* op = recvq[peer].front();
           ssize_t k = ::recv(pf.fd, op->buf + op->done, op->bytes - op->done, MSG_DONTWAIT);
+          // Re-arm quick ACKs: a delayed ACK stalls a sender whose message is
+          // larger than its current send window.
+          int one = 1;
+          setsockopt(pf.fd, IPPROTO_TCP, TCP_QUICKACK, &one, sizeof(one));
           if (k > 0) op->done += static_cast<size_t>(k);
           else if (k == 0) P2P_FATAL(strfmt("host transport: peer %d closed the connection", peer));
           else if (errno != EAGAIN && errno != EINTR)
