@@ -40,13 +40,14 @@ PY_INC    := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_paths()[
 PYBIND    := $(shell $(PYTHON) -c "import pybind11;print(pybind11.get_include())")
 EXT       := test_nccl_p2p_amd/_p2pcore$(PY_EXT)
 
-.PHONY: all gpu host ext test test-host test-gpu asan clean
+.PHONY: all gpu host ext tools test test-host test-gpu asan clean
 
-all: gpu host ext
+all: gpu host ext tools
 
 gpu: $(BUILD)/p2p_matrix
 host: $(BUILD)/p2p_matrix_host $(BUILD)/p2p_host_tests
 ext: $(EXT)
+tools: $(BUILD)/fill_probe
 
 $(BUILD)/gpu $(BUILD)/host $(BUILD)/asan:
 	mkdir -p $@
@@ -93,6 +94,10 @@ $(BUILD)/gpu/pymodule.o: csrc/pymodule.cpp $(HEADERS) | $(BUILD)/gpu
 $(EXT): $(GPU_OBJS) $(BUILD)/gpu/pymodule.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared $(GPU_OBJS) $(BUILD)/gpu/pymodule.o -o $@ \
 	    -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib -pthread
+
+# Grid-shape probe (scripts/fill_probe.hip): standalone, no framework code.
+$(BUILD)/fill_probe: scripts/fill_probe.hip | $(BUILD)/gpu
+	$(HIPCC) --offload-arch=$(ARCH) -O3 $< -o $@
 
 # AddressSanitizer / UBSan on host code only (GPU sanitizers are not available).
 ASAN := -fsanitize=address,undefined -fno-omit-frame-pointer -g -O1
