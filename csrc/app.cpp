@@ -41,7 +41,9 @@ timing
   -w, --warmup N         untimed iterations per cell                          [8]
       --timing MODE      events    hipEvents, back-to-back messages, 1 sync  [events]
                          wallclock reference semantics: host clock, sync per message
-      --reference        = --timing wallclock --warmup 0 --no-warm (the reference's methodology)
+      --reference        = --timing wallclock --warmup 0 --no-warm --two-streams
+                         (the reference's methodology, p2p_matrix.cc:141-267)
+      --two-streams      RCCL: receives on a second stream, like the reference's s_1
       --no-warm          do not pre-establish connections before timing
   -l, --latency          add a ping-pong latency matrix
       --latency-size S   [8]      --latency-iters N   [1000]
@@ -168,6 +170,9 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
       cfg->run.timing = Timing::Wallclock;
       cfg->run.warmup = 0;
       cfg->warm_connections = false;
+      cfg->two_streams = true;
+    } else if (a == "--two-streams") {
+      cfg->two_streams = true;
     } else if (a == "--no-warm") {
       cfg->warm_connections = false;
     } else if (a == "-l" || a == "--latency") {
@@ -322,6 +327,7 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
   topt.timeout_s = cfg.timeout_s;
   topt.verify_impl = cfg.verify_impl;
   topt.ipc_engine = cfg.ipc_engine;
+  topt.two_streams = cfg.two_streams;
   std::unique_ptr<Transport> t = cfg.transport == "host"  ? make_host_transport(boot, topt)
                                  : cfg.transport == "ipc" ? make_ipc_transport(boot, topt)
                                                           : make_rccl_transport(boot, topt);

@@ -47,6 +47,7 @@ struct AppConfig {
   bool dry_run = false;    // print the schedules and exit (no transport)
   bool topology_only = false;  // print the GPU link matrix and exit
   bool warm_connections = true;
+  bool two_streams = false;  // RCCL receives on a second stream (reference layout)
   int verbose = 0;
 };
 

@@ -1,11 +1,14 @@
 // Data plane abstraction: buffers, grouped point-to-point ops, timestamps.
 //
 // The measurement engine (runner.cpp) is written against this interface only.
-// Two implementations:
+// Three implementations:
 //   * RcclTransport (transport_rccl.cpp, HIP + RCCL): MI355X device buffers in
 //     HBM3E, ncclSend/ncclRecv over xGMI inside ncclGroupStart/End (reference
 //     call sites p2p_matrix.cc:156-169, 211-249), hipEvent timestamps on the
 //     comm stream, hand-written gfx950 fill/verify kernels.
+//   * IpcTransport (transport_ipc.cpp, HIP): one-sided pulls from hipIpc-mapped
+//     peer send buffers by the gfx950 multi-copy kernel (or SDMA) — the
+//     hand-written data plane, and the multi-rank path on one GPU.
 //   * HostTransport (transport_host.cpp): host memory over a TCP mesh, steady
 //     clock timestamps.  Same schedule, same runner, same report — it is the
 //     CPU plumbing path (BASELINE.json config 1) and what the CPU test tier
@@ -87,6 +90,7 @@ struct TransportOptions {
   bool nonblocking_init = true;    // RCCL: ncclCommInitRankConfig(blocking=0) + polling
   int verify_impl = 0;             // 0 = auto, 1 = register-staged, 2 = LDS-staged (global_load_lds)
   std::string ipc_engine = "kernel";  // IPC transport copy engine: kernel (gfx950 pull kernel) | sdma
+  bool two_streams = false;        // RCCL: receives on a second stream (reference layout)
 };
 
 // HIP + RCCL on the local MI355X.  Defined in transport_rccl.cpp (hipcc).

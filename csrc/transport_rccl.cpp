@@ -14,8 +14,9 @@
 //     blocking = 0) and polled with a deadline, and every sync is a bounded
 //     poll of hipStreamQuery + ncclCommGetAsyncError: a dead peer becomes
 //     ncclCommAbort + a fatal error on every rank instead of a silent hang.
-//   * One non-blocking stream: the reference's second stream for the bi
-//     direction is joined by the group anyway.
+//   * One non-blocking stream by default: the reference's second stream for
+//     the bi direction is joined by the group anyway; --two-streams (implied
+//     by --reference) restores its s_0 / s_1 layout.
 //   * hipEvents on the stream give GPU-timeline timestamps.
 //   * Payloads are written / checked by the gfx950 kernels in kernels.hip.
 #include <hip/hip_runtime.h>
@@ -56,6 +57,10 @@ class RcclTransport final : public Transport {
       P2P_FATAL(strfmt("rank %d wants GPU %d but only %d are visible: more ranks per host than GPUs", rank_, device_, ndev));
     HIPCHECK(hipSetDevice(device_));
     HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    if (opt.two_streams) {
+      HIPCHECK(hipStreamCreateWithFlags(&recv_stream_, hipStreamNonBlocking));
+      HIPCHECK(hipEventCreateWithFlags(&join_, hipEventDisableTiming));
+    }
     HIPCHECK(hipMalloc(&acc_, dev::verify_accum_bytes()));
     HIPCHECK(hipHostMalloc(&acc_host_, sizeof(dev::VerifyAccum), hipHostMallocDefault));
 
@@ -106,6 +111,8 @@ class RcclTransport final : public Transport {
     for (auto ev : events_) (void)hipEventDestroy(ev);
     if (acc_) (void)hipFree(acc_);
     if (acc_host_) (void)hipHostFree(acc_host_);
+    if (recv_stream_) (void)hipStreamDestroy(recv_stream_);
+    if (join_) (void)hipEventDestroy(join_);
     if (stream_) (void)hipStreamDestroy(stream_);
   }
 
@@ -144,13 +151,22 @@ class RcclTransport final : public Transport {
     nccl_ok(ncclSend(p, bytes, ncclUint8, peer, comm_, stream_), "ncclSend");
   }
   void recv(void* p, size_t bytes, int peer) override {
-    nccl_ok(ncclRecv(p, bytes, ncclUint8, peer, comm_, stream_), "ncclRecv");
+    nccl_ok(ncclRecv(p, bytes, ncclUint8, peer, comm_, recv_stream_ ? recv_stream_ : stream_), "ncclRecv");
+    recv_on_side_ = recv_stream_ != nullptr;
   }
   void group_end() override {
     ncclResult_t r = ncclGroupEnd();
     // Non-blocking comm: the ops are only enqueued once the comm leaves
     // ncclInProgress, so wait before any event is recorded behind them.
     wait_ready(r, "ncclGroupEnd");
+    if (recv_on_side_) {
+      // Reference two-stream layout (sends on s_0, receives on s_1,
+      // p2p_matrix.cc:214-225): join s_1 back so marks and syncs on the main
+      // stream cover the receives too.
+      HIPCHECK(hipEventRecord(join_, recv_stream_));
+      HIPCHECK(hipStreamWaitEvent(stream_, join_, 0));
+      recv_on_side_ = false;
+    }
   }
 
   int mark() override {
@@ -252,6 +268,9 @@ class RcclTransport final : public Transport {
   int device_ = 0;
   bool nonblocking_ = true;
   hipStream_t stream_ = nullptr;
+  hipStream_t recv_stream_ = nullptr;  // two-stream (reference) layout only
+  hipEvent_t join_ = nullptr;
+  bool recv_on_side_ = false;
   ncclComm_t comm_ = nullptr;
   std::vector<hipEvent_t> events_;
   std::vector<hipGraph_t> graphs_;

@@ -59,3 +59,12 @@ def test_topology_probe(exe):
     out = subprocess.run([exe, "--topology"], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     assert "GPU link topology" in out.stdout and "visible" in out.stdout
+
+
+def test_reference_methodology_two_streams(exe):
+    # --reference: wall clock, sync per message, no warmup, receives on a
+    # second stream (the reference's s_1); self path so one GPU suffices.
+    out = subprocess.run([exe, "--mode", "self", "--size", "32M", "-n", "16", "--reference", "--verify", "--no-compat"],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert "timing=wallclock warmup=0" in out.stdout and "verification: OK" in out.stdout
