@@ -1,0 +1,75 @@
+"""Python utilities: statistics parity with the native engine, report CLI,
+RCCL environment capture."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+from test_nccl_p2p_amd.utils import rccl_env
+from test_nccl_p2p_amd.utils.report import compat_matrix_text, main as report_main, summarize_compat
+from test_nccl_p2p_amd.utils.stats import offdiag_summary, percentile, summarize
+
+
+def test_percentiles_match_native_convention():
+    # Same cases as tests/host/test_main.cpp test_stats.
+    assert percentile([5, 1, 4, 2, 3], 50) == 3
+    assert percentile([1, 2, 3, 4], 50) == 2.5
+    assert abs(percentile([1, 2, 3, 4], 90) - 3.7) < 1e-12
+    s = summarize([5, 1, 4, 2, 3])
+    assert s["n"] == 5 and s["mean"] == 3 and abs(s["stdev"] - 2.5 ** 0.5) < 1e-12
+    assert summarize([])["n"] == 0
+
+
+def test_offdiag_summary():
+    m = [[0, 10, 20], [30, 0, 40], [50, 60, 0]]
+    s = offdiag_summary(m)
+    assert s == {"min": 10, "mean": 35, "max": 60, "cells": 6}
+
+
+def test_summarize_compat():
+    txt = compat_matrix_text([[0, 80.0], [160.0, 0]], "uni")
+    out = summarize_compat(txt)
+    assert "uni: 2 ranks, GB/s min 10.00 mean 15.00 max 20.00" in out
+
+
+def test_report_cli(tmp_path, capsys):
+    f = tmp_path / "result.txt"
+    f.write_text(compat_matrix_text([[0, 8.0], [16.0, 0]], "uni") + compat_matrix_text([[0, 8.0], [8.0, 0]], "bi"))
+    j = tmp_path / "bench.jsonl"
+    j.write_text(json.dumps({"metric": "m", "n_gpus": 2, "value": 100.0, "matrix_gbs_min": 50,
+                             "matrix_gbs_mean": 50, "p50_latency_us": 10}) + "\n")
+    assert report_main([str(f), str(j)]) == 0
+    out = capsys.readouterr().out
+    assert "bi: 2 ranks" in out and "| 2 | 100.0 | 50.0 |" in out
+
+
+def test_rccl_env_capture(monkeypatch):
+    monkeypatch.setenv("NCCL_DEBUG", "WARN")
+    monkeypatch.setenv("RCCL_P2P_BATCH_ENABLE", "1")
+    env = rccl_env.capture()
+    assert env["NCCL_DEBUG"] == "WARN" and env["RCCL_P2P_BATCH_ENABLE"] == "1"
+    assert all(k in env for k in rccl_env.P2P_KNOBS)
+
+
+def test_package_version_and_native(native):
+    import test_nccl_p2p_amd
+
+    assert test_nccl_p2p_amd.__version__
+    assert test_nccl_p2p_amd.native_available()
+    assert "mpirun -n N ./p2p_matrix" in native.usage()
+
+
+def test_graft_entry_build_is_importable():
+    out = subprocess.run([sys.executable, "-c", "import __graft_entry__ as g; print(callable(g.build), callable(g.smoke))"],
+                         capture_output=True, text=True, cwd=ROOT, timeout=120)
+    assert out.stdout.strip() == "True True"
+
+
+@pytest.mark.parametrize("argv", [["--dry-run", "--mode", "ring"], ["--help"]])
+def test_python_module_cli(native, argv):
+    out = subprocess.run([sys.executable, "-m", "test_nccl_p2p_amd"] + argv, capture_output=True, text=True,
+                         cwd=ROOT, timeout=120, env=dict(os.environ, RANK="0", WORLD_SIZE="1"))
+    assert out.returncode == 0, out.stderr
