@@ -76,6 +76,8 @@ def parse_args(argv=None):
     ap.add_argument("--batch", type=int, default=1, help="1: all msgs of a step in one ncclGroup (one launch)")
     ap.add_argument("--graph", type=int, default=0, help="1: replay each step as a captured hipGraph")
     ap.add_argument("--json-out", default=None, help="also write the result line to this file")
+    ap.add_argument("--ipc-extra", type=int, default=1,
+                    help="1: also run the tournament steps through the IPC transport (N > 1, after the timed region)")
     ap.add_argument("--extras", type=int, default=1,
                     help="1: also measure all-pairs 1 GiB and ring 256 MiB after the timed region (N > 1)")
     ap.add_argument("--ref-iters", type=int, default=32,
@@ -195,6 +197,37 @@ def main(argv=None) -> int:
                             "flow_gbs_min": round(min(flows), 2), "flow_gbs_mean": round(statistics.mean(flows), 2),
                             "iter_us_p50": round(statistics.median(p50s), 1), "bytes": nbytes, "iters": iters}
 
+    # The same tournament steps through the hand-written data plane (IPC
+    # transport: one-sided pulls of hipIpc-mapped peer buffers by the gfx950
+    # copy kernel) on the same links, for comparison with RCCL.  Untimed by the
+    # contract; any error is reported in the JSON instead of failing the run.
+    ipc = None
+    # (with --transport host the same code path runs on the CPU transport, for tests)
+    extra_transport = {"rccl": "ipc", "host": "host"}.get(args.transport)
+    if n > 1 and args.ipc_extra and extra_transport:
+        try:
+            isess = create_session(extra_transport, device=device)
+            idrv = nat.StepDriver(isess, mode, "bi", size, args.msgs, not args.no_verify, bool(args.batch), False)
+            idrv.connect()
+            idrv.run_steps(0, args.warmup)
+            idrv.sync()
+            isess.barrier()
+            i0 = time.perf_counter()
+            idrv.run_steps(args.warmup, args.steps)
+            idrv.sync()
+            isess.barrier()
+            ielapsed = isess.allreduce_max(time.perf_counter() - i0)
+            ijob = sum(idrv.job_bytes_per_step(args.warmup + k) for k in range(args.steps))
+            ipc = {"value_gbs": round(ijob / ielapsed / 1e9, 3), "ms_per_step": round(ielapsed / args.steps * 1e3, 4),
+                   "verify_mismatches": idrv.verify_last() if not args.no_verify else -1,
+                   "transport": isess.transport,
+                   "engine": ("gfx950 multi-copy kernel, one-sided pull over hipIpc mappings"
+                              if isess.transport == "ipc" else isess.device_desc)}
+            del idrv
+            del isess
+        except Exception as e:  # report, never fail the headline
+            ipc = {"error": str(e)[:300]}
+
     step_ms_med = statistics.median(my_ms) if my_ms else 0.0
     result = {
         "metric": METRIC,
@@ -229,6 +262,7 @@ def main(argv=None) -> int:
         "posting": {"batch": bool(args.batch), "graph": bool(args.graph)},
         "reference_semantics": ref,
         "extras": extras,
+        "ipc_transport": ipc,
     }
     if env.rank == 0:
         log("bench: GB/s matrix (row=src, col=dst), median over steps:")
