@@ -93,3 +93,24 @@ def test_kernel_bandwidth_sanity():
     assert verify(buf, 1, impl="reg").ok
     print("fill %.2f TB/s" % fill_tbs)
     assert fill_tbs > 2.0
+
+
+def test_fill_verify_beyond_16gib():
+    """Word indices >= 2^32 (bytes >= 16 GiB) switch the PRNG key; sized for
+    the 288 GB HBM3E of an MI355X."""
+    nbytes = (20 << 30) + 12
+    buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    fill_(buf, 99)
+    r = verify(buf, 99)
+    assert r.mismatches == 0
+    # Window across the 2^32-word boundary against the PyTorch reference.
+    from test_nccl_p2p_amd.ops.buffers import reference_words
+
+    start_word = (1 << 32) - 64
+    got = buf[start_word * 4:(start_word + 128) * 4].cpu().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    assert torch.equal(got, reference_words(start_word, 128, 99))
+    buf[(17 << 30) + 5] ^= 1
+    r2 = verify(buf, 99)
+    assert r2.mismatches == 1 and r2.first_bad == ((17 << 30) + 5) // 4 * 4
+    del buf
+    torch.cuda.empty_cache()

@@ -65,3 +65,10 @@ def test_step_driver(native, session):
     assert len(ms) == 5 and all(m > 0 for m in ms)
     assert d.verify_last() == 0
     assert d.job_bytes_per_step(0) == 4 * (8 << 20)
+
+
+def test_message_larger_than_4gib(session):
+    """size_t counts: the reference's `int msg_size` cannot express this."""
+    r = json.loads(session.run(mode="self", dir="uni", bytes=(5 << 30) + 16, iters=2, warmup=1, verify=True))
+    ph = r["phases"][0]
+    assert ph["mismatches"] == 0 and ph["flows"][0]["gbs"] > 1.0
