@@ -32,6 +32,7 @@
 #include "common.hpp"
 #include "kernels.hpp"
 #include "transport.hpp"
+#include "units.hpp"
 
 namespace p2p {
 namespace {
@@ -69,6 +70,7 @@ class RcclTransport final : public Transport {
     if (rank_ == 0) nccl_ok(ncclGetUniqueId(&id), "ncclGetUniqueId");
     boot.bcast(&id, sizeof(id), 0);
 
+    if (const char* mc = std::getenv("P2P_RCCL_MAX_CHUNK")) max_chunk_ = std::strcmp(mc, "0") ? parse_size(mc) : 0;
     const char* blk = std::getenv("P2P_RCCL_BLOCKING");
     nonblocking_ = opt.nonblocking_init && !(blk && std::atoi(blk));
     if (nonblocking_) {
@@ -147,11 +149,28 @@ class RcclTransport final : public Transport {
   }
 
   void group_begin() override { nccl_ok(ncclGroupStart(), "ncclGroupStart"); }
+  // Messages above max_chunk_ are posted as several back-to-back ops of at
+  // most max_chunk_ bytes inside the same group (matched in order on both
+  // sides).  On MI355X, RCCL 2.26/2.27 deliver only half of a single
+  // ncclSend/ncclRecv of >= 2 GiB (scripts/rccl_size_probe.py); 1 GiB chunks
+  // are exact and run at the same bandwidth.  P2P_RCCL_MAX_CHUNK=0 disables.
   void send(const void* p, size_t bytes, int peer) override {
-    nccl_ok(ncclSend(p, bytes, ncclUint8, peer, comm_, stream_), "ncclSend");
+    const char* c = static_cast<const char*>(p);
+    do {
+      size_t n = chunk_of(bytes);
+      nccl_ok(ncclSend(c, n, ncclUint8, peer, comm_, stream_), "ncclSend");
+      c += n;
+      bytes -= n;
+    } while (bytes);
   }
   void recv(void* p, size_t bytes, int peer) override {
-    nccl_ok(ncclRecv(p, bytes, ncclUint8, peer, comm_, recv_stream_ ? recv_stream_ : stream_), "ncclRecv");
+    char* c = static_cast<char*>(p);
+    do {
+      size_t n = chunk_of(bytes);
+      nccl_ok(ncclRecv(c, n, ncclUint8, peer, comm_, recv_stream_ ? recv_stream_ : stream_), "ncclRecv");
+      c += n;
+      bytes -= n;
+    } while (bytes);
     recv_on_side_ = recv_stream_ != nullptr;
   }
   void group_end() override {
@@ -271,6 +290,9 @@ class RcclTransport final : public Transport {
   hipStream_t recv_stream_ = nullptr;  // two-stream (reference) layout only
   hipEvent_t join_ = nullptr;
   bool recv_on_side_ = false;
+  size_t max_chunk_ = kDefaultMaxChunk;
+  static constexpr size_t kDefaultMaxChunk = size_t{1} << 30;
+  size_t chunk_of(size_t bytes) const { return (max_chunk_ && bytes > max_chunk_) ? max_chunk_ : bytes; }
   ncclComm_t comm_ = nullptr;
   std::vector<hipEvent_t> events_;
   std::vector<hipGraph_t> graphs_;
