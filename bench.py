@@ -80,6 +80,9 @@ def parse_args(argv=None):
                     help="1: also run the tournament steps through the IPC transport (N > 1, after the timed region)")
     ap.add_argument("--extras", type=int, default=1,
                     help="1: also measure all-pairs 1 GiB and ring 256 MiB after the timed region (N > 1)")
+    ap.add_argument("--sweep", type=int, default=1,
+                    help="1: also sweep the single pair 0 -> 1 over 4 KiB .. --sweep-max (N > 1, after the timed region)")
+    ap.add_argument("--sweep-max", default="4G", help="largest message of the pair sweep")
     ap.add_argument("--ref-iters", type=int, default=32,
                     help="iterations per cell of the reference-methodology comparison (0 = skip)")
     return ap.parse_args(argv)
@@ -197,6 +200,21 @@ def main(argv=None) -> int:
                             "flow_gbs_min": round(min(flows), 2), "flow_gbs_mean": round(statistics.mean(flows), 2),
                             "iter_us_p50": round(statistics.median(p50s), 1), "bytes": nbytes, "iters": iters}
 
+    # BASELINE.json config 2: single-pair (0 -> 1) send/recv bandwidth sweep,
+    # 4 KiB -> 4 GiB in x4 steps, events-timed, uni-directional; only cell
+    # (0, 1) is scheduled, so the other ranks just join the barriers.
+    if n > 1 and args.sweep:
+        sweep = []
+        for nbytes in [b for b in (4096 << (2 * k) for k in range(11)) if b <= nat.parse_size(args.sweep_max)]:
+            iters = max(4, min(200, (2 << 30) // nbytes))
+            r = json.loads(sess.run(mode="pair", dir="uni", bytes=nbytes, iters=iters, warmup=2, timing="events",
+                                    verify=False, warm=False, cells=[(0, 1)]))
+            fl = [f for ph in r["phases"] for f in ph["flows"]]
+            if fl:
+                sweep.append({"bytes": nbytes, "iters": iters, "gbs": round(fl[0]["gbs"], 2),
+                              "iter_us_p50": round(fl[0]["iter_us"]["p50"], 2)})
+        extras = dict(extras or {}, pair_sweep_0_1=sweep)
+
     # The same tournament steps through the hand-written data plane (IPC
     # transport: one-sided pulls of hipIpc-mapped peer buffers by the gfx950
     # copy kernel) on the same links, for comparison with RCCL.  Untimed by the
@@ -206,7 +224,7 @@ def main(argv=None) -> int:
     extra_transport = {"rccl": "ipc", "host": "host"}.get(args.transport)
     if n > 1 and args.ipc_extra and extra_transport:
         try:
-            isess = create_session(extra_transport, device=device)
+            isess = create_session(extra_transport, device=device, timeout_s=90.0)
             idrv = nat.StepDriver(isess, mode, "bi", size, args.msgs, not args.no_verify, bool(args.batch), False)
             idrv.connect()
             idrv.run_steps(0, args.warmup)

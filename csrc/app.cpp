@@ -292,19 +292,8 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
   // --cells: re-measure only some (src, dst) cells of the pair schedule; the
   // others stay in the schedule as idle cells (barrier, reported 0.00), so the
   // printed matrices keep their shape.
-  if (!cfg.cells.empty()) {
-    for (auto& s : scheds) {
-      if (s.mode != Mode::Pair) continue;
-      for (auto& p : s.phases) {
-        bool keep = std::find(cfg.cells.begin(), cfg.cells.end(), std::make_pair(p.row, p.col)) != cfg.cells.end();
-        if (!keep && !p.idle) {
-          p.idle = true;
-          p.flows.clear();
-          for (auto& r : p.ranks) r = RankOps{};
-        }
-      }
-    }
-  }
+  if (!cfg.cells.empty())
+    for (auto& s : scheds) restrict_cells(&s, cfg.cells, false);
   for (const auto& s : scheds) {
     std::string bad = validate(s);
     P2P_CHECK(bad.empty(), "invalid schedule " + s.name() + ": " + bad);

@@ -69,8 +69,9 @@ class Session {
 
   // One (mode, dir, size) run; returns the run JSON (report.cpp schema).
   std::string run(const std::string& mode, const std::string& dir, size_t bytes, int iters, int warmup,
-                  const std::string& timing, bool verify, bool warm) {
+                  const std::string& timing, bool verify, bool warm, const std::vector<std::pair<int, int>>& cells) {
     Schedule s = make_schedule(parse_mode(mode), parse_direction(dir), world());
+    restrict_cells(&s, cells, true);
     RunConfig cfg;
     cfg.bytes = bytes;
     cfg.iters = iters;
@@ -196,7 +197,7 @@ PYBIND11_MODULE(_p2pcore, m) {
       .def("allreduce_sum", &Session::allreduce_sum, py::call_guard<py::gil_scoped_release>())
       .def("run", &Session::run, py::arg("mode") = "pair", py::arg("dir") = "uni", py::arg("bytes") = 32u << 20,
            py::arg("iters") = 128, py::arg("warmup") = 8, py::arg("timing") = "events", py::arg("verify") = false,
-           py::arg("warm") = true, py::call_guard<py::gil_scoped_release>())
+           py::arg("warm") = true, py::arg("cells") = std::vector<std::pair<int, int>>{}, py::call_guard<py::gil_scoped_release>())
       .def("latency", &Session::latency, py::arg("bytes") = 8, py::arg("iters") = 1000, py::arg("warmup") = 100,
            py::call_guard<py::gil_scoped_release>());
 

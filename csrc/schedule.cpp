@@ -229,4 +229,23 @@ std::string validate(const Schedule& s) {
   return "";
 }
 
+void restrict_cells(Schedule* s, const std::vector<std::pair<int, int>>& cells, bool drop_others) {
+  if (s->mode != Mode::Pair || cells.empty()) return;
+  std::vector<Phase> kept;
+  for (auto& p : s->phases) {
+    bool keep = std::find(cells.begin(), cells.end(), std::make_pair(p.row, p.col)) != cells.end();
+    if (keep) {
+      kept.push_back(p);
+    } else if (!drop_others) {
+      if (!p.idle) {
+        p.idle = true;
+        p.flows.clear();
+        for (auto& r : p.ranks) r = RankOps{};
+      }
+      kept.push_back(p);
+    }
+  }
+  s->phases = std::move(kept);
+}
+
 }  // namespace p2p

@@ -81,6 +81,12 @@ Schedule make_tournament_schedule(int n, Direction dir);
 Schedule make_self_schedule(int n);
 Schedule make_schedule(Mode mode, Direction dir, int n);
 
+// Pair mode: measure only the listed (src, dst) cells.  With drop_others the
+// other phases are removed (a sweep over a few cells pays no barriers for the
+// rest); otherwise they become idle phases, so printed matrices keep their
+// shape (--cells).  Other modes are returned unchanged.
+void restrict_cells(Schedule* s, const std::vector<std::pair<int, int>>& cells, bool drop_others);
+
 // Round-robin (circle-method) pairing.  Returns rounds of disjoint unordered
 // pairs (a < b); for odd n one rank sits out each round.  Every unordered
 // pair appears exactly once.

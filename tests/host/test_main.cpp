@@ -204,6 +204,22 @@ TEST(test_ring_and_allpairs) {
   EXPECT(parse_mode("a2a") == Mode::AllPairs);
 }
 
+TEST(test_restrict_cells) {
+  std::vector<std::pair<int, int>> cells{{0, 1}, {3, 2}};
+  Schedule keep = make_pair_schedule(4, Direction::Uni);
+  restrict_cells(&keep, cells, false);
+  EXPECT(keep.phases.size() == 16);  // shape kept for the printed matrices
+  EXPECT(validate(keep).empty());
+  EXPECT(all_flows(keep) == (std::multiset<std::pair<int, int>>{{0, 1}, {3, 2}}));
+  Schedule drop = make_pair_schedule(4, Direction::Uni);
+  restrict_cells(&drop, cells, true);
+  EXPECT(drop.phases.size() == 2);
+  EXPECT(drop.phases[0].row == 0 && drop.phases[0].col == 1 && drop.phases[1].row == 3);
+  Schedule ring = make_ring_schedule(4, Direction::Uni);
+  restrict_cells(&ring, cells, true);
+  EXPECT(ring.phases.size() == 1);  // other modes untouched
+}
+
 // ----------------------------------------------------------- placement ----
 
 TEST(test_host_hash_matches_reference) {

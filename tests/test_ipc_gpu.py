@@ -62,3 +62,5 @@ def test_bench_two_ranks_ipc():
     assert len(lines) == 1
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["verify_mismatches"] == 0 and r["matrix_cells"] == "2/2"
+    sweep = r["extras"]["pair_sweep_0_1"]
+    assert len(sweep) == 11 and sweep[-1]["bytes"] == 4 << 30 and all(p["gbs"] > 0 for p in sweep)

@@ -36,7 +36,7 @@ def test_native_module_under_torchrun(native):
 
 def test_bench_cpu_two_ranks(native):
     out = torchrun(2, ["bench.py", "--gpus", "2", "--steps", "4", "--warmup", "2", "--transport", "host",
-                       "--size", "256K", "--msgs", "2", "--latency-iters", "20"])
+                       "--size", "256K", "--msgs", "2", "--latency-iters", "20", "--sweep-max", "1M"])
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1
@@ -47,3 +47,6 @@ def test_bench_cpu_two_ranks(native):
     assert r["n_gpus"] == 2 and r["steps"] == 4 and r["value"] > 0
     assert r["verify_mismatches"] == 0
     assert r["matrix_cells"] == "2/2"
+    sweep = r["extras"]["pair_sweep_0_1"]
+    assert [p["bytes"] for p in sweep] == [4096, 16384, 65536, 262144, 1048576]
+    assert all(p["gbs"] > 0 for p in sweep)
