@@ -44,7 +44,10 @@ EXT       := test_nccl_p2p_amd/_p2pcore$(PY_EXT)
 
 all: gpu host ext tools
 
+# ./p2p_matrix: where the reference's `make` leaves its binary (Makefile:1-2
+# there), so `mpirun -n N ./p2p_matrix > result.txt` works unchanged.
 gpu: $(BUILD)/p2p_matrix
+	ln -sf $(BUILD)/p2p_matrix p2p_matrix
 host: $(BUILD)/p2p_matrix_host $(BUILD)/p2p_host_tests
 ext: $(EXT)
 tools: $(BUILD)/fill_probe
@@ -116,4 +119,4 @@ test-gpu: all
 	$(PYTHON) -m pytest tests -x -q -m gpu
 
 clean:
-	rm -rf $(BUILD) test_nccl_p2p_amd/_p2pcore*.so
+	rm -rf $(BUILD) test_nccl_p2p_amd/_p2pcore*.so p2p_matrix

@@ -44,6 +44,16 @@ def test_mpirun_one_rank(exe):
     assert "bootstrap mpi" in out.stdout
 
 
+@pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
+def test_reference_invocation_from_repo_root(exe):
+    """`make` leaves ./p2p_matrix like the reference's Makefile; the reference
+    run line (README.md:5 there) works unchanged and prints the two matrices."""
+    out = subprocess.run([MPIRUN, "-n", "1", "./p2p_matrix"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.startswith("Evaluating the Uni-Directional NCCL P2P Bandwidth (Gbps)\n   D\\D     0 \n     0   0.00 \n")
+    assert "Evaluating the Bi-Directional NCCL P2P Bandwidth (Gbps)" in out.stdout
+
+
 def test_bench_contract_single_gpu():
     out = subprocess.run([sys.executable, "bench.py", "--steps", "6", "--warmup", "2", "--latency-iters", "50"],
                          capture_output=True, text=True, timeout=600, cwd=ROOT)
