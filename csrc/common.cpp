@@ -1,6 +1,7 @@
 #include "common.hpp"
 
 #include <dlfcn.h>
+#include <unistd.h>
 
 #include <chrono>
 #include <cstdarg>
@@ -143,6 +144,23 @@ void trace_mark(const char* name) {
 double now_seconds() {
   using clk = std::chrono::steady_clock;
   return std::chrono::duration<double>(clk::now().time_since_epoch()).count();
+}
+
+StdoutToStderr::StdoutToStderr(bool enable) {
+  if (!enable) return;
+  std::fflush(stdout);
+  saved_ = dup(1);
+  if (saved_ >= 0 && dup2(2, 1) < 0) {
+    close(saved_);
+    saved_ = -1;
+  }
+}
+
+StdoutToStderr::~StdoutToStderr() {
+  if (saved_ < 0) return;
+  std::fflush(stdout);
+  dup2(saved_, 1);
+  close(saved_);
 }
 
 }  // namespace p2p

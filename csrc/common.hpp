@@ -56,6 +56,21 @@ struct TraceRange {
   ~TraceRange() { trace_pop(); }
 };
 
+// While alive, file descriptor 1 points at stderr.  Libraries that print
+// banners to stdout during init (RCCL prints its version block) would
+// otherwise land in front of the reference-compatible matrices of a
+// `mpirun ... > result.txt` run.  Inactive if `enable` is false.
+class StdoutToStderr {
+ public:
+  explicit StdoutToStderr(bool enable = true);
+  ~StdoutToStderr();
+  StdoutToStderr(const StdoutToStderr&) = delete;
+  StdoutToStderr& operator=(const StdoutToStderr&) = delete;
+
+ private:
+  int saved_ = -1;
+};
+
 }  // namespace p2p
 
 #define P2P_FATAL(msg) ::p2p::fatal(__FILE__, __LINE__, (msg))

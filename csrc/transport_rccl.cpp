@@ -65,6 +65,10 @@ class RcclTransport final : public Transport {
     HIPCHECK(hipMalloc(&acc_, dev::verify_accum_bytes()));
     HIPCHECK(hipHostMalloc(&acc_host_, sizeof(dev::VerifyAccum), hipHostMallocDefault));
 
+    // RCCL prints a version banner to stdout on first use; send it to stderr
+    // so stdout keeps the reference's output (P2P_RCCL_BANNER=1 keeps it).
+    const char* banner = std::getenv("P2P_RCCL_BANNER");
+    StdoutToStderr quiet(!(banner && std::atoi(banner)));
     ncclUniqueId id;
     std::memset(&id, 0, sizeof(id));
     if (rank_ == 0) nccl_ok(ncclGetUniqueId(&id), "ncclGetUniqueId");
