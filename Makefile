@@ -25,7 +25,7 @@ HIPFLAGS  := $(CXXSTD) $(OPT) $(WARN) -fPIC --offload-arch=$(ARCH) -Icsrc
 HOSTFLAGS := $(CXXSTD) $(OPT) $(WARN) -fPIC -Icsrc -pthread
 
 CORE      := common units stats schedule bootstrap transport_host runner report app
-GPU_OBJS  := $(addprefix $(BUILD)/gpu/,$(addsuffix .o,$(CORE) transport_rccl transport_ipc topology) kernels.o)
+GPU_OBJS  := $(addprefix $(BUILD)/gpu/,$(addsuffix .o,$(CORE) transport_rccl transport_ipc topology) kernels.o pingpong.o)
 HOST_OBJS := $(addprefix $(BUILD)/host/,$(addsuffix .o,$(CORE) transport_rccl_stub))
 
 # MPICH lives in /opt/conda; putting /opt/conda/lib on the rpath would pull in
@@ -67,6 +67,9 @@ $(BUILD)/gpu/%.o: csrc/%.cpp $(HEADERS) | $(BUILD)/gpu
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(BUILD)/gpu/kernels.o: csrc/kernels.hip $(HEADERS) | $(BUILD)/gpu
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/gpu/pingpong.o: csrc/pingpong.hip $(HEADERS) | $(BUILD)/gpu
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(BUILD)/gpu/bootstrap_mpi.o: csrc/bootstrap_mpi.cpp $(HEADERS) | $(BUILD)/gpu

@@ -221,7 +221,7 @@ def main(argv=None) -> int:
     # contract; any error is reported in the JSON instead of failing the run.
     ipc = None
     # (with --transport host the same code path runs on the CPU transport, for tests)
-    extra_transport = {"rccl": "ipc", "host": "host"}.get(args.transport)
+    extra_transport = {"rccl": "ipc", "ipc": "ipc", "host": "host"}.get(args.transport)
     if n > 1 and args.ipc_extra and extra_transport:
         try:
             isess = create_session(extra_transport, device=device, timeout_s=90.0)
@@ -236,7 +236,16 @@ def main(argv=None) -> int:
             isess.barrier()
             ielapsed = isess.allreduce_max(time.perf_counter() - i0)
             ijob = sum(idrv.job_bytes_per_step(args.warmup + k) for k in range(args.steps))
+            # Device-initiated ping-pong: one wave per GPU writes the message
+            # into the peer's memory and spins on its own inbox (no host, no
+            # runtime in the loop) -- the fabric's latency, next to RCCL's.
+            dev_p50 = None
+            if isess.transport == "ipc":
+                dl = json.loads(isess.device_latency(nat.parse_size(args.latency_size), args.latency_iters,
+                                                     min(100, args.latency_iters)))
+                dev_p50 = round(statistics.median(p["one_way_us"]["p50"] for p in dl["pairs"]), 3)
             ipc = {"value_gbs": round(ijob / ielapsed / 1e9, 3), "ms_per_step": round(ielapsed / args.steps * 1e3, 4),
+                   "device_pingpong_p50_us": dev_p50,
                    "verify_mismatches": idrv.verify_last() if not args.no_verify else -1,
                    "transport": isess.transport,
                    "engine": ("gfx950 multi-copy kernel, one-sided pull over hipIpc mappings"

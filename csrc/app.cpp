@@ -46,6 +46,9 @@ timing
       --two-streams      RCCL: receives on a second stream, like the reference's s_1
       --no-warm          do not pre-establish connections before timing
   -l, --latency          add a ping-pong latency matrix
+      --device-latency   add a device-initiated ping-pong matrix (--transport ipc:
+                         one wave per GPU writes into the peer's memory, no host
+                         or runtime in the loop)
       --latency-size S   [8]      --latency-iters N   [1000]
 data
   -c, --verify           random-fill sends, verify every received buffer on the device
@@ -177,6 +180,8 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
       cfg->warm_connections = false;
     } else if (a == "-l" || a == "--latency") {
       cfg->latency = true;
+    } else if (a == "--device-latency") {
+      cfg->device_latency = true;
     } else if (a == "--latency-size") {
       cfg->latency_bytes = parse_size(next());
       cfg->latency = true;
@@ -394,6 +399,8 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
     }
   }
   if (cfg.latency) res.latency = run_latency(*t, boot, cfg.latency_bytes, cfg.latency_iters, std::min(cfg.latency_iters, 100), bufs);
+  if (cfg.device_latency)
+    res.device_latency = run_device_latency(*t, boot, cfg.latency_bytes, cfg.latency_iters, std::min(cfg.latency_iters, 100));
 
   // Device descriptions of every rank, for the banner.
   char mine[256] = {0};
@@ -409,8 +416,10 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
       if (t->name() != "host") std::fprintf(out, "%s", topology_report().c_str());
       for (const auto& rec : res.runs) print_extended(out, rec, n);
       print_latency(out, res.latency, n);
+      print_latency(out, res.device_latency, n);
     }
     if (js.is_open() && !res.latency.empty()) js << latency_to_json(res.latency, n) << "\n";
+    if (js.is_open() && !res.device_latency.empty()) js << latency_to_json(res.device_latency, n) << "\n";
     if (!cfg.trace_path.empty()) {
       std::ofstream tr(cfg.trace_path);
       P2P_CHECK(tr.good(), "cannot write " + cfg.trace_path);

@@ -29,6 +29,7 @@ struct AppConfig {
   bool iters_auto = false;       // scale iterations per size (target_bytes per cell)
   size_t target_bytes = 4ull << 30;
   bool latency = false;
+  bool device_latency = false;   // ping-pong kernel matrix (one-sided transports)
   size_t latency_bytes = 8;
   int latency_iters = 1000;
   std::string transport = "rccl";  // rccl | ipc | host
@@ -62,6 +63,7 @@ int auto_iters(size_t bytes, size_t target_bytes);
 struct AppResult {
   std::vector<RunRecord> runs;
   std::vector<LatencyResult> latency;
+  std::vector<LatencyResult> device_latency;
   uint64_t mismatches = 0;
 };
 

@@ -91,5 +91,28 @@ struct CopyOp {
 constexpr int kMaxCopyOps = 16;
 void launch_multi_copy(const CopyOp* ops, int nops, hipStream_t stream, int max_blocks = 0);
 
+// ---- device-initiated ping-pong (pingpong.hip) ----
+// One wave per role.  The leader writes message i (payload words = base+i+1,
+// then the flag) into the peer's inbox and spins on its own inbox for the
+// reply; the follower mirrors it.  stamps[0..iters] (leader only) are
+// s_memrealtime ticks; status[0] bit 0 = a spin hit the deadline, status[1] =
+// payloads that arrived without their sequence number.
+struct PingRole {
+  unsigned long long* out_flag;        // peer's inbox flag
+  unsigned char* out_payload;          // peer's inbox payload
+  const unsigned long long* in_flag;   // own inbox flag (written by the peer)
+  const unsigned char* in_payload;     // own inbox payload
+  unsigned long long bytes;            // payload bytes, multiple of 16, >= 16
+  unsigned long long base;             // sequence base
+  int iters;
+  int leader;
+  unsigned long long* stamps;          // leader: iters + 1 entries
+  unsigned int* status;                // 2 words, zeroed by the caller
+  unsigned long long timeout_ticks;    // per kernel, in s_memrealtime ticks
+};
+// b == nullptr: one wave (cross-process partner).  Otherwise both roles run
+// as two waves of one workgroup (self ping-pong on one GPU).
+void launch_pingpong(const PingRole& a, const PingRole* b, hipStream_t stream);
+
 }  // namespace dev
 }  // namespace p2p

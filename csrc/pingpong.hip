@@ -1,0 +1,96 @@
+// Device-initiated ping-pong over hipIpc-mapped memory (IPC transport).
+//
+// The reference has no latency measurement at all; the host-
+// posted ping-pong in runner.cpp (run_latency) measures what an application
+// sees through RCCL: launch, proxy and protocol overhead included.  This
+// kernel measures the fabric itself: one wave on each GPU bounces a message
+// through the peer's memory with no host or runtime in the loop:
+//
+//   leader:   write payload (seq) into the peer's inbox -> release flag=seq
+//             -> spin on its own inbox flag until >= seq -> timestamp
+//   follower: spin until its inbox flag >= seq -> check payload -> reply
+//
+// Stores to the peer travel over xGMI (remote writes, the direction xGMI and
+// RCCL's LL protocols favour); the spin is on local memory.  Flags are
+// monotonic sequence numbers, so consecutive calls need no reset.  Every spin
+// is bounded by a wall-clock deadline (s_memrealtime, constant 100 MHz on
+// CDNA), so a missing partner ends the kernel with status bit 0 set instead
+// of hanging the GPU.
+#include <hip/hip_runtime.h>
+
+#include "kernels.hpp"
+
+namespace p2p {
+namespace dev {
+namespace {
+
+typedef unsigned long long u64;
+typedef u64 u64x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u64 now_ticks() { return static_cast<u64>(wall_clock64()); }
+
+__device__ __forceinline__ void ping_send(const PingRole& r, u64 seq, int lane) {
+  const u64x2 v = {seq, seq};
+  for (u64 off = static_cast<u64>(lane) * 16; off < r.bytes; off += 64 * 16)
+    *reinterpret_cast<u64x2*>(r.out_payload + off) = v;
+  // All of this wave's payload stores are complete (vmcnt is per wave) and
+  // written back before the flag becomes visible to the peer.
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) __hip_atomic_store(r.out_flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Wave-uniform: every lane loads the same flag and reads the same scalar clock.
+__device__ __forceinline__ bool ping_wait(const PingRole& r, u64 seq, u64 deadline) {
+  while (__hip_atomic_load(r.in_flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < seq)
+    if (now_ticks() > deadline) return false;
+  return true;
+}
+
+// After the acquire: first and last 16 B of the payload must carry seq.
+__device__ __forceinline__ void ping_check(const PingRole& r, u64 seq, int lane) {
+  if (lane < 2) {
+    const u64 off = lane == 0 ? 0 : r.bytes - 16;
+    const u64x2 v = *reinterpret_cast<const u64x2*>(r.in_payload + off);
+    if (v.x != seq || v.y != seq) atomicAdd(r.status + 1, 1u);
+  }
+}
+
+__global__ __launch_bounds__(128) void pingpong_kernel(PingRole a, PingRole b) {
+  const int lane = threadIdx.x & 63;
+  const PingRole& r = (threadIdx.x >> 6) == 0 ? a : b;
+  const u64 deadline = now_ticks() + r.timeout_ticks;
+  if (r.leader) {
+    if (lane == 0) r.stamps[0] = now_ticks();
+    for (int i = 0; i < r.iters; ++i) {
+      const u64 seq = r.base + static_cast<u64>(i) + 1;
+      ping_send(r, seq, lane);
+      if (!ping_wait(r, seq, deadline)) {
+        if (lane == 0) atomicOr(r.status, 1u);
+        return;
+      }
+      ping_check(r, seq, lane);
+      if (lane == 0) r.stamps[i + 1] = now_ticks();
+    }
+  } else {
+    for (int i = 0; i < r.iters; ++i) {
+      const u64 seq = r.base + static_cast<u64>(i) + 1;
+      if (!ping_wait(r, seq, deadline)) {
+        if (lane == 0) atomicOr(r.status, 1u);
+        return;
+      }
+      ping_check(r, seq, lane);
+      ping_send(r, seq, lane);
+    }
+  }
+}
+
+}  // namespace
+
+void launch_pingpong(const PingRole& a, const PingRole* b, hipStream_t stream) {
+  PingRole second = b ? *b : a;
+  hipLaunchKernelGGL(pingpong_kernel, dim3(1), dim3(b ? 128 : 64), 0, stream, a, second);
+}
+
+}  // namespace dev
+}  // namespace p2p

@@ -96,6 +96,10 @@ class Session {
     return latency_to_json(lat, world());
   }
 
+  std::string device_latency(size_t bytes, int iters, int warmup) {
+    return latency_to_json(run_device_latency(*t_, *boot_, bytes, iters, warmup), world());
+  }
+
  private:
   std::unique_ptr<Bootstrap> boot_;
   std::unique_ptr<Transport> t_;
@@ -198,6 +202,8 @@ PYBIND11_MODULE(_p2pcore, m) {
       .def("run", &Session::run, py::arg("mode") = "pair", py::arg("dir") = "uni", py::arg("bytes") = 32u << 20,
            py::arg("iters") = 128, py::arg("warmup") = 8, py::arg("timing") = "events", py::arg("verify") = false,
            py::arg("warm") = true, py::arg("cells") = std::vector<std::pair<int, int>>{}, py::call_guard<py::gil_scoped_release>())
+      .def("device_latency", &Session::device_latency, py::arg("bytes") = 8, py::arg("iters") = 1000,
+           py::arg("warmup") = 100, py::call_guard<py::gil_scoped_release>())
       .def("latency", &Session::latency, py::arg("bytes") = 8, py::arg("iters") = 1000, py::arg("warmup") = 100,
            py::call_guard<py::gil_scoped_release>());
 

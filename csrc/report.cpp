@@ -125,7 +125,9 @@ void print_latency(FILE* out, const std::vector<LatencyResult>& lat, int n) {
     m[static_cast<size_t>(l.b) * n + l.a] = l.one_way_us.p50;
     p50s.push_back(l.one_way_us.p50);
   }
-  std::fprintf(out, "\n== latency: %s messages, ping-pong ==\n", format_size(lat[0].bytes).c_str());
+  std::fprintf(out, "\n== latency: %s messages, %s ==\n", format_size(lat[0].bytes).c_str(),
+               lat[0].method == "device" ? "device-initiated ping-pong (one wave per GPU, no host in the loop)"
+                                         : "ping-pong");
   print_matrix(out, "p50 one-way latency (us)", m, n, "%9.2f", n > 1);
   Summary s = summarize(p50s);
   std::fprintf(out, "  p50 over pairs: min %.2f  median %.2f  max %.2f us\n", s.min, s.p50, s.max);
@@ -205,7 +207,8 @@ std::string run_to_json(const RunRecord& rec, int n) {
 
 std::string latency_to_json(const std::vector<LatencyResult>& lat, int n) {
   std::ostringstream o;
-  o << "{\"type\":\"latency\",\"nranks\":" << n << ",\"bytes\":" << (lat.empty() ? 0 : lat[0].bytes) << ",\"pairs\":[";
+  o << "{\"type\":\"latency\",\"method\":\"" << (lat.empty() ? "host" : lat[0].method) << "\",\"nranks\":" << n
+    << ",\"bytes\":" << (lat.empty() ? 0 : lat[0].bytes) << ",\"pairs\":[";
   for (size_t i = 0; i < lat.size(); ++i)
     o << (i ? "," : "") << "{\"a\":" << lat[i].a << ",\"b\":" << lat[i].b << ",\"one_way_us\":" << summary_json(lat[i].one_way_us) << "}";
   o << "]}";

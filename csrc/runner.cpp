@@ -368,6 +368,51 @@ std::vector<LatencyResult> run_latency(Transport& t, Bootstrap& boot, size_t byt
   return out;
 }
 
+std::vector<LatencyResult> run_device_latency(Transport& t, Bootstrap& boot, size_t bytes, int iters, int warmup) {
+  P2P_CHECK(t.supports_device_pingpong(),
+            "device ping-pong needs a one-sided transport (--transport ipc); " + t.name() + " has none");
+  P2P_CHECK(iters >= 1 && warmup >= 0, "bad device latency iterations");
+  const int n = boot.size(), me = boot.rank();
+  t.pingpong_setup();
+  auto one = [&](int partner) -> Summary {
+    std::vector<double> us;
+    boot.barrier();  // both kernels start together (each spin has a deadline)
+    if (partner >= 0) {
+      us = t.device_pingpong(partner, bytes, warmup + iters);
+      if (!us.empty()) us.erase(us.begin(), us.begin() + std::min<size_t>(us.size(), static_cast<size_t>(warmup)));
+    }
+    return summarize(us);
+  };
+  std::vector<LatencyResult> out;
+  auto add = [&](int a, int b, const Summary& s) {
+    LatencyResult r;
+    r.a = a;
+    r.b = b;
+    r.bytes = std::max<size_t>(16, (bytes + 15) / 16 * 16);
+    r.one_way_us = s;
+    r.method = "device";
+    out.push_back(r);
+  };
+  if (n == 1) {
+    add(0, 0, one(0));
+    return out;
+  }
+  for (const auto& round : round_robin_rounds(n)) {
+    int partner = -1;
+    for (auto& pr : round) {
+      if (pr.first == me) partner = pr.second;
+      if (pr.second == me) partner = pr.first;
+    }
+    Summary s = one(partner);
+    auto all = boot.allgather_value(s);
+    for (auto& pr : round) add(pr.first, pr.second, all[static_cast<size_t>(pr.first)]);
+  }
+  std::sort(out.begin(), out.end(), [](const LatencyResult& x, const LatencyResult& y) {
+    return x.a != y.a ? x.a < y.a : x.b < y.b;
+  });
+  return out;
+}
+
 // ---------------------------------------------------------- StepDriver ----
 
 StepDriver::StepDriver(Transport& t, Bootstrap& boot, Schedule sched, size_t bytes, int msgs, bool verify, uint64_t salt,

@@ -114,6 +114,7 @@ struct LatencyResult {
   int a = -1, b = -1;   // a < b; a == b for the self path
   size_t bytes = 0;
   Summary one_way_us;   // half round trip, microseconds
+  std::string method = "host";  // host: posted ping-pong through the transport; device: ping-pong kernel
 };
 
 // Ping-pong over round-robin rounds (every unordered pair once; each round's
@@ -121,6 +122,12 @@ struct LatencyResult {
 // path (one grouped self send/recv per sample).
 std::vector<LatencyResult> run_latency(Transport& t, Bootstrap& boot, size_t bytes, int iters, int warmup,
                                        Buffers& bufs);
+
+// Device-initiated ping-pong (Transport::device_pingpong; the IPC transport):
+// one wave per GPU bounces a message through the peer's memory with no host
+// in the loop, timed on the device clock.  Same round structure as
+// run_latency; payloads are rounded up to 16 bytes (at most 64 KiB).
+std::vector<LatencyResult> run_device_latency(Transport& t, Bootstrap& boot, size_t bytes, int iters, int warmup);
 
 // ---- step driver (used by bench.py): one phase per step, no host syncs ----
 // Step k posts `msgs` iterations of phase (k mod phases) with a timestamp

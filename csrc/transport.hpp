@@ -79,6 +79,17 @@ class Transport {
   virtual int capture_end() { return -1; }
   virtual void graph_launch(int /*handle*/) {}
 
+  // ---- device-initiated ping-pong (one-sided transports) ----
+  // pingpong_setup() is collective (every rank, same order).  Then both
+  // partners call device_pingpong(peer = each other, same bytes / iters), or
+  // one rank calls it with peer == rank() for the self path.  Blocking;
+  // returns the leader's (lower rank's) per-iteration one-way times in
+  // microseconds (half of each device-timed round trip), empty on the
+  // follower.
+  virtual bool supports_device_pingpong() const { return false; }
+  virtual void pingpong_setup() {}
+  virtual std::vector<double> device_pingpong(int /*peer*/, size_t /*bytes*/, int /*iters*/) { return {}; }
+
   // ---- health ----
   // Non-empty when the transport saw an asynchronous error (e.g. a peer died).
   virtual std::string async_error() { return ""; }

@@ -74,6 +74,11 @@ class IpcTransport final : public Transport {
     (void)hipStreamSynchronize(stream_);
     for (auto& r : regs_) close_registration(r);
     regs_.clear();
+    for (size_t r = 0; r < peer_pages_.size(); ++r)
+      if (peer_pages_[r] && static_cast<int>(r) != rank_) (void)hipIpcCloseMemHandle(peer_pages_[r]);
+    if (page_) (void)hipFree(page_);
+    if (ping_scratch_) (void)hipFree(ping_scratch_);
+    if (ping_host_) (void)hipHostFree(ping_host_);
     for (auto ex : execs_) (void)hipGraphExecDestroy(ex);
     for (auto s : side_) (void)hipStreamDestroy(s);
     for (auto e : side_done_) (void)hipEventDestroy(e);
@@ -212,6 +217,105 @@ class IpcTransport final : public Transport {
   }
   void graph_launch(int h) override { HIPCHECK(hipGraphLaunch(execs_.at(static_cast<size_t>(h)), stream_)); }
 
+  // Signal pages: every rank owns one page of n + 1 inbox slots (slot r =
+  // messages from rank r, slot n = replies of the self path), exported over
+  // hipIpc so peers write into it directly.  Uncached device memory when the
+  // runtime allows it, so the spinning wave reads HBM, not a stale line.
+  bool supports_device_pingpong() const override { return true; }
+  void pingpong_setup() override {
+    if (page_) return;  // same state on every rank: they all set up together
+    const size_t bytes = kPingSlot * static_cast<size_t>(n_ + 1);
+    page_kind_ = "uncached";
+    if (hipExtMallocWithFlags(&page_, bytes, hipDeviceMallocUncached) != hipSuccess) {
+      (void)hipGetLastError();
+      page_kind_ = "coarse";
+      HIPCHECK(hipMalloc(&page_, bytes));
+    }
+    HIPCHECK(hipMemset(page_, 0, bytes));
+    HIPCHECK(hipDeviceSynchronize());
+    Export me{};
+    HIPCHECK(hipIpcGetMemHandle(&me.handle, page_));
+    me.bytes = bytes;
+    me.host_hash = host_hash(real_hostname());
+    me.device = device_;
+    me.pid = static_cast<int32_t>(getpid());
+    auto all = boot_.allgather_value(me);
+    peer_pages_.assign(static_cast<size_t>(n_), nullptr);
+    for (int r = 0; r < n_; ++r) {
+      if (r == rank_) {
+        peer_pages_[static_cast<size_t>(r)] = page_;
+        continue;
+      }
+      P2P_CHECK(all[static_cast<size_t>(r)].host_hash == me.host_hash,
+                strfmt("device ping-pong is intra-node only: rank %d is on another host", r));
+      void* mapped = nullptr;
+      HIPCHECK(hipIpcOpenMemHandle(&mapped, all[static_cast<size_t>(r)].handle, hipIpcMemLazyEnablePeerAccess));
+      peer_pages_[static_cast<size_t>(r)] = mapped;
+    }
+    seq_.assign(static_cast<size_t>(n_), 0);
+    int khz = 0;
+    HIPCHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_));
+    P2P_CHECK(khz > 0, "device reports no wall clock rate");
+    tick_hz_ = khz * 1e3;
+    HIPCHECK(hipMalloc(&ping_scratch_, kPingScratch));
+    HIPCHECK(hipHostMalloc(&ping_host_, kPingScratch, hipHostMallocDefault));
+    boot_.barrier();
+  }
+
+  std::vector<double> device_pingpong(int peer, size_t bytes, int iters) override {
+    P2P_CHECK(page_, "pingpong_setup() first");
+    P2P_CHECK(peer >= 0 && peer < n_, "bad peer");
+    P2P_CHECK(iters >= 1 && iters <= kPingMaxIters, strfmt("device ping-pong: 1..%d iterations", kPingMaxIters));
+    P2P_CHECK(bytes <= kPingMaxBytes, strfmt("device ping-pong payload is at most %zu bytes", kPingMaxBytes));
+    const unsigned long long pay = std::max<size_t>(16, (bytes + 15) / 16 * 16);
+    auto slot = [&](void* page, int k) { return static_cast<unsigned char*>(page) + kPingSlot * static_cast<size_t>(k); };
+    auto* stamps = static_cast<unsigned long long*>(ping_scratch_);
+    auto* status = reinterpret_cast<unsigned int*>(stamps + kPingMaxIters + 1);
+    HIPCHECK(hipMemsetAsync(status, 0, 2 * sizeof(unsigned int), stream_));
+    dev::PingRole a{};
+    a.bytes = pay;
+    a.base = seq_[static_cast<size_t>(peer)];
+    a.iters = iters;
+    a.stamps = stamps;
+    a.status = status;
+    a.timeout_ticks = static_cast<unsigned long long>(std::min(timeout_, 30.0) * tick_hz_);
+    const bool self = peer == rank_;
+    const bool lead = self || rank_ < peer;
+    a.leader = lead ? 1 : 0;
+    unsigned char* out = self ? slot(page_, rank_) : slot(peer_pages_[static_cast<size_t>(peer)], rank_);
+    unsigned char* in = self ? slot(page_, n_) : slot(page_, peer);
+    a.out_flag = reinterpret_cast<unsigned long long*>(out);
+    a.out_payload = out + kPingHeader;
+    a.in_flag = reinterpret_cast<const unsigned long long*>(in);
+    a.in_payload = in + kPingHeader;
+    if (self) {
+      dev::PingRole b = a;  // the reply wave: mirror image through slot n
+      b.leader = 0;
+      b.out_flag = const_cast<unsigned long long*>(a.in_flag);
+      b.out_payload = const_cast<unsigned char*>(a.in_payload);
+      b.in_flag = a.out_flag;
+      b.in_payload = a.out_payload;
+      dev::launch_pingpong(a, &b, stream_);
+    } else {
+      dev::launch_pingpong(a, nullptr, stream_);
+    }
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(ping_host_, ping_scratch_, kPingScratch, hipMemcpyDeviceToHost, stream_));
+    sync();
+    const auto* host = static_cast<const unsigned long long*>(ping_host_);
+    const auto* st = reinterpret_cast<const unsigned int*>(host + kPingMaxIters + 1);
+    seq_[static_cast<size_t>(peer)] += static_cast<unsigned long long>(iters);
+    if (st[0] & 1u)
+      P2P_FATAL(strfmt("rank %d: device ping-pong with rank %d timed out (partner kernel never answered)", rank_, peer));
+    if (st[1])
+      P2P_FATAL(strfmt("rank %d: device ping-pong with rank %d: %u payloads arrived before their data", rank_, peer, st[1]));
+    std::vector<double> us;
+    if (lead)
+      for (int i = 0; i < iters; ++i)
+        us.push_back(static_cast<double>(host[static_cast<size_t>(i) + 1] - host[static_cast<size_t>(i)]) / tick_hz_ * 1e6 / 2.0);
+    return us;
+  }
+
   void sync() override {
     double deadline = now_seconds() + timeout_;
     double t0 = now_seconds();
@@ -295,6 +399,19 @@ class IpcTransport final : public Transport {
   std::vector<Registration> regs_;
   bool in_group_ = false;
   std::vector<dev::CopyOp> ops_;
+
+  static constexpr size_t kPingHeader = 256;            // flag + padding (own cache lines)
+  static constexpr size_t kPingMaxBytes = 64u << 10;
+  static constexpr size_t kPingSlot = kPingHeader + kPingMaxBytes;
+  static constexpr int kPingMaxIters = 100000;
+  void* page_ = nullptr;
+  std::string page_kind_;
+  std::vector<void*> peer_pages_;
+  std::vector<unsigned long long> seq_;
+  double tick_hz_ = 1e8;
+  static constexpr size_t kPingScratch = sizeof(unsigned long long) * (kPingMaxIters + 1) + 64;
+  void* ping_scratch_ = nullptr;  // device: stamps[kPingMaxIters + 1], status[2]
+  void* ping_host_ = nullptr;     // pinned copy of it
 };
 
 }  // namespace

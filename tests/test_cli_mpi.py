@@ -151,3 +151,10 @@ def test_cells_filter(mpirun, host_build):
     for key in ("uni", "bi"):
         nz = {(i, j) for i in range(3) for j in range(3) if m[key][i][j] > 0}
         assert nz == {(0, 1), (2, 0)}
+
+
+def test_device_latency_needs_one_sided_transport(mpirun, host_build):
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    out = run(mpirun, exe, 2, ["--transport", "host", "--size", "16K", "-n", "2", "--compat-only", "--device-latency"])
+    assert out.returncode != 0
+    assert "one-sided transport" in out.stderr + out.stdout

@@ -36,6 +36,42 @@ def test_two_ranks_all_modes(exe, tmp_path, engine):
     assert all(ph["mismatches"] == 0 for r in runs for ph in r["phases"])
 
 
+def _device_latency(out_json):
+    lines = [json.loads(l) for l in out_json.read_text().splitlines() if '"latency"' in l]
+    dev = [l for l in lines if l.get("method") == "device"]
+    assert len(dev) == 1
+    return dev[0]
+
+
+def test_device_latency_self(exe, tmp_path):
+    """One process: leader and follower are two waves of one workgroup."""
+    js = tmp_path / "r.json"
+    out = subprocess.run([exe, "--transport", "ipc", "--mode", "self", "--size", "4K", "-n", "2", "--compat-only",
+                          "--device-latency", "--latency-size", "4K", "--latency-iters", "500", "--json", str(js)],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lat = _device_latency(js)
+    p = lat["pairs"][0]
+    assert lat["bytes"] == 4096 and p["a"] == p["b"] == 0
+    assert 0 < p["one_way_us"]["p50"] < 50, p
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_device_latency_ranks_on_one_gpu(exe, tmp_path, nranks):
+    """Several processes on one GPU bounce messages through each other's
+    hipIpc-mapped signal pages; every pair of every round reports a time."""
+    js = tmp_path / "r.json"
+    out = subprocess.run([MPIRUN, "-n", str(nranks), exe, "--transport", "ipc", "--device", "0", "--mode", "ring",
+                          "--size", "4K", "-n", "2", "--no-compat", "--device-latency", "--latency-iters", "300",
+                          "--json", str(js)], capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "device-initiated ping-pong" in out.stdout
+    lat = _device_latency(js)
+    pairs = {(p["a"], p["b"]) for p in lat["pairs"]}
+    assert pairs == {(a, b) for a in range(nranks) for b in range(a + 1, nranks)}
+    assert all(0 < p["one_way_us"]["p50"] < 100 for p in lat["pairs"]), lat
+
+
 def test_four_ranks_allpairs_large(exe):
     out = subprocess.run([MPIRUN, "-n", "4", exe, "--transport", "ipc", "--device", "0", "--mode", "allpairs,ring",
                           "--size", "256M", "-n", "4", "--verify", "--no-compat"],
@@ -62,5 +98,6 @@ def test_bench_two_ranks_ipc():
     assert len(lines) == 1
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["verify_mismatches"] == 0 and r["matrix_cells"] == "2/2"
+    assert 0 < r["ipc_transport"]["device_pingpong_p50_us"] < 100, r["ipc_transport"]
     sweep = r["extras"]["pair_sweep_0_1"]
     assert len(sweep) == 11 and sweep[-1]["bytes"] == 4 << 30 and all(p["gbs"] > 0 for p in sweep)
