@@ -105,12 +105,20 @@ $(EXT): $(GPU_OBJS) $(BUILD)/gpu/pymodule.o
 $(BUILD)/fill_probe: scripts/fill_probe.hip | $(BUILD)/gpu
 	$(HIPCC) --offload-arch=$(ARCH) -O3 $< -o $@
 
-# AddressSanitizer / UBSan on host code only (GPU sanitizers are not available).
-ASAN := -fsanitize=address,undefined -fno-omit-frame-pointer -g -O1
-asan: | $(BUILD)/asan
-	$(CXX_HOST) $(CXXSTD) $(WARN) $(ASAN) -Icsrc -pthread $(addprefix csrc/,$(addsuffix .cpp,$(CORE) transport_rccl_stub)) \
-	    tests/host/test_main.cpp -o $(BUILD)/asan/p2p_host_tests
+# AddressSanitizer / UBSan on host code only (GPU sanitizers are not available):
+# the unit tests, and the MPI host binary that tests/test_host_unit.py runs as
+# a 3-rank job over the TCP transport.
+ASAN      := -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -g -O1
+ASAN_SRCS := $(addprefix csrc/,$(addsuffix .cpp,$(CORE) transport_rccl_stub))
+asan: $(BUILD)/asan/p2p_host_tests $(BUILD)/asan/p2p_matrix_host
 	ASAN_OPTIONS=detect_leaks=1 $(BUILD)/asan/p2p_host_tests
+
+$(BUILD)/asan/p2p_host_tests: $(ASAN_SRCS) tests/host/test_main.cpp $(HEADERS) | $(BUILD)/asan
+	$(CXX_HOST) $(CXXSTD) $(WARN) $(ASAN) -Icsrc -pthread $(ASAN_SRCS) tests/host/test_main.cpp -o $@
+
+$(BUILD)/asan/p2p_matrix_host: $(ASAN_SRCS) csrc/bootstrap_mpi.cpp csrc/main.cpp $(HEADERS) $(MPILIB)/.stamp | $(BUILD)/asan
+	$(CXX_HOST) $(CXXSTD) $(WARN) $(ASAN) -Icsrc $(MPI_INC) -pthread $(ASAN_SRCS) csrc/bootstrap_mpi.cpp csrc/main.cpp \
+	    -o $@ -L$(MPILIB) -lmpi -Wl,-rpath,'$$ORIGIN/../mpilib'
 
 test-host: $(BUILD)/p2p_host_tests
 	$(BUILD)/p2p_host_tests
