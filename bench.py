@@ -67,7 +67,7 @@ def parse_args(argv=None):
     ap.add_argument("--size", default="32M", help="message size (reference: 32 MiB, p2p_matrix.cc:124)")
     ap.add_argument("--msgs", type=int, default=8, help="messages per direction per step")
     ap.add_argument("--mode", default="tournament", choices=["tournament", "ring", "allpairs", "pair", "self"])
-    ap.add_argument("--transport", default="rccl", choices=["rccl", "ipc", "ipc:sdma", "host"],
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "ipc", "ipc:sdma", "ipc:push", "host"],
                     help="rccl (headline) | ipc = one-sided gfx950 copy kernel over hipIpc mappings | host = CPU (tests)")
     ap.add_argument("--device", type=int, default=None, help="GPU index (default LOCAL_RANK)")
     ap.add_argument("--latency-iters", type=int, default=300)
@@ -175,6 +175,8 @@ def main(argv=None) -> int:
     # driver's bracket; skipped on one GPU where the reference measures nothing.
     ref = None
     if n > 1 and args.ref_iters > 0:
+        if env.rank == 0:
+            log("bench: reference-semantics matrix")
         r = json.loads(sess.run(mode="pair", dir="uni", bytes=size, iters=args.ref_iters, warmup=0,
                                 timing="wallclock", verify=False, warm=False))
         ref = {"cell_gbs_min": round(r["gbs_min"], 3), "cell_gbs_mean": round(r["gbs_mean"], 3),
@@ -187,6 +189,8 @@ def main(argv=None) -> int:
     # neighbour exchange at 256 MiB (pipeline-parallel hop).
     extras = None
     if n > 1 and args.extras:
+        if env.rank == 0:
+            log("bench: all-pairs / ring extras")
         extras = {}
         for name, mode_x, dir_x, nbytes, iters in (("allpairs_1g", "allpairs", "bi", 1 << 30, 4),
                                                    ("ring_256m", "ring", "uni", 256 << 20, 8)):
@@ -206,6 +210,8 @@ def main(argv=None) -> int:
     if n > 1 and args.sweep:
         sweep = []
         for nbytes in [b for b in (4096 << (2 * k) for k in range(11)) if b <= nat.parse_size(args.sweep_max)]:
+            if env.rank == 0:
+                log("bench: pair sweep %d B" % nbytes)
             iters = max(4, min(200, (2 << 30) // nbytes))
             r = json.loads(sess.run(mode="pair", dir="uni", bytes=nbytes, iters=iters, warmup=2, timing="events",
                                     verify=False, warm=False, cells=[(0, 1)]))
@@ -219,12 +225,14 @@ def main(argv=None) -> int:
     # transport: one-sided pulls of hipIpc-mapped peer buffers by the gfx950
     # copy kernel) on the same links, for comparison with RCCL.  Untimed by the
     # contract; any error is reported in the JSON instead of failing the run.
-    ipc = None
     # (with --transport host the same code path runs on the CPU transport, for tests)
-    extra_transport = {"rccl": "ipc", "ipc": "ipc", "host": "host"}.get(args.transport)
-    if n > 1 and args.ipc_extra and extra_transport:
+    extra_transport = {"rccl": "ipc", "ipc": "ipc", "ipc:push": "ipc", "host": "host"}.get(args.transport)
+
+    def steps_through(transport):
+        """The timed steps again through another transport session (untimed by
+        the contract); any error is reported instead of failing the run."""
         try:
-            isess = create_session(extra_transport, device=device, timeout_s=90.0)
+            isess = create_session(transport, device=device, timeout_s=90.0)
             idrv = nat.StepDriver(isess, mode, "bi", size, args.msgs, not args.no_verify, bool(args.batch), False)
             idrv.connect()
             idrv.run_steps(0, args.warmup)
@@ -236,24 +244,32 @@ def main(argv=None) -> int:
             isess.barrier()
             ielapsed = isess.allreduce_max(time.perf_counter() - i0)
             ijob = sum(idrv.job_bytes_per_step(args.warmup + k) for k in range(args.steps))
+            out = {"value_gbs": round(ijob / ielapsed / 1e9, 3), "ms_per_step": round(ielapsed / args.steps * 1e3, 4),
+                   "verify_mismatches": idrv.verify_last() if not args.no_verify else -1,
+                   "transport": transport}
             # Device-initiated ping-pong: one wave per GPU writes the message
             # into the peer's memory and spins on its own inbox (no host, no
             # runtime in the loop) -- the fabric's latency, next to RCCL's.
-            dev_p50 = None
-            if isess.transport == "ipc":
+            if transport == "ipc":
                 dl = json.loads(isess.device_latency(nat.parse_size(args.latency_size), args.latency_iters,
                                                      min(100, args.latency_iters)))
-                dev_p50 = round(statistics.median(p["one_way_us"]["p50"] for p in dl["pairs"]), 3)
-            ipc = {"value_gbs": round(ijob / ielapsed / 1e9, 3), "ms_per_step": round(ielapsed / args.steps * 1e3, 4),
-                   "device_pingpong_p50_us": dev_p50,
-                   "verify_mismatches": idrv.verify_last() if not args.no_verify else -1,
-                   "transport": isess.transport,
-                   "engine": ("gfx950 multi-copy kernel, one-sided pull over hipIpc mappings"
-                              if isess.transport == "ipc" else isess.device_desc)}
+                out["device_pingpong_p50_us"] = round(statistics.median(p["one_way_us"]["p50"] for p in dl["pairs"]), 3)
             del idrv
             del isess
+            return out
         except Exception as e:  # report, never fail the headline
-            ipc = {"error": str(e)[:300]}
+            return {"error": str(e)[:300], "transport": transport}
+
+    # The hand-written data plane on the same links: the gfx950 multi-copy
+    # kernel pulling from hipIpc-mapped peer buffers ("pull", one-sided), and
+    # the rendezvous engine that writes into the receiver's slot ("push").
+    ipc = None
+    if n > 1 and args.ipc_extra and extra_transport:
+        ipc = steps_through(extra_transport)
+        if extra_transport == "ipc":
+            ipc["engine"] = "gfx950 multi-copy kernel, one-sided pull over hipIpc mappings"
+            ipc["push"] = steps_through("ipc:push")
+            ipc["push"]["engine"] = "ready/done flags + gfx950 multi-copy kernel writing into the peer's slot"
 
     step_ms_med = statistics.median(my_ms) if my_ms else 0.0
     result = {

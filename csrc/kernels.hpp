@@ -114,5 +114,26 @@ struct PingRole {
 // as two waves of one workgroup (self ping-pong on one GPU).
 void launch_pingpong(const PingRole& a, const PingRole* b, hipStream_t stream);
 
+// ---- stream-ordered flag signalling (pingpong.hip; IPC push engine) ----
+// One wave: optionally a system-scope release fence (so the writes of earlier
+// kernels in the stream, e.g. a copy into a peer's memory, reach their
+// memory first), then every post stores its value to its flag (system scope),
+// then the wave spins until every wait flag is >= its value (system-scope
+// acquire), each spin bounded by timeout_ticks; a deadline sets bit 0 of
+// *status (host-visible memory) and ends the kernel.
+constexpr int kMaxSignals = 16;
+struct SignalArgs {
+  unsigned long long* post_flag[kMaxSignals];
+  unsigned long long post_value[kMaxSignals];
+  const unsigned long long* wait_flag[kMaxSignals];
+  unsigned long long wait_value[kMaxSignals];
+  int nposts;
+  int nwaits;
+  int release_first;
+  unsigned int* status;
+  unsigned long long timeout_ticks;
+};
+void launch_signal(const SignalArgs& args, hipStream_t stream);
+
 }  // namespace dev
 }  // namespace p2p

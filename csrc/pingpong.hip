@@ -1,4 +1,5 @@
-// Device-initiated ping-pong over hipIpc-mapped memory (IPC transport).
+// Device-initiated ping-pong and stream-ordered flag signalling over
+// hipIpc-mapped memory (IPC transport).
 //
 // The reference has no latency measurement at all; the host-
 // posted ping-pong in runner.cpp (run_latency) measures what an application
@@ -85,7 +86,29 @@ __global__ __launch_bounds__(128) void pingpong_kernel(PingRole a, PingRole b) {
   }
 }
 
+__global__ __launch_bounds__(64) void signal_kernel(SignalArgs a) {
+  const int lane = threadIdx.x;
+  if (a.release_first) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (lane < a.nposts) __hip_atomic_store(a.post_flag[lane], a.post_value[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const u64 deadline = now_ticks() + a.timeout_ticks;
+  // Lane i watches wait i; the wave leaves when every lane's flag arrived.
+  bool ok = true;
+  if (lane < a.nwaits) {
+    while (__hip_atomic_load(a.wait_flag[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.wait_value[lane]) {
+      if (now_ticks() > deadline) {
+        ok = false;
+        break;
+      }
+    }
+  }
+  if (!ok) __hip_atomic_fetch_or(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace
+
+void launch_signal(const SignalArgs& args, hipStream_t stream) {
+  hipLaunchKernelGGL(signal_kernel, dim3(1), dim3(64), 0, stream, args);
+}
 
 void launch_pingpong(const PingRole& a, const PingRole* b, hipStream_t stream) {
   PingRole second = b ? *b : a;

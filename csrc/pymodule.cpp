@@ -43,7 +43,7 @@ class Session {
     TransportOptions opt;
     opt.device = device;
     opt.timeout_s = timeout_s;
-    // "ipc" or "ipc:sdma" / "ipc:kernel"
+    // "ipc" or "ipc:kernel" / "ipc:sdma" / "ipc:push"
     std::string kind = transport.substr(0, transport.find(':'));
     if (kind == "ipc" && transport.size() > 4) opt.ipc_engine = transport.substr(4);
     if (kind == "rccl")
@@ -53,7 +53,7 @@ class Session {
     else if (kind == "host")
       t_ = make_host_transport(*boot_, opt);
     else
-      P2P_FATAL("transport must be 'rccl', 'ipc[:kernel|:sdma]' or 'host'");
+      P2P_FATAL("transport must be 'rccl', 'ipc[:kernel|:sdma|:push]' or 'host'");
   }
 
   int rank() const { return boot_->rank(); }

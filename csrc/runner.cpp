@@ -47,10 +47,17 @@ Buffers::~Buffers() {
 
 // -------------------------------------------------------------- helpers ----
 
+int remote_slot(const Phase& phase, int me, int peer) {
+  const auto& from = phase.ranks[static_cast<size_t>(peer)].recv_from;
+  auto it = std::find(from.begin(), from.end(), me);
+  P2P_CHECK(it != from.end(), strfmt("rank %d sends to %d, which does not receive from it", me, peer));
+  return static_cast<int>(it - from.begin());
+}
+
 void post_phase_iteration(Transport& t, const Phase& phase, size_t bytes, Buffers& bufs) {
   const RankOps& ops = phase.ranks[static_cast<size_t>(t.rank())];
   t.group_begin();
-  for (int peer : ops.send_to) t.send(bufs.send_buf(), bytes, peer);
+  for (int peer : ops.send_to) t.send_to_slot(bufs.send_buf(), bytes, peer, remote_slot(phase, t.rank(), peer));
   for (size_t i = 0; i < ops.recv_from.size(); ++i) t.recv(bufs.recv_buf(static_cast<int>(i)), bytes, ops.recv_from[i]);
   t.group_end();
 }
@@ -463,7 +470,7 @@ void StepDriver::post_step_ops(const Phase& p) {
   const RankOps& ops = p.ranks[static_cast<size_t>(t_.rank())];
   t_.group_begin();
   for (int m = 0; m < msgs_; ++m) {
-    for (int peer : ops.send_to) t_.send(bufs_.send_buf(), bytes_, peer);
+    for (int peer : ops.send_to) t_.send_to_slot(bufs_.send_buf(), bytes_, peer, remote_slot(p, t_.rank(), peer));
     for (size_t i = 0; i < ops.recv_from.size(); ++i) t_.recv(bufs_.recv_buf(static_cast<int>(i)), bytes_, ops.recv_from[i]);
   }
   t_.group_end();

@@ -91,6 +91,10 @@ class Buffers {
   std::vector<void*> recv_;
 };
 
+// Receive slot on `peer` that holds messages from `me` in `phase` (position
+// of `me` in the peer's recv list).
+int remote_slot(const Phase& phase, int me, int peer);
+
 // Posts one iteration (one group) of `phase` for this rank.
 void post_phase_iteration(Transport& t, const Phase& phase, size_t bytes, Buffers& bufs);
 

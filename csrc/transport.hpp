@@ -52,6 +52,10 @@ class Transport {
   virtual void send(const void* p, size_t bytes, int peer) = 0;
   virtual void recv(void* p, size_t bytes, int peer) = 0;
   virtual void group_end() = 0;
+  // A send whose payload lands in receive slot `remote_slot` of the peer's
+  // buffer set (the receiver's index of this sender in its recv list).  Push
+  // transports need it to address the peer's memory; the rest ignore it.
+  virtual void send_to_slot(const void* p, size_t bytes, int peer, int /*remote_slot*/) { send(p, bytes, peer); }
 
   // ---- timing ----
   // Enqueue a timestamp behind all work posted so far; returns its id.
@@ -100,7 +104,7 @@ struct TransportOptions {
   double timeout_s = 300.0;        // watchdog for init / sync
   bool nonblocking_init = true;    // RCCL: ncclCommInitRankConfig(blocking=0) + polling
   int verify_impl = 0;             // 0 = auto, 1 = register-staged, 2 = LDS-staged (global_load_lds)
-  std::string ipc_engine = "kernel";  // IPC transport copy engine: kernel (gfx950 pull kernel) | sdma
+  std::string ipc_engine = "kernel";  // IPC transport: kernel (gfx950 pull kernel) | sdma | push (rendezvous + remote writes)
   bool two_streams = false;        // RCCL: receives on a second stream (reference layout)
 };
 

@@ -14,6 +14,14 @@
 //            split by size, 4 x 16 B remote loads in flight per lane);
 //   sdma   — hipMemcpyAsync per receive, forked onto one stream per receive
 //            slot so the copies of an all-pairs group run concurrently.
+//   push   — two-sided rendezvous with remote writes: a receive posts a
+//            "ready" flag into the sender's signal page, the sender's stream
+//            waits for it (one-wave signal kernel), the multi-copy kernel
+//            writes the payload straight into the receiver's slot over xGMI,
+//            and a second signal kernel releases it and raises "done" on the
+//            receiver, whose stream waits for that.  Real send/recv semantics
+//            (a send never overwrites a slot the receiver has not posted) on
+//            the direction xGMI handles best (remote stores).
 //
 // Why it exists: it is the hand-written CDNA4 data plane to compare RCCL's
 // ncclSend/ncclRecv against on the same links, and, because IPC mappings
@@ -25,6 +33,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <map>
 #include <thread>
 #include <vector>
 
@@ -54,7 +63,8 @@ class IpcTransport final : public Transport {
  public:
   IpcTransport(Bootstrap& boot, const TransportOptions& opt)
       : boot_(boot), rank_(boot.rank()), n_(boot.size()), timeout_(opt.timeout_s), engine_(opt.ipc_engine) {
-    P2P_CHECK(engine_ == "kernel" || engine_ == "sdma", "ipc engine must be 'kernel' or 'sdma'");
+    P2P_CHECK(engine_ == "kernel" || engine_ == "sdma" || engine_ == "push",
+              "ipc engine must be 'kernel', 'sdma' or 'push'");
     verify_impl_ = static_cast<dev::VerifyImpl>(opt.verify_impl);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) P2P_FATAL("ipc transport: no HIP device visible");
@@ -68,6 +78,11 @@ class IpcTransport final : public Transport {
     HIPCHECK(hipGetDeviceProperties(&prop, device_));
     desc_ = strfmt("hip:%d %s (%s, %d CUs) ipc-%s", device_, prop.name, prop.gcnArchName, prop.multiProcessorCount,
                    engine_.c_str());
+    int khz = 0;
+    HIPCHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_));
+    P2P_CHECK(khz > 0, "device reports no wall clock rate");
+    tick_hz_ = khz * 1e3;
+    if (engine_ == "push") setup_sync_pages();
   }
 
   ~IpcTransport() override {
@@ -78,7 +93,12 @@ class IpcTransport final : public Transport {
       if (peer_pages_[r] && static_cast<int>(r) != rank_) (void)hipIpcCloseMemHandle(peer_pages_[r]);
     if (page_) (void)hipFree(page_);
     if (ping_scratch_) (void)hipFree(ping_scratch_);
+    for (size_t r = 0; r < sync_peer_.size(); ++r)
+      if (sync_peer_[r] && static_cast<int>(r) != rank_) (void)hipIpcCloseMemHandle(sync_peer_[r]);
+    if (sync_page_) (void)hipFree(sync_page_);
+    if (sig_status_) (void)hipHostFree(sig_status_);
     if (ping_host_) (void)hipHostFree(ping_host_);
+    drain_pool();
     for (auto ex : execs_) (void)hipGraphExecDestroy(ex);
     for (auto s : side_) (void)hipStreamDestroy(s);
     for (auto e : side_done_) (void)hipEventDestroy(e);
@@ -94,15 +114,54 @@ class IpcTransport final : public Transport {
   int nranks() const override { return n_; }
   std::string device_desc() const override { return desc_; }
 
-  bool mem_info(size_t* free_b, size_t* total_b) override { return hipMemGetInfo(free_b, total_b) == hipSuccess; }
+  bool mem_info(size_t* free_b, size_t* total_b) override {
+    if (hipMemGetInfo(free_b, total_b) != hipSuccess) return false;
+    *free_b += pool_bytes_;  // pooled blocks are handed back on demand
+    return true;
+  }
+  // At least 2 MiB, rounded to 2 MiB: small hipMallocs can be sub-allocated
+  // from a shared chunk, and hipIpcGetMemHandle rejects those ("invalid
+  // argument"); every exported buffer must be an allocation of its own.
+  //
+  // Released buffers are kept for reuse (up to kPoolBytes): a buffer set is
+  // created per run, and a just-freed block that peers mapped a moment ago
+  // can come back from hipMalloc while the runtime still tracks the old
+  // export, which makes hipIpcGetMemHandle fail intermittently ("invalid
+  // argument").  Reusing the same allocations avoids that churn entirely.
   void* alloc(size_t bytes) override {
+    constexpr size_t kGrain = size_t{2} << 20;
+    const size_t size = (std::max<size_t>(bytes, 1) + kGrain - 1) / kGrain * kGrain;
+    for (auto it = pool_.begin(); it != pool_.end(); ++it)
+      if (it->second == size) {
+        void* p = it->first;
+        pool_bytes_ -= size;
+        pool_.erase(it);
+        sizes_[p] = size;
+        return p;
+      }
     void* p = nullptr;
-    hipError_t e = hipMalloc(&p, std::max<size_t>(bytes, 256));
+    hipError_t e = hipMalloc(&p, size);
+    if (e != hipSuccess && !pool_.empty()) {  // give the pool back and retry once
+      (void)hipGetLastError();
+      drain_pool();
+      e = hipMalloc(&p, size);
+    }
     if (e != hipSuccess) P2P_FATAL(strfmt("hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e)));
+    sizes_[p] = size;
     return p;
   }
   void release(void* p) override {
-    if (p) HIPCHECK(hipFree(p));
+    if (!p) return;
+    auto it = sizes_.find(p);
+    P2P_CHECK(it != sizes_.end(), "release of a buffer this transport did not allocate");
+    const size_t size = it->second;
+    sizes_.erase(it);
+    if (pool_bytes_ + size <= kPoolBytes) {
+      pool_.emplace_back(p, size);
+      pool_bytes_ += size;
+    } else {
+      HIPCHECK(hipFree(p));
+    }
   }
   void fill(void* p, size_t bytes, uint64_t seed) override { dev::launch_fill(p, bytes, seed, stream_); }
   void zero(void* p, size_t bytes) override { HIPCHECK(hipMemsetAsync(p, 0, bytes, stream_)); }
@@ -148,6 +207,22 @@ class IpcTransport final : public Transport {
       HIPCHECK(hipIpcOpenMemHandle(&mapped, all[static_cast<size_t>(r)].handle, hipIpcMemLazyEnablePeerAccess));
       reg.peer_send[static_cast<size_t>(r)] = mapped;
     }
+    if (engine_ == "push") {
+      // The sender writes into the receiver's slot: map every peer's slots.
+      reg.peer_recvs.assign(static_cast<size_t>(n_), std::vector<void*>(recvs.size(), nullptr));
+      for (size_t k = 0; k < recvs.size(); ++k) {
+        Export slot{};
+        HIPCHECK(hipIpcGetMemHandle(&slot.handle, recvs[k]));
+        slot.bytes = bytes;
+        auto slots = boot_.allgather_value(slot);
+        for (int r = 0; r < n_; ++r) {
+          void* mapped = recvs[k];
+          if (r != rank_)
+            HIPCHECK(hipIpcOpenMemHandle(&mapped, slots[static_cast<size_t>(r)].handle, hipIpcMemLazyEnablePeerAccess));
+          reg.peer_recvs[static_cast<size_t>(r)][k] = mapped;
+        }
+      }
+    }
     regs_.push_back(std::move(reg));
     boot_.barrier();
   }
@@ -156,10 +231,14 @@ class IpcTransport final : public Transport {
     auto it = std::find_if(regs_.begin(), regs_.end(), [&](const Registration& r) { return r.send == send; });
     if (it == regs_.end()) return;
     sync();
-    // Every rank stops pulling before any rank frees the pages it exported.
+    // Every rank stops moving data before any mapping goes, and every rank
+    // has closed its mappings of a buffer before its owner frees it: a freed
+    // block that a peer still maps can come back from hipMalloc, and
+    // hipIpcGetMemHandle then refuses it ("invalid argument").
     boot_.barrier();
     close_registration(*it);
     regs_.erase(it);
+    boot_.barrier();
   }
 
   void group_begin() override {
@@ -167,14 +246,30 @@ class IpcTransport final : public Transport {
     in_group_ = true;
     ops_.clear();
   }
-  void send(const void* p, size_t bytes, int peer) override {
+  void send(const void* p, size_t bytes, int peer) override { send_to_slot(p, bytes, peer, 0); }
+  void send_to_slot(const void* p, size_t bytes, int peer, int slot) override {
     P2P_CHECK(peer >= 0 && peer < n_, "bad peer");
-    bool ok = std::any_of(regs_.begin(), regs_.end(), [&](const Registration& r) { return r.send == p && bytes <= r.bytes; });
-    P2P_CHECK(ok, "ipc transport sends only from a registered send buffer (one-sided pull)");
-    // Nothing to move: the receiver pulls.
+    const Registration* reg = nullptr;
+    for (const auto& r : regs_)
+      if (r.send == p && bytes <= r.bytes) reg = &r;
+    P2P_CHECK(reg, "ipc transport sends only from a registered send buffer");
+    if (engine_ != "push") return;  // nothing to move: the receiver pulls
+    P2P_CHECK(slot >= 0 && slot < static_cast<int>(reg->recvs.size()), "bad remote slot");
+    ops_.push_back({p, reg->peer_recvs[static_cast<size_t>(peer)][static_cast<size_t>(slot)], bytes});
+    if (peer != rank_) push_sends_.push_back(peer);
+    if (!in_group_) flush();
   }
   void recv(void* p, size_t bytes, int peer) override {
     P2P_CHECK(peer >= 0 && peer < n_, "bad peer");
+    if (engine_ == "push") {
+      bool ok = std::any_of(regs_.begin(), regs_.end(), [&](const Registration& r) {
+        return bytes <= r.bytes && std::find(r.recvs.begin(), r.recvs.end(), p) != r.recvs.end();
+      });
+      P2P_CHECK(ok, "ipc transport receives only into a registered receive slot");
+      if (peer != rank_) push_recvs_.push_back(peer);  // a self receive is the self send's copy
+      if (!in_group_) flush();
+      return;
+    }
     const Registration* reg = nullptr;
     for (const auto& r : regs_)
       if (std::find(r.recvs.begin(), r.recvs.end(), p) != r.recvs.end()) reg = &r;
@@ -204,6 +299,8 @@ class IpcTransport final : public Transport {
   }
   void clear_marks() override { next_event_ = 0; }
 
+  // Push: the flag values are baked into each launch, so a replay would wait
+  // for flags that were already consumed; no graphs there.
   bool supports_graphs() const override { return engine_ == "kernel"; }
   void capture_begin() override { HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal)); }
   int capture_end() override {
@@ -253,10 +350,6 @@ class IpcTransport final : public Transport {
       peer_pages_[static_cast<size_t>(r)] = mapped;
     }
     seq_.assign(static_cast<size_t>(n_), 0);
-    int khz = 0;
-    HIPCHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_));
-    P2P_CHECK(khz > 0, "device reports no wall clock rate");
-    tick_hz_ = khz * 1e3;
     HIPCHECK(hipMalloc(&ping_scratch_, kPingScratch));
     HIPCHECK(hipHostMalloc(&ping_host_, kPingScratch, hipHostMallocDefault));
     boot_.barrier();
@@ -321,7 +414,11 @@ class IpcTransport final : public Transport {
     double t0 = now_seconds();
     for (long it = 0;; ++it) {
       hipError_t e = hipStreamQuery(stream_);
-      if (e == hipSuccess) return;
+      if (e == hipSuccess) {
+        if (sig_status_ && (*sig_status_ & 1u))
+          P2P_FATAL(strfmt("rank %d: ipc push rendezvous timed out (a peer never posted its side)", rank_));
+        return;
+      }
       if (e != hipErrorNotReady) P2P_FATAL(strfmt("stream error: %s", hipGetErrorString(e)));
       if ((it & 255) == 0) {
         double now = now_seconds();
@@ -337,6 +434,7 @@ class IpcTransport final : public Transport {
     size_t bytes = 0;
     std::vector<void*> recvs;
     std::vector<void*> peer_send;  // mapped send buffer of every rank (own one for self)
+    std::vector<std::vector<void*>> peer_recvs;  // push: [rank][slot] mapped receive slots
   };
 
   void close_registration(Registration& reg) {
@@ -344,10 +442,104 @@ class IpcTransport final : public Transport {
       void*& m = reg.peer_send[static_cast<size_t>(r)];
       if (m && r != rank_) (void)hipIpcCloseMemHandle(m);
       m = nullptr;
+      if (static_cast<size_t>(r) < reg.peer_recvs.size())
+        for (void*& slot : reg.peer_recvs[static_cast<size_t>(r)]) {
+          if (slot && r != rank_) (void)hipIpcCloseMemHandle(slot);
+          slot = nullptr;
+        }
     }
   }
 
+  // Push group: readies out / readies in, the copies, then done out / done in.
+  void flush_push() {
+    dev::SignalArgs pre{}, post{};
+    for (int p : push_recvs_) add_post(&pre, p, kReady, ++ready_posted_[static_cast<size_t>(p)]);
+    for (int q : push_sends_) add_wait(&pre, q, kReady, ++ready_seen_[static_cast<size_t>(q)]);
+    launch_signals(pre, false);
+    if (!ops_.empty()) dev::launch_multi_copy(ops_.data(), static_cast<int>(ops_.size()), stream_);
+    for (int q : push_sends_) add_post(&post, q, kDone, ++done_posted_[static_cast<size_t>(q)]);
+    for (int p : push_recvs_) add_wait(&post, p, kDone, ++done_seen_[static_cast<size_t>(p)]);
+    launch_signals(post, true);
+    ops_.clear();
+    push_sends_.clear();
+    push_recvs_.clear();
+  }
+
+  // Signal page line of kind k (ready / done) that rank `from` writes.
+  unsigned long long* sync_line(void* page, int kind, int from) const {
+    return reinterpret_cast<unsigned long long*>(static_cast<unsigned char*>(page) +
+                                                 kSyncLine * (static_cast<size_t>(kind) * n_ + static_cast<size_t>(from)));
+  }
+  // Several messages to one peer in a group share its flag: keep one entry
+  // per flag with the highest value (lanes storing to one address at once
+  // would leave an arbitrary one of the values).
+  void add_post(dev::SignalArgs* a, int peer, int kind, unsigned long long v) {
+    unsigned long long* f = sync_line(sync_peer_[static_cast<size_t>(peer)], kind, rank_);
+    for (int i = 0; i < a->nposts; ++i)
+      if (a->post_flag[i] == f) {
+        a->post_value[i] = std::max(a->post_value[i], v);
+        return;
+      }
+    if (a->nposts == dev::kMaxSignals) launch_signals(*a, false), *a = dev::SignalArgs{};
+    a->post_flag[a->nposts] = f;
+    a->post_value[a->nposts++] = v;
+  }
+  void add_wait(dev::SignalArgs* a, int peer, int kind, unsigned long long v) {
+    const unsigned long long* f = sync_line(sync_page_, kind, peer);
+    for (int i = 0; i < a->nwaits; ++i)
+      if (a->wait_flag[i] == f) {
+        a->wait_value[i] = std::max(a->wait_value[i], v);
+        return;
+      }
+    if (a->nwaits == dev::kMaxSignals) launch_signals(*a, false), *a = dev::SignalArgs{};
+    a->wait_flag[a->nwaits] = f;
+    a->wait_value[a->nwaits++] = v;
+  }
+  void launch_signals(dev::SignalArgs a, bool release_first) {
+    if (a.nposts == 0 && a.nwaits == 0) return;
+    a.release_first = release_first ? 1 : 0;
+    a.status = sig_status_;
+    a.timeout_ticks = static_cast<unsigned long long>(timeout_ * tick_hz_);
+    dev::launch_signal(a, stream_);
+  }
+
+  // Collective (constructor): one signal page per rank, 2 x n flag lines
+  // (ready / done from every peer), exported to every peer.
+  void setup_sync_pages() {
+    const size_t bytes = kSyncLine * 2 * static_cast<size_t>(n_);
+    if (hipExtMallocWithFlags(&sync_page_, bytes, hipDeviceMallocUncached) != hipSuccess) {
+      (void)hipGetLastError();
+      HIPCHECK(hipMalloc(&sync_page_, bytes));
+    }
+    HIPCHECK(hipMemset(sync_page_, 0, bytes));
+    HIPCHECK(hipDeviceSynchronize());
+    HIPCHECK(hipHostMalloc(&sig_status_, 64, hipHostMallocMapped));
+    *sig_status_ = 0;
+    Export me{};
+    HIPCHECK(hipIpcGetMemHandle(&me.handle, sync_page_));
+    me.host_hash = host_hash(real_hostname());
+    auto all = boot_.allgather_value(me);
+    sync_peer_.assign(static_cast<size_t>(n_), nullptr);
+    for (int r = 0; r < n_; ++r) {
+      if (r == rank_) {
+        sync_peer_[static_cast<size_t>(r)] = sync_page_;
+        continue;
+      }
+      P2P_CHECK(all[static_cast<size_t>(r)].host_hash == me.host_hash,
+                strfmt("ipc transport is intra-node only: rank %d is on another host", r));
+      void* mapped = nullptr;
+      HIPCHECK(hipIpcOpenMemHandle(&mapped, all[static_cast<size_t>(r)].handle, hipIpcMemLazyEnablePeerAccess));
+      sync_peer_[static_cast<size_t>(r)] = mapped;
+    }
+    for (auto* v : {&ready_posted_, &ready_seen_, &done_posted_, &done_seen_}) v->assign(static_cast<size_t>(n_), 0);
+    boot_.barrier();
+  }
+
   void flush() {
+    if (engine_ == "push") {
+      flush_push();
+      return;
+    }
     if (ops_.empty()) return;
     if (engine_ == "kernel") {
       dev::launch_multi_copy(ops_.data(), static_cast<int>(ops_.size()), stream_);
@@ -399,6 +591,25 @@ class IpcTransport final : public Transport {
   std::vector<Registration> regs_;
   bool in_group_ = false;
   std::vector<dev::CopyOp> ops_;
+
+  void drain_pool() {
+    for (auto& b : pool_) (void)hipFree(b.first);
+    pool_.clear();
+    pool_bytes_ = 0;
+  }
+  static constexpr size_t kPoolBytes = size_t{32} << 30;
+  std::vector<std::pair<void*, size_t>> pool_;  // released, kept for reuse
+  size_t pool_bytes_ = 0;
+  std::map<void*, size_t> sizes_;               // live allocations
+
+  // Push engine state.
+  static constexpr size_t kSyncLine = 128;
+  static constexpr int kReady = 0, kDone = 1;
+  void* sync_page_ = nullptr;
+  std::vector<void*> sync_peer_;
+  unsigned int* sig_status_ = nullptr;  // host-mapped; bit 0 = a signal wait timed out
+  std::vector<unsigned long long> ready_posted_, ready_seen_, done_posted_, done_seen_;
+  std::vector<int> push_sends_, push_recvs_;
 
   static constexpr size_t kPingHeader = 256;            // flag + padding (own cache lines)
   static constexpr size_t kPingMaxBytes = 64u << 10;

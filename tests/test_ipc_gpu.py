@@ -22,12 +22,12 @@ def exe():
     return os.path.join(ROOT, "build", "p2p_matrix")
 
 
-@pytest.mark.parametrize("engine", ["kernel", "sdma"])
+@pytest.mark.parametrize("engine", ["kernel", "sdma", "push"])
 def test_two_ranks_all_modes(exe, tmp_path, engine):
     js = tmp_path / "r.json"
     out = subprocess.run([MPIRUN, "-n", "2", exe, "--transport", "ipc", "--ipc-engine", engine, "--device", "0",
                           "--mode", "all", "--sizes", "4K:16M:4", "-n", "6", "--verify", "--latency",
-                          "--latency-iters", "50", "--json", str(js)], capture_output=True, text=True, timeout=300)
+                          "--latency-iters", "50", "--json", str(js), "--timeout", "60"], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     m = parse_compat(out.stdout)
     assert m["uni"][0][1] > 0 and m["bi"][1][0] > 0
@@ -72,9 +72,11 @@ def test_device_latency_ranks_on_one_gpu(exe, tmp_path, nranks):
     assert all(0 < p["one_way_us"]["p50"] < 100 for p in lat["pairs"]), lat
 
 
-def test_four_ranks_allpairs_large(exe):
-    out = subprocess.run([MPIRUN, "-n", "4", exe, "--transport", "ipc", "--device", "0", "--mode", "allpairs,ring",
-                          "--size", "256M", "-n", "4", "--verify", "--no-compat"],
+@pytest.mark.parametrize("engine", ["kernel", "push"])
+def test_four_ranks_allpairs_large(exe, engine):
+    out = subprocess.run([MPIRUN, "-n", "4", exe, "--transport", "ipc", "--ipc-engine", engine, "--device", "0",
+                          "--mode", "allpairs,ring,tournament", "--size", "256M", "-n", "4", "--verify", "--no-compat",
+                          "--timeout", "60"],
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     assert "verification: OK" in out.stdout
@@ -88,6 +90,20 @@ def test_corruption_detected_on_gpu(exe):
     assert "VERIFICATION FAILED" in out.stderr
 
 
+def test_bench_two_ranks_ipc_push():
+    """bench.py with the push engine as the headline transport (rendezvous +
+    remote writes), graphs off by construction."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2", "--steps", "6", "--warmup", "3",
+           "--transport", "ipc:push", "--device", "0", "--latency-iters", "50", "--sweep-max", "64M", "--ipc-extra", "0"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    progress = "\n".join(l for l in out.stderr.splitlines() if "bench:" in l or "fatal" in l)
+    assert out.returncode == 0, progress
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert r["n_gpus"] == 2 and r["verify_mismatches"] == 0 and r["matrix_cells"] == "2/2" and r["value"] > 0
+    assert r["p50_latency_us"] > 0
+
+
 def test_bench_two_ranks_ipc():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2", "--steps", "6", "--warmup", "3",
@@ -99,5 +115,7 @@ def test_bench_two_ranks_ipc():
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["verify_mismatches"] == 0 and r["matrix_cells"] == "2/2"
     assert 0 < r["ipc_transport"]["device_pingpong_p50_us"] < 100, r["ipc_transport"]
+    push = r["ipc_transport"]["push"]
+    assert push["verify_mismatches"] == 0 and push["value_gbs"] > 0, push
     sweep = r["extras"]["pair_sweep_0_1"]
     assert len(sweep) == 11 and sweep[-1]["bytes"] == 4 << 30 and all(p["gbs"] > 0 for p in sweep)
