@@ -73,7 +73,9 @@ def parse_args(argv=None):
     ap.add_argument("--latency-iters", type=int, default=300)
     ap.add_argument("--latency-size", default="8")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--batch", type=int, default=1, help="1: all msgs of a step in one ncclGroup (one launch)")
+    ap.add_argument("--batch", type=int, default=-1,
+                    help="1: all msgs of a step in one group (one launch); 0: one group per message; "
+                         "-1: the W warmup steps are split between both and the faster posting is timed")
     ap.add_argument("--graph", type=int, default=0, help="1: replay each step as a captured hipGraph")
     ap.add_argument("--json-out", default=None, help="also write the result line to this file")
     ap.add_argument("--ipc-extra", type=int, default=1,
@@ -117,13 +119,38 @@ def main(argv=None) -> int:
     if env.rank == 0:
         log("bench: %d rank(s), %s, %s" % (n, sess.transport, sess.device_desc))
     mode = "self" if n == 1 else args.mode
-    drv = nat.StepDriver(sess, mode, "bi", size, args.msgs, not args.no_verify, bool(args.batch), bool(args.graph))
-    drv.connect()
 
-    # Warmup (untimed): also walks every round once when W >= phases.
-    if args.warmup > 0:
-        drv.run_steps(0, args.warmup)
-        drv.sync()
+    def make_driver(batch):
+        d = nat.StepDriver(sess, mode, "bi", size, args.msgs, not args.no_verify, bool(batch), bool(args.graph))
+        d.connect()
+        return d
+
+    # Warmup (untimed, W steps in total).  With --batch -1 the W steps are
+    # split between the two postings (one group per step vs one group per
+    # message) and the faster one, by the slowest rank's clock, is timed.
+    # connect() has already established every connection of every round.
+    choices = [args.batch] if args.batch >= 0 or args.warmup < 2 else [0, 1]
+    if choices == [-1]:
+        choices = [1]
+    tuning = {}
+    drivers = {}
+    done = 0
+    for i, b in enumerate(choices):
+        d = make_driver(b)
+        k = (args.warmup - done) // (len(choices) - i)
+        if k > 0:
+            barrier()
+            w0 = time.perf_counter()
+            d.run_steps(done, k)
+            d.sync()
+            barrier()
+            tuning[b] = sess.allreduce_max(time.perf_counter() - w0) / k
+            done += k
+        drivers[b] = d
+    batch = min(tuning, key=tuning.get) if len(tuning) == len(choices) else choices[-1]
+    drv = drivers.pop(batch)
+    del drivers, d  # the other posting's buffers go before the timed region
+    gpu_sync()
     drv.reset()
 
     barrier()
@@ -233,7 +260,7 @@ def main(argv=None) -> int:
         the contract); any error is reported instead of failing the run."""
         try:
             isess = create_session(transport, device=device, timeout_s=90.0)
-            idrv = nat.StepDriver(isess, mode, "bi", size, args.msgs, not args.no_verify, bool(args.batch), False)
+            idrv = nat.StepDriver(isess, mode, "bi", size, args.msgs, not args.no_verify, bool(batch), False)
             idrv.connect()
             idrv.run_steps(0, args.warmup)
             idrv.sync()
@@ -302,7 +329,9 @@ def main(argv=None) -> int:
         "rank0_step_ms_p50": round(step_ms_med, 4),
         "verify_mismatches": mismatches,
         "transport": sess.transport,
-        "posting": {"batch": bool(args.batch), "graph": bool(args.graph)},
+        "posting": {"batch": bool(batch), "graph": bool(args.graph),
+                    "warmup_ms_per_step": {("batch" if b else "per_message"): round(v * 1e3, 4)
+                                           for b, v in tuning.items()}},
         "reference_semantics": ref,
         "extras": extras,
         "ipc_transport": ipc,
