@@ -191,6 +191,9 @@ def main(argv=None) -> int:
     expected = n * (n - 1) if n > 1 else 1
 
     mismatches = drv.verify_last() if not args.no_verify else -1
+    # Everything below is untimed; release the timed driver's buffers first so
+    # the comparisons run on the same memory footprint as the timed steps did.
+    del drv
 
     lat = json.loads(sess.latency(nat.parse_size(args.latency_size), args.latency_iters, min(50, args.latency_iters)))
     p50s = [p["one_way_us"]["p50"] for p in lat["pairs"]]
@@ -252,6 +255,11 @@ def main(argv=None) -> int:
     # transport: one-sided pulls of hipIpc-mapped peer buffers by the gfx950
     # copy kernel) on the same links, for comparison with RCCL.  Untimed by the
     # contract; any error is reported in the JSON instead of failing the run.
+    # The comparisons below open sessions of their own; close the headline one
+    # first so they run alone, as the timed steps did.
+    headline_transport = sess.transport
+    del sess
+
     # (with --transport host the same code path runs on the CPU transport, for tests)
     extra_transport = {"rccl": "ipc", "ipc": "ipc", "ipc:push": "ipc", "host": "host"}.get(args.transport)
 
@@ -314,7 +322,7 @@ def main(argv=None) -> int:
         "data": "synthetic (device PRNG-filled payloads, verified after timing)",
         "config": {
             "model": "p2p_matrix: %s %s-bidirectional, %s x %d msgs/step"
-                     % ("RCCL ncclSend/ncclRecv" if sess.transport == "rccl" else sess.transport + " transport",
+                     % ("RCCL ncclSend/ncclRecv" if headline_transport == "rccl" else headline_transport + " transport",
                         mode, nat.format_size(size), args.msgs),
             "global_batch": args.msgs * n,
             "seq_len": size,
@@ -328,7 +336,7 @@ def main(argv=None) -> int:
         "per_gpu_gbs": round(value / n, 3),
         "rank0_step_ms_p50": round(step_ms_med, 4),
         "verify_mismatches": mismatches,
-        "transport": sess.transport,
+        "transport": headline_transport,
         "posting": {"batch": bool(batch), "graph": bool(args.graph),
                     "warmup_ms_per_step": {("batch" if b else "per_message"): round(v * 1e3, 4)
                                            for b, v in tuning.items()}},
@@ -346,8 +354,6 @@ def main(argv=None) -> int:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
     barrier()
-    del drv
-    del sess
     if n > 1 and dist.is_initialized():
         dist.destroy_process_group()
     return 0 if mismatches in (0, -1) else 3
