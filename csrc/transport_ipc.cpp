@@ -39,17 +39,12 @@
 
 #include "bootstrap.hpp"
 #include "common.hpp"
+#include "hip_check.hpp"
 #include "kernels.hpp"
 #include "transport.hpp"
 
 namespace p2p {
 namespace {
-
-#define HIPCHECK(cmd)                                                                          \
-  do {                                                                                         \
-    hipError_t e_ = (cmd);                                                                     \
-    if (e_ != hipSuccess) P2P_FATAL(strfmt("HIP error in %s: %s", #cmd, hipGetErrorString(e_))); \
-  } while (0)
 
 struct Export {
   hipIpcMemHandle_t handle;

@@ -30,18 +30,13 @@
 
 #include "bootstrap.hpp"
 #include "common.hpp"
+#include "hip_check.hpp"
 #include "kernels.hpp"
 #include "transport.hpp"
 #include "units.hpp"
 
 namespace p2p {
 namespace {
-
-#define HIPCHECK(cmd)                                                                          \
-  do {                                                                                         \
-    hipError_t e_ = (cmd);                                                                     \
-    if (e_ != hipSuccess) P2P_FATAL(strfmt("HIP error in %s: %s", #cmd, hipGetErrorString(e_))); \
-  } while (0)
 
 class RcclTransport final : public Transport {
  public:
