@@ -50,3 +50,9 @@ def test_bench_cpu_two_ranks(native):
     sweep = r["extras"]["pair_sweep_0_1"]
     assert [p["bytes"] for p in sweep] == [4096, 16384, 65536, 262144, 1048576]
     assert all(p["gbs"] > 0 for p in sweep)
+
+
+def test_session_api_under_torchrun(native):
+    out = torchrun(3, ["tests/scripts/session_api.py"])
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "SESSION API OK" in out.stdout
