@@ -68,3 +68,19 @@ def test_bench_all_gpus():
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert r["n_gpus"] == n and r["verify_mismatches"] == 0
     assert r["matrix_cells"] == "%d/%d" % (n * (n - 1), n * (n - 1))
+
+
+@pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
+@pytest.mark.parametrize("engine", ["kernel", "push"])
+def test_ipc_engines_all_gpus(exe, engine):
+    """The hand-written data plane across real xGMI links: pull (remote reads)
+    and push (rendezvous + remote writes), verified, plus the device ping-pong
+    matrix."""
+    n = _n()
+    out = subprocess.run([MPIRUN, "-n", str(n), exe, "--transport", "ipc", "--ipc-engine", engine,
+                          "--mode", "tournament,allpairs", "--sizes", "1M,256M", "-n", "8", "--verify",
+                          "--device-latency", "--latency-iters", "200", "--no-compat", "--timeout", "120"],
+                         capture_output=True, text=True, timeout=900)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "verification: OK" in out.stdout and "FAILED" not in out.stdout
+    assert "device-initiated ping-pong" in out.stdout
