@@ -78,21 +78,36 @@ def read_json_lines(path: str) -> List[dict]:
     return out
 
 
+def _get(r: dict, *path, fmt: str = "%.1f") -> str:
+    v = r
+    for k in path:
+        if not isinstance(v, dict) or v.get(k) is None:
+            return "-"
+        v = v[k]
+    return fmt % v if isinstance(v, (int, float)) else str(v)
+
+
 def scaling_table(results: Iterable[dict]) -> str:
     """Markdown table of bench.py lines (one per GPU count): aggregate GB/s,
-    per-GPU GB/s, matrix min/mean, p50 latency, and efficiency vs N=2 (the
-    first point where xGMI links are involved; N=1 is the self path)."""
+    per-GPU GB/s, matrix min/mean, p50 latency, efficiency vs N=2 (the first
+    point where xGMI links are involved; N=1 is the self path), and the
+    untimed comparisons the line carries: the reference's methodology on the
+    same communicator, all-pairs aggregate, and the IPC pull / push engines."""
     rows = sorted(results, key=lambda r: r["n_gpus"])
     base = next((r for r in rows if r["n_gpus"] == 2), None)
-    out = ["| GPUs | aggregate GB/s | per-GPU GB/s | matrix min / mean GB/s | p50 latency us | eff. vs 2 GPUs |",
-           "|---|---|---|---|---|---|"]
+    out = ["| GPUs | aggregate GB/s | per-GPU GB/s | matrix min / mean GB/s | p50 latency us | eff. vs 2 GPUs "
+           "| reference-method cell GB/s | all-pairs 1 GiB aggregate GB/s | IPC pull / push GB/s | device ping-pong us |",
+           "|---|---|---|---|---|---|---|---|---|---|"]
     for r in rows:
         eff = ""
         if base and r["n_gpus"] >= 2:
             eff = "%.1f%%" % (100.0 * r["value"] / r["n_gpus"] / (base["value"] / 2))
-        out.append("| %d | %.1f | %.1f | %s / %s | %s | %s |" % (
+        out.append("| %d | %.1f | %.1f | %s / %s | %s | %s | %s | %s | %s / %s | %s |" % (
             r["n_gpus"], r["value"], r["value"] / r["n_gpus"], r.get("matrix_gbs_min"), r.get("matrix_gbs_mean"),
-            r.get("p50_latency_us"), eff))
+            r.get("p50_latency_us"), eff, _get(r, "reference_semantics", "cell_gbs_mean"),
+            _get(r, "extras", "allpairs_1g", "aggregate_gbs"), _get(r, "ipc_transport", "value_gbs"),
+            _get(r, "ipc_transport", "push", "value_gbs"), _get(r, "ipc_transport", "device_pingpong_p50_us",
+                                                                   fmt="%.2f")))
     return "\n".join(out)
 
 
@@ -119,6 +134,7 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=main.__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("files", nargs="+")
     a = ap.parse_args(argv)
+    all_bench = []
     for path in a.files:
         text = open(path).read()
         print("== %s" % path)
@@ -134,11 +150,15 @@ def main(argv=None) -> int:
         runs = [r for r in recs if r.get("type") == "run"]
         if bench:
             print(scaling_table(bench))
+            all_bench.extend(bench)
         for r in runs:
             print("%-10s %-3s %10d B x %4d: GB/s min %.2f mean %.2f max %.2f"
                   % (r["mode"], r["dir"], r["bytes"], r["iters"], r["gbs_min"], r["gbs_mean"], r["gbs_max"]))
         if UNI_TITLE in text or BI_TITLE in text:
             print(summarize_compat(text))
+    if len({r["n_gpus"] for r in all_bench}) > 1:  # one line per GPU count across files: the scaling curve
+        print("== scaling")
+        print(scaling_table(all_bench))
     return 0
 
 

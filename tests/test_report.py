@@ -31,3 +31,22 @@ def test_scaling_table():
             {"n_gpus": 4, "value": 200.0}]
     t = scaling_table(rows)
     assert "| 4 | 200.0 | 50.0 |" in t and "100.0%" in t
+
+
+def test_scaling_table_comparisons_and_cli(tmp_path, capsys):
+    from test_nccl_p2p_amd.utils.report import main
+    rows = [{"metric": "m", "n_gpus": 2, "value": 100.0, "reference_semantics": {"cell_gbs_mean": 40.0},
+             "extras": {"allpairs_1g": {"aggregate_gbs": 300.0}},
+             "ipc_transport": {"value_gbs": 110.0, "device_pingpong_p50_us": 1.5, "push": {"value_gbs": 120.0}}},
+            {"metric": "m", "n_gpus": 8, "value": 380.0, "ipc_transport": {"error": "x"}}]
+    t = scaling_table(rows)
+    assert "| 40.0 | 300.0 | 110.0 / 120.0 | 1.50 |" in t
+    assert "| 8 | 380.0 | 47.5 |" in t and "95.0%" in t and "- / -" in t
+    files = []
+    for r in rows:
+        f = tmp_path / ("BENCH_%d.json" % r["n_gpus"])
+        f.write_text(__import__("json").dumps(r) + "\n")
+        files.append(str(f))
+    assert main(files) == 0
+    out = capsys.readouterr().out
+    assert "== scaling" in out and "| 8 | 380.0 |" in out.split("== scaling")[1]
