@@ -32,6 +32,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <thread>
@@ -42,6 +43,7 @@
 #include "hip_check.hpp"
 #include "kernels.hpp"
 #include "transport.hpp"
+#include "units.hpp"
 
 namespace p2p {
 namespace {
@@ -77,6 +79,7 @@ class IpcTransport final : public Transport {
     HIPCHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_));
     P2P_CHECK(khz > 0, "device reports no wall clock rate");
     tick_hz_ = khz * 1e3;
+    if (const char* pc = std::getenv("P2P_IPC_POOL")) pool_cap_ = std::strcmp(pc, "0") ? parse_size(pc) : 0;
     if (engine_ == "push") setup_sync_pages();
   }
 
@@ -118,7 +121,8 @@ class IpcTransport final : public Transport {
   // from a shared chunk, and hipIpcGetMemHandle rejects those ("invalid
   // argument"); every exported buffer must be an allocation of its own.
   //
-  // Released buffers are kept for reuse (up to kPoolBytes): a buffer set is
+  // Released buffers are kept for reuse (up to pool_cap_, 32 GiB, or
+  // P2P_IPC_POOL bytes -- lower it when many ranks share one GPU): a buffer set is
   // created per run, and a just-freed block that peers mapped a moment ago
   // can come back from hipMalloc while the runtime still tracks the old
   // export, which makes hipIpcGetMemHandle fail intermittently ("invalid
@@ -151,7 +155,7 @@ class IpcTransport final : public Transport {
     P2P_CHECK(it != sizes_.end(), "release of a buffer this transport did not allocate");
     const size_t size = it->second;
     sizes_.erase(it);
-    if (pool_bytes_ + size <= kPoolBytes) {
+    if (pool_bytes_ + size <= pool_cap_) {
       pool_.emplace_back(p, size);
       pool_bytes_ += size;
     } else {
@@ -592,7 +596,7 @@ class IpcTransport final : public Transport {
     pool_.clear();
     pool_bytes_ = 0;
   }
-  static constexpr size_t kPoolBytes = size_t{32} << 30;
+  size_t pool_cap_ = size_t{32} << 30;
   std::vector<std::pair<void*, size_t>> pool_;  // released, kept for reuse
   size_t pool_bytes_ = 0;
   std::map<void*, size_t> sizes_;               // live allocations

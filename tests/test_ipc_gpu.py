@@ -119,3 +119,28 @@ def test_bench_two_ranks_ipc():
     assert push["verify_mismatches"] == 0 and push["value_gbs"] > 0, push
     sweep = r["extras"]["pair_sweep_0_1"]
     assert len(sweep) == 11 and sweep[-1]["bytes"] == 4 << 30 and all(p["gbs"] > 0 for p in sweep)
+
+
+@pytest.mark.parametrize("nranks", [4, 8])
+def test_bench_emulated_node(nranks):
+    """bench.py at the driver's GPU counts with every rank on the one GPU (IPC
+    transport): tournament rounds, all-pairs with N-1 slots, ring, the pair
+    sweep, the reference-method matrix and the pull / push comparisons all
+    run through the N-rank code paths the 8-GPU scaling run uses."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nranks),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", str(nranks),
+           "--steps", "14", "--warmup", "7", "--transport", "ipc", "--device", "0", "--sweep-max", "64M",
+           "--latency-iters", "100"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT,
+                         env=dict(os.environ, P2P_IPC_POOL="1G"))
+    progress = "\n".join(l for l in out.stderr.splitlines() if "bench:" in l or "fatal" in l)
+    assert out.returncode == 0, progress
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert r["n_gpus"] == nranks and r["verify_mismatches"] == 0
+    assert r["matrix_cells"] == "%d/%d" % (nranks * (nranks - 1), nranks * (nranks - 1))
+    assert r["reference_semantics"]["cell_gbs_mean"] > 0
+    assert r["extras"]["allpairs_1g"]["aggregate_gbs"] > 0 and r["extras"]["ring_256m"]["aggregate_gbs"] > 0
+    assert len(r["extras"]["pair_sweep_0_1"]) == 7
+    ipc = r["ipc_transport"]
+    assert ipc["verify_mismatches"] == 0 and ipc["push"]["verify_mismatches"] == 0, ipc
+    assert ipc["device_pingpong_p50_us"] > 0
