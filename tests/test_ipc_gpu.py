@@ -140,7 +140,7 @@ def test_bench_emulated_node(nranks):
     assert r["matrix_cells"] == "%d/%d" % (nranks * (nranks - 1), nranks * (nranks - 1))
     assert r["reference_semantics"]["cell_gbs_mean"] > 0
     assert r["extras"]["allpairs_1g"]["aggregate_gbs"] > 0 and r["extras"]["ring_256m"]["aggregate_gbs"] > 0
-    assert len(r["extras"]["pair_sweep_0_1"]) == 7
+    assert len(r["extras"]["pair_sweep_0_1"]) == 8  # 4 KiB .. 64 MiB in x4 steps
     ipc = r["ipc_transport"]
     assert ipc["verify_mismatches"] == 0 and ipc["push"]["verify_mismatches"] == 0, ipc
     assert ipc["device_pingpong_p50_us"] > 0
