@@ -65,6 +65,8 @@ transport / launch
       --bootstrap B      auto | mpi | env | local                              [auto]
       --device N         GPU index (default: local rank from block placement)
       --timeout S        watchdog for init / waits, seconds                    [300]
+      --min-gbs X        link check: exit 3 naming every off-diagonal flow below
+                         X GB/s (use with the message size the check is for)
 output
       --json FILE        JSON lines, one object per run, appended + flushed as each run ends
       --resume           skip the runs already in the --json file (restart a killed sweep)
@@ -132,7 +134,7 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
     // Options taking a value check it before use.
     static const char* kValued[] = {"-m", "--mode", "-d", "--dir", "-b", "--size", "--sizes", "-n", "--iters", "-w",
                                     "--warmup", "--timing", "--latency-size", "--latency-iters", "--verify-impl",
-                                    "--transport", "--ipc-engine", "--bootstrap", "--device", "--timeout", "--json",
+                                    "--transport", "--ipc-engine", "--bootstrap", "--device", "--timeout", "--min-gbs", "--json",
                                     "--csv", "--trace", "--cells"};
     for (const char* v : kValued)
       if (a == v && !has_eq && i + 1 >= argc) {
@@ -210,6 +212,8 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
       cfg->bootstrap = next();
     } else if (a == "--device") {
       cfg->device = std::atoi(next().c_str());
+    } else if (a == "--min-gbs") {
+      cfg->min_gbs = std::atof(next().c_str());
     } else if (a == "--timeout") {
       cfg->timeout_s = std::atof(next().c_str());
     } else if (a == "--json") {
@@ -435,10 +439,27 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
     }
     std::fflush(out);
   }
+  // Link check (--min-gbs): every measured off-diagonal flow must reach the
+  // threshold; the slow ones are named so a bad link or GPU can be found.
+  if (cfg.min_gbs > 0)
+    for (const auto& rec : res.runs)
+      for (const auto& ph : rec.phases)
+        for (const auto& f : ph.flows)
+          if (f.flow.src != f.flow.dst && f.gbs < cfg.min_gbs) {
+            ++res.slow_flows;
+            if (root)
+              std::fprintf(stderr, "p2p_matrix: SLOW LINK: %d -> %d %.2f GB/s < %.2f (%s-%s, %s)\n", f.flow.src,
+                           f.flow.dst, f.gbs, cfg.min_gbs, mode_name(rec.mode), direction_name(rec.dir),
+                           format_size(rec.bytes).c_str());
+          }
   boot.barrier();
   if (res.mismatches) {
     if (root) std::fprintf(stderr, "p2p_matrix: VERIFICATION FAILED: %llu mismatching words\n", static_cast<unsigned long long>(res.mismatches));
     return 2;
+  }
+  if (res.slow_flows) {
+    if (root) std::fprintf(stderr, "p2p_matrix: LINK CHECK FAILED: %d flow(s) below %.2f GB/s\n", res.slow_flows, cfg.min_gbs);
+    return 3;
   }
   return 0;
 }

@@ -48,6 +48,7 @@ struct AppConfig {
   bool dry_run = false;    // print the schedules and exit (no transport)
   bool topology_only = false;  // print the GPU link matrix and exit
   bool warm_connections = true;
+  double min_gbs = 0;          // link check: any off-diagonal flow below this fails the run (exit 3)
   bool two_streams = false;  // RCCL receives on a second stream (reference layout)
   int verbose = 0;
 };
@@ -65,10 +66,11 @@ struct AppResult {
   std::vector<LatencyResult> latency;
   std::vector<LatencyResult> device_latency;
   uint64_t mismatches = 0;
+  int slow_flows = 0;  // flows under --min-gbs
 };
 
 // Runs everything collectively; rank 0 prints to `out`.  Returns 0 on success,
-// 2 if verification found corrupted data.
+// 2 if verification found corrupted data, 3 if a link ran below --min-gbs.
 int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result = nullptr);
 
 }  // namespace p2p

@@ -158,3 +158,16 @@ def test_device_latency_needs_one_sided_transport(mpirun, host_build):
     out = run(mpirun, exe, 2, ["--transport", "host", "--size", "16K", "-n", "2", "--compat-only", "--device-latency"])
     assert out.returncode != 0
     assert "one-sided transport" in out.stderr + out.stdout
+
+
+def test_min_gbs_link_check(mpirun, host_build):
+    """--min-gbs names every flow below the threshold and exits 3; a threshold
+    every link meets passes."""
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    bad = run(mpirun, exe, 3, ["--transport", "host", "--mode", "tournament", "--dir", "uni", "--size", "64K",
+                               "-n", "3", "--no-compat", "--min-gbs", "1e6"])
+    assert bad.returncode == 3, bad.stderr
+    assert bad.stderr.count("SLOW LINK") == 6 and "LINK CHECK FAILED: 6 flow(s)" in bad.stderr
+    ok = run(mpirun, exe, 3, ["--transport", "host", "--mode", "tournament", "--dir", "uni", "--size", "64K",
+                              "-n", "3", "--no-compat", "--min-gbs", "1e-6"])
+    assert ok.returncode == 0, ok.stderr
