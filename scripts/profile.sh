@@ -19,4 +19,9 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS -
     -d "$OUT/pmc_fetch" -o pmc -- python3 scripts/kernel_bench.py --sizes 1G --reps 2 > /dev/null
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE SQ_WAVES SQ_INSTS_VMEM_RD --kernel-trace --output-format csv \
     -d "$OUT/pmc_write" -o pmc -- python3 scripts/kernel_bench.py --sizes 1G --reps 2 > /dev/null
+# 4) kernel trace + stats of the hand-written data plane (one process: IPC copy
+#    kernel on the self path, device ping-pong kernel, fill / verify)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ipc" -o ipc -- \
+    ./build/p2p_matrix --transport ipc --mode self --sizes 32M,1G -n 16 --verify --device-latency \
+    --latency-iters 2000 --no-compat > "$OUT/ipc_stdout.txt"
 echo "profiles done"
