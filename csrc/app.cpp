@@ -52,7 +52,7 @@ timing
       --latency-size S   [8]      --latency-iters N   [1000]
 data
   -c, --verify           random-fill sends, verify every received buffer on the device
-      --verify-impl I    auto (= lds) | lds | lds8 | lds-cached | stride | reg
+      --verify-impl I    auto (= lds8) | lds | lds8 | lds-pipe | lds-cached | stride | reg
                          (LDS-DMA- or register-staged verify kernel variants)
 transport / launch
       --transport T      rccl  MI355X + RCCL ncclSend/ncclRecv over xGMI      [rccl]
@@ -203,6 +203,7 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
                          : v == "stride"               ? 3
                          : v == "lds8"                 ? 4
                          : v == "lds-cached"           ? 5
+                         : v == "lds-pipe"             ? 6
                                                        : 0;
     } else if (a == "--transport") {
       cfg->transport = next();

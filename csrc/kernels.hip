@@ -302,6 +302,70 @@ __global__ __launch_bounds__(kBlock) void verify_lds_kernel(const uint4* __restr
   block_commit(acc, out);
 }
 
+// Software-pipelined LDS staging: each wave owns two halves of STAGES KiB.
+// While it checks half b, the LDS-DMAs of its next chunk are already landing
+// in half b^1: issue next -> s_waitcnt vmcnt(STAGES) (only the next chunk's
+// DMAs may still be in flight, so the current half has landed) -> ds_read
+// half b -> compare.  The wave never idles on its own loads the way the
+// load-all / wait-all loop above does between chunks.  A partial final chunk
+// issues fewer DMAs, so the wait before it is a full vmcnt(0).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt();
+template <>
+__device__ __forceinline__ void wait_vmcnt<0>() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+template <>
+__device__ __forceinline__ void wait_vmcnt<4>() { asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
+
+template <bool CHECK, int STAGES, int AUX>
+__global__ __launch_bounds__(kBlock) void verify_lds_pipe_kernel(const uint4* __restrict__ p, uint64_t nvec,
+                                                                 uint64_t seed, const uint8_t* __restrict__ tail,
+                                                                 uint32_t tail_bytes, uint64_t tail_offset,
+                                                                 VerifyAccum* __restrict__ out) {
+  __shared__ uint4 slot[kWaves][2][STAGES][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x / 64;
+  const uint64_t sc_vecs = static_cast<uint64_t>(STAGES) * 64;
+  const uint64_t n_sc = (nvec + sc_vecs - 1) / sc_vecs;
+  const uint64_t step = static_cast<uint64_t>(gridDim.x) * kWaves;
+  auto issue = [&](uint64_t c, int half) {
+#pragma unroll
+    for (int s = 0; s < STAGES; ++s) {
+      const uint64_t i = c * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
+      if (i < nvec)
+        __builtin_amdgcn_global_load_lds(static_cast<const void*>(p + i),
+                                         (__attribute__((address_space(3))) void*)(&slot[wave][half][s][0]), 16, 0, AUX);
+    }
+  };
+  Partial acc{0, 0, ~0ull};
+  uint64_t sc = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
+  int half = 0;
+  if (sc < n_sc) issue(sc, 0);
+  for (; sc < n_sc; sc += step, half ^= 1) {
+    const uint64_t next = sc + step;
+    if (next < n_sc) {
+      issue(next, half ^ 1);
+      if ((next + 1) * sc_vecs <= nvec)
+        wait_vmcnt<STAGES>();
+      else
+        wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    const uint32_t lds_addr = static_cast<uint32_t>(
+        reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)(&slot[wave][half][0][lane])));
+    u32x4 rv[STAGES];
+    lds_read_stages<STAGES>(lds_addr, rv);
+    const uint32_t key = prng_key(seed, sc * sc_vecs * 4);  // wave-uniform
+#pragma unroll
+    for (int s = 0; s < STAGES; ++s) {
+      const uint64_t i = sc * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
+      if (i < nvec) check_vec<CHECK>(make_uint4(rv[s].x, rv[s].y, rv[s].z, rv[s].w), key, i, acc);
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) check_tail<CHECK>(tail, tail_bytes, tail_offset, seed, acc);
+  block_commit(acc, out);
+}
+
 __global__ void verify_reset_kernel(VerifyAccum* acc) {
   if (threadIdx.x < kVerifyShards) {
     acc[threadIdx.x].mismatches = 0;
@@ -377,15 +441,18 @@ LaunchGeom verify_geometry(size_t bytes, VerifyImpl impl, unsigned max_grid) {
   // atomic commit, so a full grid (one 4 KiB block per workgroup) pays that
   // epilogue 256K times per GiB; the defaults below cap the grid so each
   // workgroup streams tens of KiB per epilogue (kernel_bench A/B).
-  const uint64_t per_cu = (impl == VerifyImpl::Lds || impl == VerifyImpl::Lds8 || impl == VerifyImpl::LdsCached) ? kVerifyLdsPerCu
-                          : impl == VerifyImpl::Stride ? kVerifyStridePerCu
-                                                       : kVerifyGridPerCu;
+  const bool lds = impl == VerifyImpl::Lds || impl == VerifyImpl::Lds8 || impl == VerifyImpl::LdsCached ||
+                   impl == VerifyImpl::LdsPipe;
+  const uint64_t per_cu = lds ? kVerifyLdsPerCu : impl == VerifyImpl::Stride ? kVerifyStridePerCu : kVerifyGridPerCu;
   const uint64_t cap = max_grid ? max_grid : static_cast<uint64_t>(cu_count()) * per_cu;
-  if (impl == VerifyImpl::Lds || impl == VerifyImpl::Lds8 || impl == VerifyImpl::LdsCached) {
-    const uint64_t sc_vecs = static_cast<uint64_t>(impl == VerifyImpl::Lds8 ? 8 : kLdsStages) * 64;
+  if (lds) {
+    // KiB per chunk a wave checks, and KiB of LDS a wave owns.
+    const uint64_t stages = impl == VerifyImpl::Lds8 ? 8 : kLdsStages;
+    const uint64_t lds_stages = impl == VerifyImpl::LdsPipe ? 2 * stages : stages;
+    const uint64_t sc_vecs = stages * 64;
     const uint64_t waves = (nvec + sc_vecs - 1) / sc_vecs;
     g.grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min((waves + kWaves - 1) / kWaves, cap)));
-    g.lds_bytes = sizeof(uint4) * kWaves * (impl == VerifyImpl::Lds8 ? 8 : kLdsStages) * 64;
+    g.lds_bytes = sizeof(uint4) * kWaves * lds_stages * 64;
   } else if (impl == VerifyImpl::Stride) {
     const uint64_t tiles = (nvec + kBlock * kStrideUnroll - 1) / (kBlock * kStrideUnroll);
     g.grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min(tiles, cap)));
@@ -437,6 +504,9 @@ void launch_verify_t(const uint4* vp, uint64_t nvec, uint64_t seed, const uint8_
       break;
     case VerifyImpl::LdsCached:
       verify_lds_kernel<CHECK, kLdsStages, 0><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
+      break;
+    case VerifyImpl::LdsPipe:
+      verify_lds_pipe_kernel<CHECK, 4, 2><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
       break;
     case VerifyImpl::Stride:
       verify_stride_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);

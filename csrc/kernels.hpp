@@ -53,7 +53,7 @@ struct alignas(64) VerifyAccum {
 constexpr int kVerifyShards = 64;
 constexpr size_t verify_accum_bytes() { return sizeof(VerifyAccum) * kVerifyShards; }
 
-enum class VerifyImpl : int { Auto = 0, Register = 1, Lds = 2, Stride = 3, Lds8 = 4, LdsCached = 5 };
+enum class VerifyImpl : int { Auto = 0, Register = 1, Lds = 2, Stride = 3, Lds8 = 4, LdsCached = 5, LdsPipe = 6 };
 enum class FillImpl : int { Auto = 0, Grid = 1, Nontemporal = 2, Stride = 3 };
 
 // Geometry chosen for a launch (exposed for tests / profiling scripts).

@@ -50,7 +50,7 @@ def main():
         t_fill_nt = timed(lambda: nat.fill(ptr, sz, 7, stream, 2), a.reps)
         t_fill_stride = timed(lambda: nat.fill(ptr, sz, 7, stream, 3), a.reps)
         res = {}
-        for name, impl, check in [("verify_reg", 1, True), ("verify_stride", 3, True), ("verify_lds", 2, True), ("verify_lds8", 4, True),
+        for name, impl, check in [("verify_reg", 1, True), ("verify_stride", 3, True), ("verify_lds", 2, True), ("verify_lds8", 4, True), ("verify_ldspipe", 6, True),
                                   ("checksum_reg", 1, False), ("checksum_lds", 2, False)]:
             # Kernel time only: reset + verify + finalize launches, no readback.
             t = timed(lambda: nat.verify_launch(ptr, sz, 7, impl, check, stream), a.reps)
@@ -74,10 +74,10 @@ def main():
         row["verify_reg_geom"] = nat.verify_geometry(sz, 1)
         row["verify_lds_geom"] = nat.verify_geometry(sz, 2)
         rows.append(row)
-        print("%6s  fill %.2f (nt %.2f, stride %.2f)  verify grid %.2f / stride %.2f / lds %.2f / lds8 %.2f  checksum reg %.2f / lds %.2f TB/s"
+        print("%6s  fill %.2f (nt %.2f, stride %.2f)  verify grid %.2f / stride %.2f / lds %.2f / lds8 %.2f / lds-pipe %.2f  checksum reg %.2f / lds %.2f TB/s"
               "  (HBM measured roof %.2f)"
               % (nat.format_size(sz), row["fill_tbs"], row["fill_nt_tbs"], row["fill_stride_tbs"], row["verify_reg_tbs"], row["verify_stride_tbs"],
-                 row["verify_lds_tbs"], row["verify_lds8_tbs"], row["checksum_reg_tbs"], row["checksum_lds_tbs"], HBM_MEASURED_TBS), flush=True)
+                 row["verify_lds_tbs"], row["verify_lds8_tbs"], row["verify_ldspipe_tbs"], row["checksum_reg_tbs"], row["checksum_lds_tbs"], HBM_MEASURED_TBS), flush=True)
         print("        roofs: torch zero_ %.2f  torch copy_ %.2f  ours copy %.2f TB/s (copy counts bytes once)"
               % (row["torch_zero_tbs"], row["torch_copy_tbs"], row["copy_kernel_tbs"]), flush=True)
         del buf
