@@ -299,8 +299,9 @@ def main(argv=None) -> int:
             return {"error": str(e)[:300], "transport": transport}
 
     # The hand-written data plane on the same links: the gfx950 multi-copy
-    # kernel pulling from hipIpc-mapped peer buffers ("pull", one-sided), and
-    # the rendezvous engine that writes into the receiver's slot ("push").
+    # kernel pulling from hipIpc-mapped peer buffers ("pull", one-sided), the
+    # rendezvous engine that writes into the receiver's slot ("push"), and the
+    # SDMA copy engines pulling instead of CUs ("sdma").
     ipc = None
     if n > 1 and args.ipc_extra and extra_transport:
         ipc = steps_through(extra_transport)
@@ -308,6 +309,8 @@ def main(argv=None) -> int:
             ipc["engine"] = "gfx950 multi-copy kernel, one-sided pull over hipIpc mappings"
             ipc["push"] = steps_through("ipc:push")
             ipc["push"]["engine"] = "ready/done flags + gfx950 multi-copy kernel writing into the peer's slot"
+            ipc["sdma"] = steps_through("ipc:sdma")
+            ipc["sdma"]["engine"] = "one-sided pull by the SDMA copy engines (hipMemcpyAsync per receive)"
 
     step_ms_med = statistics.median(my_ms) if my_ms else 0.0
     result = {

@@ -143,4 +143,5 @@ def test_bench_emulated_node(nranks):
     assert len(r["extras"]["pair_sweep_0_1"]) == 8  # 4 KiB .. 64 MiB in x4 steps
     ipc = r["ipc_transport"]
     assert ipc["verify_mismatches"] == 0 and ipc["push"]["verify_mismatches"] == 0, ipc
+    assert ipc["sdma"]["verify_mismatches"] == 0 and ipc["sdma"]["value_gbs"] > 0, ipc
     assert ipc["device_pingpong_p50_us"] > 0

@@ -40,8 +40,8 @@ def test_scaling_table_comparisons_and_cli(tmp_path, capsys):
              "ipc_transport": {"value_gbs": 110.0, "device_pingpong_p50_us": 1.5, "push": {"value_gbs": 120.0}}},
             {"metric": "m", "n_gpus": 8, "value": 380.0, "ipc_transport": {"error": "x"}}]
     t = scaling_table(rows)
-    assert "| 40.0 | 300.0 | 110.0 / 120.0 | 1.50 |" in t
-    assert "| 8 | 380.0 | 47.5 |" in t and "95.0%" in t and "- / -" in t
+    assert "| 40.0 | 300.0 | 110.0 / 120.0 / - | 1.50 |" in t
+    assert "| 8 | 380.0 | 47.5 |" in t and "95.0%" in t and "- / - / -" in t
     files = []
     for r in rows:
         f = tmp_path / ("BENCH_%d.json" % r["n_gpus"])
