@@ -54,7 +54,7 @@ constexpr int kVerifyShards = 64;
 constexpr size_t verify_accum_bytes() { return sizeof(VerifyAccum) * kVerifyShards; }
 
 enum class VerifyImpl : int { Auto = 0, Register = 1, Lds = 2, Stride = 3, Lds8 = 4, LdsCached = 5, LdsPipe = 6 };
-enum class FillImpl : int { Auto = 0, Grid = 1, Nontemporal = 2, Stride = 3 };
+enum class FillImpl : int { Auto = 0, Grid = 1, Nontemporal = 2, Stride = 3, Xcd = 4 };
 
 // Geometry chosen for a launch (exposed for tests / profiling scripts).
 struct LaunchGeom {

@@ -31,6 +31,17 @@ def test_fill_matches_reference(nbytes):
     assert torch.all(buf[nbytes:] == 0xAB), "fill wrote past the end"
 
 
+@pytest.mark.parametrize("fill_impl", [1, 2, 3, 4])  # grid, non-temporal, grid-stride, XCD-ordered grid
+@pytest.mark.parametrize("nbytes", SIZES + [(64 << 20) + 4])
+def test_fill_variants_match_reference(fill_impl, nbytes):
+    from test_nccl_p2p_amd import require_native
+    buf = dev_bytes(nbytes)
+    require_native().fill(buf.data_ptr(), nbytes, 0xBEEF, torch.cuda.current_stream().cuda_stream, fill_impl)
+    torch.cuda.synchronize()
+    assert torch.equal(buf[:nbytes], reference_bytes(nbytes, 0xBEEF, device="cuda"))
+    assert torch.all(buf[nbytes:] == 0xAB), "fill wrote past the end"
+
+
 @pytest.mark.parametrize("impl", ["reg", "lds", "stride", "lds8", "lds-cached", "lds-pipe"])
 @pytest.mark.parametrize("nbytes", SIZES)
 def test_verify_clean_and_checksum(impl, nbytes):
