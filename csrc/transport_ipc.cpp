@@ -32,6 +32,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -80,6 +81,7 @@ class IpcTransport final : public Transport {
     P2P_CHECK(khz > 0, "device reports no wall clock rate");
     tick_hz_ = khz * 1e3;
     if (const char* pc = std::getenv("P2P_IPC_POOL")) pool_cap_ = std::strcmp(pc, "0") ? parse_size(pc) : 0;
+    if (const char* ir = std::getenv("P2P_INJECT_EXPORT_REFUSALS")) inject_refusals_ = std::atoi(ir);
     if (engine_ == "push") setup_sync_pages();
   }
 
@@ -117,47 +119,48 @@ class IpcTransport final : public Transport {
     *free_b += pool_bytes_;  // pooled blocks are handed back on demand
     return true;
   }
-  // At least 2 MiB, rounded to 2 MiB: small hipMallocs can be sub-allocated
-  // from a shared chunk, and hipIpcGetMemHandle rejects those ("invalid
-  // argument"); every exported buffer must be an allocation of its own.
+  // At least 2 MiB, rounded to 2 MiB, so every exported buffer is an
+  // allocation of its own.  Each block is exported once, when it is created
+  // (see exportable()), and keeps its handle.
   //
   // Released buffers are kept for reuse (up to pool_cap_, 32 GiB, or
-  // P2P_IPC_POOL bytes -- lower it when many ranks share one GPU): a buffer set is
-  // created per run, and a just-freed block that peers mapped a moment ago
-  // can come back from hipMalloc while the runtime still tracks the old
-  // export, which makes hipIpcGetMemHandle fail intermittently ("invalid
-  // argument").  Reusing the same allocations avoids that churn entirely.
+  // P2P_IPC_POOL bytes -- lower it when many ranks share one GPU): a buffer
+  // set is created per run, and reusing the same exported blocks avoids
+  // allocation churn between runs.
   void* alloc(size_t bytes) override {
     constexpr size_t kGrain = size_t{2} << 20;
     const size_t size = (std::max<size_t>(bytes, 1) + kGrain - 1) / kGrain * kGrain;
     for (auto it = pool_.begin(); it != pool_.end(); ++it)
-      if (it->second == size) {
+      if (it->second.size == size) {
         void* p = it->first;
         pool_bytes_ -= size;
+        blocks_[p] = it->second;
         pool_.erase(it);
-        sizes_[p] = size;
         return p;
       }
-    void* p = nullptr;
-    hipError_t e = hipMalloc(&p, size);
-    if (e != hipSuccess && !pool_.empty()) {  // give the pool back and retry once
-      (void)hipGetLastError();
-      drain_pool();
-      e = hipMalloc(&p, size);
-    }
-    if (e != hipSuccess) P2P_FATAL(strfmt("hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e)));
-    sizes_[p] = size;
+    Block b;
+    b.size = size;
+    void* p = exportable(size, &b.handle, [&](void** q) {
+      hipError_t e = hipMalloc(q, size);
+      if (e != hipSuccess && !pool_.empty()) {  // give the pool back and retry once
+        (void)hipGetLastError();
+        drain_pool();
+        e = hipMalloc(q, size);
+      }
+      return e;
+    });
+    blocks_[p] = b;
     return p;
   }
   void release(void* p) override {
     if (!p) return;
-    auto it = sizes_.find(p);
-    P2P_CHECK(it != sizes_.end(), "release of a buffer this transport did not allocate");
-    const size_t size = it->second;
-    sizes_.erase(it);
-    if (pool_bytes_ + size <= pool_cap_) {
-      pool_.emplace_back(p, size);
-      pool_bytes_ += size;
+    auto it = blocks_.find(p);
+    P2P_CHECK(it != blocks_.end(), "release of a buffer this transport did not allocate");
+    const Block b = it->second;
+    blocks_.erase(it);
+    if (pool_bytes_ + b.size <= pool_cap_) {
+      pool_.emplace_back(p, b);
+      pool_bytes_ += b.size;
     } else {
       HIPCHECK(hipFree(p));
     }
@@ -183,7 +186,7 @@ class IpcTransport final : public Transport {
   // peer.
   void register_buffers(void* send, const std::vector<void*>& recvs, size_t bytes) override {
     Export me{};
-    HIPCHECK(hipIpcGetMemHandle(&me.handle, send));
+    me.handle = handle_of(send);
     me.bytes = bytes;
     me.host_hash = host_hash(real_hostname());
     me.device = device_;
@@ -211,7 +214,7 @@ class IpcTransport final : public Transport {
       reg.peer_recvs.assign(static_cast<size_t>(n_), std::vector<void*>(recvs.size(), nullptr));
       for (size_t k = 0; k < recvs.size(); ++k) {
         Export slot{};
-        HIPCHECK(hipIpcGetMemHandle(&slot.handle, recvs[k]));
+        slot.handle = handle_of(recvs[k]);
         slot.bytes = bytes;
         auto slots = boot_.allgather_value(slot);
         for (int r = 0; r < n_; ++r) {
@@ -231,9 +234,7 @@ class IpcTransport final : public Transport {
     if (it == regs_.end()) return;
     sync();
     // Every rank stops moving data before any mapping goes, and every rank
-    // has closed its mappings of a buffer before its owner frees it: a freed
-    // block that a peer still maps can come back from hipMalloc, and
-    // hipIpcGetMemHandle then refuses it ("invalid argument").
+    // has closed its mappings of a buffer before its owner releases it.
     boot_.barrier();
     close_registration(*it);
     regs_.erase(it);
@@ -321,16 +322,10 @@ class IpcTransport final : public Transport {
   void pingpong_setup() override {
     if (page_) return;  // same state on every rank: they all set up together
     const size_t bytes = kPingSlot * static_cast<size_t>(n_ + 1);
-    page_kind_ = "uncached";
-    if (hipExtMallocWithFlags(&page_, bytes, hipDeviceMallocUncached) != hipSuccess) {
-      (void)hipGetLastError();
-      page_kind_ = "coarse";
-      HIPCHECK(hipMalloc(&page_, bytes));
-    }
+    Export me{};
+    page_ = exportable(bytes, &me.handle, [&](void** q) { return alloc_signal_page(q, bytes); });
     HIPCHECK(hipMemset(page_, 0, bytes));
     HIPCHECK(hipDeviceSynchronize());
-    Export me{};
-    HIPCHECK(hipIpcGetMemHandle(&me.handle, page_));
     me.bytes = bytes;
     me.host_hash = host_hash(real_hostname());
     me.device = device_;
@@ -506,16 +501,12 @@ class IpcTransport final : public Transport {
   // (ready / done from every peer), exported to every peer.
   void setup_sync_pages() {
     const size_t bytes = kSyncLine * 2 * static_cast<size_t>(n_);
-    if (hipExtMallocWithFlags(&sync_page_, bytes, hipDeviceMallocUncached) != hipSuccess) {
-      (void)hipGetLastError();
-      HIPCHECK(hipMalloc(&sync_page_, bytes));
-    }
+    Export me{};
+    sync_page_ = exportable(bytes, &me.handle, [&](void** q) { return alloc_signal_page(q, bytes); });
     HIPCHECK(hipMemset(sync_page_, 0, bytes));
     HIPCHECK(hipDeviceSynchronize());
     HIPCHECK(hipHostMalloc(&sig_status_, 64, hipHostMallocMapped));
     *sig_status_ = 0;
-    Export me{};
-    HIPCHECK(hipIpcGetMemHandle(&me.handle, sync_page_));
     me.host_hash = host_hash(real_hostname());
     auto all = boot_.allgather_value(me);
     sync_peer_.assign(static_cast<size_t>(n_), nullptr);
@@ -591,15 +582,67 @@ class IpcTransport final : public Transport {
   bool in_group_ = false;
   std::vector<dev::CopyOp> ops_;
 
+  struct Block {
+    size_t size = 0;
+    hipIpcMemHandle_t handle{};
+  };
+
+  // A new device allocation whose IPC export works, with its handle.  On
+  // this stack hipIpcGetMemHandle now and then refuses a fresh block
+  // ("invalid argument", seen with 8 processes allocating on one GPU); such a
+  // block is held (so the allocator cannot hand it straight back) until a
+  // good one is found, then freed, and the retry is reported on stderr.
+  template <class AllocFn>
+  void* exportable(size_t size, hipIpcMemHandle_t* handle, AllocFn&& alloc_fn) {
+    std::vector<void*> refused;
+    void* p = nullptr;
+    for (int attempt = 0;; ++attempt) {
+      hipError_t e = alloc_fn(&p);
+      if (e != hipSuccess) {
+        for (void* r : refused) (void)hipFree(r);
+        P2P_FATAL(strfmt("device allocation of %zu bytes failed: %s", size, hipGetErrorString(e)));
+      }
+      e = hipIpcGetMemHandle(handle, p);
+      if (e == hipSuccess && inject_refusals_ > 0) {  // test hook: P2P_INJECT_EXPORT_REFUSALS=<n>
+        --inject_refusals_;
+        e = hipErrorInvalidValue;
+      }
+      if (e == hipSuccess) break;
+      (void)hipGetLastError();
+      refused.push_back(p);
+      if (attempt == 7) {
+        for (void* r : refused) (void)hipFree(r);
+        P2P_FATAL(strfmt("hipIpcGetMemHandle refused 8 fresh %zu-byte blocks: %s", size, hipGetErrorString(e)));
+      }
+    }
+    if (!refused.empty())
+      std::fprintf(stderr, "p2p_matrix: rank %d: hipIpcGetMemHandle refused %zu fresh %zu-byte block(s); reallocated\n",
+                   rank_, refused.size(), size);
+    for (void* r : refused) (void)hipFree(r);
+    return p;
+  }
+  const hipIpcMemHandle_t& handle_of(void* p) const {
+    auto it = blocks_.find(p);
+    P2P_CHECK(it != blocks_.end(), "ipc transport exports only buffers it allocated");
+    return it->second.handle;
+  }
+  // Uncached device memory when the runtime allows it, so a spinning wave
+  // reads HBM rather than a stale line.
+  static hipError_t alloc_signal_page(void** q, size_t bytes) {
+    if (hipExtMallocWithFlags(q, bytes, hipDeviceMallocUncached) == hipSuccess) return hipSuccess;
+    (void)hipGetLastError();
+    return hipMalloc(q, bytes);
+  }
   void drain_pool() {
     for (auto& b : pool_) (void)hipFree(b.first);
     pool_.clear();
     pool_bytes_ = 0;
   }
   size_t pool_cap_ = size_t{32} << 30;
-  std::vector<std::pair<void*, size_t>> pool_;  // released, kept for reuse
+  int inject_refusals_ = 0;
+  std::vector<std::pair<void*, Block>> pool_;  // released, kept for reuse
   size_t pool_bytes_ = 0;
-  std::map<void*, size_t> sizes_;               // live allocations
+  std::map<void*, Block> blocks_;              // live allocations
 
   // Push engine state.
   static constexpr size_t kSyncLine = 128;
@@ -615,7 +658,6 @@ class IpcTransport final : public Transport {
   static constexpr size_t kPingSlot = kPingHeader + kPingMaxBytes;
   static constexpr int kPingMaxIters = 100000;
   void* page_ = nullptr;
-  std::string page_kind_;
   std::vector<void*> peer_pages_;
   std::vector<unsigned long long> seq_;
   double tick_hz_ = 1e8;

@@ -82,6 +82,19 @@ def test_four_ranks_allpairs_large(exe, engine):
     assert "verification: OK" in out.stdout
 
 
+def test_export_refusal_is_retried(exe):
+    """hipIpcGetMemHandle occasionally refuses a fresh block on this stack;
+    the transport reallocates and says so.  Injected here: every rank's
+    first two exports are refused."""
+    env = dict(os.environ, P2P_INJECT_EXPORT_REFUSALS="2")
+    out = subprocess.run([MPIRUN, "-n", "2", exe, "--transport", "ipc", "--device", "0", "--mode", "tournament",
+                          "--size", "1M", "-n", "4", "--verify", "--no-compat"], capture_output=True, text=True,
+                         timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "verification: OK" in out.stdout
+    assert out.stderr.count("refused 2 fresh") == 2, out.stderr
+
+
 def test_corruption_detected_on_gpu(exe):
     env = dict(os.environ, P2P_INJECT_FAULT="corrupt@1:1")
     out = subprocess.run([MPIRUN, "-n", "2", exe, "--transport", "ipc", "--device", "0", "--size", "1M", "-n", "3",
