@@ -50,7 +50,7 @@ gpu: $(BUILD)/p2p_matrix
 	ln -sf $(BUILD)/p2p_matrix p2p_matrix
 host: $(BUILD)/p2p_matrix_host $(BUILD)/p2p_host_tests
 ext: $(EXT)
-tools: $(BUILD)/fill_probe
+tools: $(BUILD)/fill_probe $(BUILD)/ipc_export_probe
 
 $(BUILD)/gpu $(BUILD)/host $(BUILD)/asan:
 	mkdir -p $@
@@ -104,6 +104,9 @@ $(EXT): $(GPU_OBJS) $(BUILD)/gpu/pymodule.o
 # Grid-shape probe (scripts/fill_probe.hip): standalone, no framework code.
 $(BUILD)/fill_probe: scripts/fill_probe.hip | $(BUILD)/gpu
 	$(HIPCC) --offload-arch=$(ARCH) -O3 $< -o $@
+
+$(BUILD)/ipc_export_probe: scripts/ipc_export_probe.hip | $(BUILD)/gpu
+	$(HIPCC) --offload-arch=$(ARCH) -O2 $< -o $@
 
 # AddressSanitizer / UBSan on host code only (GPU sanitizers are not available):
 # the unit tests, and the MPI host binary that tests/test_host_unit.py runs as
