@@ -67,7 +67,7 @@ def parse_args(argv=None):
     ap.add_argument("--size", default="32M", help="message size (reference: 32 MiB, p2p_matrix.cc:124)")
     ap.add_argument("--msgs", type=int, default=8, help="messages per direction per step")
     ap.add_argument("--mode", default="tournament", choices=["tournament", "ring", "allpairs", "pair", "self"])
-    ap.add_argument("--transport", default="rccl", choices=["rccl", "ipc", "ipc:sdma", "ipc:push", "host"],
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "ipc", "ipc:sdma", "ipc:push", "ipc:relay", "host"],
                     help="rccl (headline) | ipc = one-sided gfx950 copy kernel over hipIpc mappings | host = CPU (tests)")
     ap.add_argument("--device", type=int, default=None, help="GPU index (default LOCAL_RANK)")
     ap.add_argument("--latency-iters", type=int, default=300)
@@ -264,7 +264,7 @@ def main(argv=None) -> int:
     del sess
 
     # (with --transport host the same code path runs on the CPU transport, for tests)
-    extra_transport = {"rccl": "ipc", "ipc": "ipc", "ipc:push": "ipc", "host": "host"}.get(args.transport)
+    extra_transport = {"rccl": "ipc", "ipc": "ipc", "ipc:push": "ipc", "ipc:relay": "ipc", "host": "host"}.get(args.transport)
 
     def steps_through(transport):
         """The timed steps again through another transport session (untimed by
@@ -292,6 +292,20 @@ def main(argv=None) -> int:
                 dl = json.loads(isess.device_latency(nat.parse_size(args.latency_size), args.latency_iters,
                                                      min(100, args.latency_iters)))
                 out["device_pingpong_p50_us"] = round(statistics.median(p["one_way_us"]["p50"] for p in dl["pairs"]), 3)
+            # Multi-path: the reference's single-pair cell (0 -> 1, every
+            # other GPU idle) with the message striped over the direct link
+            # and two-hop relays through the idle GPUs.
+            if transport == "ipc:relay":
+                pair = []
+                for nbytes in (size, 256 << 20):
+                    r = json.loads(isess.run(mode="pair", dir="uni", bytes=nbytes, iters=16, warmup=2,
+                                             timing="events", verify=not args.no_verify, warm=False, cells=[(0, 1)]))
+                    fl = [f for ph in r["phases"] for f in ph["flows"]]
+                    if fl:
+                        pair.append({"bytes": nbytes, "gbs": round(fl[0]["gbs"], 2),
+                                     "iter_us_p50": round(fl[0]["iter_us"]["p50"], 2),
+                                     "mismatches": fl[0].get("mismatches", -1)})
+                out["pair_0_1"] = pair
             del idrv
             del isess
             return out
@@ -311,6 +325,10 @@ def main(argv=None) -> int:
             ipc["push"]["engine"] = "ready/done flags + gfx950 multi-copy kernel writing into the peer's slot"
             ipc["sdma"] = steps_through("ipc:sdma")
             ipc["sdma"]["engine"] = "one-sided pull by the SDMA copy engines (hipMemcpyAsync per receive)"
+            if n > 2:
+                ipc["relay"] = steps_through("ipc:relay")
+                ipc["relay"]["engine"] = ("push over the direct link + two-hop stripes relayed through GPUs whose "
+                                          "links are idle (routing.hpp)")
 
     step_ms_med = statistics.median(my_ms) if my_ms else 0.0
     result = {

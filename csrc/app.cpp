@@ -59,9 +59,12 @@ transport / launch
                          ipc   one-sided pulls from hipIpc-mapped peer buffers (gfx950 copy
                                kernel or SDMA); ranks may share a GPU
                          host  CPU sockets, no GPU
-      --ipc-engine E     kernel | sdma | push (for --transport ipc)            [kernel]
+      --ipc-engine E     kernel | sdma | push | relay (for --transport ipc)    [kernel]
                          kernel/sdma: one-sided pull of the peer's send buffer;
-                         push: rendezvous + remote writes into the peer's slot
+                         push: rendezvous + remote writes into the peer's slot;
+                         relay: push, with stripes of each message routed
+                         s -> k -> d through GPUs whose links are idle
+                         (P2P_RELAY_MIN [1M], P2P_RELAY_WEIGHT [1], P2P_RELAY_MAX)
       --bootstrap B      auto | mpi | env | local                              [auto]
       --device N         GPU index (default: local rank from block placement)
       --timeout S        watchdog for init / waits, seconds                    [300]

@@ -54,14 +54,6 @@ int remote_slot(const Phase& phase, int me, int peer) {
   return static_cast<int>(it - from.begin());
 }
 
-void post_phase_iteration(Transport& t, const Phase& phase, size_t bytes, Buffers& bufs) {
-  const RankOps& ops = phase.ranks[static_cast<size_t>(t.rank())];
-  t.group_begin();
-  for (int peer : ops.send_to) t.send_to_slot(bufs.send_buf(), bytes, peer, remote_slot(phase, t.rank(), peer));
-  for (size_t i = 0; i < ops.recv_from.size(); ++i) t.recv(bufs.recv_buf(static_cast<int>(i)), bytes, ops.recv_from[i]);
-  t.group_end();
-}
-
 namespace {
 
 // Slot on the receiver of each flow: flows were appended in the same order as
@@ -72,6 +64,37 @@ std::vector<int> flow_slots(const Phase& phase) {
   for (const auto& f : phase.flows) slots.push_back(seen[static_cast<size_t>(f.dst)]++);
   return slots;
 }
+
+// Every flow of one iteration of a phase (Transport::group_flows).
+std::vector<Transport::GroupFlow> group_flow_list(const Phase& phase) {
+  const auto slots = flow_slots(phase);
+  std::vector<Transport::GroupFlow> out(phase.flows.size());
+  for (size_t i = 0; i < phase.flows.size(); ++i) {
+    out[i].src = phase.flows[i].src;
+    out[i].dst = phase.flows[i].dst;
+    out[i].slot = slots[i];
+  }
+  return out;
+}
+
+// Whether rank r posts the groups of a phase: its endpoints, and with a
+// multi-path transport every rank (it may relay).
+bool posts_phase(const Transport& t, const Phase& phase, int r) {
+  return !phase.idle && (phase.participates(r) || t.wants_group_flows());
+}
+
+}  // namespace
+
+void post_phase_iteration(Transport& t, const Phase& phase, size_t bytes, Buffers& bufs) {
+  const RankOps& ops = phase.ranks[static_cast<size_t>(t.rank())];
+  t.group_begin();
+  if (t.wants_group_flows()) t.group_flows(bufs.send_buf(), group_flow_list(phase), bytes);
+  for (int peer : ops.send_to) t.send_to_slot(bufs.send_buf(), bytes, peer, remote_slot(phase, t.rank(), peer));
+  for (size_t i = 0; i < ops.recv_from.size(); ++i) t.recv(bufs.recv_buf(static_cast<int>(i)), bytes, ops.recv_from[i]);
+  t.group_end();
+}
+
+namespace {
 
 void prepare_payload(Transport& t, const Phase& phase, const RunConfig& cfg, Buffers& bufs) {
   const RankOps& ops = phase.ranks[static_cast<size_t>(t.rank())];
@@ -157,7 +180,9 @@ PhaseResult run_phase(Transport& t, Bootstrap& boot, const Phase& phase, size_t 
     return res;
   }
   P2P_CHECK(cfg.iters >= 1, "iters must be >= 1");
-  const bool active = phase.participates(me);
+  // Relay ranks of a multi-path transport post (and time) the phase too; a
+  // flow is still charged by its two endpoints only.
+  const bool active = posts_phase(t, phase, me);
 
   if (active) {
     prepare_payload(t, phase, cfg, bufs);
@@ -286,7 +311,7 @@ std::vector<PhaseResult> run_schedule(Transport& t, Bootstrap& boot, const Sched
 void warm_connections(Transport& t, Bootstrap& boot, const Schedule& s, Buffers& bufs, size_t bytes) {
   bytes = std::min(bytes, bufs.capacity());
   for (const Phase& p : s.phases) {
-    if (p.idle || !p.participates(t.rank())) continue;
+    if (!posts_phase(t, p, t.rank())) continue;
     post_phase_iteration(t, p, bytes, bufs);
     t.sync();
   }
@@ -468,8 +493,11 @@ void StepDriver::post_step_ops(const Phase& p) {
   }
   // One group: every message of the step, fused into one launch by RCCL.
   const RankOps& ops = p.ranks[static_cast<size_t>(t_.rank())];
+  const bool all_flows = t_.wants_group_flows();
+  const std::vector<Transport::GroupFlow> flows = all_flows ? group_flow_list(p) : std::vector<Transport::GroupFlow>();
   t_.group_begin();
   for (int m = 0; m < msgs_; ++m) {
+    if (all_flows) t_.group_flows(bufs_.send_buf(), flows, bytes_);
     for (int peer : ops.send_to) t_.send_to_slot(bufs_.send_buf(), bytes_, peer, remote_slot(p, t_.rank(), peer));
     for (size_t i = 0; i < ops.recv_from.size(); ++i) t_.recv(bufs_.recv_buf(static_cast<int>(i)), bytes_, ops.recv_from[i]);
   }
@@ -480,6 +508,7 @@ void StepDriver::step(long k) {
   const size_t pi = static_cast<size_t>(k % phases());
   const Phase& p = sched_.phases[pi];
   if (!p.participates(t_.rank())) {
+    if (posts_phase(t_, p, t_.rank())) post_step_ops(p);  // relay only: no flow of its own to time
     marks_.emplace_back(-1, -1);
   } else {
     int a = t_.mark();

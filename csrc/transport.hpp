@@ -56,6 +56,21 @@ class Transport {
   // buffer set (the receiver's index of this sender in its recv list).  Push
   // transports need it to address the peer's memory; the rest ignore it.
   virtual void send_to_slot(const void* p, size_t bytes, int peer, int /*remote_slot*/) { send(p, bytes, peer); }
+  // Multi-path transports (IPC relay engine) move parts of a message through
+  // ranks that are neither its sender nor its receiver, so every rank must
+  // know every flow of a group.  When wants_group_flows() is true the runner
+  // posts every group on EVERY rank (also ranks without sends or receives of
+  // their own) and calls group_flows() right after group_begin(), once per
+  // message of each flow, with the identical list on every rank;
+  // `set_send` names the buffer set (its send buffer on this rank).  The
+  // endpoints then post their send / recv calls as usual.
+  struct GroupFlow {
+    int src = -1;
+    int dst = -1;
+    int slot = 0;  // receive slot of the flow on dst
+  };
+  virtual bool wants_group_flows() const { return false; }
+  virtual void group_flows(const void* /*set_send*/, const std::vector<GroupFlow>& /*flows*/, size_t /*bytes*/) {}
 
   // ---- timing ----
   // Enqueue a timestamp behind all work posted so far; returns its id.
@@ -104,7 +119,10 @@ struct TransportOptions {
   double timeout_s = 300.0;        // watchdog for init / sync
   bool nonblocking_init = true;    // RCCL: ncclCommInitRankConfig(blocking=0) + polling
   int verify_impl = 0;             // 0 = auto, 1 = register-staged, 2 = LDS-staged (global_load_lds)
-  std::string ipc_engine = "kernel";  // IPC transport: kernel (gfx950 pull kernel) | sdma | push (rendezvous + remote writes)
+  // IPC transport: kernel (gfx950 pull kernel) | sdma | push (rendezvous +
+  // remote writes) | relay (push over the direct link plus two-hop relays
+  // through the other GPUs, routing.hpp)
+  std::string ipc_engine = "kernel";
   bool two_streams = false;        // RCCL: receives on a second stream (reference layout)
 };
 

@@ -22,6 +22,20 @@
 //            receiver, whose stream waits for that.  Real send/recv semantics
 //            (a send never overwrites a slot the receiver has not posted) on
 //            the direction xGMI handles best (remote stores).
+//   relay  — push, multi-path: each message is split into stripes
+//            (routing.hpp plan_routes), one over the direct link, written by
+//            the sender, and one per two-hop path s -> k -> d through a GPU k
+//            whose links s->k and k->d carry no direct flow of the group.
+//            k's copy kernel loads its stripe from s's hipIpc-mapped send
+//            buffer and stores it into d's mapped receive slot, so the bytes
+//            cross s->k and k->d and never touch k's HBM.  Every writer
+//            (sender or relay) waits for the receiver's ready flag and raises
+//            its done flag, exactly as in push.  The runner posts every group
+//            on every rank and passes the group's global flows
+//            (Transport::group_flows), so a relay knows what to move.  A
+//            single pair of an 8-GPU node can then use up to 7 links; RCCL's
+//            ncclSend/ncclRecv (and the reference's NCCL p2p) only ever use
+//            the direct one.
 //
 // Why it exists: it is the hand-written CDNA4 data plane to compare RCCL's
 // ncclSend/ncclRecv against on the same links, and, because IPC mappings
@@ -32,6 +46,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -43,6 +58,7 @@
 #include "common.hpp"
 #include "hip_check.hpp"
 #include "kernels.hpp"
+#include "routing.hpp"
 #include "transport.hpp"
 #include "units.hpp"
 
@@ -60,9 +76,11 @@ struct Export {
 class IpcTransport final : public Transport {
  public:
   IpcTransport(Bootstrap& boot, const TransportOptions& opt)
-      : boot_(boot), rank_(boot.rank()), n_(boot.size()), timeout_(opt.timeout_s), engine_(opt.ipc_engine) {
-    P2P_CHECK(engine_ == "kernel" || engine_ == "sdma" || engine_ == "push",
-              "ipc engine must be 'kernel', 'sdma' or 'push'");
+      : boot_(boot), rank_(boot.rank()), n_(boot.size()), timeout_(opt.timeout_s), engine_(opt.ipc_engine),
+        relay_(engine_ == "relay"), push_(engine_ == "push" || relay_) {
+    P2P_CHECK(engine_ == "kernel" || engine_ == "sdma" || engine_ == "push" || relay_,
+              "ipc engine must be 'kernel', 'sdma', 'push' or 'relay'");
+    if (relay_) route_opt_ = route_options_from_env();
     verify_impl_ = static_cast<dev::VerifyImpl>(opt.verify_impl);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) P2P_FATAL("ipc transport: no HIP device visible");
@@ -82,11 +100,14 @@ class IpcTransport final : public Transport {
     tick_hz_ = khz * 1e3;
     if (const char* pc = std::getenv("P2P_IPC_POOL")) pool_cap_ = std::strcmp(pc, "0") ? parse_size(pc) : 0;
     if (const char* ir = std::getenv("P2P_INJECT_EXPORT_REFUSALS")) inject_refusals_ = std::atoi(ir);
-    if (engine_ == "push") setup_sync_pages();
+    if (push_) setup_sync_pages();
   }
 
   ~IpcTransport() override {
     (void)hipStreamSynchronize(stream_);
+    if (relay_ && std::getenv("P2P_RELAY_STATS"))
+      std::fprintf(stderr, "p2p_matrix: rank %d relayed %llu bytes in %llu stripes\n", rank_, relayed_bytes_,
+                   relayed_stripes_);
     for (auto& r : regs_) close_registration(r);
     regs_.clear();
     for (size_t r = 0; r < peer_pages_.size(); ++r)
@@ -209,8 +230,9 @@ class IpcTransport final : public Transport {
       HIPCHECK(hipIpcOpenMemHandle(&mapped, all[static_cast<size_t>(r)].handle, hipIpcMemLazyEnablePeerAccess));
       reg.peer_send[static_cast<size_t>(r)] = mapped;
     }
-    if (engine_ == "push") {
-      // The sender writes into the receiver's slot: map every peer's slots.
+    if (push_) {
+      // The sender (or a relay) writes into the receiver's slot: map every
+      // peer's slots.  Every rank has the same number of slots per set.
       reg.peer_recvs.assign(static_cast<size_t>(n_), std::vector<void*>(recvs.size(), nullptr));
       for (size_t k = 0; k < recvs.size(); ++k) {
         Export slot{};
@@ -245,7 +267,48 @@ class IpcTransport final : public Transport {
     P2P_CHECK(!in_group_, "nested group");
     in_group_ = true;
     ops_.clear();
+    covered_.clear();
   }
+
+  bool wants_group_flows() const override { return relay_; }
+
+  // Relay engine: plans every flow of the group (identically on every rank)
+  // and posts this rank's part of each: the direct stripe as its sender, the
+  // stripes routed through it as a relay, the flags as the receiver.  The
+  // endpoints' own send / recv calls for these flows are then checks only.
+  void group_flows(const void* set_send, const std::vector<GroupFlow>& flows, size_t bytes) override {
+    if (!relay_) return;
+    P2P_CHECK(in_group_, "group_flows outside a group");
+    const Registration* reg = nullptr;
+    for (const auto& r : regs_)
+      if (r.send == set_send) reg = &r;
+    P2P_CHECK(reg && bytes <= reg->bytes, "ipc relay: flows of an unregistered buffer set");
+    std::vector<std::pair<int, int>> pairs;
+    pairs.reserve(flows.size());
+    for (const auto& f : flows) pairs.emplace_back(f.src, f.dst);
+    const auto plan = plan_routes(n_, pairs, bytes, route_opt_);
+    for (size_t i = 0; i < flows.size(); ++i) {
+      const GroupFlow& f = flows[i];
+      if (f.src == f.dst) continue;  // self flows: the endpoint's send / recv copy locally
+      P2P_CHECK(f.slot >= 0 && f.slot < static_cast<int>(reg->recvs.size()), "ipc relay: bad receive slot");
+      char* slot = static_cast<char*>(reg->peer_recvs[static_cast<size_t>(f.dst)][static_cast<size_t>(f.slot)]);
+      for (const Stripe& st : plan[i]) {
+        const int writer = st.via < 0 ? f.src : st.via;
+        if (rank_ == writer) {
+          const char* src = static_cast<const char*>(reg->peer_send[static_cast<size_t>(f.src)]);
+          ops_.push_back({src + st.offset, slot + st.offset, st.bytes});
+          push_sends_.push_back(f.dst);  // wait for its ready, raise its done
+          if (st.via >= 0) {
+            relayed_bytes_ += st.bytes;
+            ++relayed_stripes_;
+          }
+        }
+        if (rank_ == f.dst) push_recvs_.push_back(writer);  // post ready, wait for done
+      }
+      if (rank_ == f.src || rank_ == f.dst) covered_.push_back({f.src, f.dst, f.slot});
+    }
+  }
+
   void send(const void* p, size_t bytes, int peer) override { send_to_slot(p, bytes, peer, 0); }
   void send_to_slot(const void* p, size_t bytes, int peer, int slot) override {
     P2P_CHECK(peer >= 0 && peer < n_, "bad peer");
@@ -253,19 +316,23 @@ class IpcTransport final : public Transport {
     for (const auto& r : regs_)
       if (r.send == p && bytes <= r.bytes) reg = &r;
     P2P_CHECK(reg, "ipc transport sends only from a registered send buffer");
-    if (engine_ != "push") return;  // nothing to move: the receiver pulls
+    if (!push_) return;  // nothing to move: the receiver pulls
     P2P_CHECK(slot >= 0 && slot < static_cast<int>(reg->recvs.size()), "bad remote slot");
+    if (take_covered(rank_, peer, slot)) return;  // posted by group_flows
     ops_.push_back({p, reg->peer_recvs[static_cast<size_t>(peer)][static_cast<size_t>(slot)], bytes});
     if (peer != rank_) push_sends_.push_back(peer);
     if (!in_group_) flush();
   }
   void recv(void* p, size_t bytes, int peer) override {
     P2P_CHECK(peer >= 0 && peer < n_, "bad peer");
-    if (engine_ == "push") {
-      bool ok = std::any_of(regs_.begin(), regs_.end(), [&](const Registration& r) {
-        return bytes <= r.bytes && std::find(r.recvs.begin(), r.recvs.end(), p) != r.recvs.end();
-      });
-      P2P_CHECK(ok, "ipc transport receives only into a registered receive slot");
+    if (push_) {
+      int slot = -1;
+      for (const auto& r : regs_) {
+        auto it = std::find(r.recvs.begin(), r.recvs.end(), p);
+        if (bytes <= r.bytes && it != r.recvs.end()) slot = static_cast<int>(it - r.recvs.begin());
+      }
+      P2P_CHECK(slot >= 0, "ipc transport receives only into a registered receive slot");
+      if (take_covered(peer, rank_, slot)) return;  // posted by group_flows
       if (peer != rank_) push_recvs_.push_back(peer);  // a self receive is the self send's copy
       if (!in_group_) flush();
       return;
@@ -280,6 +347,7 @@ class IpcTransport final : public Transport {
   void group_end() override {
     P2P_CHECK(in_group_, "group_end without group_begin");
     in_group_ = false;
+    P2P_CHECK(covered_.empty(), "ipc relay: group_flows named a flow this rank did not post");
     flush();
   }
 
@@ -299,8 +367,8 @@ class IpcTransport final : public Transport {
   }
   void clear_marks() override { next_event_ = 0; }
 
-  // Push: the flag values are baked into each launch, so a replay would wait
-  // for flags that were already consumed; no graphs there.
+  // Push / relay: the flag values are baked into each launch, so a replay
+  // would wait for flags that were already consumed; no graphs there.
   bool supports_graphs() const override { return engine_ == "kernel"; }
   void capture_begin() override { HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal)); }
   int capture_end() override {
@@ -428,7 +496,7 @@ class IpcTransport final : public Transport {
     size_t bytes = 0;
     std::vector<void*> recvs;
     std::vector<void*> peer_send;  // mapped send buffer of every rank (own one for self)
-    std::vector<std::vector<void*>> peer_recvs;  // push: [rank][slot] mapped receive slots
+    std::vector<std::vector<void*>> peer_recvs;  // push / relay: [rank][slot] mapped receive slots
   };
 
   void close_registration(Registration& reg) {
@@ -442,6 +510,16 @@ class IpcTransport final : public Transport {
           slot = nullptr;
         }
     }
+  }
+
+  // A flow (src, dst, slot) that group_flows already posted for this rank;
+  // consumed by the endpoint's matching send / recv call.
+  bool take_covered(int src, int dst, int slot) {
+    const std::array<int, 3> key{src, dst, slot};
+    auto it = std::find(covered_.begin(), covered_.end(), key);
+    if (it == covered_.end()) return false;
+    covered_.erase(it);
+    return true;
   }
 
   // Push group: readies out / readies in, the copies, then done out / done in.
@@ -526,7 +604,7 @@ class IpcTransport final : public Transport {
   }
 
   void flush() {
-    if (engine_ == "push") {
+    if (push_) {
       flush_push();
       return;
     }
@@ -566,6 +644,9 @@ class IpcTransport final : public Transport {
   int rank_, n_;
   double timeout_;
   std::string engine_;
+  bool relay_;  // multi-path push (engine "relay")
+  bool push_;   // rendezvous + remote writes (engines "push" and "relay")
+  RouteOptions route_opt_;
   int device_ = 0;
   hipStream_t stream_ = nullptr;
   std::vector<hipEvent_t> events_;
@@ -581,6 +662,8 @@ class IpcTransport final : public Transport {
   std::vector<Registration> regs_;
   bool in_group_ = false;
   std::vector<dev::CopyOp> ops_;
+  std::vector<std::array<int, 3>> covered_;  // relay: (src, dst, slot) posted by group_flows
+  unsigned long long relayed_bytes_ = 0, relayed_stripes_ = 0;  // moved by this rank as a relay (P2P_RELAY_STATS)
 
   struct Block {
     size_t size = 0;
@@ -644,14 +727,14 @@ class IpcTransport final : public Transport {
   size_t pool_bytes_ = 0;
   std::map<void*, Block> blocks_;              // live allocations
 
-  // Push engine state.
+  // Push / relay engine state.
   static constexpr size_t kSyncLine = 128;
   static constexpr int kReady = 0, kDone = 1;
   void* sync_page_ = nullptr;
   std::vector<void*> sync_peer_;
   unsigned int* sig_status_ = nullptr;  // host-mapped; bit 0 = a signal wait timed out
   std::vector<unsigned long long> ready_posted_, ready_seen_, done_posted_, done_seen_;
-  std::vector<int> push_sends_, push_recvs_;
+  std::vector<int> push_sends_, push_recvs_;  // peers this rank writes to / receives from in the group
 
   static constexpr size_t kPingHeader = 256;            // flag + padding (own cache lines)
   static constexpr size_t kPingMaxBytes = 64u << 10;

@@ -44,10 +44,23 @@ def mpirun():
 
 
 def free_port() -> int:
+    """A port P with P and P + 1 both free: torchrun's store takes P and the
+    native TCP bootstrap listens on MASTER_PORT + 1 (csrc/bootstrap.cpp)."""
     import socket
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
+    for _ in range(64):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        p = s.getsockname()[1]
+        s.close()
+        if p >= 65535:
+            continue
+        t = socket.socket()
+        try:
+            t.bind(("127.0.0.1", p + 1))
+            return p
+        except OSError:
+            continue
+        finally:
+            t.close()
     return p

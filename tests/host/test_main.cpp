@@ -16,6 +16,7 @@
 #include "common.hpp"
 #include "prng.hpp"
 #include "report.hpp"
+#include "routing.hpp"
 #include "runner.hpp"
 #include "schedule.hpp"
 #include "stats.hpp"
@@ -221,6 +222,73 @@ TEST(test_restrict_cells) {
 }
 
 // ----------------------------------------------------------- placement ----
+
+// ------------------------------------------------------------- routing ----
+
+static size_t stripe_sum(const std::vector<Stripe>& v) {
+  size_t s = 0, off = 0;
+  for (const auto& x : v) {
+    EXPECT(x.offset == off);  // contiguous, direct first
+    off += x.bytes;
+    s += x.bytes;
+  }
+  return s;
+}
+
+TEST(test_routes_single_pair_uses_every_relay) {
+  const size_t bytes = 32u << 20;
+  auto plan = plan_routes(8, {{0, 1}}, bytes);
+  EXPECT(plan.size() == 1 && plan[0].size() == 7);
+  EXPECT(plan[0][0].via == -1 && stripe_sum(plan[0]) == bytes);
+  std::set<int> vias;
+  for (size_t i = 1; i < plan[0].size(); ++i) {
+    vias.insert(plan[0][i].via);
+    EXPECT(plan[0][i].bytes % 4096 == 0);
+    EXPECT(plan[0][i].bytes * 7 <= bytes && plan[0][i].bytes * 7 > bytes - 7 * 4096);  // equal shares
+  }
+  EXPECT((vias == std::set<int>{2, 3, 4, 5, 6, 7}));
+  // Small messages, two ranks, weight 0 and max_relays 0 stay direct.
+  EXPECT(plan_routes(8, {{0, 1}}, 64 << 10)[0].size() == 1);
+  EXPECT(plan_routes(2, {{0, 1}}, bytes)[0].size() == 1);
+  RouteOptions o;
+  o.relay_weight = 0;
+  EXPECT(plan_routes(8, {{0, 1}}, bytes, o)[0].size() == 1);
+  o = RouteOptions();
+  o.max_relays = 2;
+  auto capped = plan_routes(8, {{0, 1}}, bytes, o);
+  EXPECT(capped[0].size() == 3 && stripe_sum(capped[0]) == bytes);
+}
+
+TEST(test_routes_busy_links_and_duplicates) {
+  const size_t bytes = 64u << 20;
+  // All-pairs: every link carries a direct flow, nothing is relayed.
+  std::vector<std::pair<int, int>> all;
+  for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < 4; ++b)
+      if (a != b) all.emplace_back(a, b);
+  for (auto& p : plan_routes(4, all, bytes)) EXPECT(p.size() == 1 && p[0].bytes == bytes);
+  // Bi-directional tournament round on 8 ranks: 6 relays per flow at half
+  // the direct share (every relay link is shared by two segments).
+  std::vector<std::pair<int, int>> round = {{0, 1}, {1, 0}, {2, 3}, {3, 2}, {4, 5}, {5, 4}, {6, 7}, {7, 6}};
+  auto plan = plan_routes(8, round, bytes);
+  std::map<std::pair<int, int>, int> seg;  // directed link -> segments
+  for (size_t i = 0; i < round.size(); ++i) {
+    EXPECT(plan[i].size() == 7 && stripe_sum(plan[i]) == bytes);
+    EXPECT(plan[i][0].bytes > plan[i][1].bytes * 3 / 2);  // direct share 1 vs relay 1/2
+    for (size_t j = 1; j < plan[i].size(); ++j) {
+      const int k = plan[i][j].via;
+      EXPECT(k != round[i].first && k != round[i].second);
+      ++seg[{round[i].first, k}];
+      ++seg[{k, round[i].second}];
+    }
+  }
+  for (auto& kv : seg) EXPECT(kv.second <= 2);
+  for (auto& f : round) EXPECT(seg.count(f) == 0);  // no relay over a direct flow's link
+  // Duplicates plan identically; self flows stay whole.
+  auto dup = plan_routes(8, {{0, 1}, {2, 2}, {0, 1}}, bytes);
+  EXPECT(dup[0].size() == dup[2].size() && dup[0][1].bytes == dup[2][1].bytes);
+  EXPECT(dup[1].size() == 1 && dup[1][0].bytes == bytes);
+}
 
 TEST(test_host_hash_matches_reference) {
   // getHostHash (p2p_matrix.cc:44-51) computed by hand for "ab":

@@ -82,6 +82,42 @@ def test_four_ranks_allpairs_large(exe, engine):
     assert "verification: OK" in out.stdout
 
 
+def test_relay_engine_every_mode(exe, tmp_path):
+    """Multi-path relay engine with 4 ranks on one GPU: in pair mode the two
+    idle ranks carry two-hop stripes of every message above 1 MiB (their copy
+    kernel loads from the sender's mapped buffer and stores into the
+    receiver's mapped slot); tournament / ring find no idle links on 4 ranks
+    for bi but do for uni; all-pairs stays direct.  Every receive verified."""
+    js = tmp_path / "r.json"
+    env = dict(os.environ, P2P_RELAY_STATS="1")
+    out = subprocess.run([MPIRUN, "-n", "4", exe, "--transport", "ipc", "--ipc-engine", "relay", "--device", "0",
+                          "--mode", "all", "--sizes", "64K:64M:32", "-n", "4", "--verify", "--no-compat",
+                          "--json", str(js), "--timeout", "60"], capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "verification: OK" in out.stdout
+    runs = [json.loads(l) for l in js.read_text().splitlines() if '"run"' in l]
+    assert runs and all(ph["mismatches"] == 0 for r in runs for ph in r["phases"])
+    relayed = [int(l.split("relayed ")[1].split()[0]) for l in out.stderr.splitlines() if "relayed" in l]
+    assert len(relayed) == 4 and all(b > 0 for b in relayed), out.stderr[-2000:]
+
+
+def test_relay_pair_cell_with_six_relays(exe):
+    """8 ranks on one GPU, one pair cell (0 -> 1) of 32 MiB: the message goes
+    out in 7 stripes (direct + 6 relays), verified; wallclock timing too."""
+    env = dict(os.environ, P2P_RELAY_STATS="1", P2P_IPC_POOL="1G")
+    for timing in ("events", "wallclock"):
+        out = subprocess.run([MPIRUN, "-n", "8", exe, "--transport", "ipc", "--ipc-engine", "relay", "--device", "0",
+                              "--mode", "pair", "--dir", "bi", "--cells", "0:1", "--size", "32M", "-n", "3", "--verify",
+                              "--no-compat", "--timing", timing, "--timeout", "60"],
+                             capture_output=True, text=True, timeout=300, env=env)
+        assert out.returncode == 0, out.stderr[-3000:]
+        assert "verification: OK" in out.stdout
+        relayed = {int(l.split("rank ")[1].split()[0]): int(l.split("relayed ")[1].split()[0])
+                   for l in out.stderr.splitlines() if " relayed " in l}
+        assert sorted(relayed) == list(range(8)), out.stderr[-2000:]
+        assert relayed[0] == 0 and relayed[1] == 0 and all(relayed[k] > 0 for k in range(2, 8)), relayed
+
+
 def test_export_refusal_is_retried(exe):
     """hipIpcGetMemHandle occasionally refuses a fresh block on this stack;
     the transport reallocates and says so.  Injected here: every rank's
@@ -158,3 +194,6 @@ def test_bench_emulated_node(nranks):
     assert ipc["verify_mismatches"] == 0 and ipc["push"]["verify_mismatches"] == 0, ipc
     assert ipc["sdma"]["verify_mismatches"] == 0 and ipc["sdma"]["value_gbs"] > 0, ipc
     assert ipc["device_pingpong_p50_us"] > 0
+    relay = ipc["relay"]
+    assert relay["verify_mismatches"] == 0 and relay["value_gbs"] > 0, relay
+    assert [p["mismatches"] for p in relay["pair_0_1"]] == [0, 0], relay
