@@ -573,8 +573,17 @@ struct CopyArgs {
   uint64_t nvec[kMaxCopyOps];
   uint32_t tail[kMaxCopyOps];
   uint32_t block_begin[kMaxCopyOps + 1];
+  uint32_t coherent;  // bit i: op i moves between GPUs (system-coherent accesses)
   int nops;
 };
+
+// gfx940+ cache-policy bits of a buffer access: sc0 | sc1 = system scope.
+// A load with them never returns a line the reader's L2 kept from an earlier
+// run (the peer may have refilled that buffer since); a store with them is
+// written through to the owner's memory, so the flag kernel that follows only
+// has to order, not flush (kernels.hpp CopyOp::coherent).
+constexpr int kSystemCoherent = 1 | 16;
+constexpr int kRsrcFlags = 0x00020000;  // raw buffer descriptor word 3 for gfx950
 
 __global__ __launch_bounds__(kBlock) void multi_copy_kernel(const CopyArgs a) {
   // Workgroup -> op: block ranges are contiguous per op; the scan is over at
@@ -586,6 +595,24 @@ __global__ __launch_bounds__(kBlock) void multi_copy_kernel(const CopyArgs a) {
   const uint4* __restrict__ s = a.src[op];
   uint4* __restrict__ d = a.dst[op];
   const uint64_t n = a.nvec[op];
+  if ((a.coherent >> op) & 1u) {
+    // One descriptor pair per 4 KiB chunk (block-uniform base, lane offset in
+    // voffset); the range check drops the lanes past the end of the op.
+    for (uint64_t base = static_cast<uint64_t>(b) * kBlockVecs; base < n; base += static_cast<uint64_t>(nb) * kBlockVecs) {
+      const int bytes = static_cast<int>(min<uint64_t>(kBlockVecs, n - base) * 16);
+      auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(s + base), 0, bytes, kRsrcFlags);
+      auto rd = __builtin_amdgcn_make_buffer_rsrc(d + base, 0, bytes, kRsrcFlags);
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(threadIdx.x) * 16, 0, kSystemCoherent);
+      __builtin_amdgcn_raw_buffer_store_b128(v, rd, static_cast<int>(threadIdx.x) * 16, 0, kSystemCoherent);
+    }
+    if (b == 0 && threadIdx.x < a.tail[op]) {
+      auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(s + n), 0, static_cast<int>(a.tail[op]), kRsrcFlags);
+      auto rd = __builtin_amdgcn_make_buffer_rsrc(d + n, 0, static_cast<int>(a.tail[op]), kRsrcFlags);
+      const auto v = __builtin_amdgcn_raw_buffer_load_b8(rs, static_cast<int>(threadIdx.x), 0, kSystemCoherent);
+      __builtin_amdgcn_raw_buffer_store_b8(v, rd, static_cast<int>(threadIdx.x), 0, kSystemCoherent);
+    }
+    return;
+  }
   for (uint64_t i = static_cast<uint64_t>(b) * kBlockVecs + threadIdx.x; i < n; i += static_cast<uint64_t>(nb) * kBlockVecs)
     d[i] = s[i];
   if (b == 0 && threadIdx.x < a.tail[op]) {
@@ -604,6 +631,7 @@ namespace {
 void launch_copy_group(const CopyOp* ops, int cnt, hipStream_t stream, int max_blocks) {
   CopyArgs a{};
   a.nops = cnt;
+  a.coherent = 0;
   uint64_t need[kMaxCopyOps] = {0};
   uint64_t total_need = 0;
   for (int i = 0; i < cnt; ++i) {
@@ -614,6 +642,7 @@ void launch_copy_group(const CopyOp* ops, int cnt, hipStream_t stream, int max_b
     a.dst[i] = static_cast<uint4*>(o.dst);
     a.nvec[i] = o.bytes / 16;
     a.tail[i] = static_cast<uint32_t>(o.bytes - a.nvec[i] * 16);
+    if (o.coherent) a.coherent |= 1u << i;
     need[i] = std::max<uint64_t>(1, (a.nvec[i] + kBlockVecs - 1) / kBlockVecs);
     total_need += need[i];
   }
@@ -650,7 +679,7 @@ void launch_multi_copy(const CopyOp* ops, int nops, hipStream_t stream, int max_
     size_t off = 0;
     do {
       const size_t n = std::min(piece, o.bytes - off);
-      pieces.push_back({static_cast<const char*>(o.src) + off, static_cast<char*>(o.dst) + off, n});
+      pieces.push_back({static_cast<const char*>(o.src) + off, static_cast<char*>(o.dst) + off, n, o.coherent});
       off += n;
     } while (off < o.bytes);
   }

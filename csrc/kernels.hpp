@@ -83,10 +83,16 @@ int cu_count();
 // src (typically a peer GPU's buffer mapped through hipIpcOpenMemHandle, so
 // the loads travel over xGMI) to dst.  Full grid: one 16 B load + store per
 // lane, one 4 KiB block per workgroup, workgroups split across ops by size.
+// coherent = the op crosses GPUs (a hipIpc-mapped peer buffer on either side):
+// its loads and stores carry system-scope cache bits (sc0 sc1), so a reader
+// never sees a line its L2 kept from an earlier run of the peer's buffer and
+// the payload is written through to the owner's HBM before the kernel ends.
+// Local ops (the self path) keep plain accesses.
 struct CopyOp {
   const void* src;
   void* dst;
   size_t bytes;
+  bool coherent = false;
 };
 constexpr int kMaxCopyOps = 16;
 void launch_multi_copy(const CopyOp* ops, int nops, hipStream_t stream, int max_blocks = 0);

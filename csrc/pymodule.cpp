@@ -249,11 +249,13 @@ PYBIND11_MODULE(_p2pcore, m) {
                            check, as_stream(stream), max_grid);
       }, py::arg("ptr"), py::arg("bytes"), py::arg("seed"), py::arg("impl") = 0, py::arg("check") = true,
       py::arg("stream") = 0, py::arg("max_grid") = 0);
-  m.def("copy", [](uintptr_t dst, uintptr_t src, size_t bytes, uintptr_t stream, int max_blocks) {
-        dev::CopyOp op{reinterpret_cast<const void*>(src), reinterpret_cast<void*>(dst), bytes};
+  m.def("copy", [](uintptr_t dst, uintptr_t src, size_t bytes, uintptr_t stream, int max_blocks, bool coherent) {
+        dev::CopyOp op{reinterpret_cast<const void*>(src), reinterpret_cast<void*>(dst), bytes, coherent};
         dev::launch_multi_copy(&op, 1, as_stream(stream), max_blocks);
       }, py::arg("dst"), py::arg("src"), py::arg("bytes"), py::arg("stream") = 0, py::arg("max_blocks") = 0,
-      "The IPC transport's gfx950 copy kernel on one (dst, src) pair.");
+      py::arg("coherent") = false,
+      "The IPC transport's gfx950 copy kernel on one (dst, src) pair (coherent: the cross-GPU form with "
+      "system-scope sc0 sc1 buffer loads and stores).");
   m.def("fill_geometry", [](size_t bytes) {
     auto g = dev::fill_geometry(bytes);
     return py::make_tuple(g.grid, g.block, g.lds_bytes);

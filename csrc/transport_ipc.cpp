@@ -296,7 +296,7 @@ class IpcTransport final : public Transport {
         const int writer = st.via < 0 ? f.src : st.via;
         if (rank_ == writer) {
           const char* src = static_cast<const char*>(reg->peer_send[static_cast<size_t>(f.src)]);
-          ops_.push_back({src + st.offset, slot + st.offset, st.bytes});
+          ops_.push_back({src + st.offset, slot + st.offset, st.bytes, true});
           push_sends_.push_back(f.dst);  // wait for its ready, raise its done
           if (st.via >= 0) {
             relayed_bytes_ += st.bytes;
@@ -319,7 +319,7 @@ class IpcTransport final : public Transport {
     if (!push_) return;  // nothing to move: the receiver pulls
     P2P_CHECK(slot >= 0 && slot < static_cast<int>(reg->recvs.size()), "bad remote slot");
     if (take_covered(rank_, peer, slot)) return;  // posted by group_flows
-    ops_.push_back({p, reg->peer_recvs[static_cast<size_t>(peer)][static_cast<size_t>(slot)], bytes});
+    ops_.push_back({p, reg->peer_recvs[static_cast<size_t>(peer)][static_cast<size_t>(slot)], bytes, peer != rank_});
     if (peer != rank_) push_sends_.push_back(peer);
     if (!in_group_) flush();
   }
@@ -341,7 +341,7 @@ class IpcTransport final : public Transport {
     for (const auto& r : regs_)
       if (std::find(r.recvs.begin(), r.recvs.end(), p) != r.recvs.end()) reg = &r;
     P2P_CHECK(reg && bytes <= reg->bytes, "ipc transport receives only into a registered receive slot");
-    ops_.push_back({reg->peer_send[static_cast<size_t>(peer)], p, bytes});
+    ops_.push_back({reg->peer_send[static_cast<size_t>(peer)], p, bytes, peer != rank_});
     if (!in_group_) flush();
   }
   void group_end() override {

@@ -65,8 +65,15 @@ def main():
         row["torch_zero_tbs"] = sz / timed(lambda: buf.zero_(), a.reps) / 1e12
         row["torch_copy_tbs"] = sz / timed(lambda: dst.copy_(buf), a.reps) / 1e12
         row["copy_kernel_tbs"] = sz / timed(lambda: nat.copy(dst.data_ptr(), ptr, sz, stream), a.reps) / 1e12
+        # The cross-GPU form (system-scope sc0 sc1 buffer accesses) on local
+        # memory: what the coherence bits cost when nothing is remote.
+        row["copy_coherent_tbs"] = sz / timed(lambda: nat.copy(dst.data_ptr(), ptr, sz, stream, coherent=True),
+                                              a.reps) / 1e12
         nat.fill(ptr, sz, 7, stream)
         nat.copy(dst.data_ptr(), ptr, sz, stream)
+        assert nat.verify(dst.data_ptr(), sz, 7, 1, True, stream)[0] == 0
+        dst.zero_()
+        nat.copy(dst.data_ptr(), ptr, sz, stream, coherent=True)
         assert nat.verify(dst.data_ptr(), sz, 7, 1, True, stream)[0] == 0
         del dst
         for k, t in res.items():

@@ -31,6 +31,22 @@ def test_fill_matches_reference(nbytes):
     assert torch.all(buf[nbytes:] == 0xAB), "fill wrote past the end"
 
 
+@pytest.mark.parametrize("coherent", [False, True])
+@pytest.mark.parametrize("nbytes", [16, 48, 4096, 4099, 4096 * 3 + 1008, (1 << 20) + 13, 64 << 20])
+def test_copy_kernel_matches_torch(nbytes, coherent):
+    """The IPC data mover (plain, and the cross-GPU form with system-scope
+    sc0 sc1 buffer loads / stores) against torch's copy_, tails included,
+    and nothing written past the end."""
+    from test_nccl_p2p_amd import require_native
+    src = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda")
+    dst = dev_bytes(nbytes)
+    require_native().copy(dst.data_ptr(), src.data_ptr(), nbytes, torch.cuda.current_stream().cuda_stream,
+                          coherent=coherent)
+    torch.cuda.synchronize()
+    assert torch.equal(dst[:nbytes], src)
+    assert torch.all(dst[nbytes:] == 0xAB), "copy wrote past the end"
+
+
 @pytest.mark.parametrize("fill_impl", [1, 2, 3, 4])  # grid, non-temporal, grid-stride, XCD-ordered grid
 @pytest.mark.parametrize("nbytes", SIZES + [(64 << 20) + 4])
 def test_fill_variants_match_reference(fill_impl, nbytes):
