@@ -33,8 +33,11 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
+import tempfile
 import time
 
 import torch
@@ -57,6 +60,85 @@ def claim_stdout() -> int:
     real = os.dup(1)
     os.dup2(2, 1)
     return real
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def steps_through(nat, isess, args, mode, size, batch, transport):
+    """The timed steps again through another transport session (untimed by
+    the contract); any error is reported instead of failing the run."""
+    try:
+        idrv = nat.StepDriver(isess, mode, "bi", size, args.msgs, not args.no_verify, bool(batch), False)
+        idrv.connect()
+        idrv.run_steps(0, args.warmup)
+        idrv.sync()
+        isess.barrier()
+        i0 = time.perf_counter()
+        idrv.run_steps(args.warmup, args.steps)
+        idrv.sync()
+        isess.barrier()
+        ielapsed = isess.allreduce_max(time.perf_counter() - i0)
+        ijob = sum(idrv.job_bytes_per_step(args.warmup + k) for k in range(args.steps))
+        out = {"value_gbs": round(ijob / ielapsed / 1e9, 3), "ms_per_step": round(ielapsed / args.steps * 1e3, 4),
+               "verify_mismatches": idrv.verify_last() if not args.no_verify else -1,
+               "transport": transport}
+        del idrv
+        # Device-initiated ping-pong: one wave per GPU writes the message
+        # into the peer's memory and spins on its own inbox (no host, no
+        # runtime in the loop) -- the fabric's latency, next to RCCL's.
+        if transport == "ipc":
+            dl = json.loads(isess.device_latency(nat.parse_size(args.latency_size), args.latency_iters,
+                                                 min(100, args.latency_iters)))
+            out["device_pingpong_p50_us"] = round(statistics.median(p["one_way_us"]["p50"] for p in dl["pairs"]), 3)
+        # Multi-path: the reference's single-pair cell (0 -> 1, every other
+        # GPU idle) with the message striped over the direct link and two-hop
+        # relays through the idle GPUs.
+        if transport == "ipc:relay":
+            pair = []
+            for nbytes in (size, 256 << 20):
+                r = json.loads(isess.run(mode="pair", dir="uni", bytes=nbytes, iters=16, warmup=2,
+                                         timing="events", verify=not args.no_verify, warm=False, cells=[(0, 1)]))
+                fl = [f for ph in r["phases"] for f in ph["flows"]]
+                if fl:
+                    pair.append({"bytes": nbytes, "gbs": round(fl[0]["gbs"], 2),
+                                 "iter_us_p50": round(fl[0]["iter_us"]["p50"], 2),
+                                 "mismatches": fl[0].get("mismatches", -1)})
+            out["pair_0_1"] = pair
+        return out
+    except Exception as e:  # report, never fail the headline
+        return {"error": str(e)[:300], "transport": transport}
+
+
+def child_main(args) -> int:
+    """--child: one rank of an untimed comparison run (see isolated() in
+    main).  Bootstraps its own native TCP star on --child-port (no
+    torch.distributed: the parent's store is busy) and writes rank 0's result
+    to --child-out."""
+    claim_stdout()
+    from test_nccl_p2p_amd import require_native
+    from test_nccl_p2p_amd.parallel.session import dist_env
+
+    nat = require_native()
+    env = dist_env()
+    device = env.local_rank if args.device is None else args.device
+    size = nat.parse_size(args.size)
+    try:
+        sess = nat.Session(env.rank, env.world, host=env.master_addr, port=args.child_port, device=device,
+                           transport=args.child, timeout_s=90.0)
+        out = steps_through(nat, sess, args, args.mode, size, args.child_batch, args.child)
+        del sess
+    except Exception as e:
+        out = {"error": str(e)[:300], "transport": args.child}
+    if env.rank == 0:
+        with open(args.child_out, "w") as f:
+            json.dump(out, f)
+    return 0
 
 
 def parse_args(argv=None):
@@ -87,11 +169,22 @@ def parse_args(argv=None):
     ap.add_argument("--sweep-max", default="4G", help="largest message of the pair sweep")
     ap.add_argument("--ref-iters", type=int, default=128,
                     help="iterations per cell of the reference-methodology comparison (0 = skip)")
+    ap.add_argument("--isolate", type=int, default=1,
+                    help="1: run each untimed transport comparison in a child process per rank (a fault there "
+                         "cannot take the headline down); 0: in this process (halves the processes per GPU)")
+    ap.add_argument("--child-timeout", type=float, default=300.0,
+                    help="seconds allowed to each untimed comparison process")
+    ap.add_argument("--child", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--child-port", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--child-out", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--child-batch", type=int, default=1, help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
 def main(argv=None) -> int:
     args = parse_args(argv)
+    if args.child:
+        return child_main(args)
     real_stdout = claim_stdout()
     from test_nccl_p2p_amd import require_native
     from test_nccl_p2p_amd.parallel.session import create_session, init_control_plane
@@ -266,69 +359,78 @@ def main(argv=None) -> int:
     # (with --transport host the same code path runs on the CPU transport, for tests)
     extra_transport = {"rccl": "ipc", "ipc": "ipc", "ipc:push": "ipc", "ipc:relay": "ipc", "host": "host"}.get(args.transport)
 
-    def steps_through(transport):
-        """The timed steps again through another transport session (untimed by
-        the contract); any error is reported instead of failing the run."""
+    def isolated(transport):
+        """steps_through() for `transport` in a child process per rank.  The
+        comparisons drive the hand-written data plane (hipIpc mappings,
+        signal kernels, relays) across GPUs; if one of them faults or hangs
+        on some node, only the child dies, and the headline line still gets
+        printed with the error in its place."""
+        box = [free_port() if env.rank == 0 else None]
+        if n > 1:
+            dist.broadcast_object_list(box, src=0)
+        out_path = os.path.join(tempfile.gettempdir(), "p2p_bench_child_%d_%d.json" % (box[0], env.rank))
+        cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(n), "--steps", str(args.steps),
+               "--warmup", str(args.warmup), "--size", args.size, "--msgs", str(args.msgs), "--mode", mode,
+               "--latency-iters", str(args.latency_iters), "--latency-size", args.latency_size,
+               "--child", transport, "--child-port", str(box[0]), "--child-out", out_path,
+               "--child-batch", str(int(batch))]
+        if args.no_verify:
+            cmd.append("--no-verify")
+        if args.device is not None:
+            cmd += ["--device", str(args.device)]
         try:
-            isess = create_session(transport, device=device, timeout_s=90.0)
-            idrv = nat.StepDriver(isess, mode, "bi", size, args.msgs, not args.no_verify, bool(batch), False)
-            idrv.connect()
-            idrv.run_steps(0, args.warmup)
-            idrv.sync()
-            isess.barrier()
-            i0 = time.perf_counter()
-            idrv.run_steps(args.warmup, args.steps)
-            idrv.sync()
-            isess.barrier()
-            ielapsed = isess.allreduce_max(time.perf_counter() - i0)
-            ijob = sum(idrv.job_bytes_per_step(args.warmup + k) for k in range(args.steps))
-            out = {"value_gbs": round(ijob / ielapsed / 1e9, 3), "ms_per_step": round(ielapsed / args.steps * 1e3, 4),
-                   "verify_mismatches": idrv.verify_last() if not args.no_verify else -1,
-                   "transport": transport}
-            # Device-initiated ping-pong: one wave per GPU writes the message
-            # into the peer's memory and spins on its own inbox (no host, no
-            # runtime in the loop) -- the fabric's latency, next to RCCL's.
-            if transport == "ipc":
-                dl = json.loads(isess.device_latency(nat.parse_size(args.latency_size), args.latency_iters,
-                                                     min(100, args.latency_iters)))
-                out["device_pingpong_p50_us"] = round(statistics.median(p["one_way_us"]["p50"] for p in dl["pairs"]), 3)
-            # Multi-path: the reference's single-pair cell (0 -> 1, every
-            # other GPU idle) with the message striped over the direct link
-            # and two-hop relays through the idle GPUs.
-            if transport == "ipc:relay":
-                pair = []
-                for nbytes in (size, 256 << 20):
-                    r = json.loads(isess.run(mode="pair", dir="uni", bytes=nbytes, iters=16, warmup=2,
-                                             timing="events", verify=not args.no_verify, warm=False, cells=[(0, 1)]))
-                    fl = [f for ph in r["phases"] for f in ph["flows"]]
-                    if fl:
-                        pair.append({"bytes": nbytes, "gbs": round(fl[0]["gbs"], 2),
-                                     "iter_us_p50": round(fl[0]["iter_us"]["p50"], 2),
-                                     "mismatches": fl[0].get("mismatches", -1)})
-                out["pair_0_1"] = pair
-            del idrv
-            del isess
-            return out
-        except Exception as e:  # report, never fail the headline
-            return {"error": str(e)[:300], "transport": transport}
+            rc = subprocess.run(cmd, timeout=args.child_timeout).returncode
+        except subprocess.TimeoutExpired:
+            rc = "timeout"
+        barrier()
+        res = None
+        if env.rank == 0:
+            try:
+                with open(out_path) as f:
+                    res = json.load(f)
+            except (OSError, ValueError):
+                res = {"error": "comparison process failed (exit status %s)" % rc, "transport": transport}
+        try:
+            os.unlink(out_path)
+        except OSError:
+            pass
+        return res
 
     # The hand-written data plane on the same links: the gfx950 multi-copy
     # kernel pulling from hipIpc-mapped peer buffers ("pull", one-sided), the
-    # rendezvous engine that writes into the receiver's slot ("push"), and the
-    # SDMA copy engines pulling instead of CUs ("sdma").
+    # rendezvous engine that writes into the receiver's slot ("push"), the
+    # SDMA copy engines pulling instead of CUs ("sdma"), and multi-path push
+    # with two-hop relays through GPUs whose links are idle ("relay").
     ipc = None
     if n > 1 and args.ipc_extra and extra_transport:
-        ipc = steps_through(extra_transport)
+        runs = [(extra_transport, None)]
         if extra_transport == "ipc":
-            ipc["engine"] = "gfx950 multi-copy kernel, one-sided pull over hipIpc mappings"
-            ipc["push"] = steps_through("ipc:push")
-            ipc["push"]["engine"] = "ready/done flags + gfx950 multi-copy kernel writing into the peer's slot"
-            ipc["sdma"] = steps_through("ipc:sdma")
-            ipc["sdma"]["engine"] = "one-sided pull by the SDMA copy engines (hipMemcpyAsync per receive)"
-            if n > 2:
-                ipc["relay"] = steps_through("ipc:relay")
-                ipc["relay"]["engine"] = ("push over the direct link + two-hop stripes relayed through GPUs whose "
-                                          "links are idle (routing.hpp)")
+            runs += [("ipc:push", "push"), ("ipc:sdma", "sdma")] + ([("ipc:relay", "relay")] if n > 2 else [])
+        engines = {"ipc": "gfx950 multi-copy kernel, one-sided pull over hipIpc mappings",
+                   "ipc:push": "ready/done flags + gfx950 multi-copy kernel writing into the peer's slot",
+                   "ipc:sdma": "one-sided pull by the SDMA copy engines (hipMemcpyAsync per receive)",
+                   "ipc:relay": "push over the direct link + two-hop stripes relayed through GPUs whose links are "
+                                "idle (routing.hpp)"}
+        for transport, key in runs:
+            if env.rank == 0:
+                log("bench: %s comparison" % transport)
+            if args.isolate:
+                r = isolated(transport)
+            else:
+                try:
+                    isess = create_session(transport, device=device, timeout_s=90.0)
+                    r = steps_through(nat, isess, args, mode, size, batch, transport)
+                    del isess
+                except Exception as e:  # report, never fail the headline
+                    r = {"error": str(e)[:300], "transport": transport}
+            if env.rank != 0:
+                continue
+            if transport in engines:
+                r["engine"] = engines[transport]
+            if key is None:
+                ipc = r
+            else:
+                ipc[key] = r
 
     step_ms_med = statistics.median(my_ms) if my_ms else 0.0
     result = {

@@ -53,7 +53,7 @@ class Session {
     else if (kind == "host")
       t_ = make_host_transport(*boot_, opt);
     else
-      P2P_FATAL("transport must be 'rccl', 'ipc[:kernel|:sdma|:push]' or 'host'");
+      P2P_FATAL("transport must be 'rccl', 'ipc[:kernel|:sdma|:push|:relay]' or 'host'");
   }
 
   int rank() const { return boot_->rank(); }

@@ -179,7 +179,11 @@ def test_bench_emulated_node(nranks):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nranks),
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", str(nranks),
            "--steps", "14", "--warmup", "7", "--transport", "ipc", "--device", "0", "--sweep-max", "64M",
-           "--latency-iters", "100"]
+           "--latency-iters", "100",
+           # Child processes for the comparisons would double the processes
+           # on the one GPU (8 ranks + 8 children + pytest > the box's 16):
+           # isolate them only with 4 ranks.
+           "--isolate", "1" if nranks == 4 else "0"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT,
                          env=dict(os.environ, P2P_IPC_POOL="1G"))
     progress = "\n".join(l for l in out.stderr.splitlines() if "bench:" in l or "fatal" in l)

@@ -50,6 +50,20 @@ def test_bench_cpu_two_ranks(native):
     sweep = r["extras"]["pair_sweep_0_1"]
     assert [p["bytes"] for p in sweep] == [4096, 16384, 65536, 262144, 1048576]
     assert all(p["gbs"] > 0 for p in sweep)
+    # The untimed transport comparison runs in a child process per rank.
+    cmp_ = r["ipc_transport"]
+    assert cmp_["transport"] == "host" and cmp_["verify_mismatches"] == 0 and cmp_["value_gbs"] > 0, cmp_
+
+
+def test_bench_comparison_failure_is_isolated(native):
+    """A comparison process that dies or hangs (here: killed at its time
+    limit) is reported in the JSON; the headline line is still printed."""
+    out = torchrun(2, ["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "2", "--transport", "host",
+                       "--size", "64K", "--msgs", "1", "--latency-iters", "10", "--sweep", "0", "--extras", "0",
+                       "--ref-iters", "0", "--child-timeout", "0.05"])
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert r["value"] > 0 and "exit status timeout" in r["ipc_transport"]["error"], r["ipc_transport"]
 
 
 def test_session_api_under_torchrun(native):
