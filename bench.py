@@ -469,6 +469,12 @@ def main(argv=None) -> int:
         "reference_semantics": ref,
         "extras": extras,
         "ipc_transport": ipc,
+        "note": ("n_gpus=1 has no inter-GPU link: value is RCCL's on-GPU self send/recv copy (HBM-bound). "
+                 "From n_gpus=2 every step is one tournament round of disjoint pairs, each pair on its own xGMI "
+                 "link, so value grows with the number of pairs (per-GPU rate = one link's bandwidth)")
+                if n == 1 else
+                ("each step is one tournament round: %d disjoint pairs exchange in both directions, one xGMI link "
+                 "per pair; value = all pairs together" % (n // 2)),
     }
     if env.rank == 0:
         log("bench: GB/s matrix (row=src, col=dst), median over steps:")

@@ -71,14 +71,16 @@ def test_bench_all_gpus():
 
 
 @pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
-@pytest.mark.parametrize("engine", ["kernel", "push"])
+@pytest.mark.parametrize("engine", ["kernel", "push", "relay"])
 def test_ipc_engines_all_gpus(exe, engine):
-    """The hand-written data plane across real xGMI links: pull (remote reads)
-    and push (rendezvous + remote writes), verified, plus the device ping-pong
-    matrix."""
+    """The hand-written data plane across real xGMI links: pull (remote reads),
+    push (rendezvous + remote writes) and relay (push + two-hop stripes through
+    GPUs with idle links; the pair mode's single cells use every GPU),
+    verified, plus the device ping-pong matrix."""
     n = _n()
+    modes = "tournament,allpairs,pair" if engine == "relay" else "tournament,allpairs"
     out = subprocess.run([MPIRUN, "-n", str(n), exe, "--transport", "ipc", "--ipc-engine", engine,
-                          "--mode", "tournament,allpairs", "--sizes", "1M,256M", "-n", "8", "--verify",
+                          "--mode", modes, "--sizes", "1M,256M", "-n", "8", "--verify",
                           "--device-latency", "--latency-iters", "200", "--no-compat", "--timeout", "120"],
                          capture_output=True, text=True, timeout=900)
     assert out.returncode == 0, out.stderr[-3000:]
