@@ -151,6 +151,9 @@ def parse_args(argv=None):
     ap.add_argument("--mode", default="tournament", choices=["tournament", "ring", "allpairs", "pair", "self"])
     ap.add_argument("--transport", default="rccl", choices=["rccl", "ipc", "ipc:sdma", "ipc:push", "ipc:relay", "host"],
                     help="rccl (headline) | ipc = one-sided gfx950 copy kernel over hipIpc mappings | host = CPU (tests)")
+    ap.add_argument("--comms", type=int, default=-1,
+                    help="rccl: communicators per rank; the messages of a step are spread over them and their "
+                         "send/recv kernels run side by side (-1: the warmup picks 1 or 4)")
     ap.add_argument("--device", type=int, default=None, help="GPU index (default LOCAL_RANK)")
     ap.add_argument("--latency-iters", type=int, default=300)
     ap.add_argument("--latency-size", default="8")
@@ -208,28 +211,38 @@ def main(argv=None) -> int:
             torch.cuda.synchronize()
 
     size = nat.parse_size(args.size)
-    sess = create_session(args.transport, device=device)
+    headline = args.transport + (":%d" % args.comms if args.transport == "rccl" and args.comms > 1 else "")
+    sess = create_session(headline, device=device)
     if env.rank == 0:
         log("bench: %d rank(s), %s, %s" % (n, sess.transport, sess.device_desc))
     mode = "self" if n == 1 else args.mode
 
-    def make_driver(batch):
-        d = nat.StepDriver(sess, mode, "bi", size, args.msgs, not args.no_verify, bool(batch), bool(args.graph))
-        d.connect()
-        return d
+    # Warmup (untimed, W steps in total) also picks the posting: one group
+    # per step vs one group per message, and (RCCL) one communicator vs
+    # several whose send/recv kernels run side by side.  The W steps are
+    # split between the candidates and the fastest, by the slowest rank's
+    # clock, is timed.  connect() has already established every connection
+    # of every round.
+    comms_choices = ([args.comms] if args.comms > 0 else [1, 4]) if args.transport == "rccl" else [1]
+    batch_choices = [args.batch] if args.batch >= 0 or args.warmup < 2 else [0, 1]
+    if batch_choices == [-1]:
+        batch_choices = [1]
+    choices = [(c, b) for c in comms_choices for b in batch_choices if c == 1 or b == 1 or len(batch_choices) == 1]
+    if args.warmup < len(choices):
+        choices = choices[-1:]
+    sessions = {comms_choices[0]: sess}
 
-    # Warmup (untimed, W steps in total).  With --batch -1 the W steps are
-    # split between the two postings (one group per step vs one group per
-    # message) and the faster one, by the slowest rank's clock, is timed.
-    # connect() has already established every connection of every round.
-    choices = [args.batch] if args.batch >= 0 or args.warmup < 2 else [0, 1]
-    if choices == [-1]:
-        choices = [1]
+    def session_for(c):
+        if c not in sessions:
+            sessions[c] = create_session("rccl:%d" % c if c > 1 else "rccl", device=device)
+        return sessions[c]
+
     tuning = {}
     drivers = {}
     done = 0
-    for i, b in enumerate(choices):
-        d = make_driver(b)
+    for i, (c, b) in enumerate(choices):
+        d = nat.StepDriver(session_for(c), mode, "bi", size, args.msgs, not args.no_verify, bool(b), bool(args.graph))
+        d.connect()
         k = (args.warmup - done) // (len(choices) - i)
         if k > 0:
             barrier()
@@ -237,12 +250,19 @@ def main(argv=None) -> int:
             d.run_steps(done, k)
             d.sync()
             barrier()
-            tuning[b] = sess.allreduce_max(time.perf_counter() - w0) / k
+            tuning[(c, b)] = sessions[c].allreduce_max(time.perf_counter() - w0) / k
             done += k
-        drivers[b] = d
-    batch = min(tuning, key=tuning.get) if len(tuning) == len(choices) else choices[-1]
-    drv = drivers.pop(batch)
-    del drivers, d  # the other posting's buffers go before the timed region
+        drivers[(c, b)] = d
+    comms, batch = min(tuning, key=tuning.get) if len(tuning) == len(choices) else choices[-1]
+    drv = drivers.pop((comms, batch))
+    del drivers, d  # the other postings' buffers go before the timed region
+    sess = sessions[comms]
+    # A single-communicator session stays for the reference-method comparison
+    # (the reference uses one communicator); other candidates are closed.
+    ref_sess = sessions.get(1)
+    for c in list(sessions):
+        if c not in (comms, 1):
+            del sessions[c]
     gpu_sync()
     drv.reset()
 
@@ -300,7 +320,7 @@ def main(argv=None) -> int:
     if n > 1 and args.ref_iters > 0:
         if env.rank == 0:
             log("bench: reference-semantics matrix")
-        r = json.loads(sess.run(mode="pair", dir="uni", bytes=size, iters=args.ref_iters, warmup=0,
+        r = json.loads((ref_sess or sess).run(mode="pair", dir="uni", bytes=size, iters=args.ref_iters, warmup=0,
                                 timing="wallclock", verify=False, warm=False))
         ref = {"cell_gbs_min": round(r["gbs_min"], 3), "cell_gbs_mean": round(r["gbs_mean"], 3),
                "iters": args.ref_iters, "size": size,
@@ -354,7 +374,7 @@ def main(argv=None) -> int:
     # The comparisons below open sessions of their own; close the headline one
     # first so they run alone, as the timed steps did.
     headline_transport = sess.transport
-    del sess
+    del sess, ref_sess, sessions
 
     # (with --transport host the same code path runs on the CPU transport, for tests)
     extra_transport = {"rccl": "ipc", "ipc": "ipc", "ipc:push": "ipc", "ipc:relay": "ipc", "host": "host"}.get(args.transport)
@@ -463,9 +483,9 @@ def main(argv=None) -> int:
         "rank0_step_ms_p50": round(step_ms_med, 4),
         "verify_mismatches": mismatches,
         "transport": headline_transport,
-        "posting": {"batch": bool(batch), "graph": bool(args.graph),
-                    "warmup_ms_per_step": {("batch" if b else "per_message"): round(v * 1e3, 4)
-                                           for b, v in tuning.items()}},
+        "posting": {"batch": bool(batch), "graph": bool(args.graph), "rccl_comms": comms,
+                    "warmup_ms_per_step": {"comms%d_%s" % (c, "batch" if b else "per_message"): round(v * 1e3, 4)
+                                           for (c, b), v in tuning.items()}},
         "reference_semantics": ref,
         "extras": extras,
         "ipc_transport": ipc,

@@ -44,6 +44,8 @@ timing
       --reference        = --timing wallclock --warmup 0 --no-warm --two-streams
                          (the reference's methodology, p2p_matrix.cc:141-267)
       --two-streams      RCCL: receives on a second stream, like the reference's s_1
+      --comms K          RCCL: K communicators per rank on K streams; the i-th message
+                         to / from a peer uses communicator i mod K                [1]
       --no-warm          do not pre-establish connections before timing
   -l, --latency          add a ping-pong latency matrix
       --device-latency   add a device-initiated ping-pong matrix (--transport ipc:
@@ -138,7 +140,7 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
     static const char* kValued[] = {"-m", "--mode", "-d", "--dir", "-b", "--size", "--sizes", "-n", "--iters", "-w",
                                     "--warmup", "--timing", "--latency-size", "--latency-iters", "--verify-impl",
                                     "--transport", "--ipc-engine", "--bootstrap", "--device", "--timeout", "--min-gbs", "--json",
-                                    "--csv", "--trace", "--cells"};
+                                    "--csv", "--trace", "--cells", "--comms"};
     for (const char* v : kValued)
       if (a == v && !has_eq && i + 1 >= argc) {
         missing = true;
@@ -183,6 +185,8 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
       cfg->two_streams = true;
     } else if (a == "--two-streams") {
       cfg->two_streams = true;
+    } else if (a == "--comms") {
+      cfg->comms = std::atoi(next().c_str());
     } else if (a == "--no-warm") {
       cfg->warm_connections = false;
     } else if (a == "-l" || a == "--latency") {
@@ -332,6 +336,7 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
   topt.verify_impl = cfg.verify_impl;
   topt.ipc_engine = cfg.ipc_engine;
   topt.two_streams = cfg.two_streams;
+  topt.rccl_comms = cfg.comms;
   std::unique_ptr<Transport> t = cfg.transport == "host"  ? make_host_transport(boot, topt)
                                  : cfg.transport == "ipc" ? make_ipc_transport(boot, topt)
                                                           : make_rccl_transport(boot, topt);

@@ -46,6 +46,8 @@ class Session {
     // "ipc" or "ipc:kernel" / "ipc:sdma" / "ipc:push"
     std::string kind = transport.substr(0, transport.find(':'));
     if (kind == "ipc" && transport.size() > 4) opt.ipc_engine = transport.substr(4);
+    // "rccl:K": K communicators per rank (TransportOptions::rccl_comms)
+    if (kind == "rccl" && transport.size() > 5) opt.rccl_comms = std::atoi(transport.substr(5).c_str());
     if (kind == "rccl")
       t_ = make_rccl_transport(*boot_, opt);
     else if (kind == "ipc")

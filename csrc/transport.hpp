@@ -124,6 +124,7 @@ struct TransportOptions {
   // through the other GPUs, routing.hpp)
   std::string ipc_engine = "kernel";
   bool two_streams = false;        // RCCL: receives on a second stream (reference layout)
+  int rccl_comms = 1;              // RCCL: communicators per rank, messages spread over them (P2P_RCCL_COMMS)
 };
 
 // HIP + RCCL on the local MI355X.  Defined in transport_rccl.cpp (hipcc).

@@ -17,6 +17,15 @@
 //   * One non-blocking stream by default: the reference's second stream for
 //     the bi direction is joined by the group anyway; --two-streams (implied
 //     by --reference) restores its s_0 / s_1 layout.
+//   * Optionally K communicators (--comms K, TransportOptions::rccl_comms):
+//     the i-th message of at least 1 MiB from a to b goes to communicator
+//     (i + a + b) mod K on both ends (a running count per peer and direction,
+//     so every send meets its receive whatever the group structure; smaller
+//     messages stay on the first), each communicator on its own stream,
+//     forked from and joined back into the main stream by every group.  One
+//     RCCL send/recv kernel uses at most 32 channels (workgroups); several
+//     communicators run several kernels side by side, so the messages of a
+//     group are moved by K x 32 workgroups.
 //   * hipEvents on the stream give GPU-timeline timestamps.
 //   * Payloads are written / checked by the gfx950 kernels in kernels.hip.
 #include <hip/hip_runtime.h>
@@ -51,12 +60,28 @@ class RcclTransport final : public Transport {
     // The reference never checks this and lets cudaSetDevice fail.
     if (device_ >= ndev)
       P2P_FATAL(strfmt("rank %d wants GPU %d but only %d are visible: more ranks per host than GPUs", rank_, device_, ndev));
+    int ncomms = opt.rccl_comms;
+    if (const char* kc = std::getenv("P2P_RCCL_COMMS")) ncomms = std::atoi(kc);
+    P2P_CHECK(ncomms >= 1 && ncomms <= kMaxComms, strfmt("rccl communicators per rank: 1..%d", kMaxComms));
+    P2P_CHECK(ncomms == 1 || !opt.two_streams, "--two-streams (the reference layout) uses one communicator");
     HIPCHECK(hipSetDevice(device_));
     HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     if (opt.two_streams) {
       HIPCHECK(hipStreamCreateWithFlags(&recv_stream_, hipStreamNonBlocking));
       HIPCHECK(hipEventCreateWithFlags(&join_, hipEventDisableTiming));
     }
+    cstreams_.push_back(stream_);
+    for (int j = 1; j < ncomms; ++j) {
+      hipStream_t s;
+      HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      cstreams_.push_back(s);
+      hipEvent_t ev;
+      HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      cjoin_.push_back(ev);
+    }
+    if (ncomms > 1) HIPCHECK(hipEventCreateWithFlags(&fork_, hipEventDisableTiming));
+    send_seq_.assign(static_cast<size_t>(n_), 0);
+    recv_seq_.assign(static_cast<size_t>(n_), 0);
     HIPCHECK(hipMalloc(&acc_, dev::verify_accum_bytes()));
     HIPCHECK(hipHostMalloc(&acc_host_, sizeof(dev::VerifyAccum), hipHostMallocDefault));
 
@@ -64,26 +89,29 @@ class RcclTransport final : public Transport {
     // so stdout keeps the reference's output (P2P_RCCL_BANNER=1 keeps it).
     const char* banner = std::getenv("P2P_RCCL_BANNER");
     StdoutToStderr quiet(!(banner && std::atoi(banner)));
-    ncclUniqueId id;
-    std::memset(&id, 0, sizeof(id));
-    if (rank_ == 0) nccl_ok(ncclGetUniqueId(&id), "ncclGetUniqueId");
-    boot.bcast(&id, sizeof(id), 0);
+    std::vector<ncclUniqueId> ids(static_cast<size_t>(ncomms));
+    std::memset(ids.data(), 0, sizeof(ncclUniqueId) * ids.size());
+    if (rank_ == 0)
+      for (auto& id : ids) nccl_ok(ncclGetUniqueId(&id), "ncclGetUniqueId");
+    boot.bcast(ids.data(), sizeof(ncclUniqueId) * ids.size(), 0);
 
     if (const char* mc = std::getenv("P2P_RCCL_MAX_CHUNK")) max_chunk_ = std::strcmp(mc, "0") ? parse_size(mc) : 0;
+    if (const char* sm = std::getenv("P2P_RCCL_SPLIT_MIN")) split_min_ = parse_size(sm);
     const char* blk = std::getenv("P2P_RCCL_BLOCKING");
     nonblocking_ = opt.nonblocking_init && !(blk && std::atoi(blk));
-    if (nonblocking_) {
-      ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-      cfg.blocking = 0;
-      ncclResult_t r = ncclCommInitRankConfig(&comm_, n_, id, rank_, &cfg);
-      wait_ready(r, "ncclCommInitRankConfig");
-    } else {
-      nccl_ok(ncclCommInitRank(&comm_, n_, id, rank_), "ncclCommInitRank");
+    comms_.assign(static_cast<size_t>(ncomms), nullptr);
+    hook_ = push_abort_hook([this](int) { abort_all(); });
+    // One communicator after the other, in the same order on every rank.
+    for (int j = 0; j < ncomms; ++j) {
+      if (nonblocking_) {
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        ncclResult_t r = ncclCommInitRankConfig(&comms_[static_cast<size_t>(j)], n_, ids[static_cast<size_t>(j)], rank_, &cfg);
+        wait_ready(r, "ncclCommInitRankConfig");
+      } else {
+        nccl_ok(ncclCommInitRank(&comms_[static_cast<size_t>(j)], n_, ids[static_cast<size_t>(j)], rank_), "ncclCommInitRank");
+      }
     }
-    hook_ = push_abort_hook([this](int) {
-      if (comm_) ncclCommAbort(comm_);
-      comm_ = nullptr;
-    });
     hipDeviceProp_t prop;
     HIPCHECK(hipGetDeviceProperties(&prop, device_));
     char pci[64] = {0};
@@ -92,11 +120,13 @@ class RcclTransport final : public Transport {
     ncclGetVersion(&ver);
     desc_ = strfmt("hip:%d %s (%s, %d CUs, %.0f GiB, pci %s) rccl %d", device_, prop.name, prop.gcnArchName,
                    prop.multiProcessorCount, static_cast<double>(prop.totalGlobalMem) / (1ull << 30), pci, ver);
+    if (ncomms > 1) desc_ += strfmt(" x%d comms", ncomms);
   }
 
   ~RcclTransport() override {
     remove_abort_hook(hook_);
     (void)hipStreamSynchronize(stream_);
+    for (size_t j = 1; j < cstreams_.size(); ++j) (void)hipStreamSynchronize(cstreams_[j]);
     // Graphs that captured RCCL work hold references to the communicator's
     // persistent resources: release them before the communicator, or
     // ncclCommDestroy waits for them forever.
@@ -104,16 +134,20 @@ class RcclTransport final : public Transport {
     for (auto g : graphs_) (void)hipGraphDestroy(g);
     execs_.clear();
     graphs_.clear();
-    if (comm_) {
-      // Destroy (unlike the unchecked p2p_matrix.cc:270 we drained first).
-      ncclCommDestroy(comm_);
-      comm_ = nullptr;
-    }
+    for (auto& c : comms_)
+      if (c) {
+        // Destroy (unlike the unchecked p2p_matrix.cc:270 we drained first).
+        ncclCommDestroy(c);
+        c = nullptr;
+      }
     for (auto ev : events_) (void)hipEventDestroy(ev);
+    for (auto ev : cjoin_) (void)hipEventDestroy(ev);
+    if (fork_) (void)hipEventDestroy(fork_);
     if (acc_) (void)hipFree(acc_);
     if (acc_host_) (void)hipHostFree(acc_host_);
     if (recv_stream_) (void)hipStreamDestroy(recv_stream_);
     if (join_) (void)hipEventDestroy(join_);
+    for (size_t j = 1; j < cstreams_.size(); ++j) (void)hipStreamDestroy(cstreams_[j]);
     if (stream_) (void)hipStreamDestroy(stream_);
   }
 
@@ -147,26 +181,37 @@ class RcclTransport final : public Transport {
     return r;
   }
 
-  void group_begin() override { nccl_ok(ncclGroupStart(), "ncclGroupStart"); }
+  void group_begin() override {
+    nccl_ok(ncclGroupStart(), "ncclGroupStart");
+    if (cstreams_.size() > 1) {
+      std::fill(used_.begin(), used_.end(), false);
+      used_.resize(cstreams_.size(), false);
+      forked_ = false;
+    }
+  }
   // Messages above max_chunk_ are posted as several back-to-back ops of at
   // most max_chunk_ bytes inside the same group (matched in order on both
   // sides).  On MI355X, RCCL 2.26/2.27 deliver only half of a single
   // ncclSend/ncclRecv of >= 2 GiB (scripts/rccl_size_probe.py); 1 GiB chunks
   // are exact and run at the same bandwidth.  P2P_RCCL_MAX_CHUNK=0 disables.
   void send(const void* p, size_t bytes, int peer) override {
+    const int j = pick(&send_seq_, peer, bytes);
     const char* c = static_cast<const char*>(p);
     do {
       size_t n = chunk_of(bytes);
-      nccl_ok(ncclSend(c, n, ncclUint8, peer, comm_, stream_), "ncclSend");
+      nccl_ok(ncclSend(c, n, ncclUint8, peer, comms_[static_cast<size_t>(j)], cstreams_[static_cast<size_t>(j)]),
+              "ncclSend");
       c += n;
       bytes -= n;
     } while (bytes);
   }
   void recv(void* p, size_t bytes, int peer) override {
+    const int j = pick(&recv_seq_, peer, bytes);
+    hipStream_t s = j == 0 && recv_stream_ ? recv_stream_ : cstreams_[static_cast<size_t>(j)];
     char* c = static_cast<char*>(p);
     do {
       size_t n = chunk_of(bytes);
-      nccl_ok(ncclRecv(c, n, ncclUint8, peer, comm_, recv_stream_ ? recv_stream_ : stream_), "ncclRecv");
+      nccl_ok(ncclRecv(c, n, ncclUint8, peer, comms_[static_cast<size_t>(j)], s), "ncclRecv");
       c += n;
       bytes -= n;
     } while (bytes);
@@ -185,6 +230,12 @@ class RcclTransport final : public Transport {
       HIPCHECK(hipStreamWaitEvent(stream_, join_, 0));
       recv_on_side_ = false;
     }
+    for (size_t j = 1; j < used_.size(); ++j)
+      if (used_[j]) {
+        HIPCHECK(hipEventRecord(cjoin_[j - 1], cstreams_[j]));
+        HIPCHECK(hipStreamWaitEvent(stream_, cjoin_[j - 1], 0));
+        used_[j] = false;
+      }
   }
 
   int mark() override {
@@ -205,8 +256,10 @@ class RcclTransport final : public Transport {
 
   // hipGraph capture of grouped ncclSend/ncclRecv: a step's back-to-back
   // groups become one graph launch, removing the per-group host launch cost
-  // (microarch price list: ~3.3-3.8 us host launch per kernel eager).
-  bool supports_graphs() const override { return true; }
+  // (microarch price list: ~3.3-3.8 us host launch per kernel eager).  One
+  // communicator only: the replay would have to repeat the per-message
+  // communicator choice exactly.
+  bool supports_graphs() const override { return comms_.size() == 1; }
   void capture_begin() override { HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal)); }
   int capture_end() override {
     hipGraph_t g = nullptr;
@@ -223,6 +276,7 @@ class RcclTransport final : public Transport {
     // Bounded poll instead of hipStreamSynchronize: spins for the first 2 ms
     // (so per-message syncs in wallclock mode are not inflated by sleeps),
     // then backs off; checks RCCL's async error so a failed peer aborts.
+    // Every side stream is joined into the main stream by its group.
     double t0 = now_seconds();
     double deadline = t0 + timeout_;
     for (long it = 0;; ++it) {
@@ -241,41 +295,85 @@ class RcclTransport final : public Transport {
   }
 
   std::string async_error() override {
-    if (!comm_) return "communicator aborted";
-    ncclResult_t st = ncclSuccess;
-    ncclResult_t r = ncclCommGetAsyncError(comm_, &st);
-    if (r != ncclSuccess) return ncclGetErrorString(r);
-    if (st != ncclSuccess && st != ncclInProgress) return ncclGetErrorString(st);
+    for (auto c : comms_) {
+      if (!c) return "communicator aborted";
+      ncclResult_t st = ncclSuccess;
+      ncclResult_t r = ncclCommGetAsyncError(c, &st);
+      if (r != ncclSuccess) return ncclGetErrorString(r);
+      if (st != ncclSuccess && st != ncclInProgress) return ncclGetErrorString(st);
+    }
     return "";
   }
 
  private:
+  static constexpr int kMaxComms = 8;
+
+  // Communicator of the next message to / from `peer`.  Messages below
+  // split_min_ stay on communicator 0 and do not advance the count (both ends
+  // see the same sizes, so they still agree): a small message gains nothing
+  // from a side stream and would pay the fork / join.
+  int pick(std::vector<unsigned long long>* seq, int peer, size_t bytes) {
+    P2P_CHECK(peer >= 0 && peer < n_, "bad peer");
+    if (comms_.size() == 1 || bytes < split_min_) return 0;
+    // (count + sender + receiver): both ends know all three, and the
+    // messages of an all-pairs group spread over the communicators too.
+    const unsigned long long key = (*seq)[static_cast<size_t>(peer)]++ + static_cast<unsigned long long>(rank_ + peer);
+    const int j = static_cast<int>(key % comms_.size());
+    if (j > 0 && !used_[static_cast<size_t>(j)]) {
+      if (!forked_) {
+        // Recorded at the first side-stream use of the group: nothing of the
+        // group is on the main stream before ncclGroupEnd, so the side
+        // streams still follow exactly the work posted before the group.
+        HIPCHECK(hipEventRecord(fork_, stream_));
+        forked_ = true;
+      }
+      HIPCHECK(hipStreamWaitEvent(cstreams_[static_cast<size_t>(j)], fork_, 0));
+      used_[static_cast<size_t>(j)] = true;
+    }
+    return j;
+  }
+
+  void abort_all() {
+    for (auto& c : comms_)
+      if (c) {
+        ncclCommAbort(c);
+        c = nullptr;
+      }
+  }
+
   void nccl_ok(ncclResult_t r, const char* what) {
     if (r == ncclSuccess) return;
-    if (r == ncclInProgress && nonblocking_ && comm_) {
+    if (r == ncclInProgress && nonblocking_ && !comms_.empty()) {
       wait_ready(r, what);
       return;
     }
-    P2P_FATAL(strfmt("rank %d: %s failed: %s (%s)", rank_, what, ncclGetErrorString(r),
-                     comm_ ? ncclGetLastError(comm_) : ""));
+    ncclComm_t c = comms_.empty() ? nullptr : comms_[0];
+    P2P_FATAL(strfmt("rank %d: %s failed: %s (%s)", rank_, what, ncclGetErrorString(r), c ? ncclGetLastError(c) : ""));
   }
 
+  // Polls every communicator created so far until none is in progress.
   void wait_ready(ncclResult_t r, const char* what) {
     double deadline = now_seconds() + timeout_;
     while (r == ncclInProgress) {
       if (now_seconds() > deadline) {
-        if (comm_) ncclCommAbort(comm_);
-        comm_ = nullptr;
+        abort_all();
         P2P_FATAL(strfmt("rank %d: %s did not complete within %.0f s (peer missing?)", rank_, what, timeout_));
       }
       std::this_thread::yield();
-      ncclResult_t st = ncclSuccess;
-      ncclResult_t q = ncclCommGetAsyncError(comm_, &st);
-      if (q != ncclSuccess) {
-        r = q;
-        break;
+      r = ncclSuccess;
+      for (auto c : comms_) {
+        if (!c) continue;
+        ncclResult_t st = ncclSuccess;
+        ncclResult_t q = ncclCommGetAsyncError(c, &st);
+        if (q != ncclSuccess) {
+          r = q;
+          break;
+        }
+        if (st != ncclSuccess) {
+          r = st;
+          if (st != ncclInProgress) break;
+        }
       }
-      r = st;
     }
     if (r != ncclSuccess)
       P2P_FATAL(strfmt("rank %d: %s failed: %s", rank_, what, ncclGetErrorString(r)));
@@ -292,7 +390,14 @@ class RcclTransport final : public Transport {
   size_t max_chunk_ = kDefaultMaxChunk;
   static constexpr size_t kDefaultMaxChunk = size_t{1} << 30;
   size_t chunk_of(size_t bytes) const { return (max_chunk_ && bytes > max_chunk_) ? max_chunk_ : bytes; }
-  ncclComm_t comm_ = nullptr;
+  std::vector<ncclComm_t> comms_;      // comms_[0] on stream_
+  std::vector<hipStream_t> cstreams_;  // stream of each communicator (cstreams_[0] == stream_)
+  std::vector<hipEvent_t> cjoin_;      // per side communicator: joins its stream into stream_
+  hipEvent_t fork_ = nullptr;          // recorded on stream_ by a group's first side-stream message
+  bool forked_ = false;
+  size_t split_min_ = size_t{1} << 20;  // smaller messages stay on communicator 0 (P2P_RCCL_SPLIT_MIN)
+  std::vector<bool> used_;             // side communicators used by the open group
+  std::vector<unsigned long long> send_seq_, recv_seq_;  // messages posted to / from each peer
   std::vector<hipEvent_t> events_;
   std::vector<hipGraph_t> graphs_;
   std::vector<hipGraphExec_t> execs_;

@@ -78,3 +78,12 @@ def test_reference_methodology_two_streams(exe):
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr
     assert "timing=wallclock warmup=0" in out.stdout and "verification: OK" in out.stdout
+
+
+def test_cli_several_communicators(exe):
+    """--comms 4 through the binary: all self-path modes, verified, a size
+    sweep that crosses the 1 MiB spreading threshold."""
+    out = subprocess.run([exe, "--mode", "self,ring,allpairs", "--sizes", "64K:64M:16", "-n", "6", "--comms", "4",
+                          "--verify", "--no-compat"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "verification: OK" in out.stdout

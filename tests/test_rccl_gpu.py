@@ -72,3 +72,25 @@ def test_message_larger_than_4gib(session):
     r = json.loads(session.run(mode="self", dir="uni", bytes=(5 << 30) + 16, iters=2, warmup=1, verify=True))
     ph = r["phases"][0]
     assert ph["mismatches"] == 0 and ph["flows"][0]["gbs"] > 1.0
+
+
+@pytest.mark.parametrize("comms", [2, 4])
+def test_several_communicators(native, comms):
+    """K communicators per rank (messages of >= 1 MiB spread over them, each on
+    its own stream, joined back per group): verified step driver, verified
+    runs incl. a > 1 GiB message (chunks stay on their message's
+    communicator), small-message latency on the first communicator."""
+    s = native.Session(0, 1, device=0, transport="rccl:%d" % comms, timeout_s=120)
+    assert ("x%d comms" % comms) in s.device_desc
+    d = native.StepDriver(s, "self", "bi", 8 << 20, 8, True, True, False)
+    d.connect()
+    d.run_steps(0, 6)
+    d.sync()
+    assert len(d.step_ms()) == 6 and d.verify_last() == 0
+    del d
+    for nbytes in [4096, (4 << 20) + 12, (1 << 30) + 4096]:
+        r = json.loads(s.run(mode="self", dir="bi", bytes=nbytes, iters=3, warmup=1, verify=True))
+        assert r["phases"][0]["mismatches"] == 0
+    lat = json.loads(s.latency(8, 100, 10))
+    assert 0 < lat["pairs"][0]["one_way_us"]["p50"] < 1000
+    del s
