@@ -257,8 +257,9 @@ class RcclTransport final : public Transport {
   // hipGraph capture of grouped ncclSend/ncclRecv: a step's back-to-back
   // groups become one graph launch, removing the per-group host launch cost
   // (microarch price list: ~3.3-3.8 us host launch per kernel eager).  One
-  // communicator only: the replay would have to repeat the per-message
-  // communicator choice exactly.
+  // communicator only: capturing the fork / join of several communicators'
+  // streams crashed inside RCCL 2.26 on MI355X (scripts/comms_probe.py
+  // --graph 1, profiles/r1_comms/).
   bool supports_graphs() const override { return comms_.size() == 1; }
   void capture_begin() override { HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal)); }
   int capture_end() override {
