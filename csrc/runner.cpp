@@ -466,6 +466,13 @@ StepDriver::~StepDriver() = default;
 
 void StepDriver::connect() {
   warm_connections(t_, boot_, sched_, bufs_, std::min<size_t>(bytes_, 4096));
+  // One full step of every phase: small messages may take another path than
+  // the step's (RCCL with several communicators keeps them on the first), so
+  // every connection the timed steps use is made here, not in a timed step.
+  for (const Phase& p : sched_.phases)
+    if (posts_phase(t_, p, t_.rank())) post_step_ops(p);
+  t_.sync();
+  boot_.barrier();
   // Restore the payload the tiny warm-up may have overwritten on receivers.
   if (verify_)
     for (int i = 0; i < bufs_.slots(); ++i) t_.zero(bufs_.recv_buf(i), bytes_);
