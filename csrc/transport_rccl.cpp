@@ -21,8 +21,12 @@
 //     the i-th message of at least 1 MiB from a to b goes to communicator
 //     (i + a + b) mod K on both ends (a running count per peer and direction,
 //     so every send meets its receive whatever the group structure; smaller
-//     messages stay on the first), each communicator on its own stream,
-//     forked from and joined back into the main stream by every group.  One
+//     messages stay on the first), each communicator on its own stream.
+//     Every group joins the side streams back into the main stream (so marks
+//     and syncs cover them); a side stream waits for the main stream only
+//     after it wrote or read payload buffers (fill, zero, verify), so
+//     back-to-back steps flow on the side streams without a per-step
+//     barrier.  One
 //     RCCL send/recv kernel uses at most 32 channels (workgroups); several
 //     communicators run several kernels side by side, so the messages of a
 //     group are moved by K x 32 workgroups.
@@ -80,6 +84,7 @@ class RcclTransport final : public Transport {
       cjoin_.push_back(ev);
     }
     if (ncomms > 1) HIPCHECK(hipEventCreateWithFlags(&fork_, hipEventDisableTiming));
+    stale_.assign(static_cast<size_t>(ncomms), true);
     send_seq_.assign(static_cast<size_t>(n_), 0);
     recv_seq_.assign(static_cast<size_t>(n_), 0);
     HIPCHECK(hipMalloc(&acc_, dev::verify_accum_bytes()));
@@ -166,10 +171,17 @@ class RcclTransport final : public Transport {
   void release(void* p) override {
     if (p) HIPCHECK(hipFree(p));
   }
-  void fill(void* p, size_t bytes, uint64_t seed) override { dev::launch_fill(p, bytes, seed, stream_); }
-  void zero(void* p, size_t bytes) override { HIPCHECK(hipMemsetAsync(p, 0, bytes, stream_)); }
+  void fill(void* p, size_t bytes, uint64_t seed) override {
+    buffer_work();
+    dev::launch_fill(p, bytes, seed, stream_);
+  }
+  void zero(void* p, size_t bytes) override {
+    buffer_work();
+    HIPCHECK(hipMemsetAsync(p, 0, bytes, stream_));
+  }
 
   VerifyResult verify(const void* p, size_t bytes, uint64_t seed) override {
+    buffer_work();
     dev::launch_verify_reset(acc_, stream_);
     dev::launch_verify(p, bytes, seed, acc_, verify_impl_, true, stream_);
     HIPCHECK(hipMemcpyAsync(acc_host_, acc_, sizeof(dev::VerifyAccum), hipMemcpyDeviceToHost, stream_));
@@ -186,7 +198,6 @@ class RcclTransport final : public Transport {
     if (cstreams_.size() > 1) {
       std::fill(used_.begin(), used_.end(), false);
       used_.resize(cstreams_.size(), false);
-      forked_ = false;
     }
   }
   // Messages above max_chunk_ are posted as several back-to-back ops of at
@@ -309,6 +320,13 @@ class RcclTransport final : public Transport {
  private:
   static constexpr int kMaxComms = 8;
 
+  // The main stream is about to touch payload buffers: side streams must wait
+  // for it before their next transfer.
+  void buffer_work() {
+    forked_ = false;
+    std::fill(stale_.begin(), stale_.end(), true);
+  }
+
   // Communicator of the next message to / from `peer`.  Messages below
   // split_min_ stay on communicator 0 and do not advance the count (both ends
   // see the same sizes, so they still agree): a small message gains nothing
@@ -321,14 +339,20 @@ class RcclTransport final : public Transport {
     const unsigned long long key = (*seq)[static_cast<size_t>(peer)]++ + static_cast<unsigned long long>(rank_ + peer);
     const int j = static_cast<int>(key % comms_.size());
     if (j > 0 && !used_[static_cast<size_t>(j)]) {
-      if (!forked_) {
-        // Recorded at the first side-stream use of the group: nothing of the
-        // group is on the main stream before ncclGroupEnd, so the side
-        // streams still follow exactly the work posted before the group.
-        HIPCHECK(hipEventRecord(fork_, stream_));
-        forked_ = true;
+      if (stale_[static_cast<size_t>(j)]) {
+        // The main stream wrote payload / receive buffers (fill, zero) or read
+        // them (verify) since this side stream last waited for it.  The fork
+        // is recorded at the group's first such message: nothing of the group
+        // is on the main stream before ncclGroupEnd.  Between steps that only
+        // move data no fork is needed, so the side streams run back to back
+        // and only the main stream waits for them (its join per group).
+        if (!forked_) {
+          HIPCHECK(hipEventRecord(fork_, stream_));
+          forked_ = true;
+        }
+        HIPCHECK(hipStreamWaitEvent(cstreams_[static_cast<size_t>(j)], fork_, 0));
+        stale_[static_cast<size_t>(j)] = false;
       }
-      HIPCHECK(hipStreamWaitEvent(cstreams_[static_cast<size_t>(j)], fork_, 0));
       used_[static_cast<size_t>(j)] = true;
     }
     return j;
@@ -394,8 +418,9 @@ class RcclTransport final : public Transport {
   std::vector<ncclComm_t> comms_;      // comms_[0] on stream_
   std::vector<hipStream_t> cstreams_;  // stream of each communicator (cstreams_[0] == stream_)
   std::vector<hipEvent_t> cjoin_;      // per side communicator: joins its stream into stream_
-  hipEvent_t fork_ = nullptr;          // recorded on stream_ by a group's first side-stream message
-  bool forked_ = false;
+  hipEvent_t fork_ = nullptr;          // recorded on stream_ when a stale side stream is first used
+  bool forked_ = false;                // fork_ covers the main stream's latest buffer work
+  std::vector<bool> stale_;            // side stream j has not waited for the latest buffer work
   size_t split_min_ = size_t{1} << 20;  // smaller messages stay on communicator 0 (P2P_RCCL_SPLIT_MIN)
   std::vector<bool> used_;             // side communicators used by the open group
   std::vector<unsigned long long> send_seq_, recv_seq_;  // messages posted to / from each peer
