@@ -365,7 +365,18 @@ def main(argv=None) -> int:
             if fl:
                 sweep.append({"bytes": nbytes, "iters": iters, "gbs": round(fl[0]["gbs"], 2),
                               "iter_us_p50": round(fl[0]["iter_us"]["p50"], 2)})
-        extras = dict(extras or {}, pair_sweep_0_1=sweep)
+        extras = dict(extras or {}, pair_sweep_0_1=sweep, pair_sweep_rccl_comms=comms)
+        if ref_sess is not None and ref_sess is not sess:
+            # The same single pair on one communicator (what the sweep above
+            # ran with K of them), at the bench's message size and 256 MiB.
+            one = []
+            for nbytes in (size, 256 << 20):
+                r = json.loads(ref_sess.run(mode="pair", dir="uni", bytes=nbytes, iters=16, warmup=2,
+                                            timing="events", verify=False, warm=False, cells=[(0, 1)]))
+                fl = [f for ph in r["phases"] for f in ph["flows"]]
+                if fl:
+                    one.append({"bytes": nbytes, "gbs": round(fl[0]["gbs"], 2)})
+            extras["pair_0_1_one_comm"] = one
 
     # The same tournament steps through the hand-written data plane (IPC
     # transport: one-sided pulls of hipIpc-mapped peer buffers by the gfx950
