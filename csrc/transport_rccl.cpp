@@ -74,13 +74,13 @@ class RcclTransport final : public Transport {
       HIPCHECK(hipStreamCreateWithFlags(&recv_stream_, hipStreamNonBlocking));
       HIPCHECK(hipEventCreateWithFlags(&join_, hipEventDisableTiming));
     }
-    cstreams_.push_back(stream_);
-    for (int j = 1; j < ncomms; ++j) {
-      hipStream_t s;
-      HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    if (const char* mi = std::getenv("P2P_RCCL_MAIN_IDLE")) main_idle_ = ncomms > 1 && std::atoi(mi) != 0;
+    for (int j = 0; j < ncomms; ++j) {
+      hipStream_t s = stream_;
+      if (j > 0 || main_idle_) HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
       cstreams_.push_back(s);
-      hipEvent_t ev;
-      HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      hipEvent_t ev = nullptr;
+      if (ncomms > 1) HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
       cjoin_.push_back(ev);
     }
     if (ncomms > 1) HIPCHECK(hipEventCreateWithFlags(&fork_, hipEventDisableTiming));
@@ -131,7 +131,8 @@ class RcclTransport final : public Transport {
   ~RcclTransport() override {
     remove_abort_hook(hook_);
     (void)hipStreamSynchronize(stream_);
-    for (size_t j = 1; j < cstreams_.size(); ++j) (void)hipStreamSynchronize(cstreams_[j]);
+    for (auto cs : cstreams_)
+      if (cs != stream_) (void)hipStreamSynchronize(cs);
     // Graphs that captured RCCL work hold references to the communicator's
     // persistent resources: release them before the communicator, or
     // ncclCommDestroy waits for them forever.
@@ -146,13 +147,15 @@ class RcclTransport final : public Transport {
         c = nullptr;
       }
     for (auto ev : events_) (void)hipEventDestroy(ev);
-    for (auto ev : cjoin_) (void)hipEventDestroy(ev);
+    for (auto ev : cjoin_)
+      if (ev) (void)hipEventDestroy(ev);
     if (fork_) (void)hipEventDestroy(fork_);
     if (acc_) (void)hipFree(acc_);
     if (acc_host_) (void)hipHostFree(acc_host_);
     if (recv_stream_) (void)hipStreamDestroy(recv_stream_);
     if (join_) (void)hipEventDestroy(join_);
-    for (size_t j = 1; j < cstreams_.size(); ++j) (void)hipStreamDestroy(cstreams_[j]);
+    for (auto cs : cstreams_)
+      if (cs != stream_) (void)hipStreamDestroy(cs);
     if (stream_) (void)hipStreamDestroy(stream_);
   }
 
@@ -241,10 +244,10 @@ class RcclTransport final : public Transport {
       HIPCHECK(hipStreamWaitEvent(stream_, join_, 0));
       recv_on_side_ = false;
     }
-    for (size_t j = 1; j < used_.size(); ++j)
+    for (size_t j = 0; j < used_.size(); ++j)
       if (used_[j]) {
-        HIPCHECK(hipEventRecord(cjoin_[j - 1], cstreams_[j]));
-        HIPCHECK(hipStreamWaitEvent(stream_, cjoin_[j - 1], 0));
+        HIPCHECK(hipEventRecord(cjoin_[j], cstreams_[j]));
+        HIPCHECK(hipStreamWaitEvent(stream_, cjoin_[j], 0));
         used_[j] = false;
       }
   }
@@ -333,12 +336,15 @@ class RcclTransport final : public Transport {
   // from a side stream and would pay the fork / join.
   int pick(std::vector<unsigned long long>* seq, int peer, size_t bytes) {
     P2P_CHECK(peer >= 0 && peer < n_, "bad peer");
-    if (comms_.size() == 1 || bytes < split_min_) return 0;
-    // (count + sender + receiver): both ends know all three, and the
-    // messages of an all-pairs group spread over the communicators too.
-    const unsigned long long key = (*seq)[static_cast<size_t>(peer)]++ + static_cast<unsigned long long>(rank_ + peer);
-    const int j = static_cast<int>(key % comms_.size());
-    if (j > 0 && !used_[static_cast<size_t>(j)]) {
+    if (comms_.size() == 1) return 0;
+    int j = 0;
+    if (bytes >= split_min_) {
+      // (count + sender + receiver): both ends know all three, and the
+      // messages of an all-pairs group spread over the communicators too.
+      const unsigned long long key = (*seq)[static_cast<size_t>(peer)]++ + static_cast<unsigned long long>(rank_ + peer);
+      j = static_cast<int>(key % comms_.size());
+    }
+    if (cstreams_[static_cast<size_t>(j)] != stream_ && !used_[static_cast<size_t>(j)]) {
       if (stale_[static_cast<size_t>(j)]) {
         // The main stream wrote payload / receive buffers (fill, zero) or read
         // them (verify) since this side stream last waited for it.  The fork
@@ -416,8 +422,9 @@ class RcclTransport final : public Transport {
   static constexpr size_t kDefaultMaxChunk = size_t{1} << 30;
   size_t chunk_of(size_t bytes) const { return (max_chunk_ && bytes > max_chunk_) ? max_chunk_ : bytes; }
   std::vector<ncclComm_t> comms_;      // comms_[0] on stream_
-  std::vector<hipStream_t> cstreams_;  // stream of each communicator (cstreams_[0] == stream_)
-  std::vector<hipEvent_t> cjoin_;      // per side communicator: joins its stream into stream_
+  std::vector<hipStream_t> cstreams_;  // stream of each communicator (cstreams_[0] == stream_ unless main_idle_)
+  std::vector<hipEvent_t> cjoin_;      // per communicator with a side stream: joins it into stream_
+  bool main_idle_ = false;             // P2P_RCCL_MAIN_IDLE=1: communicator 0 on a side stream too
   hipEvent_t fork_ = nullptr;          // recorded on stream_ when a stale side stream is first used
   bool forked_ = false;                // fork_ covers the main stream's latest buffer work
   std::vector<bool> stale_;            // side stream j has not waited for the latest buffer work
