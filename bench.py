@@ -149,7 +149,7 @@ def parse_args(argv=None):
     ap.add_argument("--size", default="32M", help="message size (reference: 32 MiB, p2p_matrix.cc:124)")
     ap.add_argument("--msgs", type=int, default=8, help="messages per direction per step")
     ap.add_argument("--mode", default="tournament", choices=["tournament", "ring", "allpairs", "pair", "self"])
-    ap.add_argument("--transport", default="rccl", choices=["rccl", "ipc", "ipc:sdma", "ipc:push", "ipc:relay", "host"],
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "ipc", "ipc:sdma", "ipc:push", "ipc:relay", "host", "shm"],
                     help="rccl (headline) | ipc = one-sided gfx950 copy kernel over hipIpc mappings | host = CPU (tests)")
     ap.add_argument("--comms", type=int, default=-1,
                     help="rccl: communicators per rank; the messages of a step are spread over them and their "
@@ -197,7 +197,7 @@ def main(argv=None) -> int:
     if args.gpus != env.world:
         log("bench: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, env.world))
     n = env.world
-    use_gpu = args.transport != "host"
+    use_gpu = args.transport not in ("host", "shm")
     device = env.local_rank if args.device is None else args.device
     if use_gpu:
         torch.cuda.set_device(device)
@@ -388,7 +388,8 @@ def main(argv=None) -> int:
     del sess, ref_sess, sessions
 
     # (with --transport host the same code path runs on the CPU transport, for tests)
-    extra_transport = {"rccl": "ipc", "ipc": "ipc", "ipc:push": "ipc", "ipc:relay": "ipc", "host": "host"}.get(args.transport)
+    extra_transport = {"rccl": "ipc", "ipc": "ipc", "ipc:push": "ipc", "ipc:relay": "ipc", "host": "host",
+                       "shm": "host"}.get(args.transport)
 
     def isolated(transport):
         """steps_through() for `transport` in a child process per rank.  The

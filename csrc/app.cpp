@@ -61,6 +61,7 @@ transport / launch
                          ipc   one-sided pulls from hipIpc-mapped peer buffers (gfx950 copy
                                kernel or SDMA); ranks may share a GPU
                          host  CPU sockets, no GPU
+                         shm   CPU shared-memory rings (one host), no GPU
       --ipc-engine E     kernel | sdma | push | relay (for --transport ipc)    [kernel]
                          kernel/sdma: one-sided pull of the peer's send buffer;
                          push: rendezvous + remote writes into the peer's slot;
@@ -272,8 +273,8 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
     return false;
   }
   if (cfg->run.warmup < 0) cfg->run.warmup = 0;
-  if (cfg->transport != "rccl" && cfg->transport != "host" && cfg->transport != "ipc") {
-    std::fprintf(stderr, "p2p_matrix: --transport must be rccl, ipc or host\n");
+  if (cfg->transport != "rccl" && cfg->transport != "host" && cfg->transport != "ipc" && cfg->transport != "shm") {
+    std::fprintf(stderr, "p2p_matrix: --transport must be rccl, ipc, host or shm\n");
     *exit_code = 1;
     return false;
   }
@@ -338,6 +339,7 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
   topt.two_streams = cfg.two_streams;
   topt.rccl_comms = cfg.comms;
   std::unique_ptr<Transport> t = cfg.transport == "host"  ? make_host_transport(boot, topt)
+                                 : cfg.transport == "shm" ? make_shm_transport(boot, topt)
                                  : cfg.transport == "ipc" ? make_ipc_transport(boot, topt)
                                                           : make_rccl_transport(boot, topt);
 
@@ -428,7 +430,7 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
       std::fprintf(out, "\n== p2p_matrix: %d rank(s), transport %s, bootstrap %s, %d host(s) ==\n", n, t->name().c_str(),
                    boot.name().c_str(), pl.num_hosts);
       for (int r = 0; r < n; ++r) std::fprintf(out, "  rank %d: %s\n", r, &all_desc[static_cast<size_t>(r) * sizeof(mine)]);
-      if (t->name() != "host") std::fprintf(out, "%s", topology_report().c_str());
+      if (t->name() != "host" && t->name() != "shm") std::fprintf(out, "%s", topology_report().c_str());
       for (const auto& rec : res.runs) print_extended(out, rec, n);
       print_latency(out, res.latency, n);
       print_latency(out, res.device_latency, n);

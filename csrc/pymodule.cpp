@@ -54,8 +54,10 @@ class Session {
       t_ = make_ipc_transport(*boot_, opt);
     else if (kind == "host")
       t_ = make_host_transport(*boot_, opt);
+    else if (kind == "shm")
+      t_ = make_shm_transport(*boot_, opt);
     else
-      P2P_FATAL("transport must be 'rccl', 'ipc[:kernel|:sdma|:push|:relay]' or 'host'");
+      P2P_FATAL("transport must be 'rccl[:K]', 'ipc[:kernel|:sdma|:push|:relay]', 'host' or 'shm'");
   }
 
   int rank() const { return boot_->rank(); }

@@ -1,7 +1,7 @@
 // Data plane abstraction: buffers, grouped point-to-point ops, timestamps.
 //
 // The measurement engine (runner.cpp) is written against this interface only.
-// Three implementations:
+// Implementations:
 //   * RcclTransport (transport_rccl.cpp, HIP + RCCL): MI355X device buffers in
 //     HBM3E, ncclSend/ncclRecv over xGMI inside ncclGroupStart/End (reference
 //     call sites p2p_matrix.cc:156-169, 211-249), hipEvent timestamps on the
@@ -13,6 +13,9 @@
 //     clock timestamps.  Same schedule, same runner, same report — it is the
 //     CPU plumbing path (BASELINE.json config 1) and what the CPU test tier
 //     drives, so the whole engine is exercised without a GPU.
+//   * ShmTransport (transport_shm.cpp): host memory over lock-free rings in
+//     one POSIX shared-memory segment; the single-host CPU path without
+//     syscalls per message.
 #pragma once
 
 #include <cstddef>
@@ -138,6 +141,10 @@ std::unique_ptr<Transport> make_ipc_transport(Bootstrap& boot, const TransportOp
 
 // Host memory over TCP sockets.  Defined in transport_host.cpp.
 std::unique_ptr<Transport> make_host_transport(Bootstrap& boot, const TransportOptions& opt);
+
+// Host memory over single-producer / single-consumer rings in one POSIX
+// shared-memory segment (all ranks on one host).  Defined in transport_shm.cpp.
+std::unique_ptr<Transport> make_shm_transport(Bootstrap& boot, const TransportOptions& opt);
 
 // CPU reference of the verify kernel, bit-compatible with it (tests and the
 // host transport use it).

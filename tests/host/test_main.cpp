@@ -432,7 +432,7 @@ TEST(test_cli_defaults_match_reference) {
 
 // ------------------------------------------- multi-rank engine (threads) ----
 
-static void run_ranks(int n, const std::function<void(Bootstrap&, Transport&)>& body) {
+static void run_ranks(int n, const std::function<void(Bootstrap&, Transport&)>& body, bool shm = false) {
   TcpListener listener(0, "127.0.0.1");
   int port = listener.port();
   std::vector<std::thread> th;
@@ -441,7 +441,7 @@ static void run_ranks(int n, const std::function<void(Bootstrap&, Transport&)>& 
       auto boot = make_tcp_bootstrap(r, n, "127.0.0.1", port, 60.0, r == 0 ? &listener : nullptr);
       TransportOptions opt;
       opt.timeout_s = 60;
-      auto t = make_host_transport(*boot, opt);
+      auto t = shm ? make_shm_transport(*boot, opt) : make_host_transport(*boot, opt);
       body(*boot, *t);
     });
   }
@@ -488,6 +488,41 @@ TEST(test_engine_all_modes_host_transport) {
     }
     mism[b.rank()] = bad;
   });
+  for (auto v : mism) EXPECT(v == 0);
+}
+
+TEST(test_engine_all_modes_shm_transport) {
+  // Same engine over the shared-memory rings: every mode, odd sizes, and a
+  // message larger than the ring (wraps and back-pressure).
+  const int n = 4;
+  std::vector<uint64_t> mism(n, 1);
+  run_ranks(n, [&](Bootstrap& b, Transport& t) {
+    EXPECT(t.name() == "shm");
+    uint64_t bad = 0;
+    for (size_t bytes : {size_t{4099}, size_t{3} << 20}) {
+      for (Mode m : {Mode::Pair, Mode::Ring, Mode::AllPairs, Mode::Tournament, Mode::Self}) {
+        for (Direction d : {Direction::Uni, Direction::Bi}) {
+          Schedule s = make_schedule(m, d, n);
+          RunConfig cfg;
+          cfg.bytes = bytes;
+          cfg.iters = 2;
+          cfg.warmup = 1;
+          cfg.verify = true;
+          Buffers bufs(t, cfg.bytes, std::max(1, s.max_recv_slots()));
+          auto res = run_schedule(t, b, s, cfg, bufs);
+          for (auto& ph : res) {
+            bad += ph.total_mismatches;
+            if (!ph.idle)
+              for (auto& f : ph.flows) EXPECT(f.verified && f.gbs > 0);
+          }
+        }
+      }
+    }
+    auto lat = run_latency(t, b, 4096, 50, 5, *std::make_unique<Buffers>(t, 4096, 1));
+    EXPECT(lat.size() == 6);
+    for (auto& l : lat) EXPECT(l.one_way_us.p50 > 0);
+    mism[b.rank()] = bad;
+  }, true);
   for (auto v : mism) EXPECT(v == 0);
 }
 

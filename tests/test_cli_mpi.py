@@ -171,3 +171,20 @@ def test_min_gbs_link_check(mpirun, host_build):
     ok = run(mpirun, exe, 3, ["--transport", "host", "--mode", "tournament", "--dir", "uni", "--size", "64K",
                               "-n", "3", "--no-compat", "--min-gbs", "1e-6"])
     assert ok.returncode == 0, ok.stderr
+
+
+def test_shm_transport_all_modes(mpirun, host_build, tmp_path):
+    """The shared-memory CPU transport under mpirun: every mode verified, a
+    message larger than the 1 MiB ring, and the 4 KiB ping-pong (BASELINE
+    config 1's shape) well under the TCP transport's latency."""
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    js = tmp_path / "r.json"
+    out = run(mpirun, exe, 3, ["--transport", "shm", "--mode", "all", "--sizes", "4K,3M", "-n", "3", "--verify",
+                               "--latency", "--latency-size", "4K", "--latency-iters", "500", "--json", str(js)])
+    assert out.returncode == 0, out.stderr
+    assert "verification: OK" in out.stdout and "transport shm" in out.stdout
+    recs = [json.loads(l) for l in js.read_text().splitlines()]
+    assert all(ph["mismatches"] == 0 for r in recs if r["type"] == "run" for ph in r["phases"])
+    lat = [r for r in recs if r["type"] == "latency"][0]
+    assert all(0 < p["one_way_us"]["p50"] < 50 for p in lat["pairs"]), lat
+    assert not [f for f in os.listdir("/dev/shm") if f.startswith("p2p_shm_")], "segment left in /dev/shm"
