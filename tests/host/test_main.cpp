@@ -1,5 +1,6 @@
 // Host-only unit tests (tier T0 in SURVEY.md §4): no GPU, no MPI launcher.
 // Built with g++ by `make host`; run directly or through tests/test_host_unit.py.
+#include <array>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -524,6 +525,77 @@ TEST(test_engine_all_modes_shm_transport) {
     mism[b.rank()] = bad;
   }, true);
   for (auto v : mism) EXPECT(v == 0);
+}
+
+// A transport that asks for the group's global flows (like the IPC relay
+// engine) on top of the host transport: every rank must then post every
+// group, and every rank must see the same flow list in the same order.
+class FlowRecorder final : public Transport {
+ public:
+  explicit FlowRecorder(Transport& t) : t_(&t) {}
+  std::string name() const override { return "flow-recorder"; }
+  int rank() const override { return t_->rank(); }
+  int nranks() const override { return t_->nranks(); }
+  void* alloc(size_t b) override { return t_->alloc(b); }
+  void release(void* p) override { t_->release(p); }
+  void fill(void* p, size_t b, uint64_t s) override { t_->fill(p, b, s); }
+  void zero(void* p, size_t b) override { t_->zero(p, b); }
+  VerifyResult verify(const void* p, size_t b, uint64_t s) override { return t_->verify(p, b, s); }
+  void group_begin() override {
+    ++groups;
+    t_->group_begin();
+  }
+  void send(const void* p, size_t b, int peer) override { t_->send(p, b, peer); }
+  void recv(void* p, size_t b, int peer) override { t_->recv(p, b, peer); }
+  void group_end() override { t_->group_end(); }
+  int mark() override { return t_->mark(); }
+  double elapsed_ms(int a, int b) override { return t_->elapsed_ms(a, b); }
+  void clear_marks() override { t_->clear_marks(); }
+  void sync() override { t_->sync(); }
+  bool wants_group_flows() const override { return true; }
+  void group_flows(const void*, const std::vector<GroupFlow>& flows, size_t bytes) override {
+    for (const auto& f : flows) log.push_back({f.src, f.dst, f.slot, static_cast<int>(bytes & 0x7fffffff)});
+  }
+  std::vector<std::array<int, 4>> log;
+  long groups = 0;
+
+ private:
+  Transport* t_;
+};
+
+TEST(test_group_flows_posted_on_every_rank) {
+  const int n = 4;
+  std::vector<std::vector<std::array<int, 4>>> logs(n);
+  std::vector<long> groups(n, 0);
+  run_ranks(n, [&](Bootstrap& b, Transport& host) {
+    FlowRecorder t(host);
+    uint64_t bad = 0;
+    for (Mode m : {Mode::Pair, Mode::Tournament, Mode::Ring}) {
+      Schedule s = make_schedule(m, Direction::Uni, n);
+      RunConfig cfg;
+      cfg.bytes = 8192;
+      cfg.iters = 2;
+      cfg.warmup = 1;
+      cfg.verify = true;
+      Buffers bufs(t, cfg.bytes, std::max(1, s.max_recv_slots()));
+      for (auto& ph : run_schedule(t, b, s, cfg, bufs)) bad += ph.total_mismatches;
+    }
+    StepDriver d(t, b, make_tournament_schedule(n, Direction::Bi), 4096, 2, true);
+    d.connect();
+    for (long k = 0; k < 3; ++k) d.step(k);
+    d.sync();
+    EXPECT(d.verify_last() == 0 && bad == 0);
+    logs[b.rank()] = t.log;
+    groups[b.rank()] = t.groups;
+    b.barrier();
+  });
+  for (int r = 1; r < n; ++r) {
+    EXPECT(logs[r] == logs[0]);      // same flows, same order, on every rank
+    EXPECT(groups[r] == groups[0]);  // pair cells: idle ranks post too
+  }
+  EXPECT(!logs[0].empty());
+  // Every logged flow's slot is the receiver's index of the sender.
+  for (const auto& e : logs[0]) EXPECT(e[0] != e[1] && e[2] >= 0 && e[2] < n - 1);
 }
 
 TEST(test_wallclock_and_latency_host) {
