@@ -22,11 +22,12 @@
 //     (i + a + b) mod K on both ends (a running count per peer and direction,
 //     so every send meets its receive whatever the group structure; smaller
 //     messages stay on the first), each communicator on its own stream.
-//     Every group joins the side streams back into the main stream (so marks
-//     and syncs cover them); a side stream waits for the main stream only
-//     after it wrote or read payload buffers (fill, zero, verify), so
-//     back-to-back steps flow on the side streams without a per-step
-//     barrier.  One
+//     Streams are synchronised only where data requires it: a side stream
+//     waits for the main stream after the main stream wrote or read payload
+//     buffers (fill, zero, verify), and the main stream waits for the side
+//     streams before such buffer work and at sync().  A mark is an event on
+//     every stream that ran work since the previous mark, so back-to-back
+//     steps flow on all K streams without any per-step barrier.  One
 //     RCCL send/recv kernel uses at most 32 channels (workgroups); several
 //     communicators run several kernels side by side, so the messages of a
 //     group are moved by K x 32 workgroups.
@@ -85,6 +86,8 @@ class RcclTransport final : public Transport {
     }
     if (ncomms > 1) HIPCHECK(hipEventCreateWithFlags(&fork_, hipEventDisableTiming));
     stale_.assign(static_cast<size_t>(ncomms), true);
+    pending_.assign(static_cast<size_t>(ncomms), false);
+    unjoined_.assign(static_cast<size_t>(ncomms), false);
     send_seq_.assign(static_cast<size_t>(n_), 0);
     recv_seq_.assign(static_cast<size_t>(n_), 0);
     HIPCHECK(hipMalloc(&acc_, dev::verify_accum_bytes()));
@@ -147,6 +150,9 @@ class RcclTransport final : public Transport {
         c = nullptr;
       }
     for (auto ev : events_) (void)hipEventDestroy(ev);
+    for (auto& v : side_ev_)
+      for (auto ev : v)
+        if (ev) (void)hipEventDestroy(ev);
     for (auto ev : cjoin_)
       if (ev) (void)hipEventDestroy(ev);
     if (fork_) (void)hipEventDestroy(fork_);
@@ -244,27 +250,58 @@ class RcclTransport final : public Transport {
       HIPCHECK(hipStreamWaitEvent(stream_, join_, 0));
       recv_on_side_ = false;
     }
+    // Side streams are not joined here: each keeps running its
+    // communicator's groups back to back.  A mark records on every stream
+    // used since the previous one; the main stream waits for them only
+    // before it touches buffers and at sync() (join_all).
     for (size_t j = 0; j < used_.size(); ++j)
       if (used_[j]) {
-        HIPCHECK(hipEventRecord(cjoin_[j], cstreams_[j]));
-        HIPCHECK(hipStreamWaitEvent(stream_, cjoin_[j], 0));
+        pending_[j] = true;
+        unjoined_[j] = true;
         used_[j] = false;
       }
   }
 
+  // A mark is an event on the main stream plus one on every side stream
+  // that ran work since the previous mark; it completes when all of them
+  // have.  elapsed_ms(a, b) = (latest event of b) - (latest event of a):
+  // with side streams running ahead of the main one, the time between the
+  // completions of all work up to a and all work up to b.
   int mark() override {
-    if (next_event_ == static_cast<int>(events_.size())) {
+    const size_t m = static_cast<size_t>(next_event_);
+    if (m == events_.size()) {
       hipEvent_t ev;
       HIPCHECK(hipEventCreate(&ev));
       events_.push_back(ev);
+      side_ev_.emplace_back(cstreams_.size(), nullptr);
+      side_rec_.emplace_back(cstreams_.size(), 0);
     }
-    HIPCHECK(hipEventRecord(events_[static_cast<size_t>(next_event_)], stream_));
+    HIPCHECK(hipEventRecord(events_[m], stream_));
+    for (size_t j = 0; j < cstreams_.size(); ++j) {
+      side_rec_[m][j] = 0;
+      if (j < pending_.size() && pending_[j]) {
+        if (!side_ev_[m][j]) HIPCHECK(hipEventCreate(&side_ev_[m][j]));
+        HIPCHECK(hipEventRecord(side_ev_[m][j], cstreams_[j]));
+        side_rec_[m][j] = 1;
+        pending_[j] = false;
+      }
+    }
     return next_event_++;
   }
   double elapsed_ms(int a, int b) override {
-    float ms = 0;
-    HIPCHECK(hipEventElapsedTime(&ms, events_.at(static_cast<size_t>(a)), events_.at(static_cast<size_t>(b))));
-    return ms;
+    const size_t ia = static_cast<size_t>(a), ib = static_cast<size_t>(b);
+    hipEvent_t ref = events_.at(ia);
+    auto since_ref = [&](hipEvent_t e) {
+      float ms = 0;
+      HIPCHECK(hipEventElapsedTime(&ms, ref, e));
+      return static_cast<double>(ms);
+    };
+    double start = 0, end = since_ref(events_.at(ib));
+    for (size_t j = 0; j < cstreams_.size(); ++j) {
+      if (side_rec_[ia][j]) start = std::max(start, since_ref(side_ev_[ia][j]));
+      if (side_rec_[ib][j]) end = std::max(end, since_ref(side_ev_[ib][j]));
+    }
+    return end - start;
   }
   void clear_marks() override { next_event_ = 0; }
 
@@ -291,7 +328,7 @@ class RcclTransport final : public Transport {
     // Bounded poll instead of hipStreamSynchronize: spins for the first 2 ms
     // (so per-message syncs in wallclock mode are not inflated by sleeps),
     // then backs off; checks RCCL's async error so a failed peer aborts.
-    // Every side stream is joined into the main stream by its group.
+    join_all();
     double t0 = now_seconds();
     double deadline = t0 + timeout_;
     for (long it = 0;; ++it) {
@@ -326,8 +363,20 @@ class RcclTransport final : public Transport {
   // The main stream is about to touch payload buffers: side streams must wait
   // for it before their next transfer.
   void buffer_work() {
+    join_all();
     forked_ = false;
     std::fill(stale_.begin(), stale_.end(), true);
+  }
+
+  // The main stream waits for every side stream that ran work since the
+  // last join.
+  void join_all() {
+    for (size_t j = 0; j < unjoined_.size(); ++j)
+      if (unjoined_[j]) {
+        HIPCHECK(hipEventRecord(cjoin_[j], cstreams_[j]));
+        HIPCHECK(hipStreamWaitEvent(stream_, cjoin_[j], 0));
+        unjoined_[j] = false;
+      }
   }
 
   // Communicator of the next message to / from `peer`.  Messages below
@@ -431,7 +480,11 @@ class RcclTransport final : public Transport {
   size_t split_min_ = size_t{1} << 20;  // smaller messages stay on communicator 0 (P2P_RCCL_SPLIT_MIN)
   std::vector<bool> used_;             // side communicators used by the open group
   std::vector<unsigned long long> send_seq_, recv_seq_;  // messages posted to / from each peer
-  std::vector<hipEvent_t> events_;
+  std::vector<hipEvent_t> events_;                 // per mark: on the main stream
+  std::vector<std::vector<hipEvent_t>> side_ev_;   // per mark: on each side stream (lazily created)
+  std::vector<std::vector<char>> side_rec_;        // per mark: side event j recorded by that mark
+  std::vector<bool> pending_;                      // side stream ran work since the last mark
+  std::vector<bool> unjoined_;                     // side stream ran work since the last join
   std::vector<hipGraph_t> graphs_;
   std::vector<hipGraphExec_t> execs_;
   int next_event_ = 0;
