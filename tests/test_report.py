@@ -37,11 +37,14 @@ def test_scaling_table_comparisons_and_cli(tmp_path, capsys):
     from test_nccl_p2p_amd.utils.report import main
     rows = [{"metric": "m", "n_gpus": 2, "value": 100.0, "reference_semantics": {"cell_gbs_mean": 40.0},
              "extras": {"allpairs_1g": {"aggregate_gbs": 300.0}},
-             "ipc_transport": {"value_gbs": 110.0, "device_pingpong_p50_us": 1.5, "push": {"value_gbs": 120.0}}},
+             "posting": {"rccl_comms": 4},
+             "ipc_transport": {"value_gbs": 110.0, "device_pingpong_p50_us": 1.5, "push": {"value_gbs": 120.0},
+                               "relay": {"value_gbs": 150.0, "pair_0_1": [{"bytes": 1, "gbs": 250.5}]}}},
             {"metric": "m", "n_gpus": 8, "value": 380.0, "ipc_transport": {"error": "x"}}]
     t = scaling_table(rows)
-    assert "| 40.0 | 300.0 | 110.0 / 120.0 / - | 1.50 |" in t
-    assert "| 8 | 380.0 | 47.5 |" in t and "95.0%" in t and "- / - / -" in t
+    assert "| 2 | 100.0 | 50.0 | 4 |" in t
+    assert "| 40.0 | 300.0 | 110.0 / 120.0 / - / 150.0 | 250.5 | 1.50 |" in t
+    assert "| 8 | 380.0 | 47.5 | - |" in t and "95.0%" in t and "- / - / - / - | - |" in t
     files = []
     for r in rows:
         f = tmp_path / ("BENCH_%d.json" % r["n_gpus"])
