@@ -70,6 +70,28 @@ def free_port() -> int:
     return port
 
 
+def first_comms(transport: str, comms: int) -> int:
+    """Communicators of the session bench.py opens first (the headline one)."""
+    return comms if transport == "rccl" and comms > 0 else 1
+
+
+def posting_candidates(transport: str, comms: int, batch: int, warmup: int):
+    """(communicators, batch) pairs the warmup steps time against each other.
+
+    comms: > 0 fixed, -1 = RCCL picks between 1 and 4 (other transports: 1).
+    batch: 1 one group per step, 0 one group per message, -1 = both (K = 1
+    only: with several communicators per-message groups cannot overlap).
+    With fewer warmup steps than candidates only the last one is kept."""
+    comms_choices = ([comms] if comms > 0 else [1, 4]) if transport == "rccl" else [1]
+    batch_choices = [batch] if batch >= 0 or warmup < 2 else [0, 1]
+    if batch_choices == [-1]:
+        batch_choices = [1]
+    choices = [(c, b) for c in comms_choices for b in batch_choices if c == 1 or b == 1 or len(batch_choices) == 1]
+    if warmup < len(choices):
+        choices = choices[-1:]
+    return choices
+
+
 def steps_through(nat, isess, args, mode, size, batch, transport):
     """The timed steps again through another transport session (untimed by
     the contract); any error is reported instead of failing the run."""
@@ -223,14 +245,8 @@ def main(argv=None) -> int:
     # split between the candidates and the fastest, by the slowest rank's
     # clock, is timed.  connect() has already established every connection
     # of every round.
-    comms_choices = ([args.comms] if args.comms > 0 else [1, 4]) if args.transport == "rccl" else [1]
-    batch_choices = [args.batch] if args.batch >= 0 or args.warmup < 2 else [0, 1]
-    if batch_choices == [-1]:
-        batch_choices = [1]
-    choices = [(c, b) for c in comms_choices for b in batch_choices if c == 1 or b == 1 or len(batch_choices) == 1]
-    if args.warmup < len(choices):
-        choices = choices[-1:]
-    sessions = {comms_choices[0]: sess}
+    choices = posting_candidates(args.transport, args.comms, args.batch, args.warmup)
+    sessions = {first_comms(args.transport, args.comms): sess}
 
     def session_for(c):
         if c not in sessions:
