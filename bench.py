@@ -253,12 +253,42 @@ def main(argv=None) -> int:
             sessions[c] = create_session("rccl:%d" % c if c > 1 else "rccl", device=device)
         return sessions[c]
 
+    def agree(ok: bool) -> bool:
+        """True when every rank reports ok (the candidates are collective)."""
+        if n == 1:
+            return ok
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
     tuning = {}
     drivers = {}
+    failed = {}
     done = 0
     for i, (c, b) in enumerate(choices):
-        d = nat.StepDriver(session_for(c), mode, "bi", size, args.msgs, not args.no_verify, bool(b), bool(args.graph))
-        d.connect()
+        # A candidate other than the first that fails anywhere (e.g. a second
+        # RCCL communicator on a node where it was never tried) is dropped on
+        # every rank instead of ending the run.
+        d, err = None, None
+        try:
+            d = nat.StepDriver(session_for(c), mode, "bi", size, args.msgs, not args.no_verify, bool(b),
+                               bool(args.graph))
+            d.connect()
+            # Test hook: P2P_BENCH_FAIL_CANDIDATE="<comms>,<batch>" fails that
+            # candidate on the last rank only.
+            if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d" % (c, b) and env.rank == n - 1:
+                raise RuntimeError("injected candidate failure")
+        except Exception as e:  # noqa: BLE001 -- reported, and the candidate is skipped everywhere
+            err = str(e)[:200]
+        if (c, b) != choices[0] and not agree(err is None):
+            failed["comms%d_%s" % (c, "batch" if b else "per_message")] = err or "failed on another rank"
+            log("bench: posting candidate %s dropped: %s" % ((c, b), err or "failed on another rank"))
+            d = None
+            if c != first_comms(args.transport, args.comms):
+                sessions.pop(c, None)
+            continue
+        if err is not None:
+            raise RuntimeError(err)
         k = (args.warmup - done) // (len(choices) - i)
         if k > 0:
             barrier()
@@ -269,7 +299,8 @@ def main(argv=None) -> int:
             tuning[(c, b)] = sessions[c].allreduce_max(time.perf_counter() - w0) / k
             done += k
         drivers[(c, b)] = d
-    comms, batch = min(tuning, key=tuning.get) if len(tuning) == len(choices) else choices[-1]
+    comms, batch = (min(tuning, key=tuning.get) if len(tuning) == len(drivers) and tuning
+                    else list(drivers)[-1])
     drv = drivers.pop((comms, batch))
     del drivers, d  # the other postings' buffers go before the timed region
     sess = sessions[comms]
@@ -511,7 +542,7 @@ def main(argv=None) -> int:
         "rank0_step_ms_p50": round(step_ms_med, 4),
         "verify_mismatches": mismatches,
         "transport": headline_transport,
-        "posting": {"batch": bool(batch), "graph": bool(args.graph), "rccl_comms": comms,
+        "posting": {"batch": bool(batch), "graph": bool(args.graph), "rccl_comms": comms, "dropped": failed or None,
                     "warmup_ms_per_step": {"comms%d_%s" % (c, "batch" if b else "per_message"): round(v * 1e3, 4)
                                            for (c, b), v in tuning.items()}},
         "reference_semantics": ref,

@@ -70,3 +70,15 @@ def test_session_api_under_torchrun(native):
     out = torchrun(3, ["tests/scripts/session_api.py"])
     assert out.returncode == 0, out.stderr[-3000:]
     assert "SESSION API OK" in out.stdout
+
+
+def test_bench_drops_a_failing_posting_candidate(native):
+    """A warmup candidate that fails on one rank is dropped on every rank and
+    reported; the run goes on with the others."""
+    out = torchrun(2, ["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "4", "--transport", "host",
+                       "--size", "64K", "--msgs", "2", "--latency-iters", "10", "--sweep", "0", "--extras", "0",
+                       "--ref-iters", "0", "--ipc-extra", "0"], env={"P2P_BENCH_FAIL_CANDIDATE": "1,1"})
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert r["value"] > 0 and r["posting"]["batch"] is False
+    assert "injected" in r["posting"]["dropped"]["comms1_batch"] or "another rank" in r["posting"]["dropped"]["comms1_batch"]
