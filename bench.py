@@ -355,31 +355,61 @@ def main(argv=None) -> int:
     # the comparisons run on the same memory footprint as the timed steps did.
     del drv
 
-    lat = json.loads(sess.latency(nat.parse_size(args.latency_size), args.latency_iters, min(50, args.latency_iters)))
-    p50s = [p["one_way_us"]["p50"] for p in lat["pairs"]]
-    p50 = statistics.median(p50s) if p50s else None
+    def guarded(name, fn):
+        """Runs one untimed measurement; an error is logged and returned in
+        its place ({"error": ...}), so the headline line is still printed.
+        (The RCCL transport bounds every wait, so a failure on one rank
+        surfaces on the others as an error too, not as a hang.)"""
+        try:
+            return fn()
+        except Exception as e:  # noqa: BLE001 -- reported in the JSON
+            log("bench: %s failed: %s" % (name, e))
+            return {"error": str(e)[:300]}
 
-    # The reference's own methodology on the same communicator, for comparison
+    def latency():
+        lat = json.loads(sess.latency(nat.parse_size(args.latency_size), args.latency_iters,
+                                      min(50, args.latency_iters)))
+        p50s = [p["one_way_us"]["p50"] for p in lat["pairs"]]
+        return statistics.median(p50s) if p50s else None
+
+    p50 = guarded("latency", latency)
+    if isinstance(p50, dict):  # the error is in the log; the field stays null
+        p50 = None
+
+    # The reference's own methodology on one communicator, for comparison
     # (serial ordered pairs, host clock, one stream sync per message,
     # p2p_matrix.cc:141-186), at the same message size.  Untimed by the
     # driver's bracket; skipped on one GPU where the reference measures nothing.
+    def reference_semantics():
+        r = json.loads((ref_sess or sess).run(mode="pair", dir="uni", bytes=size, iters=args.ref_iters, warmup=0,
+                                              timing="wallclock", verify=False, warm=False))
+        return {"cell_gbs_min": round(r["gbs_min"], 3), "cell_gbs_mean": round(r["gbs_mean"], 3),
+                "iters": args.ref_iters, "size": size,
+                "method": "reference semantics: serial ordered pairs, wall clock, stream sync per message",
+                # The reference moves one cell at a time, so its matrix-wide
+                # throughput is its cell rate; ours is `value`.
+                "value_ratio": round(value / r["gbs_mean"], 3) if r["gbs_mean"] > 0 else None}
+
     ref = None
     if n > 1 and args.ref_iters > 0:
         if env.rank == 0:
             log("bench: reference-semantics matrix")
-        r = json.loads((ref_sess or sess).run(mode="pair", dir="uni", bytes=size, iters=args.ref_iters, warmup=0,
-                                timing="wallclock", verify=False, warm=False))
-        ref = {"cell_gbs_min": round(r["gbs_min"], 3), "cell_gbs_mean": round(r["gbs_mean"], 3),
-               "iters": args.ref_iters, "size": size,
-               "method": "reference semantics: serial ordered pairs, wall clock, stream sync per message",
-               # The reference moves one cell at a time, so its matrix-wide
-               # throughput is its cell rate; ours is `value`.
-               "value_ratio": round(value / r["gbs_mean"], 3) if r["gbs_mean"] > 0 else None}
+        ref = guarded("reference semantics", reference_semantics)
 
     # The other BASELINE.json configs, measured after the timed region so one
     # driver run records them too: all-pairs concurrent exchange at 1 GiB
     # (bisection: every GPU drives all N-1 xGMI links at once) and the ring
     # neighbour exchange at 256 MiB (pipeline-parallel hop).
+    def concurrent_config(mode_x, dir_x, nbytes, iters):
+        r = json.loads(sess.run(mode=mode_x, dir=dir_x, bytes=nbytes, iters=iters, warmup=1, timing="events",
+                                verify=False, warm=True))
+        ph = r["phases"][0]
+        flows = [f["gbs"] for f in ph["flows"]]
+        p50s = [f["iter_us"]["p50"] for f in ph["flows"]]
+        return {"aggregate_gbs": round(ph["agg_gbs"], 2), "per_gpu_egress_gbs": round(ph["agg_gbs"] / n, 2),
+                "flow_gbs_min": round(min(flows), 2), "flow_gbs_mean": round(statistics.mean(flows), 2),
+                "iter_us_p50": round(statistics.median(p50s), 1), "bytes": nbytes, "iters": iters}
+
     extras = None
     if n > 1 and args.extras:
         if env.rank == 0:
@@ -387,43 +417,39 @@ def main(argv=None) -> int:
         extras = {}
         for name, mode_x, dir_x, nbytes, iters in (("allpairs_1g", "allpairs", "bi", 1 << 30, 4),
                                                    ("ring_256m", "ring", "uni", 256 << 20, 8)):
-            r = json.loads(sess.run(mode=mode_x, dir=dir_x, bytes=nbytes, iters=iters, warmup=1, timing="events",
-                                    verify=False, warm=True))
-            ph = r["phases"][0]
-            flows = [f["gbs"] for f in ph["flows"]]
-            p50s = [f["iter_us"]["p50"] for f in ph["flows"]]
-            extras[name] = {"aggregate_gbs": round(ph["agg_gbs"], 2),
-                            "per_gpu_egress_gbs": round(ph["agg_gbs"] / n, 2),
-                            "flow_gbs_min": round(min(flows), 2), "flow_gbs_mean": round(statistics.mean(flows), 2),
-                            "iter_us_p50": round(statistics.median(p50s), 1), "bytes": nbytes, "iters": iters}
+            extras[name] = guarded(name, lambda: concurrent_config(mode_x, dir_x, nbytes, iters))
 
     # BASELINE.json config 2: single-pair (0 -> 1) send/recv bandwidth sweep,
     # 4 KiB -> 4 GiB in x4 steps, events-timed, uni-directional; only cell
     # (0, 1) is scheduled, so the other ranks just join the barriers.
-    if n > 1 and args.sweep:
+    def pair_cell(session, nbytes, iters):
+        r = json.loads(session.run(mode="pair", dir="uni", bytes=nbytes, iters=iters, warmup=2, timing="events",
+                                   verify=False, warm=False, cells=[(0, 1)]))
+        fl = [f for ph in r["phases"] for f in ph["flows"]]
+        return fl[0] if fl else None
+
+    def pair_sweep():
         sweep = []
         for nbytes in [b for b in (4096 << (2 * k) for k in range(11)) if b <= nat.parse_size(args.sweep_max)]:
             if env.rank == 0:
                 log("bench: pair sweep %d B" % nbytes)
             iters = max(4, min(200, (2 << 30) // nbytes))
-            r = json.loads(sess.run(mode="pair", dir="uni", bytes=nbytes, iters=iters, warmup=2, timing="events",
-                                    verify=False, warm=False, cells=[(0, 1)]))
-            fl = [f for ph in r["phases"] for f in ph["flows"]]
-            if fl:
-                sweep.append({"bytes": nbytes, "iters": iters, "gbs": round(fl[0]["gbs"], 2),
-                              "iter_us_p50": round(fl[0]["iter_us"]["p50"], 2)})
-        extras = dict(extras or {}, pair_sweep_0_1=sweep, pair_sweep_rccl_comms=comms)
+            f = pair_cell(sess, nbytes, iters)
+            if f:
+                sweep.append({"bytes": nbytes, "iters": iters, "gbs": round(f["gbs"], 2),
+                              "iter_us_p50": round(f["iter_us"]["p50"], 2)})
+        return sweep
+
+    def pair_one_comm():
+        # The same single pair on one communicator (what the sweep ran with K
+        # of them), at the bench's message size and 256 MiB.
+        return [{"bytes": nb, "gbs": round(f["gbs"], 2)}
+                for nb in (size, 256 << 20) for f in [pair_cell(ref_sess, nb, 16)] if f]
+
+    if n > 1 and args.sweep:
+        extras = dict(extras or {}, pair_sweep_0_1=guarded("pair sweep", pair_sweep), pair_sweep_rccl_comms=comms)
         if ref_sess is not None and ref_sess is not sess:
-            # The same single pair on one communicator (what the sweep above
-            # ran with K of them), at the bench's message size and 256 MiB.
-            one = []
-            for nbytes in (size, 256 << 20):
-                r = json.loads(ref_sess.run(mode="pair", dir="uni", bytes=nbytes, iters=16, warmup=2,
-                                            timing="events", verify=False, warm=False, cells=[(0, 1)]))
-                fl = [f for ph in r["phases"] for f in ph["flows"]]
-                if fl:
-                    one.append({"bytes": nbytes, "gbs": round(fl[0]["gbs"], 2)})
-            extras["pair_0_1_one_comm"] = one
+            extras["pair_0_1_one_comm"] = guarded("one-communicator pair", pair_one_comm)
 
     # The same tournament steps through the hand-written data plane (IPC
     # transport: one-sided pulls of hipIpc-mapped peer buffers by the gfx950
