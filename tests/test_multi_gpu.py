@@ -86,3 +86,16 @@ def test_ipc_engines_all_gpus(exe, engine):
     assert out.returncode == 0, out.stderr[-3000:]
     assert "verification: OK" in out.stdout and "FAILED" not in out.stdout
     assert "device-initiated ping-pong" in out.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
+def test_several_communicators_all_gpus(exe):
+    """--comms 4 across real xGMI links: messages >= 1 MiB spread over four
+    RCCL communicators per rank (side streams synchronised only around buffer
+    work), every mode verified."""
+    n = _n()
+    out = subprocess.run([MPIRUN, "-n", str(n), exe, "--comms", "4", "--mode", "pair,tournament,ring,allpairs",
+                          "--sizes", "64K,1M,256M", "-n", "8", "--verify", "--no-compat", "--timeout", "120"],
+                         capture_output=True, text=True, timeout=900)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "verification: OK" in out.stdout and "FAILED" not in out.stdout
