@@ -485,7 +485,7 @@ class IpcTransport final : public Transport {
       if ((it & 255) == 0) {
         double now = now_seconds();
         if (now > deadline) P2P_FATAL(strfmt("rank %d: ipc stream did not finish within %.0f s", rank_, timeout_));
-        if (now - t0 > 2e-3) std::this_thread::sleep_for(std::chrono::microseconds(50));
+        if (now - t0 > 20e-3) std::this_thread::sleep_for(std::chrono::microseconds(20));
       }
     }
   }

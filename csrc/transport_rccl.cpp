@@ -325,7 +325,7 @@ class RcclTransport final : public Transport {
   void graph_launch(int h) override { HIPCHECK(hipGraphLaunch(execs_.at(static_cast<size_t>(h)), stream_)); }
 
   void sync() override {
-    // Bounded poll instead of hipStreamSynchronize: spins for the first 2 ms
+    // Bounded poll instead of hipStreamSynchronize: spins for the first 20 ms
     // (so per-message syncs in wallclock mode are not inflated by sleeps),
     // then backs off; checks RCCL's async error so a failed peer aborts.
     join_all();
@@ -341,7 +341,7 @@ class RcclTransport final : public Transport {
         double now = now_seconds();
         if (now > deadline)
           P2P_FATAL(strfmt("rank %d: stream did not finish within %.0f s (peer hung or dead?); aborting", rank_, timeout_));
-        if (now - t0 > 2e-3) std::this_thread::sleep_for(std::chrono::microseconds(50));
+        if (now - t0 > 20e-3) std::this_thread::sleep_for(std::chrono::microseconds(20));
       }
     }
   }
