@@ -12,17 +12,20 @@ def test_native_host_unit_tests(host_build):
 
 def test_host_code_under_asan_ubsan(mpirun):
     """Host code under AddressSanitizer + UBSan (SURVEY.md §5 race detection /
-    sanitizers row): the unit tests, then a 3-rank MPI job over the TCP
-    transport through every mode with verification and latency."""
+    sanitizers row): the unit tests, then 3-rank MPI jobs over the TCP and
+    shared-memory transports through every mode with verification and
+    latency."""
     from conftest import ROOT
     out = subprocess.run(["make", "-j2", "asan"], cwd=ROOT, capture_output=True, text=True, timeout=900)
     assert out.returncode == 0, out.stdout[-4000:] + out.stderr[-4000:]
     assert " 0 failures" in out.stdout
     exe = os.path.join(ROOT, "build", "asan", "p2p_matrix_host")
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0", UBSAN_OPTIONS="print_stacktrace=1")
-    run = subprocess.run([mpirun, "-n", "3", exe, "--transport", "host", "--mode", "all", "--sizes", "4K:64K:4",
-                          "-n", "3", "--verify", "--latency", "--latency-iters", "20"],
-                         capture_output=True, text=True, timeout=300, env=env)
-    assert run.returncode == 0, run.stderr[-4000:]
-    assert "AddressSanitizer" not in run.stderr and "runtime error" not in run.stderr
-    assert "verification: OK" in run.stdout
+    for transport, sizes in (("host", "4K:64K:4"), ("shm", "4K,2M")):
+        # shm: 2 MiB messages wrap the 1 MiB rings, under the sanitizers too.
+        run = subprocess.run([mpirun, "-n", "3", exe, "--transport", transport, "--mode", "all", "--sizes", sizes,
+                              "-n", "3", "--verify", "--latency", "--latency-iters", "20"],
+                             capture_output=True, text=True, timeout=300, env=env)
+        assert run.returncode == 0, run.stderr[-4000:]
+        assert "AddressSanitizer" not in run.stderr and "runtime error" not in run.stderr
+        assert "verification: OK" in run.stdout
