@@ -22,6 +22,7 @@
 #include "kernels.hpp"
 #include "report.hpp"
 #include "runner.hpp"
+#include "routing.hpp"
 #include "schedule.hpp"
 #include "transport.hpp"
 #include "units.hpp"
@@ -287,6 +288,25 @@ PYBIND11_MODULE(_p2pcore, m) {
   // ---- pure host helpers ----
   m.def("schedule", &schedule_py, py::arg("mode"), py::arg("dir"), py::arg("n"));
   m.def("round_robin_rounds", &round_robin_rounds);
+  m.def("plan_routes",
+        [](int n, const std::vector<std::pair<int, int>>& flows, size_t bytes, size_t min_bytes, double relay_weight,
+           int max_relays) {
+          RouteOptions o;
+          o.min_bytes = min_bytes;
+          o.relay_weight = relay_weight;
+          o.max_relays = max_relays;
+          py::list out;
+          for (const auto& stripes : plan_routes(n, flows, bytes, o)) {
+            py::list l;
+            for (const auto& st : stripes) l.append(py::make_tuple(st.via, st.offset, st.bytes));
+            out.append(l);
+          }
+          return out;
+        },
+        py::arg("n"), py::arg("flows"), py::arg("bytes"), py::arg("min_bytes") = size_t{1} << 20,
+        py::arg("relay_weight") = 1.0, py::arg("max_relays") = -1,
+        "The relay engine's split of each flow of a group: [(via, offset, bytes), ...] per flow, direct stripe "
+        "first (via = -1).");
   m.def("parse_size", &parse_size);
   m.def("parse_size_list", &parse_size_list);
   m.def("format_size", &format_size);

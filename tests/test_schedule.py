@@ -46,3 +46,23 @@ def test_allpairs_slots():
     p = make_schedule("allpairs", "bi", 8)[0]
     assert len(p.flows) == 56
     assert all(sorted(p.recv_from[r]) == [x for x in range(8) if x != r] for r in range(8))
+
+
+def test_plan_routes_binding(native):
+    """The relay engine's route planner through the Python binding: a single
+    pair on 8 ranks gets the direct link + 6 relays in equal 4 KiB-aligned
+    shares; a bi-directional tournament round gets 6 half-share relays per
+    flow; all-pairs is never relayed; small messages stay direct."""
+    size = 32 << 20
+    (single,) = native.plan_routes(8, [(0, 1)], size)
+    assert [s[0] for s in single][0] == -1 and sorted(s[0] for s in single[1:]) == [2, 3, 4, 5, 6, 7]
+    assert sum(s[2] for s in single) == size and all(s[2] % 4096 == 0 for s in single[1:])
+    offs = [s[1] for s in single]
+    assert offs == sorted(offs) and offs[0] == 0
+    rnd = [(0, 1), (1, 0), (2, 3), (3, 2), (4, 5), (5, 4), (6, 7), (7, 6)]
+    for plan in native.plan_routes(8, rnd, size):
+        assert len(plan) == 7 and plan[0][2] > 1.5 * plan[1][2]
+    allp = [(a, b) for a in range(4) for b in range(4) if a != b]
+    assert all(len(p) == 1 for p in native.plan_routes(4, allp, size))
+    assert len(native.plan_routes(8, [(0, 1)], 64 << 10)[0]) == 1
+    assert len(native.plan_routes(8, [(0, 1)], size, max_relays=2)[0]) == 3
