@@ -65,7 +65,10 @@ inline void cpu_relax() {
 class ShmTransport final : public Transport {
  public:
   ShmTransport(Bootstrap& boot, const TransportOptions& opt) : rank_(boot.rank()), n_(boot.size()), timeout_(opt.timeout_s) {
-    ring_ = size_t{1} << 20;
+    // 1 MiB per ordered pair, shrunk so the segment stays within 256 MiB
+    // (n^2 rings) for large jobs; P2P_SHM_RING overrides.
+    const size_t pairs = static_cast<size_t>(n_) * static_cast<size_t>(n_);
+    ring_ = std::max<size_t>(size_t{64} << 10, std::min<size_t>(size_t{1} << 20, (size_t{256} << 20) / pairs) / kLine * kLine);
     if (const char* r = std::getenv("P2P_SHM_RING")) ring_ = parse_size(r);
     P2P_CHECK(ring_ >= 4096 && ring_ % kLine == 0, "P2P_SHM_RING must be a multiple of 64 bytes, at least 4 KiB");
     const uint64_t my_hash = host_hash(real_hostname());
