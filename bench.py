@@ -415,8 +415,11 @@ def main(argv=None) -> int:
         if env.rank == 0:
             log("bench: all-pairs / ring extras")
         extras = {}
+        # ring_hop_8b: the pipeline-parallel hop latency -- every rank sends
+        # 8 bytes to its successor each iteration; iter_us_p50 is the hop time.
         for name, mode_x, dir_x, nbytes, iters in (("allpairs_1g", "allpairs", "bi", 1 << 30, 4),
-                                                   ("ring_256m", "ring", "uni", 256 << 20, 8)):
+                                                   ("ring_256m", "ring", "uni", 256 << 20, 8),
+                                                   ("ring_hop_8b", "ring", "uni", 8, 200)):
             extras[name] = guarded(name, lambda: concurrent_config(mode_x, dir_x, nbytes, iters))
 
     # BASELINE.json config 2: single-pair (0 -> 1) send/recv bandwidth sweep,
