@@ -97,19 +97,20 @@ def scaling_table(results: Iterable[dict]) -> str:
     base = next((r for r in rows if r["n_gpus"] == 2), None)
     out = ["| GPUs | aggregate GB/s | per-GPU GB/s | RCCL comms | matrix min / mean GB/s | p50 latency us "
            "| eff. vs 2 GPUs | reference-method cell GB/s | all-pairs 1 GiB aggregate GB/s "
-           "| IPC pull / push / SDMA / relay GB/s | relay pair 0->1 GB/s | device ping-pong us |",
-           "|---|---|---|---|---|---|---|---|---|---|---|---|"]
+           "| ring hop 8 B us | IPC pull / push / SDMA / relay GB/s | relay pair 0->1 GB/s | device ping-pong us |",
+           "|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
     for r in rows:
         eff = ""
         if base and r["n_gpus"] >= 2:
             eff = "%.1f%%" % (100.0 * r["value"] / r["n_gpus"] / (base["value"] / 2))
         relay = (r.get("ipc_transport") or {}).get("relay") or {}
         relay_pair = (relay.get("pair_0_1") or [{}])[0]
-        out.append("| %d | %.1f | %.1f | %s | %s / %s | %s | %s | %s | %s | %s / %s / %s / %s | %s | %s |" % (
+        out.append("| %d | %.1f | %.1f | %s | %s / %s | %s | %s | %s | %s | %s | %s / %s / %s / %s | %s | %s |" % (
             r["n_gpus"], r["value"], r["value"] / r["n_gpus"], _get(r, "posting", "rccl_comms", fmt="%d"),
             r.get("matrix_gbs_min"), r.get("matrix_gbs_mean"),
             r.get("p50_latency_us"), eff, _get(r, "reference_semantics", "cell_gbs_mean"),
-            _get(r, "extras", "allpairs_1g", "aggregate_gbs"), _get(r, "ipc_transport", "value_gbs"),
+            _get(r, "extras", "allpairs_1g", "aggregate_gbs"), _get(r, "extras", "ring_hop_8b", "iter_us_p50"),
+            _get(r, "ipc_transport", "value_gbs"),
             _get(r, "ipc_transport", "push", "value_gbs"), _get(r, "ipc_transport", "sdma", "value_gbs"),
             _get(r, "ipc_transport", "relay", "value_gbs"), relay_pair.get("gbs", "-"),
             _get(r, "ipc_transport", "device_pingpong_p50_us", fmt="%.2f")))

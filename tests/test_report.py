@@ -43,7 +43,7 @@ def test_scaling_table_comparisons_and_cli(tmp_path, capsys):
             {"metric": "m", "n_gpus": 8, "value": 380.0, "ipc_transport": {"error": "x"}}]
     t = scaling_table(rows)
     assert "| 2 | 100.0 | 50.0 | 4 |" in t
-    assert "| 40.0 | 300.0 | 110.0 / 120.0 / - / 150.0 | 250.5 | 1.50 |" in t
+    assert "| 40.0 | 300.0 | - | 110.0 / 120.0 / - / 150.0 | 250.5 | 1.50 |" in t
     assert "| 8 | 380.0 | 47.5 | - |" in t and "95.0%" in t and "- / - / - / - | - |" in t
     files = []
     for r in rows:
