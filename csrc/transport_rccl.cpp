@@ -105,6 +105,7 @@ class RcclTransport final : public Transport {
 
     if (const char* mc = std::getenv("P2P_RCCL_MAX_CHUNK")) max_chunk_ = std::strcmp(mc, "0") ? parse_size(mc) : 0;
     if (const char* sm = std::getenv("P2P_RCCL_SPLIT_MIN")) split_min_ = parse_size(sm);
+    if (const char* rg = std::getenv("P2P_RCCL_REGISTER")) register_ = std::atoi(rg);
     const char* blk = std::getenv("P2P_RCCL_BLOCKING");
     nonblocking_ = opt.nonblocking_init && !(blk && std::atoi(blk));
     comms_.assign(static_cast<size_t>(ncomms), nullptr);
@@ -143,6 +144,12 @@ class RcclTransport final : public Transport {
     for (auto g : graphs_) (void)hipGraphDestroy(g);
     execs_.clear();
     graphs_.clear();
+    for (auto& r : reg_sets_)
+      for (auto& ch : r.handles)
+        if (ch.first) ncclCommDeregister(ch.first, ch.second);
+    reg_sets_.clear();
+    for (void* p : nccl_alloc_) ncclMemFree(p);
+    nccl_alloc_.clear();
     for (auto& c : comms_)
       if (c) {
         // Destroy (unlike the unchecked p2p_matrix.cc:270 we drained first).
@@ -173,12 +180,50 @@ class RcclTransport final : public Transport {
   bool mem_info(size_t* free_b, size_t* total_b) override { return hipMemGetInfo(free_b, total_b) == hipSuccess; }
   void* alloc(size_t bytes) override {
     void* p = nullptr;
+    if (register_ == 2) {  // RCCL's own allocator (P2P_RCCL_REGISTER=2)
+      nccl_ok(ncclMemAlloc(&p, std::max<size_t>(bytes, 256)), "ncclMemAlloc");
+      nccl_alloc_.push_back(p);
+      return p;
+    }
     hipError_t e = hipMalloc(&p, std::max<size_t>(bytes, 256));
     if (e != hipSuccess) P2P_FATAL(strfmt("hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e)));
     return p;
   }
   void release(void* p) override {
-    if (p) HIPCHECK(hipFree(p));
+    if (!p) return;
+    auto it = std::find(nccl_alloc_.begin(), nccl_alloc_.end(), p);
+    if (it != nccl_alloc_.end()) {
+      nccl_alloc_.erase(it);
+      nccl_ok(ncclMemFree(p), "ncclMemFree");
+      return;
+    }
+    HIPCHECK(hipFree(p));
+  }
+
+  // P2P_RCCL_REGISTER=1|2: every buffer of a set is registered with every
+  // communicator (ncclCommRegister), which lets RCCL move point-to-point
+  // messages between registered user buffers without its staging FIFOs
+  // where it supports that.  An experiment knob (profiles/r1_comms/).
+  void register_buffers(void* send, const std::vector<void*>& recvs, size_t bytes) override {
+    if (!register_) return;
+    RegSet r;
+    r.send = send;
+    std::vector<void*> all{send};
+    all.insert(all.end(), recvs.begin(), recvs.end());
+    for (auto c : comms_)
+      for (void* p : all) {
+        void* h = nullptr;
+        nccl_ok(ncclCommRegister(c, p, bytes, &h), "ncclCommRegister");
+        r.handles.emplace_back(c, h);
+      }
+    reg_sets_.push_back(std::move(r));
+  }
+  void unregister_buffers(void* send) override {
+    auto it = std::find_if(reg_sets_.begin(), reg_sets_.end(), [&](const RegSet& r) { return r.send == send; });
+    if (it == reg_sets_.end()) return;
+    sync();
+    for (auto& ch : it->handles) nccl_ok(ncclCommDeregister(ch.first, ch.second), "ncclCommDeregister");
+    reg_sets_.erase(it);
   }
   void fill(void* p, size_t bytes, uint64_t seed) override {
     buffer_work();
@@ -480,6 +525,13 @@ class RcclTransport final : public Transport {
   size_t split_min_ = size_t{1} << 20;  // smaller messages stay on communicator 0 (P2P_RCCL_SPLIT_MIN)
   std::vector<bool> used_;             // side communicators used by the open group
   std::vector<unsigned long long> send_seq_, recv_seq_;  // messages posted to / from each peer
+  struct RegSet {
+    void* send = nullptr;
+    std::vector<std::pair<ncclComm_t, void*>> handles;
+  };
+  int register_ = 0;                 // P2P_RCCL_REGISTER: 0 off, 1 ncclCommRegister, 2 + ncclMemAlloc
+  std::vector<RegSet> reg_sets_;
+  std::vector<void*> nccl_alloc_;    // buffers from ncclMemAlloc
   std::vector<hipEvent_t> events_;                 // per mark: on the main stream
   std::vector<std::vector<hipEvent_t>> side_ev_;   // per mark: on each side stream (lazily created)
   std::vector<std::vector<char>> side_rec_;        // per mark: side event j recorded by that mark
