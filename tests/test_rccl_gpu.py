@@ -94,3 +94,21 @@ def test_several_communicators(native, comms):
     lat = json.loads(s.latency(8, 100, 10))
     assert 0 < lat["pairs"][0]["one_way_us"]["p50"] < 1000
     del s
+
+
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_buffer_registration_knob(native, monkeypatch, mode):
+    """P2P_RCCL_REGISTER=1 (ncclCommRegister of every buffer) and =2 (plus
+    ncclMemAlloc): verified steps and runs, buffers deregistered and freed
+    when the sets go away."""
+    monkeypatch.setenv("P2P_RCCL_REGISTER", mode)
+    s = native.Session(0, 1, device=0, transport="rccl:2", timeout_s=120)
+    d = native.StepDriver(s, "self", "bi", 4 << 20, 4, True, True, False)
+    d.connect()
+    d.run_steps(0, 4)
+    d.sync()
+    assert d.verify_last() == 0
+    del d
+    r = json.loads(s.run(mode="self", dir="bi", bytes=(2 << 20) + 4, iters=3, warmup=1, verify=True))
+    assert r["phases"][0]["mismatches"] == 0
+    del s
