@@ -280,7 +280,10 @@ def main(argv=None) -> int:
                 raise RuntimeError("injected candidate failure")
         except Exception as e:  # noqa: BLE001 -- reported, and the candidate is skipped everywhere
             err = str(e)[:200]
-        if (c, b) != choices[0] and not agree(err is None):
+        # The headline session's first candidate must work; anything else
+        # (another communicator count, another posting) may be dropped.
+        droppable = (c, b) != choices[0] or c != first_comms(args.transport, args.comms)
+        if droppable and not agree(err is None):
             failed["comms%d_%s" % (c, "batch" if b else "per_message")] = err or "failed on another rank"
             log("bench: posting candidate %s dropped: %s" % ((c, b), err or "failed on another rank"))
             d = None
@@ -299,6 +302,11 @@ def main(argv=None) -> int:
             tuning[(c, b)] = sessions[c].allreduce_max(time.perf_counter() - w0) / k
             done += k
         drivers[(c, b)] = d
+    if not drivers:  # every candidate was dropped: the headline session, one group per step
+        c0 = first_comms(args.transport, args.comms)
+        d = nat.StepDriver(sessions[c0], mode, "bi", size, args.msgs, not args.no_verify, True, bool(args.graph))
+        d.connect()
+        drivers[(c0, 1)] = d
     comms, batch = (min(tuning, key=tuning.get) if len(tuning) == len(drivers) and tuning
                     else list(drivers)[-1])
     drv = drivers.pop((comms, batch))

@@ -82,3 +82,4 @@ def test_bench_drops_a_failing_posting_candidate(native):
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert r["value"] > 0 and r["posting"]["batch"] is False
     assert "injected" in r["posting"]["dropped"]["comms1_batch"] or "another rank" in r["posting"]["dropped"]["comms1_batch"]
+
