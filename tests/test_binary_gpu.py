@@ -87,3 +87,17 @@ def test_cli_several_communicators(exe):
                           "--verify", "--no-compat"], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     assert "verification: OK" in out.stdout
+
+
+def test_bench_drops_a_failing_communicator_candidate():
+    """If the 4-communicator candidate fails (injected), bench.py reports it
+    in posting.dropped and times the single-communicator posting instead; with
+    one warmup step (only that candidate tried) it falls back the same way."""
+    for warmup in ("1", "4"):
+        out = subprocess.run([sys.executable, "bench.py", "--steps", "4", "--warmup", warmup, "--latency-iters", "20"],
+                             capture_output=True, text=True, timeout=600, cwd=ROOT,
+                             env=dict(os.environ, P2P_BENCH_FAIL_CANDIDATE="4,1"))
+        assert out.returncode == 0, out.stderr[-3000:]
+        r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+        assert r["posting"]["rccl_comms"] == 1 and "injected" in r["posting"]["dropped"]["comms4_batch"]
+        assert r["verify_mismatches"] == 0 and r["value"] > 10
