@@ -374,9 +374,13 @@ def main(argv=None) -> int:
             log("bench: %s failed: %s" % (name, e))
             return {"error": str(e)[:300]}
 
+    lat_matrix = [[0.0] * n for _ in range(n)]
+
     def latency():
         lat = json.loads(sess.latency(nat.parse_size(args.latency_size), args.latency_iters,
                                       min(50, args.latency_iters)))
+        for p in lat["pairs"]:  # a < b; the ping-pong's one-way time holds for both directions
+            lat_matrix[p["a"]][p["b"]] = lat_matrix[p["b"]][p["a"]] = round(p["one_way_us"]["p50"], 3)
         p50s = [p["one_way_us"]["p50"] for p in lat["pairs"]]
         return statistics.median(p50s) if p50s else None
 
@@ -573,6 +577,10 @@ def main(argv=None) -> int:
         "matrix_gbs_min": round(min(offdiag), 3) if offdiag else None,
         "matrix_gbs_mean": round(statistics.mean(offdiag), 3) if offdiag else None,
         "matrix_cells": "%d/%d" % (covered, expected),
+        # BASELINE config 3: the full N x N pairwise matrices (row = sender;
+        # GB/s per direction, median over steps; p50 one-way latency, us).
+        "matrix_gbs": [[round(v, 2) for v in row] for row in matrix],
+        "latency_p50_us_matrix": lat_matrix,
         "p50_latency_us": round(p50, 3) if p50 is not None else None,
         "latency_bytes": nat.parse_size(args.latency_size),
         "per_gpu_gbs": round(value / n, 3),

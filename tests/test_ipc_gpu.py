@@ -191,6 +191,9 @@ def test_bench_emulated_node(nranks):
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert r["n_gpus"] == nranks and r["verify_mismatches"] == 0
     assert r["matrix_cells"] == "%d/%d" % (nranks * (nranks - 1), nranks * (nranks - 1))
+    m, lat = r["matrix_gbs"], r["latency_p50_us_matrix"]
+    assert len(m) == nranks and all(m[a][b] > 0 for a in range(nranks) for b in range(nranks) if a != b)
+    assert all(lat[a][b] > 0 for a in range(nranks) for b in range(nranks) if a != b)
     assert r["reference_semantics"]["cell_gbs_mean"] > 0
     assert r["extras"]["allpairs_1g"]["aggregate_gbs"] > 0 and r["extras"]["ring_256m"]["aggregate_gbs"] > 0
     assert len(r["extras"]["pair_sweep_0_1"]) == 8  # 4 KiB .. 64 MiB in x4 steps

@@ -47,6 +47,8 @@ def test_bench_cpu_two_ranks(native):
     assert r["n_gpus"] == 2 and r["steps"] == 4 and r["value"] > 0
     assert r["verify_mismatches"] == 0
     assert r["matrix_cells"] == "2/2"
+    assert r["matrix_gbs"][0][1] > 0 and r["matrix_gbs"][1][0] > 0 and r["matrix_gbs"][0][0] == 0
+    assert r["latency_p50_us_matrix"][0][1] > 0 and r["latency_p50_us_matrix"][0][1] == r["latency_p50_us_matrix"][1][0]
     sweep = r["extras"]["pair_sweep_0_1"]
     assert [p["bytes"] for p in sweep] == [4096, 16384, 65536, 262144, 1048576]
     assert all(p["gbs"] > 0 for p in sweep)
