@@ -101,6 +101,8 @@ class Session {
     return latency_to_json(lat, world());
   }
 
+  uint64_t fuzz(int rounds, uint64_t seed, size_t max_bytes) { return fuzz_transport(*t_, *boot_, rounds, seed, max_bytes); }
+
   std::string device_latency(size_t bytes, int iters, int warmup) {
     return latency_to_json(run_device_latency(*t_, *boot_, bytes, iters, warmup), world());
   }
@@ -210,7 +212,10 @@ PYBIND11_MODULE(_p2pcore, m) {
       .def("device_latency", &Session::device_latency, py::arg("bytes") = 8, py::arg("iters") = 1000,
            py::arg("warmup") = 100, py::call_guard<py::gil_scoped_release>())
       .def("latency", &Session::latency, py::arg("bytes") = 8, py::arg("iters") = 1000, py::arg("warmup") = 100,
-           py::call_guard<py::gil_scoped_release>());
+           py::call_guard<py::gil_scoped_release>())
+      .def("fuzz", &Session::fuzz, py::arg("rounds") = 20, py::arg("seed") = 1, py::arg("max_bytes") = size_t{4} << 20,
+           py::call_guard<py::gil_scoped_release>(),
+           "Random groups of verified messages through the transport (collective); returns mismatching words.");
 
   py::class_<PyStepDriver>(m, "StepDriver")
       .def(py::init<std::shared_ptr<Session>, const std::string&, const std::string&, size_t, int, bool, bool, bool>(),

@@ -445,6 +445,61 @@ std::vector<LatencyResult> run_device_latency(Transport& t, Bootstrap& boot, siz
   return out;
 }
 
+// ----------------------------------------------------------------- fuzz ----
+
+uint64_t fuzz_transport(Transport& t, Bootstrap& boot, int rounds, uint64_t seed, size_t max_bytes) {
+  const int n = boot.size(), me = boot.rank();
+  P2P_CHECK(max_bytes >= 16, "fuzz: max_bytes >= 16");
+  uint64_t rng = seed;
+  auto next = [&]() {
+    rng = rng * 6364136223846793005ull + 1442695040888963407ull;
+    return static_cast<uint64_t>(rng >> 33);
+  };
+  uint64_t mism = 0;
+  struct Msg {
+    int src, dst;
+    size_t bytes;
+  };
+  for (int r = 0; r < rounds; ++r) {
+    std::vector<Msg> plan;
+    const int count = 1 + static_cast<int>(next() % 12);
+    for (int k = 0; k < count; ++k) {
+      Msg m{static_cast<int>(next() % static_cast<uint64_t>(n)), static_cast<int>(next() % static_cast<uint64_t>(n)), 0};
+      const uint64_t kind = next() % 4;  // tiny, one page, odd, large
+      m.bytes = kind == 0 ? 1 + next() % 16 : kind == 1 ? 4096 : kind == 2 ? 1 + next() % (max_bytes / 4) : max_bytes / 2 + next() % (max_bytes / 2);
+      m.bytes = std::min(std::max<size_t>(m.bytes, 1), max_bytes);
+      plan.push_back(m);
+    }
+    auto seed_of = [&](size_t k) { return payload_seed(plan[k].src, plan[k].bytes, static_cast<uint64_t>(r) * 1000 + k); };
+    std::vector<void*> sends;
+    std::vector<std::pair<void*, size_t>> recvs;
+    for (size_t k = 0; k < plan.size(); ++k)
+      if (plan[k].src == me) {
+        sends.push_back(t.alloc(plan[k].bytes));
+        t.fill(sends.back(), plan[k].bytes, seed_of(k));
+      }
+    for (size_t k = 0; k < plan.size(); ++k)
+      if (plan[k].dst == me) {
+        recvs.emplace_back(t.alloc(plan[k].bytes), k);
+        t.zero(recvs.back().first, plan[k].bytes);
+      }
+    t.group_begin();
+    size_t si = 0;
+    for (size_t k = 0; k < plan.size(); ++k)
+      if (plan[k].src == me) t.send(sends[si++], plan[k].bytes, plan[k].dst);
+    for (auto& rv : recvs) t.recv(rv.first, plan[rv.second].bytes, plan[rv.second].src);
+    t.group_end();
+    t.sync();
+    for (auto& rv : recvs) {
+      mism += t.verify(rv.first, plan[rv.second].bytes, seed_of(rv.second)).mismatches;
+      t.release(rv.first);
+    }
+    for (void* p : sends) t.release(p);
+    boot.barrier();
+  }
+  return mism;
+}
+
 // ---------------------------------------------------------- StepDriver ----
 
 StepDriver::StepDriver(Transport& t, Bootstrap& boot, Schedule sched, size_t bytes, int msgs, bool verify, uint64_t salt,

@@ -133,6 +133,15 @@ std::vector<LatencyResult> run_latency(Transport& t, Bootstrap& boot, size_t byt
 // run_latency; payloads are rounded up to 16 bytes (at most 64 KiB).
 std::vector<LatencyResult> run_device_latency(Transport& t, Bootstrap& boot, size_t bytes, int iters, int warmup);
 
+// ---- transport fuzz (tests) ----
+// `rounds` groups of random messages (src, dst, size <= max_bytes; self
+// messages and repeated pairs included) drawn from `seed`, identical on every
+// rank; each rank posts its sends and receives in plan order inside one group,
+// then checks every received message against the sender's PRNG stream.
+// Collective; returns this rank's mismatching words.  Transports that only
+// move registered buffer sets (IPC) are not supported.
+uint64_t fuzz_transport(Transport& t, Bootstrap& boot, int rounds, uint64_t seed, size_t max_bytes);
+
 // ---- step driver (used by bench.py): one phase per step, no host syncs ----
 // Step k posts `msgs` iterations of phase (k mod phases) with a timestamp
 // around them; nothing blocks until sync().  Per-step durations are read

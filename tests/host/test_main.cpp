@@ -598,6 +598,18 @@ TEST(test_group_flows_posted_on_every_rank) {
   for (const auto& e : logs[0]) EXPECT(e[0] != e[1] && e[2] >= 0 && e[2] < n - 1);
 }
 
+// Transport-level fuzz (runner.cpp fuzz_transport): random groups of
+// messages, self and repeated pairs included, sizes up to twice the shm ring.
+static void fuzz_transport_test(bool shm) {
+  const int n = 4;
+  std::vector<uint64_t> bad(n, 1);
+  run_ranks(n, [&](Bootstrap& b, Transport& t) { bad[b.rank()] = fuzz_transport(t, b, 40, 0x5EED, size_t{2} << 20); }, shm);
+  for (auto v : bad) EXPECT(v == 0);
+}
+
+TEST(test_fuzz_host_transport) { fuzz_transport_test(false); }
+TEST(test_fuzz_shm_transport) { fuzz_transport_test(true); }
+
 TEST(test_wallclock_and_latency_host) {
   run_ranks(3, [&](Bootstrap& b, Transport& t) {
     Schedule s = make_pair_schedule(3, Direction::Bi);

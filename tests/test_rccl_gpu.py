@@ -112,3 +112,15 @@ def test_buffer_registration_knob(native, monkeypatch, mode):
     r = json.loads(s.run(mode="self", dir="bi", bytes=(2 << 20) + 4, iters=3, warmup=1, verify=True))
     assert r["phases"][0]["mismatches"] == 0
     del s
+
+
+@pytest.mark.parametrize("transport,chunk", [("rccl", "0"), ("rccl:4", "0"), ("rccl:4", "1M")])
+def test_fuzz_random_groups(native, monkeypatch, transport, chunk):
+    """Random groups of self messages (1 B .. 4 MiB, several per group)
+    through one or four communicators; with P2P_RCCL_MAX_CHUNK=1M the larger
+    messages go out as several chunks on their message's communicator."""
+    if chunk != "0":
+        monkeypatch.setenv("P2P_RCCL_MAX_CHUNK", chunk)
+    s = native.Session(0, 1, device=0, transport=transport, timeout_s=120)
+    assert s.fuzz(rounds=30, seed=7, max_bytes=4 << 20) == 0
+    del s
