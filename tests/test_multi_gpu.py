@@ -99,3 +99,16 @@ def test_several_communicators_all_gpus(exe):
                          capture_output=True, text=True, timeout=900)
     assert out.returncode == 0, out.stderr[-3000:]
     assert "verification: OK" in out.stdout and "FAILED" not in out.stdout
+
+
+def test_fuzz_all_gpus():
+    """Random verified message groups across every GPU through RCCL with one
+    and with four communicators per rank."""
+    n = _n()
+    for transport in ("rccl", "rccl:4"):
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "tests/scripts/fuzz_session.py",
+               transport, "20"]
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT)
+        assert out.returncode == 0, out.stderr[-3000:]
+        assert "FUZZ %s mismatches 0" % transport in out.stdout

@@ -85,3 +85,12 @@ def test_bench_drops_a_failing_posting_candidate(native):
     assert r["value"] > 0 and r["posting"]["batch"] is False
     assert "injected" in r["posting"]["dropped"]["comms1_batch"] or "another rank" in r["posting"]["dropped"]["comms1_batch"]
 
+
+
+def test_fuzz_session_over_shm_and_host(native):
+    """Random verified message groups, 3 processes, over the shared-memory and
+    TCP transports through the Python session."""
+    for transport in ("shm", "host"):
+        out = torchrun(3, ["tests/scripts/fuzz_session.py", transport, "15"])
+        assert out.returncode == 0, out.stderr[-3000:]
+        assert "FUZZ %s mismatches 0" % transport in out.stdout
