@@ -450,6 +450,12 @@ std::vector<LatencyResult> run_device_latency(Transport& t, Bootstrap& boot, siz
 uint64_t fuzz_transport(Transport& t, Bootstrap& boot, int rounds, uint64_t seed, size_t max_bytes) {
   const int n = boot.size(), me = boot.rank();
   P2P_CHECK(max_bytes >= 16, "fuzz: max_bytes >= 16");
+  constexpr int kMaxMsgs = 12;
+  // One buffer set for the whole run, like a schedule's: every message a rank
+  // sends in a round is a prefix of its send buffer (filled with the round's
+  // stream), and the i-th message it receives lands in slot i.  This is what
+  // the one-sided transports (IPC pull / push / relay) can move.
+  Buffers bufs(t, max_bytes, kMaxMsgs);
   uint64_t rng = seed;
   auto next = [&]() {
     rng = rng * 6364136223846793005ull + 1442695040888963407ull;
@@ -459,43 +465,40 @@ uint64_t fuzz_transport(Transport& t, Bootstrap& boot, int rounds, uint64_t seed
   struct Msg {
     int src, dst;
     size_t bytes;
+    int slot;  // receive slot on dst
   };
   for (int r = 0; r < rounds; ++r) {
     std::vector<Msg> plan;
-    const int count = 1 + static_cast<int>(next() % 12);
+    std::vector<int> slots(static_cast<size_t>(n), 0);
+    const int count = 1 + static_cast<int>(next() % kMaxMsgs);
     for (int k = 0; k < count; ++k) {
-      Msg m{static_cast<int>(next() % static_cast<uint64_t>(n)), static_cast<int>(next() % static_cast<uint64_t>(n)), 0};
+      Msg m{static_cast<int>(next() % static_cast<uint64_t>(n)), static_cast<int>(next() % static_cast<uint64_t>(n)), 0, 0};
       const uint64_t kind = next() % 4;  // tiny, one page, odd, large
       m.bytes = kind == 0 ? 1 + next() % 16 : kind == 1 ? 4096 : kind == 2 ? 1 + next() % (max_bytes / 4) : max_bytes / 2 + next() % (max_bytes / 2);
       m.bytes = std::min(std::max<size_t>(m.bytes, 1), max_bytes);
+      m.slot = slots[static_cast<size_t>(m.dst)]++;
       plan.push_back(m);
     }
-    auto seed_of = [&](size_t k) { return payload_seed(plan[k].src, plan[k].bytes, static_cast<uint64_t>(r) * 1000 + k); };
-    std::vector<void*> sends;
-    std::vector<std::pair<void*, size_t>> recvs;
-    for (size_t k = 0; k < plan.size(); ++k)
-      if (plan[k].src == me) {
-        sends.push_back(t.alloc(plan[k].bytes));
-        t.fill(sends.back(), plan[k].bytes, seed_of(k));
-      }
-    for (size_t k = 0; k < plan.size(); ++k)
-      if (plan[k].dst == me) {
-        recvs.emplace_back(t.alloc(plan[k].bytes), k);
-        t.zero(recvs.back().first, plan[k].bytes);
-      }
+    auto seed_of = [&](int src) { return payload_seed(src, max_bytes, static_cast<uint64_t>(r) * 1000 + 7); };
+    bool sends = false;
+    for (const Msg& m : plan) sends = sends || m.src == me;
+    if (sends) t.fill(bufs.send_buf(), max_bytes, seed_of(me));
+    for (const Msg& m : plan)
+      if (m.dst == me) t.zero(bufs.recv_buf(m.slot), m.bytes);
+    t.sync();
+    boot.barrier();  // every payload written and every slot poisoned before anyone moves data
     t.group_begin();
-    size_t si = 0;
-    for (size_t k = 0; k < plan.size(); ++k)
-      if (plan[k].src == me) t.send(sends[si++], plan[k].bytes, plan[k].dst);
-    for (auto& rv : recvs) t.recv(rv.first, plan[rv.second].bytes, plan[rv.second].src);
+    if (t.wants_group_flows())
+      for (const Msg& m : plan) t.group_flows(bufs.send_buf(), {Transport::GroupFlow{m.src, m.dst, m.slot}}, m.bytes);
+    for (const Msg& m : plan)
+      if (m.src == me) t.send_to_slot(bufs.send_buf(), m.bytes, m.dst, m.slot);
+    for (const Msg& m : plan)
+      if (m.dst == me) t.recv(bufs.recv_buf(m.slot), m.bytes, m.src);
     t.group_end();
     t.sync();
-    for (auto& rv : recvs) {
-      mism += t.verify(rv.first, plan[rv.second].bytes, seed_of(rv.second)).mismatches;
-      t.release(rv.first);
-    }
-    for (void* p : sends) t.release(p);
-    boot.barrier();
+    for (const Msg& m : plan)
+      if (m.dst == me) mism += t.verify(bufs.recv_buf(m.slot), m.bytes, seed_of(m.src)).mismatches;
+    boot.barrier();  // nobody refills its send buffer while a peer may still read it
   }
   return mism;
 }

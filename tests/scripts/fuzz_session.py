@@ -14,10 +14,14 @@ from test_nccl_p2p_amd.parallel.session import create_session  # noqa: E402
 def main():
     transport = sys.argv[1] if len(sys.argv) > 1 else "host"
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    device = None
     if not transport.startswith(("host", "shm")):
         import torch
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)))
-    sess = create_session(transport, timeout_s=120)
+        # P2P_FUZZ_DEVICE pins every rank to one GPU (the IPC transport's
+        # several-processes-per-GPU emulation); default: LOCAL_RANK.
+        device = int(os.environ.get("P2P_FUZZ_DEVICE", os.environ.get("LOCAL_RANK", 0)))
+        torch.cuda.set_device(device)
+    sess = create_session(transport, device=device, timeout_s=120)
     bad = sess.fuzz(rounds=rounds, seed=11, max_bytes=8 << 20)
     total = sess.allreduce_sum(float(bad))
     if sess.rank == 0:

@@ -204,3 +204,15 @@ def test_bench_emulated_node(nranks):
     relay = ipc["relay"]
     assert relay["verify_mismatches"] == 0 and relay["value_gbs"] > 0, relay
     assert [p["mismatches"] for p in relay["pair_0_1"]] == [0, 0], relay
+
+
+@pytest.mark.parametrize("engine", ["kernel", "sdma", "push", "relay"])
+def test_fuzz_every_engine(engine):
+    """Random groups of verified messages (1 B .. 8 MiB, self messages and
+    repeated pairs included) through every IPC engine, 4 processes on one GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "tests/scripts/fuzz_session.py", "ipc:" + engine, "15"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT,
+                         env=dict(os.environ, P2P_FUZZ_DEVICE="0", P2P_IPC_POOL="1G"))
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "FUZZ ipc:%s mismatches 0" % engine in out.stdout
