@@ -80,11 +80,15 @@ std::vector<std::vector<Stripe>> plan_routes(int nranks, const std::vector<std::
         relayed += s.bytes;
       }
     }
+    // Byte layout: the relay stripes first (whole `align` units, so every
+    // stripe starts aligned for the 16-byte copy kernel), the direct stripe
+    // last with the remainder and the message's unaligned tail.
     std::vector<Stripe> out;
     Stripe direct;
+    direct.offset = relayed;
     direct.bytes = bytes - relayed;
     out.push_back(direct);
-    size_t off = direct.bytes;
+    size_t off = 0;
     for (Stripe& s : relays) {
       s.offset = off;
       off += s.bytes;

@@ -21,7 +21,8 @@
 //   * C(a,b) = number of two-hop segments that would cross directed link a->b;
 //     a path's share is 1 for the direct link and relay_weight / max(C(s,k),
 //     C(k,d)) for a relay, and bytes are split in proportion to the shares,
-//     in `align`-byte units, the direct stripe taking the remainder.
+//     in `align`-byte units, the direct stripe taking the remainder (at the
+//     end of the message, so that every stripe starts aligned).
 // A single pair on N GPUs thus gets N-1 equal stripes (up to (N-1)x one
 // link); the N/2 disjoint pairs of a tournament round get a direct share of 1
 // and N-2 relay shares of 1/2 (up to N/2x one link); all-pairs stays direct.
@@ -51,7 +52,10 @@ struct RouteOptions {
 RouteOptions route_options_from_env();
 
 // One entry per flow of `flows` (same order; duplicates allowed and planned
-// identically): the stripes that cover [0, bytes), direct stripe first.
+// identically): the stripes that cover [0, bytes), direct stripe first in the
+// vector.  In the message the relay stripes come first (each a whole number
+// of `align` units, so every stripe offset is aligned) and the direct stripe
+// takes the rest, including any unaligned tail.
 // Self flows (src == dst) are one direct stripe.
 std::vector<std::vector<Stripe>> plan_routes(int nranks, const std::vector<std::pair<int, int>>& flows, size_t bytes,
                                              const RouteOptions& opt = RouteOptions());

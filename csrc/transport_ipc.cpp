@@ -527,6 +527,18 @@ class IpcTransport final : public Transport {
     dev::SignalArgs pre{}, post{};
     for (int p : push_recvs_) add_post(&pre, p, kReady, ++ready_posted_[static_cast<size_t>(p)]);
     for (int q : push_sends_) add_wait(&pre, q, kReady, ++ready_seen_[static_cast<size_t>(q)]);
+    if (debug_) {
+      std::string msg = strfmt("[ipc %d] group %ld sends-to:", rank_, groups_);
+      for (int q : push_sends_) msg += strfmt(" %d", q);
+      msg += " recvs-from:";
+      for (int p : push_recvs_) msg += strfmt(" %d", p);
+      msg += " ready_posted:";
+      for (auto v : ready_posted_) msg += strfmt(" %llu", v);
+      msg += " ready_seen:";
+      for (auto v : ready_seen_) msg += strfmt(" %llu", v);
+      std::fprintf(stderr, "%s ops %zu\n", msg.c_str(), ops_.size());
+    }
+    ++groups_;
     launch_signals(pre, false);
     if (!ops_.empty()) dev::launch_multi_copy(ops_.data(), static_cast<int>(ops_.size()), stream_);
     for (int q : push_sends_) add_post(&post, q, kDone, ++done_posted_[static_cast<size_t>(q)]);
@@ -664,6 +676,8 @@ class IpcTransport final : public Transport {
   std::vector<dev::CopyOp> ops_;
   std::vector<std::array<int, 3>> covered_;  // relay: (src, dst, slot) posted by group_flows
   unsigned long long relayed_bytes_ = 0, relayed_stripes_ = 0;  // moved by this rank as a relay (P2P_RELAY_STATS)
+  bool debug_ = std::getenv("P2P_IPC_DEBUG") != nullptr;     // per-group flag bookkeeping on stderr
+  long groups_ = 0;
 
   struct Block {
     size_t size = 0;

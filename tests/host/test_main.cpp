@@ -1,5 +1,6 @@
 // Host-only unit tests (tier T0 in SURVEY.md §4): no GPU, no MPI launcher.
 // Built with g++ by `make host`; run directly or through tests/test_host_unit.py.
+#include <algorithm>
 #include <array>
 #include <atomic>
 #include <cmath>
@@ -226,13 +227,25 @@ TEST(test_restrict_cells) {
 
 // ------------------------------------------------------------- routing ----
 
+// Total bytes of a plan; checks that the stripes tile [0, total) without gaps
+// or overlaps and that every stripe starts 4 KiB-aligned (direct stripe last
+// in the message, first in the vector).
 static size_t stripe_sum(const std::vector<Stripe>& v) {
-  size_t s = 0, off = 0;
+  std::vector<std::pair<size_t, size_t>> spans;
+  size_t s = 0;
   for (const auto& x : v) {
-    EXPECT(x.offset == off);  // contiguous, direct first
-    off += x.bytes;
+    spans.emplace_back(x.offset, x.bytes);
     s += x.bytes;
+    EXPECT(x.offset % 4096 == 0);
   }
+  EXPECT(!v.empty() && v[0].via == -1);
+  std::sort(spans.begin(), spans.end());
+  size_t off = 0;
+  for (auto& sp : spans) {
+    EXPECT(sp.first == off);
+    off += sp.second;
+  }
+  EXPECT(v[0].offset + v[0].bytes == s);  // the direct stripe ends the message
   return s;
 }
 
@@ -289,6 +302,11 @@ TEST(test_routes_busy_links_and_duplicates) {
   auto dup = plan_routes(8, {{0, 1}, {2, 2}, {0, 1}}, bytes);
   EXPECT(dup[0].size() == dup[2].size() && dup[0][1].bytes == dup[2][1].bytes);
   EXPECT(dup[1].size() == 1 && dup[1][0].bytes == bytes);
+  // Unaligned sizes: every stripe still starts aligned; the tail is direct.
+  for (size_t odd : {size_t{1822205}, (size_t{5} << 20) + 13}) {
+    auto p = plan_routes(8, {{3, 1}}, odd);
+    EXPECT(p[0].size() == 7 && stripe_sum(p[0]) == odd);
+  }
 }
 
 TEST(test_host_hash_matches_reference) {

@@ -21,7 +21,7 @@ def main():
         # several-processes-per-GPU emulation); default: LOCAL_RANK.
         device = int(os.environ.get("P2P_FUZZ_DEVICE", os.environ.get("LOCAL_RANK", 0)))
         torch.cuda.set_device(device)
-    sess = create_session(transport, device=device, timeout_s=120)
+    sess = create_session(transport, device=device, timeout_s=float(os.environ.get("P2P_FUZZ_TIMEOUT", "120")))
     bad = sess.fuzz(rounds=rounds, seed=11, max_bytes=8 << 20)
     total = sess.allreduce_sum(float(bad))
     if sess.rank == 0:

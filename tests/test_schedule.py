@@ -57,8 +57,11 @@ def test_plan_routes_binding(native):
     (single,) = native.plan_routes(8, [(0, 1)], size)
     assert [s[0] for s in single][0] == -1 and sorted(s[0] for s in single[1:]) == [2, 3, 4, 5, 6, 7]
     assert sum(s[2] for s in single) == size and all(s[2] % 4096 == 0 for s in single[1:])
-    offs = [s[1] for s in single]
-    assert offs == sorted(offs) and offs[0] == 0
+    spans = sorted((s[1], s[2]) for s in single)
+    assert spans[0][0] == 0 and all(a[0] + a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    assert all(s[1] % 4096 == 0 for s in single) and single[0][1] + single[0][2] == size
+    (odd,) = native.plan_routes(4, [(3, 1)], 1822205)  # unaligned: stripes still start aligned
+    assert all(s[1] % 4096 == 0 for s in odd) and sum(s[2] for s in odd) == 1822205
     rnd = [(0, 1), (1, 0), (2, 3), (3, 2), (4, 5), (5, 4), (6, 7), (7, 6)]
     for plan in native.plan_routes(8, rnd, size):
         assert len(plan) == 7 and plan[0][2] > 1.5 * plan[1][2]
