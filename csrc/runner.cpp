@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <thread>
 
 #include "bootstrap.hpp"
@@ -40,9 +41,16 @@ Buffers::Buffers(Transport& t, size_t max_bytes, int recv_slots) : t_(t), cap_(s
 }
 
 Buffers::~Buffers() {
-  t_.unregister_buffers(send_);
-  for (void* p : recv_) t_.release(p);
-  if (send_) t_.release(send_);
+  // A destructor must not throw (the Python bindings turn fatal errors into
+  // exceptions): when tearing down after an error fails too, say so and go
+  // on, so the first error is the one that surfaces.
+  try {
+    t_.unregister_buffers(send_);
+    for (void* p : recv_) t_.release(p);
+    if (send_) t_.release(send_);
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "p2p_matrix: buffer teardown failed: %s\n", e.what());
+  }
 }
 
 // -------------------------------------------------------------- helpers ----
