@@ -91,7 +91,7 @@ def test_relay_engine_every_mode(exe, tmp_path):
     js = tmp_path / "r.json"
     env = dict(os.environ, P2P_RELAY_STATS="1")
     out = subprocess.run([MPIRUN, "-n", "4", exe, "--transport", "ipc", "--ipc-engine", "relay", "--device", "0",
-                          "--mode", "all", "--sizes", "64K:64M:32", "-n", "4", "--verify", "--no-compat",
+                          "--mode", "all", "--sizes", "64K,2M,1822205,64M", "-n", "4", "--verify", "--no-compat",
                           "--json", str(js), "--timeout", "60"], capture_output=True, text=True, timeout=300, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     assert "verification: OK" in out.stdout
