@@ -52,6 +52,9 @@ timing
                          one wave per GPU writes into the peer's memory, no host
                          or runtime in the loop)
       --latency-size S   [8]      --latency-iters N   [1000]
+      --fuzz N           data-integrity stress: N groups of random messages (random
+                         pairs incl. self, sizes 1 B .. the largest --size, at most
+                         64 MiB), every one verified; failures exit 2
 data
   -c, --verify           random-fill sends, verify every received buffer on the device
       --verify-impl I    auto (= lds8) | lds | lds8 | lds-pipe | lds-cached | stride | reg
@@ -141,7 +144,7 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
     static const char* kValued[] = {"-m", "--mode", "-d", "--dir", "-b", "--size", "--sizes", "-n", "--iters", "-w",
                                     "--warmup", "--timing", "--latency-size", "--latency-iters", "--verify-impl",
                                     "--transport", "--ipc-engine", "--bootstrap", "--device", "--timeout", "--min-gbs", "--json",
-                                    "--csv", "--trace", "--cells", "--comms"};
+                                    "--csv", "--trace", "--cells", "--comms", "--fuzz"};
     for (const char* v : kValued)
       if (a == v && !has_eq && i + 1 >= argc) {
         missing = true;
@@ -194,6 +197,8 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
       cfg->latency = true;
     } else if (a == "--device-latency") {
       cfg->device_latency = true;
+    } else if (a == "--fuzz") {
+      cfg->fuzz_rounds = std::atoi(next().c_str());
     } else if (a == "--latency-size") {
       cfg->latency_bytes = parse_size(next());
       cfg->latency = true;
@@ -418,6 +423,13 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
   if (cfg.latency) res.latency = run_latency(*t, boot, cfg.latency_bytes, cfg.latency_iters, std::min(cfg.latency_iters, 100), bufs);
   if (cfg.device_latency)
     res.device_latency = run_device_latency(*t, boot, cfg.latency_bytes, cfg.latency_iters, std::min(cfg.latency_iters, 100));
+  uint64_t fuzz_bad = 0;
+  size_t fuzz_max = 0;
+  if (cfg.fuzz_rounds > 0) {
+    fuzz_max = std::max<size_t>(16, std::min<size_t>(max_bytes, size_t{64} << 20));
+    fuzz_bad = boot.allreduce_sum_u64(fuzz_transport(*t, boot, cfg.fuzz_rounds, 0xF022, fuzz_max));
+    res.mismatches += fuzz_bad;
+  }
 
   // Device descriptions of every rank, for the banner.
   char mine[256] = {0};
@@ -434,6 +446,11 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
       for (const auto& rec : res.runs) print_extended(out, rec, n);
       print_latency(out, res.latency, n);
       print_latency(out, res.device_latency, n);
+      if (cfg.fuzz_rounds > 0)
+        std::fprintf(out, "\n== fuzz: %d groups of random messages (1 B .. %s, random pairs incl. self): %s ==\n",
+                     cfg.fuzz_rounds, format_size(fuzz_max).c_str(),
+                     fuzz_bad ? strfmt("%llu mismatching words", static_cast<unsigned long long>(fuzz_bad)).c_str()
+                              : "all verified");
     }
     if (js.is_open() && !res.latency.empty()) js << latency_to_json(res.latency, n) << "\n";
     if (js.is_open() && !res.device_latency.empty()) js << latency_to_json(res.device_latency, n) << "\n";

@@ -30,6 +30,7 @@ struct AppConfig {
   size_t target_bytes = 4ull << 30;
   bool latency = false;
   bool device_latency = false;   // ping-pong kernel matrix (one-sided transports)
+  int fuzz_rounds = 0;           // --fuzz N: N groups of random verified messages (data-integrity stress)
   size_t latency_bytes = 8;
   int latency_iters = 1000;
   std::string transport = "rccl";  // rccl | ipc | host

@@ -89,6 +89,16 @@ def test_cli_several_communicators(exe):
     assert "verification: OK" in out.stdout
 
 
+@pytest.mark.parametrize("comms", ["1", "4"])
+def test_cli_fuzz_rccl(exe, comms):
+    """--fuzz through the binary on the GPU: random message groups (self pairs
+    on one rank, sizes 1 B .. 64 MiB) over one or four communicators."""
+    out = subprocess.run([exe, "--mode", "self", "--size", "64M", "-n", "2", "--comms", comms, "--fuzz", "40",
+                          "--no-compat"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "groups of random messages" in out.stdout and "all verified" in out.stdout
+
+
 def test_bench_drops_a_failing_communicator_candidate():
     """If the 4-communicator candidate fails (injected), bench.py reports it
     in posting.dropped and times the single-communicator posting instead; with

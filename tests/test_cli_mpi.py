@@ -188,3 +188,14 @@ def test_shm_transport_all_modes(mpirun, host_build, tmp_path):
     lat = [r for r in recs if r["type"] == "latency"][0]
     assert all(0 < p["one_way_us"]["p50"] < 50 for p in lat["pairs"]), lat
     assert not [f for f in os.listdir("/dev/shm") if f.startswith("p2p_shm_")], "segment left in /dev/shm"
+
+
+def test_fuzz_option(mpirun, host_build):
+    """--fuzz N: random verified message groups after the matrices, over the
+    TCP and shared-memory transports (csrc/runner.cpp fuzz_transport)."""
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    for transport, n in (("host", 2), ("shm", 3)):
+        out = run(mpirun, exe, n, ["--transport", transport, "--mode", "pair", "--size", "256K", "-n", "2",
+                                   "--fuzz", "12"])
+        assert out.returncode == 0, out.stderr[-3000:]
+        assert "== fuzz: 12 groups of random messages (1 B .. 256K" in out.stdout and "all verified" in out.stdout
