@@ -31,6 +31,16 @@
 //     RCCL send/recv kernel uses at most 32 channels (workgroups); several
 //     communicators run several kernels side by side, so the messages of a
 //     group are moved by K x 32 workgroups.
+//     The ops of a group are handed to RCCL sorted by communicator (stable,
+//     so each communicator's per-peer order is kept), which makes every rank
+//     launch its kernels in the same (group, communicator) order.  HIP maps
+//     more streams than GPU_MAX_HW_QUEUES (4 on the box) onto shared hardware
+//     queues that run in order; were rank a to launch communicator 1 before 0
+//     on a queue where rank b launches 0 before 1, each would wait for a
+//     kernel the other has queued behind its own: a cross-rank deadlock (ring
+//     bi and all-pairs groups start on different communicators per rank).
+//     With one global launch order the earliest unfinished kernel on every
+//     rank has only finished work ahead of it in any queue.
 //   * hipEvents on the stream give GPU-timeline timestamps.
 //   * Payloads are written / checked by the gfx950 kernels in kernels.hip.
 #include <hip/hip_runtime.h>
@@ -249,6 +259,7 @@ class RcclTransport final : public Transport {
 
   void group_begin() override {
     nccl_ok(ncclGroupStart(), "ncclGroupStart");
+    in_group_ = true;
     if (cstreams_.size() > 1) {
       std::fill(used_.begin(), used_.end(), false);
       used_.resize(cstreams_.size(), false);
@@ -264,8 +275,7 @@ class RcclTransport final : public Transport {
     const char* c = static_cast<const char*>(p);
     do {
       size_t n = chunk_of(bytes);
-      nccl_ok(ncclSend(c, n, ncclUint8, peer, comms_[static_cast<size_t>(j)], cstreams_[static_cast<size_t>(j)]),
-              "ncclSend");
+      issue({j, true, const_cast<char*>(c), n, peer, cstreams_[static_cast<size_t>(j)]});
       c += n;
       bytes -= n;
     } while (bytes);
@@ -276,13 +286,19 @@ class RcclTransport final : public Transport {
     char* c = static_cast<char*>(p);
     do {
       size_t n = chunk_of(bytes);
-      nccl_ok(ncclRecv(c, n, ncclUint8, peer, comms_[static_cast<size_t>(j)], s), "ncclRecv");
+      issue({j, false, c, n, peer, s});
       c += n;
       bytes -= n;
     } while (bytes);
     recv_on_side_ = recv_stream_ != nullptr;
   }
   void group_end() override {
+    if (!deferred_.empty()) {
+      std::stable_sort(deferred_.begin(), deferred_.end(), [](const Op& a, const Op& b) { return a.comm < b.comm; });
+      for (const Op& o : deferred_) post(o);
+      deferred_.clear();
+    }
+    in_group_ = false;
     ncclResult_t r = ncclGroupEnd();
     // Non-blocking comm: the ops are only enqueued once the comm leaves
     // ncclInProgress, so wait before any event is recorded behind them.
@@ -458,6 +474,30 @@ class RcclTransport final : public Transport {
     return j;
   }
 
+  struct Op {
+    int comm;
+    bool send;
+    char* p;
+    size_t n;
+    int peer;
+    hipStream_t stream;
+  };
+  void post(const Op& o) {
+    ncclComm_t c = comms_[static_cast<size_t>(o.comm)];
+    if (o.send)
+      nccl_ok(ncclSend(o.p, o.n, ncclUint8, o.peer, c, o.stream), "ncclSend");
+    else
+      nccl_ok(ncclRecv(o.p, o.n, ncclUint8, o.peer, c, o.stream), "ncclRecv");
+  }
+  // Several communicators: a group's ops are posted at group_end, sorted by
+  // communicator (header comment).  One communicator: posted right away.
+  void issue(const Op& o) {
+    if (in_group_ && comms_.size() > 1)
+      deferred_.push_back(o);
+    else
+      post(o);
+  }
+
   void abort_all() {
     for (auto& c : comms_)
       if (c) {
@@ -524,6 +564,8 @@ class RcclTransport final : public Transport {
   std::vector<bool> stale_;            // side stream j has not waited for the latest buffer work
   size_t split_min_ = size_t{1} << 20;  // smaller messages stay on communicator 0 (P2P_RCCL_SPLIT_MIN)
   std::vector<bool> used_;             // side communicators used by the open group
+  bool in_group_ = false;              // between group_begin and group_end
+  std::vector<Op> deferred_;           // the open group's ops (several communicators)
   std::vector<unsigned long long> send_seq_, recv_seq_;  // messages posted to / from each peer
   struct RegSet {
     void* send = nullptr;
