@@ -250,7 +250,9 @@ def main(argv=None) -> int:
 
     def session_for(c):
         if c not in sessions:
-            sessions[c] = create_session("rccl:%d" % c if c > 1 else "rccl", device=device)
+            # A shorter limit than the headline session's: a candidate that
+            # stalls is aborted and dropped within two minutes.
+            sessions[c] = create_session("rccl:%d" % c if c > 1 else "rccl", device=device, timeout_s=120.0)
         return sessions[c]
 
     def agree(ok: bool) -> bool:
@@ -296,8 +298,23 @@ def main(argv=None) -> int:
         if k > 0:
             barrier()
             w0 = time.perf_counter()
-            d.run_steps(done, k)
-            d.sync()
+            try:
+                d.run_steps(done, k)
+                d.sync()
+                # Test hook: "<comms>,<batch>,warmup" fails it here instead.
+                if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d,warmup" % (c, b) and env.rank == n - 1:
+                    raise RuntimeError("injected warmup failure")
+            except Exception as e:  # noqa: BLE001 -- same agreement as above
+                err = str(e)[:200]
+            if not agree(err is None):
+                if not droppable:
+                    raise RuntimeError(err or "warmup failed on another rank")
+                failed["comms%d_%s" % (c, "batch" if b else "per_message")] = err or "failed on another rank"
+                log("bench: posting candidate %s dropped in warmup: %s" % ((c, b), err or "failed on another rank"))
+                d = None
+                if c != first_comms(args.transport, args.comms):
+                    sessions.pop(c, None)
+                continue
             barrier()
             tuning[(c, b)] = sessions[c].allreduce_max(time.perf_counter() - w0) / k
             done += k

@@ -103,6 +103,23 @@ class Session {
 
   uint64_t fuzz(int rounds, uint64_t seed, size_t max_bytes) { return fuzz_transport(*t_, *boot_, rounds, seed, max_bytes); }
 
+  // Test hook for the transports' watchdogs: a receive from this rank that
+  // no send matches, then sync().  Returns the error the watchdog raised (""
+  // if none did).  The buffer is kept: an aborted transfer may not have let go.
+  std::string unmatched_recv(size_t bytes) {
+    void* p = t_->alloc(bytes);
+    try {
+      t_->group_begin();
+      t_->recv(p, bytes, rank());
+      t_->group_end();
+      t_->sync();
+    } catch (const Error& e) {
+      return e.what();
+    }
+    t_->release(p);
+    return "";
+  }
+
   std::string device_latency(size_t bytes, int iters, int warmup) {
     return latency_to_json(run_device_latency(*t_, *boot_, bytes, iters, warmup), world());
   }
@@ -215,7 +232,9 @@ PYBIND11_MODULE(_p2pcore, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("fuzz", &Session::fuzz, py::arg("rounds") = 20, py::arg("seed") = 1, py::arg("max_bytes") = size_t{4} << 20,
            py::call_guard<py::gil_scoped_release>(),
-           "Random groups of verified messages through the transport (collective); returns mismatching words.");
+           "Random groups of verified messages through the transport (collective); returns mismatching words.")
+      .def("_unmatched_recv", &Session::unmatched_recv, py::arg("bytes") = size_t{1} << 20,
+           py::call_guard<py::gil_scoped_release>(), "Test hook: a receive no send matches; returns the watchdog's error.");
 
   py::class_<PyStepDriver>(m, "StepDriver")
       .def(py::init<std::shared_ptr<Session>, const std::string&, const std::string&, size_t, int, bool, bool, bool>(),

@@ -397,11 +397,20 @@ class RcclTransport final : public Transport {
       if (e == hipSuccess) return;
       if (e != hipErrorNotReady) P2P_FATAL(strfmt("stream error: %s", hipGetErrorString(e)));
       if ((it & 255) == 0) {
+        // Either way the communicators are aborted first: RCCL's kernels poll
+        // the abort flag and exit, so the streams (and any hardware queue they
+        // share with another session's streams) drain instead of staying
+        // stuck behind a transfer that will never complete.
         std::string err = async_error();
-        if (!err.empty()) P2P_FATAL("RCCL asynchronous error while waiting: " + err);
+        if (!err.empty()) {
+          abort_all();
+          P2P_FATAL("RCCL asynchronous error while waiting: " + err);
+        }
         double now = now_seconds();
-        if (now > deadline)
+        if (now > deadline) {
+          abort_all();
           P2P_FATAL(strfmt("rank %d: stream did not finish within %.0f s (peer hung or dead?); aborting", rank_, timeout_));
+        }
         if (now - t0 > 20e-3) std::this_thread::sleep_for(std::chrono::microseconds(20));
       }
     }
@@ -513,7 +522,9 @@ class RcclTransport final : public Transport {
       return;
     }
     ncclComm_t c = comms_.empty() ? nullptr : comms_[0];
-    P2P_FATAL(strfmt("rank %d: %s failed: %s (%s)", rank_, what, ncclGetErrorString(r), c ? ncclGetLastError(c) : ""));
+    std::string msg = strfmt("rank %d: %s failed: %s (%s)", rank_, what, ncclGetErrorString(r), c ? ncclGetLastError(c) : "");
+    abort_all();  // a communicator that returned an error is not used again
+    P2P_FATAL(msg);
   }
 
   // Polls every communicator created so far until none is in progress.
@@ -540,8 +551,10 @@ class RcclTransport final : public Transport {
         }
       }
     }
-    if (r != ncclSuccess)
+    if (r != ncclSuccess) {
+      abort_all();
       P2P_FATAL(strfmt("rank %d: %s failed: %s", rank_, what, ncclGetErrorString(r)));
+    }
   }
 
   int rank_, n_;

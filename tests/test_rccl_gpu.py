@@ -1,9 +1,13 @@
 """Tier T3: the RCCL transport on one MI355X (1-rank communicator: self
 send/recv through ncclGroupStart/End), through every engine entry point."""
 import json
+import subprocess
+import sys
 
 import pytest
 import torch
+
+from conftest import ROOT
 
 pytestmark = pytest.mark.gpu
 
@@ -124,3 +128,20 @@ def test_fuzz_random_groups(native, monkeypatch, transport, chunk):
     s = native.Session(0, 1, device=0, transport=transport, timeout_s=120)
     assert s.fuzz(rounds=30, seed=7, max_bytes=4 << 20) == 0
     del s
+
+
+
+
+@pytest.mark.parametrize("transport", ["rccl", "rccl:4"])
+def test_unmatched_receive_is_reported(transport):
+    """A receive no send matches ends in an error, not a hang: RCCL rejects a
+    lone self receive at ncclGroupEnd ("invalid usage"); the transport
+    aborts its communicators and raises.  In a child process: RCCL 2.26 leaves
+    thread-local group state behind after a failed ncclGroupEnd, which breaks
+    the next communicator created on that thread."""
+    code = ("from test_nccl_p2p_amd import require_native\n"
+            "s = require_native().Session(0, 1, device=0, transport=%r, timeout_s=5)\n"
+            "print('ERR:', s._unmatched_recv(1 << 20))\n" % transport)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "ERR: " in out.stdout and ("ncclGroupEnd failed" in out.stdout or "did not finish" in out.stdout), out.stdout

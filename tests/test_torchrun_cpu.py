@@ -86,6 +86,17 @@ def test_bench_drops_a_failing_posting_candidate(native):
     assert "injected" in r["posting"]["dropped"]["comms1_batch"] or "another rank" in r["posting"]["dropped"]["comms1_batch"]
 
 
+def test_bench_drops_a_candidate_failing_in_warmup(native):
+    """The same when the candidate connects but its warmup steps fail."""
+    out = torchrun(2, ["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "4", "--transport", "host",
+                       "--size", "64K", "--msgs", "2", "--latency-iters", "10", "--sweep", "0", "--extras", "0",
+                       "--ref-iters", "0", "--ipc-extra", "0"], env={"P2P_BENCH_FAIL_CANDIDATE": "1,1,warmup"})
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert r["value"] > 0 and r["posting"]["batch"] is False
+    assert r["posting"]["dropped"]["comms1_batch"] in ("injected warmup failure", "failed on another rank")
+
+
 
 def test_fuzz_session_over_shm_and_host(native):
     """Random verified message groups, 3 processes, over the shared-memory and
