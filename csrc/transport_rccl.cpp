@@ -324,10 +324,12 @@ class RcclTransport final : public Transport {
   }
 
   // A mark is an event on the main stream plus one on every side stream
-  // that ran work since the previous mark; it completes when all of them
-  // have.  elapsed_ms(a, b) = (latest event of b) - (latest event of a):
-  // with side streams running ahead of the main one, the time between the
-  // completions of all work up to a and all work up to b.
+  // that ran work since the previous mark; a side stream that did not stands
+  // for itself by its latest earlier event (nothing ran on it since).  The
+  // mark completes when all of them have.  elapsed_ms(a, b) = (latest event
+  // of b) - (latest event of a): the time between the completions of all
+  // work up to a and all work up to b, so back-to-back intervals add up to
+  // the whole run even when side streams finish a step after the main one.
   int mark() override {
     const size_t m = static_cast<size_t>(next_event_);
     if (m == events_.size()) {
@@ -336,7 +338,9 @@ class RcclTransport final : public Transport {
       events_.push_back(ev);
       side_ev_.emplace_back(cstreams_.size(), nullptr);
       side_rec_.emplace_back(cstreams_.size(), 0);
+      side_ref_.emplace_back(cstreams_.size(), -1);
     }
+    last_side_.resize(cstreams_.size(), -1);
     HIPCHECK(hipEventRecord(events_[m], stream_));
     for (size_t j = 0; j < cstreams_.size(); ++j) {
       side_rec_[m][j] = 0;
@@ -345,7 +349,9 @@ class RcclTransport final : public Transport {
         HIPCHECK(hipEventRecord(side_ev_[m][j], cstreams_[j]));
         side_rec_[m][j] = 1;
         pending_[j] = false;
+        last_side_[j] = static_cast<int>(m);
       }
+      side_ref_[m][j] = last_side_[j];
     }
     return next_event_++;
   }
@@ -359,12 +365,18 @@ class RcclTransport final : public Transport {
     };
     double start = 0, end = since_ref(events_.at(ib));
     for (size_t j = 0; j < cstreams_.size(); ++j) {
-      if (side_rec_[ia][j]) start = std::max(start, since_ref(side_ev_[ia][j]));
-      if (side_rec_[ib][j]) end = std::max(end, since_ref(side_ev_[ib][j]));
+      const int ra = side_ref_[ia][j], rb = side_ref_[ib][j];
+      if (ra >= 0) start = std::max(start, since_ref(side_ev_[static_cast<size_t>(ra)][j]));
+      if (rb >= 0) end = std::max(end, since_ref(side_ev_[static_cast<size_t>(rb)][j]));
     }
     return end - start;
   }
-  void clear_marks() override { next_event_ = 0; }
+  // Reused event slots must not stand in for a stream's latest work: the
+  // caller clears marks with the streams idle, so no reference is needed.
+  void clear_marks() override {
+    next_event_ = 0;
+    std::fill(last_side_.begin(), last_side_.end(), -1);
+  }
 
   // hipGraph capture of grouped ncclSend/ncclRecv: a step's back-to-back
   // groups become one graph launch, removing the per-group host launch cost
@@ -590,6 +602,8 @@ class RcclTransport final : public Transport {
   std::vector<hipEvent_t> events_;                 // per mark: on the main stream
   std::vector<std::vector<hipEvent_t>> side_ev_;   // per mark: on each side stream (lazily created)
   std::vector<std::vector<char>> side_rec_;        // per mark: side event j recorded by that mark
+  std::vector<std::vector<int>> side_ref_;         // per mark: the mark whose side event j stands for stream j (-1 none)
+  std::vector<int> last_side_;                     // latest mark that recorded on side stream j
   std::vector<bool> pending_;                      // side stream ran work since the last mark
   std::vector<bool> unjoined_;                     // side stream ran work since the last join
   std::vector<hipGraph_t> graphs_;
