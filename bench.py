@@ -197,6 +197,10 @@ def parse_args(argv=None):
     ap.add_argument("--isolate", type=int, default=1,
                     help="1: run each untimed transport comparison in a child process per rank (a fault there "
                          "cannot take the headline down); 0: in this process (halves the processes per GPU)")
+    ap.add_argument("--timeout", type=float, default=120.0,
+                    help="seconds any one wait of the headline session may take before it aborts and fails")
+    ap.add_argument("--untimed-budget", type=float, default=480.0,
+                    help="seconds for all untimed sections after the timed steps; later ones are skipped")
     ap.add_argument("--child-timeout", type=float, default=300.0,
                     help="seconds allowed to each untimed comparison process")
     ap.add_argument("--child", default=None, help=argparse.SUPPRESS)
@@ -234,7 +238,7 @@ def main(argv=None) -> int:
 
     size = nat.parse_size(args.size)
     headline = args.transport + (":%d" % args.comms if args.transport == "rccl" and args.comms > 1 else "")
-    sess = create_session(headline, device=device)
+    sess = create_session(headline, device=device, timeout_s=args.timeout)
     if env.rank == 0:
         log("bench: %d rank(s), %s, %s" % (n, sess.transport, sess.device_desc))
     mode = "self" if n == 1 else args.mode
@@ -250,9 +254,8 @@ def main(argv=None) -> int:
 
     def session_for(c):
         if c not in sessions:
-            # A shorter limit than the headline session's: a candidate that
-            # stalls is aborted and dropped within two minutes.
-            sessions[c] = create_session("rccl:%d" % c if c > 1 else "rccl", device=device, timeout_s=120.0)
+            # A candidate that stalls is aborted and dropped after --timeout.
+            sessions[c] = create_session("rccl:%d" % c if c > 1 else "rccl", device=device, timeout_s=args.timeout)
         return sessions[c]
 
     def agree(ok: bool) -> bool:
@@ -380,6 +383,24 @@ def main(argv=None) -> int:
     # the comparisons run on the same memory footprint as the timed steps did.
     del drv
 
+    # The untimed sections share one time budget (--untimed-budget): each
+    # starts only if every rank still has time left, so a section that stalls
+    # until its session's --timeout cannot push the JSON line past a driver's
+    # limit.  Skipped sections are listed in the JSON.
+    untimed_t0 = time.perf_counter()
+    skipped = []
+
+    def budget_left():
+        return args.untimed_budget - (time.perf_counter() - untimed_t0)
+
+    def in_budget(name):
+        if agree(budget_left() > 0):
+            return True
+        skipped.append(name)
+        if env.rank == 0:
+            log("bench: untimed budget spent; skipping %s" % name)
+        return False
+
     def guarded(name, fn):
         """Runs one untimed measurement; an error is logged and returned in
         its place ({"error": ...}), so the headline line is still printed.
@@ -420,7 +441,7 @@ def main(argv=None) -> int:
                 "value_ratio": round(value / r["gbs_mean"], 3) if r["gbs_mean"] > 0 else None}
 
     ref = None
-    if n > 1 and args.ref_iters > 0:
+    if n > 1 and args.ref_iters > 0 and in_budget("reference_semantics"):
         if env.rank == 0:
             log("bench: reference-semantics matrix")
         ref = guarded("reference semantics", reference_semantics)
@@ -449,7 +470,8 @@ def main(argv=None) -> int:
         for name, mode_x, dir_x, nbytes, iters in (("allpairs_1g", "allpairs", "bi", 1 << 30, 4),
                                                    ("ring_256m", "ring", "uni", 256 << 20, 8),
                                                    ("ring_hop_8b", "ring", "uni", 8, 200)):
-            extras[name] = guarded(name, lambda: concurrent_config(mode_x, dir_x, nbytes, iters))
+            if in_budget(name):
+                extras[name] = guarded(name, lambda: concurrent_config(mode_x, dir_x, nbytes, iters))
 
     # BASELINE.json config 2: single-pair (0 -> 1) send/recv bandwidth sweep,
     # 4 KiB -> 4 GiB in x4 steps, events-timed, uni-directional; only cell
@@ -478,9 +500,9 @@ def main(argv=None) -> int:
         return [{"bytes": nb, "gbs": round(f["gbs"], 2)}
                 for nb in (size, 256 << 20) for f in [pair_cell(ref_sess, nb, 16)] if f]
 
-    if n > 1 and args.sweep:
+    if n > 1 and args.sweep and in_budget("pair_sweep_0_1"):
         extras = dict(extras or {}, pair_sweep_0_1=guarded("pair sweep", pair_sweep), pair_sweep_rccl_comms=comms)
-        if ref_sess is not None and ref_sess is not sess:
+        if ref_sess is not None and ref_sess is not sess and in_budget("pair_0_1_one_comm"):
             extras["pair_0_1_one_comm"] = guarded("one-communicator pair", pair_one_comm)
 
     # The same tournament steps through the hand-written data plane (IPC
@@ -516,7 +538,7 @@ def main(argv=None) -> int:
         if args.device is not None:
             cmd += ["--device", str(args.device)]
         try:
-            rc = subprocess.run(cmd, timeout=args.child_timeout).returncode
+            rc = subprocess.run(cmd, timeout=min(args.child_timeout, max(30.0, budget_left()))).returncode
         except subprocess.TimeoutExpired:
             rc = "timeout"
         barrier()
@@ -549,6 +571,8 @@ def main(argv=None) -> int:
                    "ipc:relay": "push over the direct link + two-hop stripes relayed through GPUs whose links are "
                                 "idle (routing.hpp)"}
         for transport, key in runs:
+            if not in_budget(transport):
+                continue
             if env.rank == 0:
                 log("bench: %s comparison" % transport)
             if args.isolate:
@@ -610,6 +634,7 @@ def main(argv=None) -> int:
         "reference_semantics": ref,
         "extras": extras,
         "ipc_transport": ipc,
+        "untimed_skipped": skipped or None,
         "note": ("n_gpus=1 has no inter-GPU link: value is RCCL's on-GPU self send/recv copy (HBM-bound). "
                  "From n_gpus=2 every step is one tournament round of disjoint pairs, each pair on its own xGMI "
                  "link, so value grows with the number of pairs (per-GPU rate = one link's bandwidth)")

@@ -105,3 +105,16 @@ def test_fuzz_session_over_shm_and_host(native):
         out = torchrun(3, ["tests/scripts/fuzz_session.py", transport, "15"])
         assert out.returncode == 0, out.stderr[-3000:]
         assert "FUZZ %s mismatches 0" % transport in out.stdout
+
+
+def test_bench_untimed_budget_skips_sections(native):
+    """With the untimed budget spent, every section after the timed steps is
+    skipped on all ranks together and listed; the headline line still comes."""
+    out = torchrun(2, ["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "2", "--transport", "host",
+                       "--size", "64K", "--msgs", "1", "--latency-iters", "10", "--untimed-budget", "0"])
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert r["value"] > 0 and r["p50_latency_us"] > 0
+    assert r["reference_semantics"] is None and r["ipc_transport"] is None
+    assert set(r["untimed_skipped"]) >= {"reference_semantics", "allpairs_1g", "ring_256m", "ring_hop_8b",
+                                         "pair_sweep_0_1", "host"}, r["untimed_skipped"]
