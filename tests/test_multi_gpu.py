@@ -112,3 +112,17 @@ def test_fuzz_all_gpus():
         out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT)
         assert out.returncode == 0, out.stderr[-3000:]
         assert "FUZZ %s mismatches 0" % transport in out.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
+@pytest.mark.parametrize("args", [["--comms", "4"], ["--transport", "ipc", "--ipc-engine", "relay"]])
+def test_cli_fuzz_all_gpus(exe, args):
+    """p2p_matrix --fuzz across every GPU: random groups (random pairs incl.
+    self, 1 B .. 64 MiB) over four RCCL communicators, and over the relay
+    engine, whose stripes cross third GPUs."""
+    n = _n()
+    out = subprocess.run([MPIRUN, "-n", str(n), exe] + args + ["--mode", "pair", "--size", "64M", "-n", "2",
+                                                                "--fuzz", "40", "--no-compat", "--timeout", "120"],
+                         capture_output=True, text=True, timeout=900)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "all verified" in out.stdout
