@@ -216,3 +216,16 @@ def test_fuzz_every_engine(engine):
                          env=dict(os.environ, P2P_FUZZ_DEVICE="0", P2P_IPC_POOL="1G"))
     assert out.returncode == 0, out.stderr[-3000:]
     assert "FUZZ ipc:%s mismatches 0" % engine in out.stdout
+
+
+
+@pytest.mark.parametrize("engine", ["kernel", "relay"])
+def test_cli_fuzz_four_ranks(exe, engine):
+    """p2p_matrix --fuzz with 4 processes on the one GPU through the IPC
+    transport: random groups (random pairs incl. self, 1 B .. 16 MiB), relay
+    stripes through the third and fourth rank."""
+    out = subprocess.run([MPIRUN, "-n", "4", exe, "--transport", "ipc", "--ipc-engine", engine, "--device", "0",
+                          "--mode", "pair", "--size", "16M", "-n", "2", "--fuzz", "30", "--no-compat",
+                          "--timeout", "60"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "all verified" in out.stdout
