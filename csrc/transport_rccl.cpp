@@ -371,8 +371,10 @@ class RcclTransport final : public Transport {
     }
     return end - start;
   }
-  // Reused event slots must not stand in for a stream's latest work: the
-  // caller clears marks with the streams idle, so no reference is needed.
+  // Reused event slots must not stand in for a stream's latest work, so the
+  // references are dropped: the first mark after a clear covers the main
+  // stream and the side streams that ran since their last mark (callers
+  // clear between runs, with the streams drained or about to be).
   void clear_marks() override {
     next_event_ = 0;
     std::fill(last_side_.begin(), last_side_.end(), -1);
