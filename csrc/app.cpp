@@ -454,6 +454,10 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
     }
     if (js.is_open() && !res.latency.empty()) js << latency_to_json(res.latency, n) << "\n";
     if (js.is_open() && !res.device_latency.empty()) js << latency_to_json(res.device_latency, n) << "\n";
+    if (js.is_open() && cfg.fuzz_rounds > 0)
+      js << strfmt("{\"type\":\"fuzz\",\"rounds\":%d,\"max_bytes\":%zu,\"mismatches\":%llu}", cfg.fuzz_rounds, fuzz_max,
+                   static_cast<unsigned long long>(fuzz_bad))
+         << "\n";
     if (!cfg.trace_path.empty()) {
       std::ofstream tr(cfg.trace_path);
       P2P_CHECK(tr.good(), "cannot write " + cfg.trace_path);

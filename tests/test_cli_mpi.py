@@ -190,12 +190,16 @@ def test_shm_transport_all_modes(mpirun, host_build, tmp_path):
     assert not [f for f in os.listdir("/dev/shm") if f.startswith("p2p_shm_")], "segment left in /dev/shm"
 
 
-def test_fuzz_option(mpirun, host_build):
+def test_fuzz_option(mpirun, host_build, tmp_path):
     """--fuzz N: random verified message groups after the matrices, over the
-    TCP and shared-memory transports (csrc/runner.cpp fuzz_transport)."""
+    TCP and shared-memory transports (csrc/runner.cpp fuzz_transport), with a
+    `"type":"fuzz"` JSON line."""
     exe = os.path.join(host_build, "p2p_matrix_host")
     for transport, n in (("host", 2), ("shm", 3)):
+        js = tmp_path / ("%s.json" % transport)
         out = run(mpirun, exe, n, ["--transport", transport, "--mode", "pair", "--size", "256K", "-n", "2",
-                                   "--fuzz", "12"])
+                                   "--fuzz", "12", "--json", str(js)])
         assert out.returncode == 0, out.stderr[-3000:]
         assert "== fuzz: 12 groups of random messages (1 B .. 256K" in out.stdout and "all verified" in out.stdout
+        rec = [json.loads(l) for l in js.read_text().splitlines() if '"fuzz"' in l]
+        assert rec == [{"type": "fuzz", "rounds": 12, "max_bytes": 262144, "mismatches": 0}]
