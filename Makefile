@@ -24,7 +24,7 @@ OPT       ?= -O3
 HIPFLAGS  := $(CXXSTD) $(OPT) $(WARN) -fPIC --offload-arch=$(ARCH) -Icsrc
 HOSTFLAGS := $(CXXSTD) $(OPT) $(WARN) -fPIC -Icsrc -pthread
 
-CORE      := common units stats schedule routing bootstrap transport_host transport_shm runner report app
+CORE      := common units stats schedule routing bootstrap transport_host transport_shm runner report provenance app
 GPU_OBJS  := $(addprefix $(BUILD)/gpu/,$(addsuffix .o,$(CORE) transport_rccl transport_ipc topology) kernels.o pingpong.o)
 HOST_OBJS := $(addprefix $(BUILD)/host/,$(addsuffix .o,$(CORE) transport_rccl_stub))
 
@@ -34,6 +34,27 @@ HOST_OBJS := $(addprefix $(BUILD)/host/,$(addsuffix .o,$(CORE) transport_rccl_st
 MPILIB    := $(BUILD)/mpilib
 MPI_LINK  := -L$(MPILIB) -lmpi -Wl,-rpath,'$$ORIGIN/mpilib'
 MPI_INC   := -I$(MPI_HOME)/include
+
+# One HIP / RCCL runtime for every entry point (RUNTIME=torch, the default):
+# bench.py and the tests run inside torch processes, which load torch's
+# bundled libamdhip64 / librccl; build/p2p_matrix and the extension are linked
+# against the same files through build/rt (symlinks with the sonames the
+# loader looks for), so a cell measured through either entry point runs on
+# one RCCL.  RUNTIME=rocm links /opt/rocm's instead.  Both JSON outputs
+# record the library path and version (csrc/provenance.cpp).
+RUNTIME   ?= torch
+TORCH_LIB := $(shell $(PYTHON) -c "import os,importlib.util as u;s=u.find_spec('torch');print(os.path.join(os.path.dirname(s.origin),'lib') if s else '')")
+RTDIR     := $(BUILD)/rt
+RT_LIBS   := amdhip64 hsa-runtime64 amd_comgr rocprofiler-register rccl rocm_smi64 rocm-core roctx64 drm drm_amdgpu numa
+ifeq ($(RUNTIME)$(if $(TORCH_LIB),,none),torch)
+RT_STAMP  := $(RTDIR)/.stamp
+BIN_RPATH := -Wl,--disable-new-dtags -Wl,-rpath,'$$ORIGIN/rt'
+EXT_RPATH := -Wl,--disable-new-dtags -Wl,-rpath,'$$ORIGIN/../$(RTDIR)'
+else
+RT_STAMP  :=
+BIN_RPATH := -Wl,-rpath,$(ROCM)/lib
+EXT_RPATH := -Wl,-rpath,$(ROCM)/lib
+endif
 
 PY_EXT    := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
 PY_INC    := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_paths()['include'])")
@@ -54,6 +75,13 @@ tools: $(BUILD)/fill_probe $(BUILD)/ipc_export_probe
 
 $(BUILD)/gpu $(BUILD)/host $(BUILD)/asan:
 	mkdir -p $@
+
+$(RTDIR)/.stamp:
+	mkdir -p $(RTDIR)
+	for l in $(RT_LIBS); do [ ! -e $(TORCH_LIB)/lib$$l.so ] || ln -sf $(TORCH_LIB)/lib$$l.so $(RTDIR)/lib$$l.so; done
+	ln -sf $(TORCH_LIB)/librccl.so $(RTDIR)/librccl.so.1
+	ln -sf $(TORCH_LIB)/libamdhip64.so $(RTDIR)/libamdhip64.so.7
+	touch $@
 
 $(MPILIB)/.stamp:
 	mkdir -p $(MPILIB)
@@ -84,9 +112,9 @@ $(BUILD)/host/%.o: csrc/%.cpp $(HEADERS) | $(BUILD)/host
 $(BUILD)/host/bootstrap_mpi.o: csrc/bootstrap_mpi.cpp $(HEADERS) | $(BUILD)/host
 	$(CXX_HOST) $(HOSTFLAGS) $(MPI_INC) -c $< -o $@
 
-$(BUILD)/p2p_matrix: $(GPU_OBJS) $(BUILD)/gpu/bootstrap_mpi.o $(BUILD)/gpu/main.o $(MPILIB)/.stamp
+$(BUILD)/p2p_matrix: $(GPU_OBJS) $(BUILD)/gpu/bootstrap_mpi.o $(BUILD)/gpu/main.o $(MPILIB)/.stamp $(RT_STAMP)
 	$(HIPCC) --offload-arch=$(ARCH) $(GPU_OBJS) $(BUILD)/gpu/bootstrap_mpi.o $(BUILD)/gpu/main.o -o $@ \
-	    -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib $(MPI_LINK) -pthread
+	    $(BIN_RPATH) -L$(ROCM)/lib -lrccl $(MPI_LINK) -pthread
 
 $(BUILD)/p2p_matrix_host: $(HOST_OBJS) $(BUILD)/host/bootstrap_mpi.o $(BUILD)/host/main.o $(MPILIB)/.stamp
 	$(CXX_HOST) $(HOST_OBJS) $(BUILD)/host/bootstrap_mpi.o $(BUILD)/host/main.o -o $@ $(MPI_LINK) -pthread
@@ -97,9 +125,9 @@ $(BUILD)/p2p_host_tests: $(HOST_OBJS) tests/host/test_main.cpp $(HEADERS)
 $(BUILD)/gpu/pymodule.o: csrc/pymodule.cpp $(HEADERS) | $(BUILD)/gpu
 	$(HIPCC) $(HIPFLAGS) -fvisibility=hidden -I$(PY_INC) -I$(PYBIND) -c $< -o $@
 
-$(EXT): $(GPU_OBJS) $(BUILD)/gpu/pymodule.o
+$(EXT): $(GPU_OBJS) $(BUILD)/gpu/pymodule.o $(RT_STAMP)
 	$(HIPCC) --offload-arch=$(ARCH) -shared $(GPU_OBJS) $(BUILD)/gpu/pymodule.o -o $@ \
-	    -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib -pthread
+	    $(EXT_RPATH) -L$(ROCM)/lib -lrccl -pthread
 
 # Grid-shape probe (scripts/fill_probe.hip): standalone, no framework code.
 $(BUILD)/fill_probe: scripts/fill_probe.hip | $(BUILD)/gpu

@@ -4,9 +4,10 @@
 Metric and configs come from BASELINE.json ("pairwise P2P GB/s matrix
 (min/mean) + p50 latency at 1/2/4/8 MI355X").  The reference
 (/root/reference/p2p_matrix.cc) measures an N x N matrix of NCCL send/recv
-bandwidth at 32 MiB per message; this bench measures the same matrix on
-MI355X through the native engine (RCCL ncclSend/ncclRecv over xGMI, hipEvent
-timing, gfx950 fill/verify kernels).
+bandwidth at 32 MiB per message (:124), one cell at a time, 128 messages per
+cell (:132); this bench measures the same matrix on MI355X through the native
+engine (RCCL ncclSend/ncclRecv over xGMI, hipEvent timing, gfx950 fill /
+verify kernels).
 
 One step = one round of the round-robin "tournament" schedule: the N ranks
 form N/2 disjoint pairs (xGMI is fully connected point-to-point, so pairs never
@@ -14,17 +15,29 @@ share a link) and every pair exchanges --msgs messages of --size bytes in both
 directions, posted back to back inside ncclGroupStart/End.  Consecutive steps
 walk through the N-1 rounds, so after N-1 steps every cell of the matrix has
 been measured; per-GPU work per step is constant as N grows (weak scaling).
-With one GPU the step is a self send/recv (the reference prints only the
-diagonal 0.00 there).
+With one GPU the step is a self send/recv (uni: the GPU copies to itself; the
+reference prints only the diagonal 0.00 there).
 
-value = bytes sent by all ranks during the K timed steps / the slowest rank's
-wall time between two barrier + torch.cuda.synchronize() brackets, in GB/s
-(1e9 B/s).  Payloads are PRNG-filled on the device and the last step's receive
-buffers are verified on the device after the timed region.
+value = the mean cell of the matrix: bytes delivered by all flows during the K
+timed steps / the slowest rank's wall time between two barrier +
+torch.cuda.synchronize() brackets / the mean number of flows per step, in GB/s
+(1e9 B/s) per direction.  aggregate_gbs is the same numerator without the
+division (all flows together).
+
+Verification covers the timed work: every message of a step is sent from its
+own region of the send buffer (its own PRNG stream) into its own receive slot,
+every step into its own generation of slots; all slots are zeroed after the
+warmup and every slot a timed step wrote is checked on the device afterwards
+(verify_mismatches / verify_coverage).
+
+Every untimed section after the timed steps is bounded by one deadline counted
+from process start (--deadline): each section's waits are shortened to the
+time left, sections that would not fit are skipped (untimed_skipped), and a
+watchdog prints the JSON line with what is done when the deadline passes.
 
 Usage (driver contract):
   python bench.py --gpus 1 --steps K --warmup W
-  python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N \\
       --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
 """
 
@@ -32,19 +45,24 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import socket
 import statistics
 import subprocess
 import sys
 import tempfile
+import threading
 import time
 
-import torch
-import torch.distributed as dist
+T0 = time.monotonic()  # the deadline counts from here (process start, give or take the interpreter)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 METRIC = "pairwise P2P GB/s matrix (min/mean) + p50 latency at 1/2/4/8 MI355X"
 BASELINE_VALUE = None  # the reference publishes no numbers
+RESERVE_S = 15.0  # kept free at the end of the deadline for the JSON line and teardown
 
 
 def log(*a):
@@ -75,49 +93,167 @@ def first_comms(transport: str, comms: int) -> int:
     return comms if transport == "rccl" and comms > 0 else 1
 
 
-def posting_candidates(transport: str, comms: int, batch: int, warmup: int):
-    """(communicators, batch) pairs the warmup steps time against each other.
+def posting_candidates(transport: str, comms: int, batch: int):
+    """(communicators, batch) pairs the tuning laps time against each other.
 
     comms: > 0 fixed, -1 = RCCL picks between 1 and 4 (other transports: 1).
     batch: 1 one group per step, 0 one group per message, -1 = both (K = 1
-    only: with several communicators per-message groups cannot overlap).
-    With fewer warmup steps than candidates only the last one is kept."""
+    only: with several communicators per-message groups cannot overlap)."""
     comms_choices = ([comms] if comms > 0 else [1, 4]) if transport == "rccl" else [1]
-    batch_choices = [batch] if batch >= 0 or warmup < 2 else [0, 1]
-    if batch_choices == [-1]:
-        batch_choices = [1]
-    choices = [(c, b) for c in comms_choices for b in batch_choices if c == 1 or b == 1 or len(batch_choices) == 1]
-    if warmup < len(choices):
-        choices = choices[-1:]
-    return choices
+    batch_choices = [batch] if batch >= 0 else [0, 1]
+    return [(c, b) for c in comms_choices for b in batch_choices if c == 1 or b == 1 or len(batch_choices) == 1]
 
 
-def steps_through(nat, isess, args, mode, size, batch, transport):
+def tuning_steps(phases: int, min_steps: int = 4) -> int:
+    """Steps per candidate: whole laps of the schedule (every cell once per
+    lap), at least min_steps so a one-round schedule is not timed on one step."""
+    return phases * max(1, math.ceil(min_steps / phases))
+
+
+def headline_stats(job_bytes: float, flows_total: int, steps: int, elapsed: float):
+    """(value, aggregate): the mean per-flow, per-direction rate and the sum
+    over all flows, both from the barrier-bracketed wall clock, in GB/s."""
+    aggregate = job_bytes / elapsed / 1e9
+    mean_flows = flows_total / steps
+    return aggregate / mean_flows, aggregate
+
+
+def cell_matrix(n: int, steps, flows_of, all_ms, bytes_per_flow: float):
+    """Per-cell GB/s medians and sample counts.  A flow's time in a step is
+    the LONGER of its two endpoints' step durations (the conservative choice,
+    the same as p2p_matrix's per-flow time, csrc/runner.cpp run_phase): the
+    endpoint that started first also waited for its partner."""
+    cells = {}
+    for i, k in enumerate(steps):
+        for (src, dst) in flows_of(k):
+            ms = max(all_ms[src][i], all_ms[dst][i])
+            if ms > 0:
+                cells.setdefault((src, dst), []).append(bytes_per_flow / (ms * 1e-3) / 1e9)
+    matrix = [[0.0] * n for _ in range(n)]
+    samples = [[0] * n for _ in range(n)]
+    for (s, d), v in cells.items():
+        matrix[s][d] = statistics.median(v)
+        samples[s][d] = len(v)
+    return matrix, samples, cells
+
+
+def pick_depth(steps: int, phases: int) -> int:
+    """Receive generations so that no timed step overwrites another's slots."""
+    return max(1, math.ceil(steps / phases))
+
+
+class Deadline:
+    """One deadline for the whole run, counted from process start."""
+
+    def __init__(self, seconds: float):
+        self.end = T0 + seconds
+
+    def left(self) -> float:
+        return self.end - time.monotonic()
+
+
+class Reporter:
+    """Holds the result and prints it exactly once (rank 0): at the normal end
+    of the run, or from the watchdog when the deadline passes first."""
+
+    def __init__(self, rank: int, real_stdout: int, json_out):
+        self.rank = rank
+        self.fd = real_stdout
+        self.json_out = json_out
+        self.lock = threading.Lock()
+        self.result = None  # set once the timed region is measured
+        self.done = False
+
+    def update(self, **kv):
+        with self.lock:
+            if self.result is not None:
+                self.result.update(kv)
+
+    def emit(self, **extra) -> bool:
+        with self.lock:
+            if self.done:
+                return False
+            self.done = True
+            if self.rank != 0:
+                return True
+            res = dict(self.result) if self.result is not None else {
+                "metric": METRIC, "value": None, "unit": "GB/s", "error": "the timed steps did not finish"}
+            res.update(extra)
+            line = json.dumps(res)
+            os.write(self.fd, (line + "\n").encode())
+            if self.json_out:
+                with open(self.json_out, "w") as f:
+                    f.write(line + "\n")
+            return True
+
+
+def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> threading.Event:
+    """At the deadline: print the JSON line with what is finished (the section
+    still running is named), abort every RCCL communicator so its kernels exit,
+    and end the process.  Exit 0 when the headline was measured."""
+    stop = threading.Event()
+
+    def run():
+        while not stop.wait(max(0.05, min(1.0, deadline.left()))):
+            if deadline.left() <= 0:
+                break
+        if stop.is_set():
+            return
+        log("bench: deadline reached during %s; printing what is done" % state.get("section"))
+        errors = dict(state.get("errors") or {})
+        if state.get("section"):
+            errors[state["section"]] = "deadline reached while running"
+        reporter.emit(deadline_hit=True, untimed_skipped=state.get("skipped") or None, section_errors=errors or None)
+        try:
+            nat.run_abort_hooks()
+        except Exception:  # noqa: BLE001 -- the process ends either way
+            pass
+        sys.stderr.flush()
+        os._exit(0 if reporter.result is not None else 4)
+
+    threading.Thread(target=run, name="bench-watchdog", daemon=True).start()
+    return stop
+
+
+def steps_through(nat, isess, args, mode, size, batch, transport, deadline=None):
     """The timed steps again through another transport session (untimed by
     the contract); any error is reported instead of failing the run."""
     try:
-        idrv = nat.StepDriver(isess, mode, "bi", size, args.msgs, not args.no_verify, bool(batch), False)
+        n = isess.world
+        phases = len(nat.schedule(mode, "bi", n))
+        idrv = nat.StepDriver(isess, mode, "bi", size, args.msgs, not args.no_verify, bool(batch), False,
+                              depth=pick_depth(args.steps, phases), salt=2)
         idrv.connect()
         idrv.run_steps(0, args.warmup)
         idrv.sync()
+        idrv.poison()
         isess.barrier()
         i0 = time.perf_counter()
         idrv.run_steps(args.warmup, args.steps)
         idrv.sync()
         isess.barrier()
         ielapsed = isess.allreduce_max(time.perf_counter() - i0)
-        ijob = sum(idrv.job_bytes_per_step(args.warmup + k) for k in range(args.steps))
-        out = {"value_gbs": round(ijob / ielapsed / 1e9, 3), "ms_per_step": round(ielapsed / args.steps * 1e3, 4),
-               "verify_mismatches": idrv.verify_last() if not args.no_verify else -1,
+        steps = range(args.warmup, args.warmup + args.steps)
+        value, aggregate = headline_stats(sum(idrv.job_bytes_per_step(k) for k in steps),
+                                          sum(idrv.flows_per_step(k) for k in steps), args.steps, ielapsed)
+        vr = idrv.verify_steps(args.warmup, args.steps) if not args.no_verify else None
+        out = {"value_gbs": round(value, 3), "aggregate_gbs": round(aggregate, 3),
+               "ms_per_step": round(ielapsed / args.steps * 1e3, 4),
+               "verify_mismatches": vr["mismatches"] if vr else -1,
+               "verify_coverage": round(vr["verified_msgs"] / vr["timed_msgs"], 4) if vr and vr["timed_msgs"] else None,
                "transport": transport}
         del idrv
-        # Device-initiated ping-pong: one wave per GPU writes the message
-        # into the peer's memory and spins on its own inbox (no host, no
-        # runtime in the loop) -- the fabric's latency, next to RCCL's.
+        # Device-initiated ping-pong and ring token chain: one wave per GPU
+        # writes into the peer's memory and spins on its own inbox (no host,
+        # no runtime in the loop) -- the fabric's latency, next to RCCL's.
         if transport == "ipc":
             dl = json.loads(isess.device_latency(nat.parse_size(args.latency_size), args.latency_iters,
                                                  min(100, args.latency_iters)))
             out["device_pingpong_p50_us"] = round(statistics.median(p["one_way_us"]["p50"] for p in dl["pairs"]), 3)
+            if n > 1:
+                rl = json.loads(isess.ring_latency(nat.parse_size(args.latency_size), 100, 10, True))
+                out["device_ring_hop_p50_us"] = round(rl["hop_us"]["p50"], 3)
+                out["device_ring_lap_p50_us"] = round(rl["lap_us"]["p50"], 3)
         # Multi-path: the reference's single-pair cell (0 -> 1, every other
         # GPU idle) with the message striped over the direct link and two-hop
         # relays through the idle GPUs.
@@ -152,7 +288,7 @@ def child_main(args) -> int:
     size = nat.parse_size(args.size)
     try:
         sess = nat.Session(env.rank, env.world, host=env.master_addr, port=args.child_port, device=device,
-                           transport=args.child, timeout_s=90.0)
+                           transport=args.child, timeout_s=min(90.0, args.timeout))
         out = steps_through(nat, sess, args, args.mode, size, args.child_batch, args.child)
         del sess
     except Exception as e:
@@ -175,20 +311,27 @@ def parse_args(argv=None):
                     help="rccl (headline) | ipc = one-sided gfx950 copy kernel over hipIpc mappings | host = CPU (tests)")
     ap.add_argument("--comms", type=int, default=-1,
                     help="rccl: communicators per rank; the messages of a step are spread over them and their "
-                         "send/recv kernels run side by side (-1: the warmup picks 1 or 4)")
+                         "send/recv kernels run side by side (-1: the tuning laps pick 1 or 4)")
     ap.add_argument("--device", type=int, default=None, help="GPU index (default LOCAL_RANK)")
     ap.add_argument("--latency-iters", type=int, default=300)
     ap.add_argument("--latency-size", default="8")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--batch", type=int, default=-1,
                     help="1: all msgs of a step in one group (one launch); 0: one group per message; "
-                         "-1: the W warmup steps are split between both and the faster posting is timed")
+                         "-1: the tuning laps time both and the faster posting is used")
+    ap.add_argument("--tune-laps", type=int, default=1,
+                    help="untimed laps of the schedule per posting candidate, before the W warmup steps "
+                         "(0: no tuning, the first candidate is used)")
     ap.add_argument("--graph", type=int, default=0, help="1: replay each step as a captured hipGraph")
+    ap.add_argument("--recv-budget", default="0",
+                    help="receive-slot memory per rank (0: 40%% of free HBM / ranks per GPU); caps the slot "
+                         "generations, and so verify_coverage")
     ap.add_argument("--json-out", default=None, help="also write the result line to this file")
     ap.add_argument("--ipc-extra", type=int, default=1,
                     help="1: also run the tournament steps through the IPC transport (N > 1, after the timed region)")
     ap.add_argument("--extras", type=int, default=1,
-                    help="1: also measure all-pairs 1 GiB and ring 256 MiB after the timed region (N > 1)")
+                    help="1: also measure all-pairs 1 GiB, ring 256 MiB and the ring token hop after the timed "
+                         "region (N > 1)")
     ap.add_argument("--sweep", type=int, default=1,
                     help="1: also sweep the single pair 0 -> 1 over 4 KiB .. --sweep-max (N > 1, after the timed region)")
     ap.add_argument("--sweep-max", default="4G", help="largest message of the pair sweep")
@@ -199,8 +342,11 @@ def parse_args(argv=None):
                          "cannot take the headline down); 0: in this process (halves the processes per GPU)")
     ap.add_argument("--timeout", type=float, default=120.0,
                     help="seconds any one wait of the headline session may take before it aborts and fails")
+    ap.add_argument("--deadline", type=float, default=300.0,
+                    help="seconds from process start by which the JSON line is printed; untimed sections are "
+                         "shortened or skipped to fit, and a watchdog prints what is done when it passes")
     ap.add_argument("--untimed-budget", type=float, default=480.0,
-                    help="seconds for all untimed sections after the timed steps; later ones are skipped")
+                    help="seconds for all untimed sections after the timed steps (within --deadline)")
     ap.add_argument("--child-timeout", type=float, default=300.0,
                     help="seconds allowed to each untimed comparison process")
     ap.add_argument("--child", default=None, help=argparse.SUPPRESS)
@@ -208,6 +354,13 @@ def parse_args(argv=None):
     ap.add_argument("--child-out", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--child-batch", type=int, default=1, help=argparse.SUPPRESS)
     return ap.parse_args(argv)
+
+
+def hang_requested(section: str, rank: int) -> bool:
+    """Test hook: P2P_BENCH_HANG="<section>@<rank>" makes that rank stop
+    responding inside that untimed section."""
+    spec = os.environ.get("P2P_BENCH_HANG", "")
+    return bool(spec) and spec == "%s@%d" % (section, rank)
 
 
 def main(argv=None) -> int:
@@ -219,7 +372,8 @@ def main(argv=None) -> int:
     from test_nccl_p2p_amd.parallel.session import create_session, init_control_plane
 
     nat = require_native()
-    env = init_control_plane("gloo")
+    deadline = Deadline(args.deadline)
+    env = init_control_plane("gloo", timeout_s=max(60.0, args.deadline))
     if args.gpus != env.world:
         log("bench: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, env.world))
     n = env.world
@@ -227,6 +381,9 @@ def main(argv=None) -> int:
     device = env.local_rank if args.device is None else args.device
     if use_gpu:
         torch.cuda.set_device(device)
+    reporter = Reporter(env.rank, real_stdout, args.json_out)
+    state = {"section": "setup", "skipped": [], "errors": {}}
+    start_watchdog(deadline, reporter, nat, state)
 
     def barrier():
         if n > 1:
@@ -236,28 +393,6 @@ def main(argv=None) -> int:
         if use_gpu:
             torch.cuda.synchronize()
 
-    size = nat.parse_size(args.size)
-    headline = args.transport + (":%d" % args.comms if args.transport == "rccl" and args.comms > 1 else "")
-    sess = create_session(headline, device=device, timeout_s=args.timeout)
-    if env.rank == 0:
-        log("bench: %d rank(s), %s, %s" % (n, sess.transport, sess.device_desc))
-    mode = "self" if n == 1 else args.mode
-
-    # Warmup (untimed, W steps in total) also picks the posting: one group
-    # per step vs one group per message, and (RCCL) one communicator vs
-    # several whose send/recv kernels run side by side.  The W steps are
-    # split between the candidates and the fastest, by the slowest rank's
-    # clock, is timed.  connect() has already established every connection
-    # of every round.
-    choices = posting_candidates(args.transport, args.comms, args.batch, args.warmup)
-    sessions = {first_comms(args.transport, args.comms): sess}
-
-    def session_for(c):
-        if c not in sessions:
-            # A candidate that stalls is aborted and dropped after --timeout.
-            sessions[c] = create_session("rccl:%d" % c if c > 1 else "rccl", device=device, timeout_s=args.timeout)
-        return sessions[c]
-
     def agree(ok: bool) -> bool:
         """True when every rank reports ok (the candidates are collective)."""
         if n == 1:
@@ -266,78 +401,104 @@ def main(argv=None) -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         return bool(t.item())
 
-    tuning = {}
-    drivers = {}
-    failed = {}
-    done = 0
-    for i, (c, b) in enumerate(choices):
-        # A candidate other than the first that fails anywhere (e.g. a second
-        # RCCL communicator on a node where it was never tried) is dropped on
-        # every rank instead of ending the run.
-        d, err = None, None
-        try:
-            d = nat.StepDriver(session_for(c), mode, "bi", size, args.msgs, not args.no_verify, bool(b),
-                               bool(args.graph))
-            d.connect()
-            # Test hook: P2P_BENCH_FAIL_CANDIDATE="<comms>,<batch>" fails that
-            # candidate on the last rank only.
-            if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d" % (c, b) and env.rank == n - 1:
-                raise RuntimeError("injected candidate failure")
-        except Exception as e:  # noqa: BLE001 -- reported, and the candidate is skipped everywhere
-            err = str(e)[:200]
-        # The headline session's first candidate must work; anything else
-        # (another communicator count, another posting) may be dropped.
-        droppable = (c, b) != choices[0] or c != first_comms(args.transport, args.comms)
-        if droppable and not agree(err is None):
-            failed["comms%d_%s" % (c, "batch" if b else "per_message")] = err or "failed on another rank"
-            log("bench: posting candidate %s dropped: %s" % ((c, b), err or "failed on another rank"))
-            d = None
-            if c != first_comms(args.transport, args.comms):
-                sessions.pop(c, None)
-            continue
-        if err is not None:
-            raise RuntimeError(err)
-        k = (args.warmup - done) // (len(choices) - i)
-        if k > 0:
-            barrier()
-            w0 = time.perf_counter()
+    size = nat.parse_size(args.size)
+    headline = args.transport + (":%d" % args.comms if args.transport == "rccl" and args.comms > 1 else "")
+    sess = create_session(headline, device=device, timeout_s=args.timeout)
+    if env.rank == 0:
+        log("bench: %d rank(s), %s, %s" % (n, sess.transport, sess.device_desc))
+    mode = "self" if n == 1 else args.mode
+    provenance = json.loads(sess.provenance(device if use_gpu else -1))
+    provenance.pop("type", None)
+
+    # Receive-slot budget: every message of every timed step gets its own
+    # slot, up to this much memory per rank (ranks sharing a GPU split it).
+    budget = 0 if args.recv_budget.strip() in ("", "0") else nat.parse_size(args.recv_budget)
+    if budget == 0 and use_gpu:
+        free_b, _ = torch.cuda.mem_get_info(device)
+        same_gpu = sum(1 for d in provenance.get("rank_devices", []) if d["device"] == device) or 1
+        budget = int(0.4 * free_b / same_gpu)
+    elif budget == 0:
+        budget = 256 << 20
+
+    # ---- posting selection: one untimed lap of the schedule per candidate --
+    # (one group per step vs one per message; RCCL: one communicator vs four
+    # whose send/recv kernels run side by side), timed by the slowest rank,
+    # before the W warmup steps of the chosen one.
+    state["section"] = "tuning"
+    choices = posting_candidates(args.transport, args.comms, args.batch)
+    c0 = first_comms(args.transport, args.comms)
+    sessions = {c0: sess}
+
+    def session_for(c):
+        if c not in sessions:
+            # A candidate that stalls is aborted and dropped after --timeout.
+            sessions[c] = create_session("rccl:%d" % c if c > 1 else "rccl", device=device, timeout_s=args.timeout)
+        return sessions[c]
+
+    tuning, failed = {}, {}
+    phases = len(nat.schedule(mode, "bi", n))
+    tune_k = tuning_steps(phases) * args.tune_laps
+    if args.tune_laps > 0 and len(choices) > 1:
+        for i, (c, b) in enumerate(choices):
+            key = "comms%d_%s" % (c, "batch" if b else "per_message")
+            # The headline session's first candidate must work; anything else
+            # (another communicator count, another posting) may be dropped.
+            droppable = i > 0 or c != c0
+            d, err = None, None
             try:
-                d.run_steps(done, k)
-                d.sync()
-                # Test hook: "<comms>,<batch>,warmup" fails it here instead.
-                if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d,warmup" % (c, b) and env.rank == n - 1:
-                    raise RuntimeError("injected warmup failure")
-            except Exception as e:  # noqa: BLE001 -- same agreement as above
+                d = nat.StepDriver(session_for(c), mode, "bi", size, args.msgs, False, bool(b), bool(args.graph))
+                d.connect()
+                # Test hook: P2P_BENCH_FAIL_CANDIDATE="<comms>,<batch>" fails
+                # that candidate on the last rank only.
+                if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d" % (c, b) and env.rank == n - 1:
+                    raise RuntimeError("injected candidate failure")
+            except Exception as e:  # noqa: BLE001 -- reported, and the candidate is skipped everywhere
                 err = str(e)[:200]
-            if not agree(err is None):
-                if not droppable:
-                    raise RuntimeError(err or "warmup failed on another rank")
-                failed["comms%d_%s" % (c, "batch" if b else "per_message")] = err or "failed on another rank"
-                log("bench: posting candidate %s dropped in warmup: %s" % ((c, b), err or "failed on another rank"))
-                d = None
-                if c != first_comms(args.transport, args.comms):
-                    sessions.pop(c, None)
-                continue
-            barrier()
-            tuning[(c, b)] = sessions[c].allreduce_max(time.perf_counter() - w0) / k
-            done += k
-        drivers[(c, b)] = d
-    if not drivers:  # every candidate was dropped: the headline session, one group per step
-        c0 = first_comms(args.transport, args.comms)
-        d = nat.StepDriver(sessions[c0], mode, "bi", size, args.msgs, not args.no_verify, True, bool(args.graph))
-        d.connect()
-        drivers[(c0, 1)] = d
-    comms, batch = (min(tuning, key=tuning.get) if len(tuning) == len(drivers) and tuning
-                    else list(drivers)[-1])
-    drv = drivers.pop((comms, batch))
-    del drivers, d  # the other postings' buffers go before the timed region
-    sess = sessions[comms]
+            if agree(err is None):
+                barrier()
+                w0 = time.perf_counter()
+                try:
+                    d.run_steps(0, tune_k)
+                    d.sync()
+                    if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d,tuning" % (c, b) and env.rank == n - 1:
+                        raise RuntimeError("injected tuning failure")
+                except Exception as e:  # noqa: BLE001 -- same agreement as above
+                    err = str(e)[:200]
+                w = time.perf_counter() - w0
+                if agree(err is None):
+                    tuning[(c, b)] = sess.allreduce_max(w) / tune_k
+                    del d
+                    continue
+            if not droppable:
+                raise RuntimeError(err or "the first posting candidate failed on another rank")
+            failed[key] = err or "failed on another rank"
+            log("bench: posting candidate %s dropped: %s" % ((c, b), failed[key]))
+            del d
+            if c != c0 and not any(cc == c for (cc, _) in tuning):
+                sessions.pop(c, None)
+        comms, batch = min(tuning, key=tuning.get)
+        reason = "fastest of %d candidate(s) over %d untimed step(s) each (%s lap(s) of %d round(s)), slowest rank's " \
+                 "clock" % (len(tuning), tune_k, args.tune_laps, phases)
+    else:
+        comms, batch = choices[0]
+        reason = "single candidate" if len(choices) == 1 else "no tuning laps (--tune-laps 0): first candidate"
+    sess = session_for(comms)
     # A single-communicator session stays for the reference-method comparison
     # (the reference uses one communicator); other candidates are closed.
     ref_sess = sessions.get(1)
     for c in list(sessions):
         if c not in (comms, 1):
             del sessions[c]
+
+    # ---- the headline driver: W warmup steps, poison, K timed steps -------
+    state["section"] = "headline"
+    phases = len(nat.schedule(mode, "bi", n))
+    drv = nat.StepDriver(sess, mode, "bi", size, args.msgs, not args.no_verify, bool(batch), bool(args.graph),
+                         depth=pick_depth(args.steps, phases), recv_budget=budget, salt=1)
+    drv.connect()
+    drv.run_steps(0, args.warmup)
+    drv.sync()
+    drv.poison()  # untimed: every receive slot zeroed; a slot passes verification only if a timed step wrote it
     gpu_sync()
     drv.reset()
 
@@ -352,67 +513,133 @@ def main(argv=None) -> int:
     t1 = time.perf_counter()
     elapsed = sess.allreduce_max(t1 - t0)
 
-    job_bytes = sum(drv.job_bytes_per_step(args.warmup + k) for k in range(args.steps))
-    value = job_bytes / elapsed / 1e9
+    steps = list(range(args.warmup, args.warmup + args.steps))
+    job_bytes = sum(drv.job_bytes_per_step(k) for k in steps)
+    flows_total = sum(drv.flows_per_step(k) for k in steps)
+    value, aggregate = headline_stats(job_bytes, flows_total, args.steps, elapsed)
 
-    # Per-step GPU durations of every rank -> per-flow bandwidth.  The later
-    # arriving endpoint of a pair sees only the transfer (the earlier one also
-    # waits), so a flow's time is the min of its two endpoints' step times.
+    # Per-step GPU durations of every rank -> per-cell bandwidth.
     my_ms = drv.step_ms()
     all_ms = [None] * n
     if n > 1:
         dist.all_gather_object(all_ms, my_ms)
     else:
         all_ms = [my_ms]
-    cells = {}
-    for k in range(args.steps):
-        step = args.warmup + k
-        for (src, dst) in drv.phase_flows(step):
-            ms = min(all_ms[src][k], all_ms[dst][k]) if src != dst else all_ms[src][k]
-            if ms > 0:
-                cells.setdefault((src, dst), []).append(size * args.msgs / (ms * 1e-3) / 1e9)
-    matrix = [[0.0] * n for _ in range(n)]
-    for (s, d), v in cells.items():
-        matrix[s][d] = statistics.median(v)
-    offdiag = [v for (s, d), vs in cells.items() for v in [statistics.median(vs)] if s != d or n == 1]
-    covered = len(cells)
+    matrix, samples, cells = cell_matrix(n, steps, drv.phase_flows, all_ms, size * args.msgs)
+    offdiag = [matrix[s][d] for (s, d) in cells if s != d or n == 1]
     expected = n * (n - 1) if n > 1 else 1
 
-    mismatches = drv.verify_last() if not args.no_verify else -1
+    vr = drv.verify_steps(args.warmup, args.steps) if not args.no_verify else None
+    mismatches = vr["mismatches"] if vr else -1
+    depth, recv_bytes = drv.depth, drv.recv_bytes
     # Everything below is untimed; release the timed driver's buffers first so
     # the comparisons run on the same memory footprint as the timed steps did.
     del drv
 
-    # The untimed sections share one time budget (--untimed-budget): each
-    # starts only if every rank still has time left, so a section that stalls
-    # until its session's --timeout cannot push the JSON line past a driver's
-    # limit.  Skipped sections are listed in the JSON.
-    untimed_t0 = time.perf_counter()
-    skipped = []
+    step_ms_med = statistics.median(my_ms) if my_ms else 0.0
+    headline_transport = sess.transport
+    lat_matrix = [[0.0] * n for _ in range(n)]
+    reporter.result = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GB/s",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
+        "dtype": "uint8",
+        "data": "synthetic (device PRNG-filled payloads, one stream per message; every timed delivery verified on "
+                "the device after timing)",
+        "config": {
+            "model": "p2p_matrix: %s %s %s, %s x %d msgs/step"
+                     % ("RCCL ncclSend/ncclRecv" if headline_transport == "rccl" else headline_transport + " transport",
+                        mode, "self send/recv (uni)" if mode == "self" else "bidirectional",
+                        nat.format_size(size), args.msgs),
+            "global_batch": args.msgs * n,
+            "seq_len": size,
+            "parallelism": "p2p%d" % n,
+        },
+        "value_definition": "mean cell of the GB/s matrix: all flows' bytes / slowest rank's barrier-bracketed wall "
+                            "time / mean flows per step (per direction, 1 GB = 1e9 B)",
+        "aggregate_gbs": round(aggregate, 3),
+        "flows_per_step": round(flows_total / args.steps, 3),
+        "matrix_gbs_min": round(min(offdiag), 3) if offdiag else None,
+        "matrix_gbs_mean": round(statistics.mean(offdiag), 3) if offdiag else None,
+        "matrix_cells": "%d/%d" % (len(cells), expected),
+        # BASELINE config 3: the full N x N pairwise matrices (row = sender;
+        # GB/s per direction, median over steps, a cell's time = the longer of
+        # its endpoints'; p50 one-way latency, us).
+        "matrix_gbs": [[round(v, 2) for v in row] for row in matrix],
+        "matrix_samples": samples,
+        "latency_p50_us_matrix": lat_matrix,
+        "p50_latency_us": None,
+        "latency_bytes": nat.parse_size(args.latency_size),
+        "per_gpu_gbs": round(aggregate / n, 3),
+        "rank0_step_ms_p50": round(step_ms_med, 4),
+        "verify_mismatches": mismatches,
+        "verify_coverage": (round(vr["verified_msgs"] / vr["timed_msgs"], 4) if vr and vr["timed_msgs"] else None),
+        "verify_detail": vr,
+        "recv_slot_generations": depth,
+        "recv_slot_bytes_per_rank": recv_bytes,
+        "transport": headline_transport,
+        "posting": {"batch": bool(batch), "graph": bool(args.graph), "rccl_comms": comms, "dropped": failed or None,
+                    "selection": reason,
+                    "tuning_ms_per_step": {"comms%d_%s" % (c, "batch" if b else "per_message"): round(v * 1e3, 4)
+                                           for (c, b), v in tuning.items()} or None},
+        "provenance": provenance,
+        "reference_semantics": None,
+        "extras": None,
+        "ipc_transport": None,
+        "untimed_skipped": None,
+        "note": ("n_gpus=1 has no inter-GPU link: value is RCCL's on-GPU self send/recv copy (HBM-bound), the "
+                 "diagonal the reference prints as 0.00. From n_gpus=2 every step is one tournament round of disjoint "
+                 "pairs, each pair on its own xGMI link; value is the mean per-link, per-direction cell rate and "
+                 "aggregate_gbs the whole fabric")
+                if n == 1 else
+                ("each step is one tournament round: %d disjoint pairs exchange in both directions, one xGMI link "
+                 "per pair; value = mean cell (per link and direction), aggregate_gbs = all pairs together" % (n // 2)),
+    }
+    if env.rank == 0:
+        log("bench: value %.2f GB/s per cell (aggregate %.2f GB/s), %.4f ms/step, verify %s" % (
+            value, aggregate, elapsed / args.steps * 1e3, vr))
+
+    # ---- untimed sections: one deadline, waits shortened to the time left --
+    untimed_t0 = time.monotonic()
+    skipped, errors = state["skipped"], state["errors"]
+    live = [s for s in {id(x): x for x in (sess, ref_sess) if x is not None}.values()]
 
     def budget_left():
-        return args.untimed_budget - (time.perf_counter() - untimed_t0)
+        return min(args.untimed_budget - (time.monotonic() - untimed_t0), deadline.left() - RESERVE_S)
 
-    def in_budget(name):
-        if agree(budget_left() > 0):
-            return True
-        skipped.append(name)
-        if env.rank == 0:
-            log("bench: untimed budget spent; skipping %s" % name)
-        return False
-
-    def guarded(name, fn):
-        """Runs one untimed measurement; an error is logged and returned in
-        its place ({"error": ...}), so the headline line is still printed.
-        (The RCCL transport bounds every wait, so a failure on one rank
-        surfaces on the others as an error too, not as a hang.)"""
+    def section(name, fn, min_s=2.0, budgeted=True):
+        """Runs one untimed section if every rank has time for it, with every
+        wait of the live sessions bounded by the time left; an error is logged
+        and returned in its place ({"error": ...}).  budgeted=False: only the
+        deadline counts, not --untimed-budget (the headline's own latency)."""
+        left = budget_left() if budgeted else deadline.left() - RESERVE_S
+        if not agree(left > min_s):
+            skipped.append(name)
+            if env.rank == 0:
+                log("bench: no time left; skipping %s" % name)
+            return None
+        for s in live:
+            s.set_timeout(max(1.0, min(args.timeout, left)))
+        state["section"] = name
+        if hang_requested(name, env.rank):
+            log("bench: injected hang in %s on rank %d" % (name, env.rank))
+            while True:
+                time.sleep(1)
         try:
             return fn()
         except Exception as e:  # noqa: BLE001 -- reported in the JSON
             log("bench: %s failed: %s" % (name, e))
+            errors[name] = str(e)[:300]
             return {"error": str(e)[:300]}
-
-    lat_matrix = [[0.0] * n for _ in range(n)]
+        finally:
+            state["section"] = None
 
     def latency():
         lat = json.loads(sess.latency(nat.parse_size(args.latency_size), args.latency_iters,
@@ -422,63 +649,77 @@ def main(argv=None) -> int:
         p50s = [p["one_way_us"]["p50"] for p in lat["pairs"]]
         return statistics.median(p50s) if p50s else None
 
-    p50 = guarded("latency", latency)
-    if isinstance(p50, dict):  # the error is in the log; the field stays null
-        p50 = None
+    p50 = section("latency", latency, budgeted=False)
+    reporter.update(p50_latency_us=round(p50, 3) if isinstance(p50, float) else None, latency_p50_us_matrix=lat_matrix)
 
     # The reference's own methodology on one communicator, for comparison
-    # (serial ordered pairs, host clock, one stream sync per message,
-    # p2p_matrix.cc:141-186), at the same message size.  Untimed by the
-    # driver's bracket; skipped on one GPU where the reference measures nothing.
+    # (serial ordered pairs, host clock, one stream sync per message, no
+    # warmup, p2p_matrix.cc:141-186), at the same message size.  With one GPU
+    # the reference prints only the diagonal; its methodology is then applied
+    # to the self cell, so the ratio still compares the two methods.
     def reference_semantics():
-        r = json.loads((ref_sess or sess).run(mode="pair", dir="uni", bytes=size, iters=args.ref_iters, warmup=0,
-                                              timing="wallclock", verify=False, warm=False))
-        return {"cell_gbs_min": round(r["gbs_min"], 3), "cell_gbs_mean": round(r["gbs_mean"], 3),
+        r = json.loads((ref_sess or sess).run(mode="pair" if n > 1 else "self", dir="uni", bytes=size,
+                                              iters=args.ref_iters, warmup=0, timing="wallclock", verify=False,
+                                              warm=False))
+        fl = [f["gbs"] for ph in r["phases"] for f in ph["flows"] if f["src"] != f["dst"] or n == 1]
+        mean = statistics.mean(fl) if fl else 0.0
+        return {"cell_gbs_min": round(min(fl), 3) if fl else None, "cell_gbs_mean": round(mean, 3),
                 "iters": args.ref_iters, "size": size,
-                "method": "reference semantics: serial ordered pairs, wall clock, stream sync per message",
-                # The reference moves one cell at a time, so its matrix-wide
-                # throughput is its cell rate; ours is `value`.
-                "value_ratio": round(value / r["gbs_mean"], 3) if r["gbs_mean"] > 0 else None}
+                "method": "reference semantics: serial ordered pairs, wall clock, stream sync per message, no warmup"
+                          + ("" if n > 1 else " (applied to the self cell)"),
+                # Both are per-cell rates: ours from the pipelined timed
+                # steps, the reference's from its serial cells.
+                "value_ratio": round(value / mean, 3) if mean > 0 else None}
 
-    ref = None
-    if n > 1 and args.ref_iters > 0 and in_budget("reference_semantics"):
+    if args.ref_iters > 0:
         if env.rank == 0:
             log("bench: reference-semantics matrix")
-        ref = guarded("reference semantics", reference_semantics)
+        reporter.update(reference_semantics=section("reference_semantics", reference_semantics, 5.0))
 
     # The other BASELINE.json configs, measured after the timed region so one
     # driver run records them too: all-pairs concurrent exchange at 1 GiB
-    # (bisection: every GPU drives all N-1 xGMI links at once) and the ring
-    # neighbour exchange at 256 MiB (pipeline-parallel hop).
+    # (bisection: every GPU drives all N-1 xGMI links at once), the ring
+    # neighbour exchange at 256 MiB, and the pipeline-parallel hop latency as
+    # a dependent token chain 0 -> 1 -> ... -> N-1 -> 0.
     def concurrent_config(mode_x, dir_x, nbytes, iters):
         r = json.loads(sess.run(mode=mode_x, dir=dir_x, bytes=nbytes, iters=iters, warmup=1, timing="events",
-                                verify=False, warm=True))
+                                verify=not args.no_verify, warm=True))
         ph = r["phases"][0]
         flows = [f["gbs"] for f in ph["flows"]]
         p50s = [f["iter_us"]["p50"] for f in ph["flows"]]
         return {"aggregate_gbs": round(ph["agg_gbs"], 2), "per_gpu_egress_gbs": round(ph["agg_gbs"] / n, 2),
                 "flow_gbs_min": round(min(flows), 2), "flow_gbs_mean": round(statistics.mean(flows), 2),
-                "iter_us_p50": round(statistics.median(p50s), 1), "bytes": nbytes, "iters": iters}
+                "iter_us_p50": round(statistics.median(p50s), 1), "bytes": nbytes, "iters": iters,
+                "mismatches": ph["mismatches"]}
+
+    def ring_hop():
+        r = json.loads(sess.ring_latency(nat.parse_size(args.latency_size), 100, 10, False))
+        return {"hop_us_p50": round(r["hop_us"]["p50"], 3), "hop_us_p99": round(r["hop_us"]["p99"], 3),
+                "lap_us_p50": round(r["lap_us"]["p50"], 3), "laps": r["laps"], "bytes": r["bytes"],
+                "method": "dependent token chain 0 -> 1 -> ... -> N-1 -> 0, each hop forwards after its receive "
+                          "completed (grouped send/recv on the stream); hop = lap / N, rank 0's hipEvents"}
 
     extras = None
     if n > 1 and args.extras:
         if env.rank == 0:
             log("bench: all-pairs / ring extras")
         extras = {}
-        # ring_hop_8b: the pipeline-parallel hop latency -- every rank sends
-        # 8 bytes to its successor each iteration; iter_us_p50 is the hop time.
         for name, mode_x, dir_x, nbytes, iters in (("allpairs_1g", "allpairs", "bi", 1 << 30, 4),
-                                                   ("ring_256m", "ring", "uni", 256 << 20, 8),
-                                                   ("ring_hop_8b", "ring", "uni", 8, 200)):
-            if in_budget(name):
-                extras[name] = guarded(name, lambda: concurrent_config(mode_x, dir_x, nbytes, iters))
+                                                   ("ring_256m", "ring", "uni", 256 << 20, 8)):
+            v = section(name, lambda: concurrent_config(mode_x, dir_x, nbytes, iters), 5.0)
+            if v is not None:
+                extras[name] = v
+        v = section("ring_hop", ring_hop)
+        if v is not None:
+            extras["ring_hop"] = v
+        reporter.update(extras=extras)
 
     # BASELINE.json config 2: single-pair (0 -> 1) send/recv bandwidth sweep,
     # 4 KiB -> 4 GiB in x4 steps, events-timed, uni-directional; only cell
     # (0, 1) is scheduled, so the other ranks just join the barriers.
     def pair_cell(session, nbytes, iters):
         r = json.loads(session.run(mode="pair", dir="uni", bytes=nbytes, iters=iters, warmup=2, timing="events",
-                                   verify=False, warm=False, cells=[(0, 1)]))
+                                   verify=not args.no_verify, warm=False, cells=[(0, 1)]))
         fl = [f for ph in r["phases"] for f in ph["flows"]]
         return fl[0] if fl else None
 
@@ -491,7 +732,7 @@ def main(argv=None) -> int:
             f = pair_cell(sess, nbytes, iters)
             if f:
                 sweep.append({"bytes": nbytes, "iters": iters, "gbs": round(f["gbs"], 2),
-                              "iter_us_p50": round(f["iter_us"]["p50"], 2)})
+                              "iter_us_p50": round(f["iter_us"]["p50"], 2), "mismatches": f.get("mismatches", -1)})
         return sweep
 
     def pair_one_comm():
@@ -500,10 +741,15 @@ def main(argv=None) -> int:
         return [{"bytes": nb, "gbs": round(f["gbs"], 2)}
                 for nb in (size, 256 << 20) for f in [pair_cell(ref_sess, nb, 16)] if f]
 
-    if n > 1 and args.sweep and in_budget("pair_sweep_0_1"):
-        extras = dict(extras or {}, pair_sweep_0_1=guarded("pair sweep", pair_sweep), pair_sweep_rccl_comms=comms)
-        if ref_sess is not None and ref_sess is not sess and in_budget("pair_0_1_one_comm"):
-            extras["pair_0_1_one_comm"] = guarded("one-communicator pair", pair_one_comm)
+    if n > 1 and args.sweep:
+        sw = section("pair_sweep_0_1", pair_sweep, 10.0)
+        if sw is not None:
+            extras = dict(extras or {}, pair_sweep_0_1=sw, pair_sweep_rccl_comms=comms)
+            if ref_sess is not None and ref_sess is not sess:
+                oc = section("pair_0_1_one_comm", pair_one_comm)
+                if oc is not None:
+                    extras["pair_0_1_one_comm"] = oc
+        reporter.update(extras=extras)
 
     # The same tournament steps through the hand-written data plane (IPC
     # transport: one-sided pulls of hipIpc-mapped peer buffers by the gfx950
@@ -511,7 +757,7 @@ def main(argv=None) -> int:
     # contract; any error is reported in the JSON instead of failing the run.
     # The comparisons below open sessions of their own; close the headline one
     # first so they run alone, as the timed steps did.
-    headline_transport = sess.transport
+    live.clear()
     del sess, ref_sess, sessions
 
     # (with --transport host the same code path runs on the CPU transport, for tests)
@@ -528,17 +774,18 @@ def main(argv=None) -> int:
         if n > 1:
             dist.broadcast_object_list(box, src=0)
         out_path = os.path.join(tempfile.gettempdir(), "p2p_bench_child_%d_%d.json" % (box[0], env.rank))
+        limit = min(args.child_timeout, max(5.0, budget_left()))
         cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(n), "--steps", str(args.steps),
                "--warmup", str(args.warmup), "--size", args.size, "--msgs", str(args.msgs), "--mode", mode,
                "--latency-iters", str(args.latency_iters), "--latency-size", args.latency_size,
                "--child", transport, "--child-port", str(box[0]), "--child-out", out_path,
-               "--child-batch", str(int(batch))]
+               "--child-batch", str(int(batch)), "--timeout", str(max(5.0, min(args.timeout, limit)))]
         if args.no_verify:
             cmd.append("--no-verify")
         if args.device is not None:
             cmd += ["--device", str(args.device)]
         try:
-            rc = subprocess.run(cmd, timeout=min(args.child_timeout, max(30.0, budget_left()))).returncode
+            rc = subprocess.run(cmd, timeout=limit).returncode
         except subprocess.TimeoutExpired:
             rc = "timeout"
         barrier()
@@ -570,87 +817,38 @@ def main(argv=None) -> int:
                    "ipc:sdma": "one-sided pull by the SDMA copy engines (hipMemcpyAsync per receive)",
                    "ipc:relay": "push over the direct link + two-hop stripes relayed through GPUs whose links are "
                                 "idle (routing.hpp)"}
+
+        def compare(transport):
+            if args.isolate:
+                return isolated(transport)
+            isess = create_session(transport, device=device, timeout_s=min(90.0, max(5.0, budget_left())))
+            try:
+                return steps_through(nat, isess, args, mode, size, batch, transport)
+            finally:
+                del isess
+
         for transport, key in runs:
-            if not in_budget(transport):
-                continue
             if env.rank == 0:
                 log("bench: %s comparison" % transport)
-            if args.isolate:
-                r = isolated(transport)
-            else:
-                try:
-                    isess = create_session(transport, device=device, timeout_s=90.0)
-                    r = steps_through(nat, isess, args, mode, size, batch, transport)
-                    del isess
-                except Exception as e:  # report, never fail the headline
-                    r = {"error": str(e)[:300], "transport": transport}
-            if env.rank != 0:
+            r = section(transport, lambda: compare(transport), 20.0)
+            if r is None or env.rank != 0:
                 continue
             if transport in engines:
                 r["engine"] = engines[transport]
             if key is None:
                 ipc = r
-            else:
+            elif ipc is not None:
                 ipc[key] = r
+            reporter.update(ipc_transport=ipc)
 
-    step_ms_med = statistics.median(my_ms) if my_ms else 0.0
-    result = {
-        "metric": METRIC,
-        "value": round(value, 3),
-        "unit": "GB/s",
-        "n_gpus": n,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
-        "dtype": "uint8",
-        "data": "synthetic (device PRNG-filled payloads, verified after timing)",
-        "config": {
-            "model": "p2p_matrix: %s %s-bidirectional, %s x %d msgs/step"
-                     % ("RCCL ncclSend/ncclRecv" if headline_transport == "rccl" else headline_transport + " transport",
-                        mode, nat.format_size(size), args.msgs),
-            "global_batch": args.msgs * n,
-            "seq_len": size,
-            "parallelism": "p2p%d" % n,
-        },
-        "matrix_gbs_min": round(min(offdiag), 3) if offdiag else None,
-        "matrix_gbs_mean": round(statistics.mean(offdiag), 3) if offdiag else None,
-        "matrix_cells": "%d/%d" % (covered, expected),
-        # BASELINE config 3: the full N x N pairwise matrices (row = sender;
-        # GB/s per direction, median over steps; p50 one-way latency, us).
-        "matrix_gbs": [[round(v, 2) for v in row] for row in matrix],
-        "latency_p50_us_matrix": lat_matrix,
-        "p50_latency_us": round(p50, 3) if p50 is not None else None,
-        "latency_bytes": nat.parse_size(args.latency_size),
-        "per_gpu_gbs": round(value / n, 3),
-        "rank0_step_ms_p50": round(step_ms_med, 4),
-        "verify_mismatches": mismatches,
-        "transport": headline_transport,
-        "posting": {"batch": bool(batch), "graph": bool(args.graph), "rccl_comms": comms, "dropped": failed or None,
-                    "warmup_ms_per_step": {"comms%d_%s" % (c, "batch" if b else "per_message"): round(v * 1e3, 4)
-                                           for (c, b), v in tuning.items()}},
-        "reference_semantics": ref,
-        "extras": extras,
-        "ipc_transport": ipc,
-        "untimed_skipped": skipped or None,
-        "note": ("n_gpus=1 has no inter-GPU link: value is RCCL's on-GPU self send/recv copy (HBM-bound). "
-                 "From n_gpus=2 every step is one tournament round of disjoint pairs, each pair on its own xGMI "
-                 "link, so value grows with the number of pairs (per-GPU rate = one link's bandwidth)")
-                if n == 1 else
-                ("each step is one tournament round: %d disjoint pairs exchange in both directions, one xGMI link "
-                 "per pair; value = all pairs together" % (n // 2)),
-    }
+    reporter.update(untimed_skipped=skipped or None, section_errors=errors or None)
     if env.rank == 0:
         log("bench: GB/s matrix (row=src, col=dst), median over steps:")
         for r in range(n):
             log("  " + " ".join("%8.2f" % matrix[r][c] for c in range(n)))
-        line = json.dumps(result)
-        os.write(real_stdout, (line + "\n").encode())
-        if args.json_out:
-            with open(args.json_out, "w") as f:
-                f.write(line + "\n")
+    reporter.emit()
+    # The watchdog stays armed: should the teardown below hang, it ends the
+    # process at the deadline (the line is out already, so it exits 0).
     barrier()
     if n > 1 and dist.is_initialized():
         dist.destroy_process_group()

@@ -8,6 +8,7 @@
 
 #include "bootstrap.hpp"
 #include "common.hpp"
+#include "provenance.hpp"
 #include "report.hpp"
 #include "topology.hpp"
 #include "transport.hpp"
@@ -45,9 +46,11 @@ timing
                          (the reference's methodology, p2p_matrix.cc:141-267)
       --two-streams      RCCL: receives on a second stream, like the reference's s_1
       --comms K          RCCL: K communicators per rank on K streams; the i-th message
-                         to / from a peer uses communicator i mod K                [1]
+                         of >= 1 MiB from a to b uses communicator (i + a + b) mod K on both
+                         ends, smaller messages stay on the first (P2P_RCCL_SPLIT_MIN)  [1]
       --no-warm          do not pre-establish connections before timing
-  -l, --latency          add a ping-pong latency matrix
+  -l, --latency          add a ping-pong latency matrix (with --mode ring also the dependent
+                         ring token chain: per-hop latency of a pipeline 0 -> 1 -> ... -> 0)
       --device-latency   add a device-initiated ping-pong matrix (--transport ipc:
                          one wave per GPU writes into the peer's memory, no host
                          or runtime in the loop)
@@ -348,6 +351,12 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
                                  : cfg.transport == "ipc" ? make_ipc_transport(boot, topt)
                                                           : make_rccl_transport(boot, topt);
 
+  // Provenance (collective): the runtime, RCCL library and knobs, every
+  // rank's GPU and the links between them -- the first line of --json.
+  const bool gpu_transport = cfg.transport == "rccl" || cfg.transport == "ipc";
+  const std::string provenance =
+      cfg.json_path.empty() ? std::string() : provenance_json(boot, gpu_transport ? topt.device : -1);
+
   size_t max_bytes = *std::max_element(cfg.sizes.begin(), cfg.sizes.end());
   if (cfg.latency) max_bytes = std::max(max_bytes, cfg.latency_bytes);
   int slots = 1;
@@ -382,6 +391,8 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
     }
     js.open(cfg.json_path, cfg.resume ? std::ios::app : std::ios::trunc);
     P2P_CHECK(js.good(), "cannot write " + cfg.json_path);
+    js << provenance << "\n";
+    js.flush();
   }
   if (!skip.empty()) boot.bcast(skip.data(), skip.size(), 0);
 
@@ -423,6 +434,14 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
   if (cfg.latency) res.latency = run_latency(*t, boot, cfg.latency_bytes, cfg.latency_iters, std::min(cfg.latency_iters, 100), bufs);
   if (cfg.device_latency)
     res.device_latency = run_device_latency(*t, boot, cfg.latency_bytes, cfg.latency_iters, std::min(cfg.latency_iters, 100));
+  // Ring mode: also the dependent token chain (pipeline-parallel hop latency).
+  if (std::find(cfg.modes.begin(), cfg.modes.end(), Mode::Ring) != cfg.modes.end()) {
+    const int laps = std::max(1, cfg.latency_iters / std::max(1, n));
+    if (cfg.latency)
+      res.ring_latency.push_back(run_ring_latency(*t, boot, cfg.latency_bytes, laps, std::min(laps, 20), bufs));
+    if (cfg.device_latency)
+      res.ring_latency.push_back(run_device_ring_latency(*t, boot, cfg.latency_bytes, laps, std::min(laps, 20)));
+  }
   uint64_t fuzz_bad = 0;
   size_t fuzz_max = 0;
   if (cfg.fuzz_rounds > 0) {
@@ -446,6 +465,7 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
       for (const auto& rec : res.runs) print_extended(out, rec, n);
       print_latency(out, res.latency, n);
       print_latency(out, res.device_latency, n);
+      for (const auto& rl : res.ring_latency) print_ring_latency(out, rl);
       if (cfg.fuzz_rounds > 0)
         std::fprintf(out, "\n== fuzz: %d groups of random messages (1 B .. %s, random pairs incl. self): %s ==\n",
                      cfg.fuzz_rounds, format_size(fuzz_max).c_str(),
@@ -454,6 +474,8 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
     }
     if (js.is_open() && !res.latency.empty()) js << latency_to_json(res.latency, n) << "\n";
     if (js.is_open() && !res.device_latency.empty()) js << latency_to_json(res.device_latency, n) << "\n";
+    for (const auto& rl : res.ring_latency)
+      if (js.is_open()) js << ring_latency_to_json(rl) << "\n";
     if (js.is_open() && cfg.fuzz_rounds > 0)
       js << strfmt("{\"type\":\"fuzz\",\"rounds\":%d,\"max_bytes\":%zu,\"mismatches\":%llu}", cfg.fuzz_rounds, fuzz_max,
                    static_cast<unsigned long long>(fuzz_bad))

@@ -67,6 +67,7 @@ struct AppResult {
   std::vector<RunRecord> runs;
   std::vector<LatencyResult> latency;
   std::vector<LatencyResult> device_latency;
+  std::vector<RingLatencyResult> ring_latency;  // --mode ring with --latency / --device-latency
   uint64_t mismatches = 0;
   int slow_flows = 0;  // flows under --min-gbs
 };

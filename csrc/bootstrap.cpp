@@ -190,6 +190,7 @@ class TcpBootstrap final : public Bootstrap {
 
   ~TcpBootstrap() override { close_all(); }
 
+  void set_timeout(double seconds) override { timeout_ = seconds; }
   int rank() const override { return rank_; }
   int size() const override { return size_; }
   std::string name() const override { return "tcp"; }

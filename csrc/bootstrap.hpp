@@ -32,6 +32,8 @@ class Bootstrap {
   // Tear the job down from this rank (called from the fatal() hook).
   virtual void abort(int code) = 0;
   virtual std::string name() const = 0;
+  // Seconds any one receive may wait (TCP); shrunk as a deadline approaches.
+  virtual void set_timeout(double /*seconds*/) {}
 
   template <class T>
   std::vector<T> allgather_value(const T& v) {

@@ -45,6 +45,15 @@ void clear_abort_hooks() {
   hooks().clear();
 }
 
+void run_abort_hooks(int code) {
+  std::vector<std::pair<int, AbortHook>> hs;
+  {
+    std::lock_guard<std::mutex> lk(g_hook_mu);
+    hs.swap(hooks());
+  }
+  for (auto it = hs.rbegin(); it != hs.rend(); ++it) it->second(code);
+}
+
 void set_throw_on_fatal(bool enable) { g_throw = enable; }
 
 void fatal(const char* file, int line, const std::string& what) {

@@ -23,6 +23,10 @@ using AbortHook = std::function<void(int code)>;
 int push_abort_hook(AbortHook hook);  // returns a handle for remove_abort_hook
 void remove_abort_hook(int handle);
 void clear_abort_hooks();
+// Runs (and removes) every registered hook, innermost first, without exiting:
+// a watchdog that must end the process calls it so RCCL communicators are
+// aborted (their kernels exit) before the process goes.
+void run_abort_hooks(int code);
 
 [[noreturn]] void fatal(const char* file, int line, const std::string& what);
 

@@ -109,7 +109,9 @@ struct PingRole {
   const unsigned long long* in_flag;   // own inbox flag (written by the peer)
   const unsigned char* in_payload;     // own inbox payload
   unsigned long long bytes;            // payload bytes, multiple of 16, >= 16
-  unsigned long long base;             // sequence base
+  unsigned long long base;             // sequence base of what this wave writes (iteration i: base + i + 1)
+  unsigned long long in_base;          // sequence base of what it waits for (== base for a ping-pong pair;
+                                       // a ring token chain reads its predecessor's count, writes its own)
   int iters;
   int leader;
   unsigned long long* stamps;          // leader: iters + 1 entries

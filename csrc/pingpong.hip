@@ -1,5 +1,5 @@
-// Device-initiated ping-pong and stream-ordered flag signalling over
-// hipIpc-mapped memory (IPC transport).
+// Device-initiated ping-pong, ring token chain and stream-ordered flag
+// signalling over hipIpc-mapped memory (IPC transport).
 //
 // The reference has no latency measurement at all; the host-
 // posted ping-pong in runner.cpp (run_latency) measures what an application
@@ -10,6 +10,12 @@
 //   leader:   write payload (seq) into the peer's inbox -> release flag=seq
 //             -> spin on its own inbox flag until >= seq -> timestamp
 //   follower: spin until its inbox flag >= seq -> check payload -> reply
+//
+// The same kernel runs the ring token chain (pipeline-parallel hop latency,
+// runner.cpp run_ring_latency): every rank's `out` is its successor's inbox,
+// its `in` is the slot its predecessor writes; rank 0 leads (writes, then
+// waits for the token to come round), every other rank follows (waits, then
+// forwards), so one leader iteration is one lap of N dependent hops.
 //
 // Stores to the peer travel over xGMI (remote writes, the direction xGMI and
 // RCCL's LL protocols favour); the spin is on local memory.  Flags are
@@ -48,7 +54,8 @@ __device__ __forceinline__ bool ping_wait(const PingRole& r, u64 seq, u64 deadli
   return true;
 }
 
-// After the acquire: first and last 16 B of the payload must carry seq.
+// After the acquire: first and last 16 B of the payload must carry seq (the
+// writer's sequence number for this message).
 __device__ __forceinline__ void ping_check(const PingRole& r, u64 seq, int lane) {
   if (lane < 2) {
     const u64 off = lane == 0 ? 0 : r.bytes - 16;
@@ -65,22 +72,24 @@ __global__ __launch_bounds__(128) void pingpong_kernel(PingRole a, PingRole b) {
     if (lane == 0) r.stamps[0] = now_ticks();
     for (int i = 0; i < r.iters; ++i) {
       const u64 seq = r.base + static_cast<u64>(i) + 1;
+      const u64 want = r.in_base + static_cast<u64>(i) + 1;
       ping_send(r, seq, lane);
-      if (!ping_wait(r, seq, deadline)) {
+      if (!ping_wait(r, want, deadline)) {
         if (lane == 0) atomicOr(r.status, 1u);
         return;
       }
-      ping_check(r, seq, lane);
+      ping_check(r, want, lane);
       if (lane == 0) r.stamps[i + 1] = now_ticks();
     }
   } else {
     for (int i = 0; i < r.iters; ++i) {
       const u64 seq = r.base + static_cast<u64>(i) + 1;
-      if (!ping_wait(r, seq, deadline)) {
+      const u64 want = r.in_base + static_cast<u64>(i) + 1;
+      if (!ping_wait(r, want, deadline)) {
         if (lane == 0) atomicOr(r.status, 1u);
         return;
       }
-      ping_check(r, seq, lane);
+      ping_check(r, want, lane);
       ping_send(r, seq, lane);
     }
   }

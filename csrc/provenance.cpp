@@ -1,0 +1,107 @@
+#include "provenance.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "bootstrap.hpp"
+#include "common.hpp"
+#include "report.hpp"
+#include "topology.hpp"
+
+extern char** environ;
+
+namespace p2p {
+
+namespace {
+
+bool is_knob(const std::string& name) {
+  static const char* kPrefixes[] = {"NCCL_", "RCCL_", "HSA_", "HIP_", "ROCR_", "GPU_", "AMD_", "P2P_", "ROCM_", "MSCCL"};
+  for (const char* p : kPrefixes)
+    if (name.rfind(p, 0) == 0) return true;
+  return name == "CUDA_VISIBLE_DEVICES" || name == "OMP_NUM_THREADS";
+}
+
+std::string quoted(const std::string& s) { return "\"" + json_escape(s) + "\""; }
+
+}  // namespace
+
+std::string env_knobs_json() {
+  std::vector<std::pair<std::string, std::string>> kv;
+  for (char** e = environ; e && *e; ++e) {
+    const char* eq = std::strchr(*e, '=');
+    if (!eq) continue;
+    std::string name(*e, static_cast<size_t>(eq - *e));
+    if (is_knob(name)) kv.emplace_back(name, eq + 1);
+  }
+  std::sort(kv.begin(), kv.end());
+  std::string o = "{";
+  bool hwq = false;
+  for (size_t i = 0; i < kv.size(); ++i) {
+    o += (i ? "," : "") + quoted(kv[i].first) + ":" + quoted(kv[i].second);
+    hwq = hwq || kv[i].first == "GPU_MAX_HW_QUEUES";
+  }
+  // HIP's hardware queues per process bound how many communicators' kernels
+  // run side by side (docs/DESIGN.md §3); unset means the runtime default, 4.
+  if (!hwq) o += std::string(kv.empty() ? "" : ",") + "\"GPU_MAX_HW_QUEUES\":null";
+  return o + "}";
+}
+
+std::string runtime_json() {
+  int n = 0;
+  auto links = probe_topology(&n);
+  std::string o = "{\"hip\":" + hip_runtime_json() + ",\"rccl\":" + rccl_runtime_json() +
+                  strfmt(",\"visible_devices\":%d,\"device_links\":[", n);
+  for (int a = 0; a < n; ++a) {
+    o += a ? ",[" : "[";
+    for (int b = 0; b < n; ++b) {
+      const LinkInfo& li = links[static_cast<size_t>(a) * n + b];
+      o += (b ? "," : "") + quoted(a == b ? "self" : strfmt("%s/%d", li.type.c_str(), li.hops));
+    }
+    o += "]";
+  }
+  return o + "]}";
+}
+
+std::string provenance_json(Bootstrap& boot, int device) {
+  struct RankDev {
+    int32_t device;
+    char pci[60];
+    uint64_t host;
+  };
+  RankDev mine{};
+  mine.device = device;
+  std::snprintf(mine.pci, sizeof(mine.pci), "%s", device >= 0 ? device_pci_id(device).c_str() : "");
+  mine.host = host_hash(real_hostname());
+  auto all = boot.allgather_value(mine);
+  const int n = boot.size();
+  int ndev = 0;
+  auto links = probe_topology(&ndev);
+  std::string o = "{\"type\":\"provenance\",\"runtime\":" + runtime_json() + ",\"env\":" + env_knobs_json() +
+                  ",\"rank_devices\":[";
+  for (int r = 0; r < n; ++r)
+    o += strfmt("%s{\"rank\":%d,\"device\":%d,\"pci\":%s}", r ? "," : "", r, all[static_cast<size_t>(r)].device,
+                quoted(all[static_cast<size_t>(r)].pci).c_str());
+  // Link between the GPUs of every two ranks, from this host's probe (ranks
+  // on other hosts, or ranks without a GPU, read "n/a").
+  o += "],\"rank_links\":[";
+  for (int a = 0; a < n; ++a) {
+    o += a ? ",[" : "[";
+    for (int b = 0; b < n; ++b) {
+      const int da = all[static_cast<size_t>(a)].device, db = all[static_cast<size_t>(b)].device;
+      std::string v = "n/a";
+      const bool local = all[static_cast<size_t>(a)].host == mine.host && all[static_cast<size_t>(b)].host == mine.host;
+      if (local && da >= 0 && db >= 0 && da < ndev && db < ndev) {
+        const LinkInfo& li = links[static_cast<size_t>(da) * ndev + db];
+        v = da == db ? "same-gpu" : strfmt("%s/%d", li.type.c_str(), li.hops);
+      }
+      o += (b ? "," : "") + quoted(v);
+    }
+    o += "]";
+  }
+  return o + "]}";
+}
+
+}  // namespace p2p

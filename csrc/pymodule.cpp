@@ -20,6 +20,7 @@
 #include "bootstrap.hpp"
 #include "common.hpp"
 #include "kernels.hpp"
+#include "provenance.hpp"
 #include "report.hpp"
 #include "runner.hpp"
 #include "routing.hpp"
@@ -124,6 +125,23 @@ class Session {
     return latency_to_json(run_device_latency(*t_, *boot_, bytes, iters, warmup), world());
   }
 
+  // Dependent ring token chain (runner.hpp run_ring_latency); device=true
+  // runs it as the one-wave kernel of the IPC transport.
+  std::string ring_latency(size_t bytes, int laps, int warmup, bool device) {
+    if (device) return ring_latency_to_json(run_device_ring_latency(*t_, *boot_, bytes, laps, warmup));
+    Buffers bufs(*t_, std::max<size_t>(bytes, 16), 1);
+    return ring_latency_to_json(run_ring_latency(*t_, *boot_, bytes, laps, warmup, bufs));
+  }
+
+  // Bounds every later wait of this session (transport and bootstrap).
+  void set_timeout(double seconds) {
+    t_->set_timeout(seconds);
+    boot_->set_timeout(seconds);
+  }
+
+  // Collective: provenance_json() for this session's ranks.
+  std::string provenance(int device) { return provenance_json(*boot_, device); }
+
  private:
   std::unique_ptr<Bootstrap> boot_;
   std::unique_ptr<Transport> t_;
@@ -134,10 +152,10 @@ class Session {
 class PyStepDriver {
  public:
   PyStepDriver(std::shared_ptr<Session> s, const std::string& mode, const std::string& dir, size_t bytes, int msgs,
-               bool verify, bool batch, bool graph)
+               bool verify, bool batch, bool graph, int depth, size_t recv_budget, uint64_t salt)
       : session_(std::move(s)),
         d_(session_->t(), session_->boot(), make_schedule(parse_mode(mode), parse_direction(dir), session_->world()),
-           bytes, msgs, verify, 0, StepOptions{batch, graph}) {}
+           bytes, msgs, verify, salt, StepOptions{batch, graph, depth, recv_budget}) {}
   StepDriver& d() { return d_; }
 
  private:
@@ -233,14 +251,43 @@ PYBIND11_MODULE(_p2pcore, m) {
       .def("fuzz", &Session::fuzz, py::arg("rounds") = 20, py::arg("seed") = 1, py::arg("max_bytes") = size_t{4} << 20,
            py::call_guard<py::gil_scoped_release>(),
            "Random groups of verified messages through the transport (collective); returns mismatching words.")
+      .def("ring_latency", &Session::ring_latency, py::arg("bytes") = 8, py::arg("laps") = 200, py::arg("warmup") = 20,
+           py::arg("device") = false, py::call_guard<py::gil_scoped_release>(),
+           "Dependent ring token chain 0 -> 1 -> ... -> 0 (collective); JSON with per-hop and per-lap times.")
+      .def("set_timeout", &Session::set_timeout, py::arg("seconds"),
+           "Bounds every later wait of the session (transport sync / rendezvous, bootstrap receives).")
+      .def("provenance", &Session::provenance, py::arg("device") = -1, py::call_guard<py::gil_scoped_release>(),
+           "Collective: runtime, RCCL library, knobs, every rank's GPU and the links between them (JSON).")
       .def("_unmatched_recv", &Session::unmatched_recv, py::arg("bytes") = size_t{1} << 20,
            py::call_guard<py::gil_scoped_release>(), "Test hook: a receive no send matches; returns the watchdog's error.");
 
   py::class_<PyStepDriver>(m, "StepDriver")
-      .def(py::init<std::shared_ptr<Session>, const std::string&, const std::string&, size_t, int, bool, bool, bool>(),
+      .def(py::init<std::shared_ptr<Session>, const std::string&, const std::string&, size_t, int, bool, bool, bool, int,
+                    size_t, uint64_t>(),
            py::arg("session"), py::arg("mode") = "tournament", py::arg("dir") = "bi", py::arg("bytes") = 32u << 20,
            py::arg("msgs") = 8, py::arg("verify") = false, py::arg("batch") = false, py::arg("graph") = false,
+           py::arg("depth") = 1, py::arg("recv_budget") = size_t{0}, py::arg("salt") = uint64_t{0},
            py::call_guard<py::gil_scoped_release>())
+      .def("poison", [](PyStepDriver& s) { s.d().poison(); }, py::call_guard<py::gil_scoped_release>(),
+           "Collective: zero every receive slot (after the warmup, before the timed steps).")
+      .def("verify_steps", [](PyStepDriver& s, long first, long count) {
+            StepVerifyReport r;
+            {
+              py::gil_scoped_release nogil;
+              r = s.d().verify_steps(first, count);
+            }
+            py::dict d;
+            d["mismatches"] = r.mismatches;
+            d["verified_msgs"] = r.verified_msgs;
+            d["timed_msgs"] = r.timed_msgs;
+            d["slots"] = r.slots;
+            return d;
+          }, py::arg("first"), py::arg("count"),
+           "Collective: checks every receive slot steps [first, first+count) wrote (all ranks' totals).")
+      .def("flows_per_step", [](PyStepDriver& s, long k) { return s.d().flows_per_step(k); })
+      .def_property_readonly("depth", [](PyStepDriver& s) { return s.d().depth(); })
+      .def_property_readonly("msgs", [](PyStepDriver& s) { return s.d().msgs(); })
+      .def_property_readonly("recv_bytes", [](PyStepDriver& s) { return s.d().recv_bytes(); })
       .def("connect", [](PyStepDriver& s) { s.d().connect(); }, py::call_guard<py::gil_scoped_release>())
       .def("step", [](PyStepDriver& s, long k) { s.d().step(k); }, py::call_guard<py::gil_scoped_release>())
       .def("run_steps", [](PyStepDriver& s, long first, long count) {
@@ -294,6 +341,11 @@ PYBIND11_MODULE(_p2pcore, m) {
     return py::make_tuple(g.grid, g.block, g.lds_bytes);
   });
   m.def("rccl_available", &rccl_transport_available);
+  m.def("runtime_json", &runtime_json, "HIP runtime / RCCL library versions and paths, visible devices and links.");
+  m.def("env_knobs_json", &env_knobs_json, "Every NCCL_/RCCL_/HSA_/HIP_/GPU_... environment knob that is set.");
+  m.def("run_abort_hooks", []() { run_abort_hooks(1); }, py::call_guard<py::gil_scoped_release>(),
+        "Aborts every live RCCL communicator / bootstrap (their kernels exit); for a watchdog about to end the "
+        "process.");
 
   // ---- host reference (bit-compatible with the kernels) ----
   m.def("host_fill", [](size_t bytes, uint64_t seed) {

@@ -215,6 +215,21 @@ std::string latency_to_json(const std::vector<LatencyResult>& lat, int n) {
   return o.str();
 }
 
+std::string ring_latency_to_json(const RingLatencyResult& r) {
+  return strfmt("{\"type\":\"ring_latency\",\"method\":\"%s\",\"nranks\":%d,\"bytes\":%zu,\"laps\":%d,\"hop_us\":%s,"
+                "\"lap_us\":%s}",
+                r.method.c_str(), r.nranks, r.bytes, r.laps, summary_json(r.hop_us).c_str(), summary_json(r.lap_us).c_str());
+}
+
+void print_ring_latency(FILE* out, const RingLatencyResult& r) {
+  std::fprintf(out, "\n== ring token latency: %d rank(s), %s, %s dependent chain 0 -> 1 -> ... -> 0, %d laps ==\n",
+               r.nranks, format_size(r.bytes).c_str(),
+               r.method == "device" ? "device-initiated (one wave per GPU)" : "host-posted", r.laps);
+  std::fprintf(out, "  per hop (lap / %d): p50 %.2f  p99 %.2f us   per lap: p50 %.2f  p99 %.2f us\n", r.nranks,
+               r.hop_us.p50, r.hop_us.p99, r.lap_us.p50, r.lap_us.p99);
+  std::fflush(out);
+}
+
 std::string chrome_trace(const std::vector<RunRecord>& runs, int n) {
   double t0 = 0;
   bool have = false;

@@ -56,6 +56,9 @@ void print_matrix(FILE* out, const std::string& title, const std::vector<double>
 // Machine-readable JSON (one object per run / latency set).
 std::string run_to_json(const RunRecord& rec, int n);
 std::string latency_to_json(const std::vector<LatencyResult>& lat, int n);
+// {"type":"ring_latency","method":...,"nranks":N,"bytes":B,"laps":L,"hop_us":{...},"lap_us":{...}}
+std::string ring_latency_to_json(const RingLatencyResult& r);
+void print_ring_latency(FILE* out, const RingLatencyResult& r);
 
 // CSV rows: mode,dir,bytes,iters,timing,phase,src,dst,seconds,gbps,gbs,p50_us,p99_us,mismatches
 std::string csv_header();

@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <exception>
+#include <map>
 #include <thread>
 
 #include "bootstrap.hpp"
@@ -24,20 +25,33 @@ Timing parse_timing(const std::string& s) {
 
 // ------------------------------------------------------------- Buffers ----
 
-Buffers::Buffers(Transport& t, size_t max_bytes, int recv_slots) : t_(t), cap_(std::max<size_t>(max_bytes, 16)) {
-  // One send buffer + one receive slot per concurrent peer, all sized for the
-  // largest message: check against free HBM up front so a 288 GB sweep fails
-  // with an explanation instead of a hipMalloc error mid-run.
+namespace {
+size_t slot_stride(size_t bytes) { return (std::max<size_t>(bytes, 16) + 4095) / 4096 * 4096; }
+}  // namespace
+
+Buffers::Buffers(Transport& t, size_t slot_bytes, int recv_slots, size_t send_bytes)
+    : t_(t), cap_(std::max<size_t>(slot_bytes, 16)), send_cap_(std::max(send_bytes, cap_)), stride_(slot_stride(cap_)),
+      nslots_(std::max(recv_slots, 1)) {
+  // One send buffer + one receive arena: check against free HBM up front so a
+  // 288 GB sweep fails with an explanation instead of a hipMalloc error mid-run.
   size_t free_b = 0, total_b = 0;
-  const double need = static_cast<double>(cap_) * (1.0 + recv_slots);
+  const double arena = static_cast<double>(stride_) * static_cast<double>(nslots_);
+  const double need = static_cast<double>(send_cap_) + arena;
   if (t_.mem_info(&free_b, &total_b) && need > 0.98 * static_cast<double>(free_b))
-    P2P_FATAL(strfmt("buffers need %.2f GiB (%d x %s) but only %.2f of %.2f GiB are free on this GPU; use a smaller "
-                     "--size/--sizes maximum or a mode with fewer concurrent peers",
-                     need / (1ull << 30), recv_slots + 1, format_size(cap_).c_str(),
+    P2P_FATAL(strfmt("buffers need %.2f GiB (send %s + %d receive slots of %s) but only %.2f of %.2f GiB are free on "
+                     "this GPU; use a smaller --size/--sizes maximum or a mode with fewer concurrent peers",
+                     need / (1ull << 30), format_size(send_cap_).c_str(), nslots_, format_size(cap_).c_str(),
                      static_cast<double>(free_b) / (1ull << 30), static_cast<double>(total_b) / (1ull << 30)));
-  send_ = t_.alloc(cap_);
-  for (int i = 0; i < recv_slots; ++i) recv_.push_back(t_.alloc(cap_));
-  t_.register_buffers(send_, recv_, cap_);
+  send_ = t_.alloc(send_cap_);
+  recv_ = t_.alloc(stride_ * static_cast<size_t>(nslots_));
+  Transport::BufferSet set;
+  set.send = send_;
+  set.send_bytes = send_cap_;
+  set.recv = recv_;
+  set.stride = stride_;
+  set.slot_bytes = cap_;
+  set.nslots = nslots_;
+  t_.register_buffers(set);
 }
 
 Buffers::~Buffers() {
@@ -46,11 +60,16 @@ Buffers::~Buffers() {
   // on, so the first error is the one that surfaces.
   try {
     t_.unregister_buffers(send_);
-    for (void* p : recv_) t_.release(p);
+    if (recv_) t_.release(recv_);
     if (send_) t_.release(send_);
   } catch (const std::exception& e) {
     std::fprintf(stderr, "p2p_matrix: buffer teardown failed: %s\n", e.what());
   }
+}
+
+void* Buffers::recv_buf(int slot) const {
+  P2P_CHECK(slot >= 0 && slot < nslots_, strfmt("receive slot %d of %d", slot, nslots_));
+  return static_cast<char*>(recv_) + stride_ * static_cast<size_t>(slot);
 }
 
 // -------------------------------------------------------------- helpers ----
@@ -60,6 +79,23 @@ int remote_slot(const Phase& phase, int me, int peer) {
   auto it = std::find(from.begin(), from.end(), me);
   P2P_CHECK(it != from.end(), strfmt("rank %d sends to %d, which does not receive from it", me, peer));
   return static_cast<int>(it - from.begin());
+}
+
+std::vector<int> remote_slots(const Phase& phase, int me) {
+  const auto& to = phase.ranks[static_cast<size_t>(me)].send_to;
+  std::vector<int> out;
+  out.reserve(to.size());
+  for (size_t j = 0; j < to.size(); ++j) {
+    const int peer = to[j];
+    const int kth = static_cast<int>(std::count(to.begin(), to.begin() + static_cast<long>(j), peer));
+    const auto& from = phase.ranks[static_cast<size_t>(peer)].recv_from;
+    int seen = 0, slot = -1;
+    for (size_t i = 0; i < from.size() && slot < 0; ++i)
+      if (from[i] == me && seen++ == kth) slot = static_cast<int>(i);
+    P2P_CHECK(slot >= 0, strfmt("rank %d sends to %d, which does not receive from it", me, peer));
+    out.push_back(slot);
+  }
+  return out;
 }
 
 namespace {
@@ -95,9 +131,10 @@ bool posts_phase(const Transport& t, const Phase& phase, int r) {
 
 void post_phase_iteration(Transport& t, const Phase& phase, size_t bytes, Buffers& bufs) {
   const RankOps& ops = phase.ranks[static_cast<size_t>(t.rank())];
+  const std::vector<int> rs = remote_slots(phase, t.rank());
   t.group_begin();
   if (t.wants_group_flows()) t.group_flows(bufs.send_buf(), group_flow_list(phase), bytes);
-  for (int peer : ops.send_to) t.send_to_slot(bufs.send_buf(), bytes, peer, remote_slot(phase, t.rank(), peer));
+  for (size_t j = 0; j < ops.send_to.size(); ++j) t.send_to_slot(bufs.send_buf(), bytes, ops.send_to[j], rs[j]);
   for (size_t i = 0; i < ops.recv_from.size(); ++i) t.recv(bufs.recv_buf(static_cast<int>(i)), bytes, ops.recv_from[i]);
   t.group_end();
 }
@@ -117,6 +154,9 @@ void prepare_payload(Transport& t, const Phase& phase, const RunConfig& cfg, Buf
 // "<kind>@<rank>[:<phase>]" with kind one of
 //   corrupt — zero the first 64 B of receive slot 0 after the timed loop
 //             (verification must report it, exit code 2),
+//   skip    — the rank's transport silently moves no payload during the
+//             timed iterations (Transport::set_discard; the protocol still
+//             runs, so nothing hangs): verification must report it, exit 2,
 //   exit    — the rank dies abruptly (peers must fail, not hang),
 //   hang    — the rank stops responding (peers' watchdogs must fire).
 struct FaultSpec {
@@ -143,9 +183,15 @@ const FaultSpec& fault_spec() {
   return spec;
 }
 
+bool fault_applies(const char* kind, int rank, long phase_index) {
+  const FaultSpec& f = fault_spec();
+  if (f.kind != kind || f.rank != rank) return false;
+  return f.phase < 0 || f.phase == phase_index;
+}
+
 void maybe_inject_fault(Transport& t, Buffers& bufs, int rank, size_t phase_index, size_t bytes) {
   const FaultSpec& f = fault_spec();
-  if (f.kind.empty() || f.rank != rank) return;
+  if (f.kind.empty() || f.kind == "skip" || f.rank != rank) return;
   if (f.phase >= 0 && static_cast<size_t>(f.phase) != phase_index) return;
   if (f.kind == "corrupt") {
     if (bufs.slots() > 0) {
@@ -197,6 +243,22 @@ PhaseResult run_phase(Transport& t, Bootstrap& boot, const Phase& phase, size_t 
     for (int i = 0; i < cfg.warmup; ++i) post_phase_iteration(t, phase, cfg.bytes, bufs);
     t.sync();
   }
+  if (cfg.verify && cfg.warmup > 0) {
+    // The warmup delivered the payload already: poison the slots again (after
+    // every rank drained its warmup), so the check after timing passes only
+    // for data the timed iterations delivered.
+    boot.barrier();
+    if (active) {
+      const RankOps& ops = phase.ranks[static_cast<size_t>(me)];
+      for (size_t i = 0; i < ops.recv_from.size(); ++i) t.zero(bufs.recv_buf(static_cast<int>(i)), cfg.bytes);
+      t.sync();
+    }
+  }
+  const bool skip = active && fault_applies("skip", me, static_cast<long>(phase_index));
+  if (skip) {
+    std::fprintf(stderr, "[p2p] injected fault: rank %d moves no payload in the timed iterations\n", me);
+    t.set_discard(true);
+  }
 
   double my_seconds = 0;
   std::vector<double> iter_samples;
@@ -242,6 +304,7 @@ PhaseResult run_phase(Transport& t, Bootstrap& boot, const Phase& phase, size_t 
   }
   const double w1 = now_seconds();
   res.wall_seconds = w1 - w0;
+  if (skip) t.set_discard(false);
 
   if (active) maybe_inject_fault(t, bufs, me, phase_index, cfg.bytes);
 
@@ -453,6 +516,92 @@ std::vector<LatencyResult> run_device_latency(Transport& t, Bootstrap& boot, siz
   return out;
 }
 
+// ------------------------------------------------------ ring token chain ----
+
+namespace {
+RingLatencyResult ring_result(Bootstrap& boot, size_t bytes, int laps, const std::vector<double>& lap_us,
+                              const char* method) {
+  // Rank 0's samples, for every rank.
+  const Summary lap = summarize(lap_us);
+  std::vector<double> hop;
+  for (double v : lap_us) hop.push_back(v / boot.size());
+  const Summary h = summarize(hop);
+  RingLatencyResult r;
+  r.nranks = boot.size();
+  r.bytes = bytes;
+  r.laps = laps;
+  r.lap_us = boot.allgather_value(lap)[0];
+  r.hop_us = boot.allgather_value(h)[0];
+  r.method = method;
+  return r;
+}
+}  // namespace
+
+RingLatencyResult run_ring_latency(Transport& t, Bootstrap& boot, size_t bytes, int laps, int warmup, Buffers& bufs) {
+  const int n = boot.size(), me = boot.rank();
+  P2P_CHECK(bytes <= bufs.capacity() && laps >= 1 && warmup >= 0, "ring latency: bad arguments");
+  const int succ = (me + 1) % n, pred = (me + n - 1) % n;
+  auto lap = [&]() {
+    if (n == 1) {
+      t.group_begin();
+      t.send(bufs.send_buf(), bytes, me);
+      t.recv(bufs.recv_buf(0), bytes, me);
+      t.group_end();
+      return;
+    }
+    auto send = [&] { t.group_begin(); t.send_to_slot(bufs.send_buf(), bytes, succ, 0); t.group_end(); };
+    auto recv = [&] { t.group_begin(); t.recv(bufs.recv_buf(0), bytes, pred); t.group_end(); };
+    if (me == 0) {
+      send();
+      recv();
+    } else {
+      recv();
+      send();
+    }
+  };
+  for (int i = 0; i < warmup; ++i) lap();
+  t.sync();
+  boot.barrier();
+  t.clear_marks();
+  std::vector<int> marks{t.mark()};
+  for (int i = 0; i < laps; ++i) {
+    lap();
+    marks.push_back(t.mark());
+  }
+  t.sync();
+  std::vector<double> us;
+  if (me == 0)
+    for (size_t i = 1; i < marks.size(); ++i) us.push_back(t.elapsed_ms(marks[i - 1], marks[i]) * 1e3);
+  boot.barrier();
+  return ring_result(boot, bytes, laps, us, "host");
+}
+
+RingLatencyResult run_device_ring_latency(Transport& t, Bootstrap& boot, size_t bytes, int laps, int warmup) {
+  P2P_CHECK(t.supports_device_pingpong(),
+            "device ring latency needs a one-sided transport (--transport ipc); " + t.name() + " has none");
+  P2P_CHECK(laps >= 1 && warmup >= 0, "device ring latency: bad arguments");
+  const int n = boot.size(), me = boot.rank();
+  t.pingpong_setup();
+  std::vector<double> us;
+  if (n == 1) {
+    // One rank: the token's hop is a self round trip through its own inbox.
+    boot.barrier();
+    us = t.device_pingpong(me, bytes, warmup + laps);
+    us.erase(us.begin(), us.begin() + std::min<size_t>(us.size(), static_cast<size_t>(warmup)));
+    for (double& v : us) v *= 2.0;  // device_pingpong returns half round trips
+  } else {
+    const int succ = (me + 1) % n, pred = (me + n - 1) % n;
+    if (warmup > 0) {
+      boot.barrier();  // every rank's kernel starts together (each spin has a deadline)
+      t.device_ring_token(pred, succ, me == 0, bytes, warmup);
+    }
+    boot.barrier();
+    us = t.device_ring_token(pred, succ, me == 0, bytes, laps);
+  }
+  boot.barrier();
+  return ring_result(boot, std::max<size_t>(16, (bytes + 15) / 16 * 16), laps, us, "device");
+}
+
 // ----------------------------------------------------------------- fuzz ----
 
 uint64_t fuzz_transport(Transport& t, Bootstrap& boot, int rounds, uint64_t seed, size_t max_bytes) {
@@ -513,82 +662,163 @@ uint64_t fuzz_transport(Transport& t, Bootstrap& boot, int rounds, uint64_t seed
 
 // ---------------------------------------------------------- StepDriver ----
 
+namespace {
+
+// [rank][phase] -> first slot of the phase within a generation; the last
+// entry of each row is the generation size.
+std::vector<std::vector<int>> step_layout(const Schedule& s, int msgs) {
+  P2P_CHECK(msgs >= 1, "msgs per step must be >= 1");
+  std::vector<std::vector<int>> base(static_cast<size_t>(s.nranks));
+  for (int r = 0; r < s.nranks; ++r) {
+    int at = 0;
+    for (const Phase& p : s.phases) {
+      base[static_cast<size_t>(r)].push_back(at);
+      at += p.recv_slots(r) * msgs;
+    }
+    base[static_cast<size_t>(r)].push_back(at);
+  }
+  return base;
+}
+
+std::vector<int> generation_sizes(const std::vector<std::vector<int>>& base) {
+  std::vector<int> out;
+  for (const auto& row : base) out.push_back(row.back());
+  return out;
+}
+
+// Receive generations: as many as asked and the budget allows, the same on
+// every rank (every rank computes every peer's slot numbers).
+int agreed_depth(Transport& t, Bootstrap& boot, const StepOptions& o, size_t per_gen_bytes) {
+  long d = std::max(1, o.depth);
+  size_t budget = o.recv_budget;
+  if (budget == 0) {
+    size_t free_b = 0, total_b = 0;
+    budget = t.mem_info(&free_b, &total_b) ? free_b / 4 : size_t{256} << 20;
+  }
+  if (per_gen_bytes > 0) d = std::min<long>(d, std::max<long>(1, static_cast<long>(budget / per_gen_bytes)));
+  return static_cast<int>(-boot.allreduce_max(-static_cast<double>(d)));
+}
+
+}  // namespace
+
 StepDriver::StepDriver(Transport& t, Bootstrap& boot, Schedule sched, size_t bytes, int msgs, bool verify, uint64_t salt,
                        StepOptions opt)
     : t_(t), boot_(boot), sched_(std::move(sched)), bytes_(bytes), msgs_(msgs), verify_(verify), salt_(salt), opt_(opt),
-      bufs_(t, bytes, std::max(1, sched_.max_recv_slots())) {
+      phase_base_(step_layout(sched_, msgs)), gen_slots_(generation_sizes(phase_base_)),
+      depth_(agreed_depth(t, boot, opt, slot_stride(bytes) * static_cast<size_t>(gen_slots_.at(static_cast<size_t>(t.rank()))))),
+      bufs_(t, bytes, std::max(1, depth_ * gen_slots_[static_cast<size_t>(t.rank())]),
+            slot_stride(bytes) * static_cast<size_t>(msgs)) {
   if (opt_.graph && !t_.supports_graphs()) opt_.graph = false;
   std::string bad = validate(sched_);
   P2P_CHECK(bad.empty(), "invalid schedule: " + bad);
   P2P_CHECK(!sched_.phases.empty(), "empty schedule");
-  P2P_CHECK(msgs_ >= 1, "msgs per step must be >= 1");
-  t_.fill(bufs_.send_buf(), bytes_, payload_seed(t_.rank(), bytes_, salt_));
-  if (verify_)
-    for (int i = 0; i < bufs_.slots(); ++i) t_.zero(bufs_.recv_buf(i), bytes_);
+  P2P_CHECK(sched_.nranks == t_.nranks(), "schedule and transport disagree on the number of ranks");
+  // Message m is sent from region m; regions start at 4 KiB boundaries like
+  // the receive slots, so every kernel sees 16-byte aligned payloads.
+  for (int m = 0; m < msgs_; ++m) t_.fill(bufs_.send_at(region_offset(m)), bytes_, msg_seed(t_.rank(), m));
+  if (verify_) t_.zero(bufs_.recv_base(), recv_bytes());
   t_.sync();
 }
 
-StepDriver::~StepDriver() = default;
+StepDriver::~StepDriver() {
+  if (skip_armed_) t_.set_discard(false);
+}
+
+int StepDriver::slot_index(int rank, int gen, int phase, int msg, int i) const {
+  const Phase& p = sched_.phases[static_cast<size_t>(phase)];
+  const int r = p.recv_slots(rank);
+  P2P_CHECK(i >= 0 && i < r && msg >= 0 && msg < msgs_ && gen >= 0 && gen < depth_, "bad step slot");
+  return gen * gen_slots_[static_cast<size_t>(rank)] + phase_base_[static_cast<size_t>(rank)][static_cast<size_t>(phase)] +
+         msg * r + i;
+}
+
+size_t StepDriver::region_offset(int msg) const { return slot_stride(bytes_) * static_cast<size_t>(msg); }
+
+uint64_t StepDriver::msg_seed(int src, int msg) const {
+  return payload_seed(src, bytes_, salt_ * 1000003ull + static_cast<uint64_t>(msg) + 1);
+}
 
 void StepDriver::connect() {
   warm_connections(t_, boot_, sched_, bufs_, std::min<size_t>(bytes_, 4096));
   // One full step of every phase: small messages may take another path than
   // the step's (RCCL with several communicators keeps them on the first), so
   // every connection the timed steps use is made here, not in a timed step.
-  for (const Phase& p : sched_.phases)
-    if (posts_phase(t_, p, t_.rank())) post_step_ops(p);
+  for (size_t pi = 0; pi < sched_.phases.size(); ++pi)
+    if (posts_phase(t_, sched_.phases[pi], t_.rank())) post_step_ops(sched_.phases[pi], static_cast<int>(pi), 0);
   t_.sync();
   boot_.barrier();
-  // Restore the payload the tiny warm-up may have overwritten on receivers.
-  if (verify_)
-    for (int i = 0; i < bufs_.slots(); ++i) t_.zero(bufs_.recv_buf(i), bytes_);
+  if (verify_) t_.zero(bufs_.recv_base(), recv_bytes());
   t_.sync();
   // Graph capture only records launches (no peer interaction), so it must
   // follow the warm-up that established every lazy connection.
   if (opt_.graph && graphs_.empty()) {
-    for (const Phase& p : sched_.phases) {
-      if (!p.participates(t_.rank())) {
-        graphs_.push_back(-1);
-        continue;
+    for (int g = 0; g < depth_; ++g)
+      for (size_t pi = 0; pi < sched_.phases.size(); ++pi) {
+        const Phase& p = sched_.phases[pi];
+        if (!p.participates(t_.rank())) {
+          graphs_.push_back(-1);
+          continue;
+        }
+        t_.capture_begin();
+        post_step_ops(p, static_cast<int>(pi), g);
+        graphs_.push_back(t_.capture_end());
       }
-      t_.capture_begin();
-      post_step_ops(p);
-      graphs_.push_back(t_.capture_end());
-    }
     boot_.barrier();
   }
 }
 
-void StepDriver::post_step_ops(const Phase& p) {
-  if (!opt_.batch) {
-    for (int m = 0; m < msgs_; ++m) post_phase_iteration(t_, p, bytes_, bufs_);
-    return;
-  }
-  // One group: every message of the step, fused into one launch by RCCL.
-  const RankOps& ops = p.ranks[static_cast<size_t>(t_.rank())];
+void StepDriver::post_step_ops(const Phase& p, int pi, int gen) {
+  const int me = t_.rank();
+  const RankOps& ops = p.ranks[static_cast<size_t>(me)];
+  const std::vector<int> rs = remote_slots(p, me);
   const bool all_flows = t_.wants_group_flows();
-  const std::vector<Transport::GroupFlow> flows = all_flows ? group_flow_list(p) : std::vector<Transport::GroupFlow>();
-  t_.group_begin();
-  for (int m = 0; m < msgs_; ++m) {
-    if (all_flows) t_.group_flows(bufs_.send_buf(), flows, bytes_);
-    for (int peer : ops.send_to) t_.send_to_slot(bufs_.send_buf(), bytes_, peer, remote_slot(p, t_.rank(), peer));
-    for (size_t i = 0; i < ops.recv_from.size(); ++i) t_.recv(bufs_.recv_buf(static_cast<int>(i)), bytes_, ops.recv_from[i]);
+  std::vector<int> fslot;
+  if (all_flows) fslot = flow_slots(p);
+  auto one_message = [&](int m) {
+    const size_t off = region_offset(m);
+    if (all_flows) {
+      std::vector<Transport::GroupFlow> flows(p.flows.size());
+      for (size_t i = 0; i < p.flows.size(); ++i) {
+        flows[i].src = p.flows[i].src;
+        flows[i].dst = p.flows[i].dst;
+        flows[i].slot = slot_index(p.flows[i].dst, gen, pi, m, fslot[i]);
+        flows[i].src_offset = off;
+      }
+      t_.group_flows(bufs_.send_buf(), flows, bytes_);
+    }
+    for (size_t j = 0; j < ops.send_to.size(); ++j)
+      t_.send_to_slot(bufs_.send_at(off), bytes_, ops.send_to[j], slot_index(ops.send_to[j], gen, pi, m, rs[j]));
+    for (size_t i = 0; i < ops.recv_from.size(); ++i)
+      t_.recv_from(bufs_.recv_buf(slot_index(me, gen, pi, m, static_cast<int>(i))), bytes_, ops.recv_from[i], off);
+  };
+  if (opt_.batch) {
+    // One group: every message of the step, fused into one launch by RCCL.
+    t_.group_begin();
+    for (int m = 0; m < msgs_; ++m) one_message(m);
+    t_.group_end();
+  } else {
+    for (int m = 0; m < msgs_; ++m) {
+      t_.group_begin();
+      one_message(m);
+      t_.group_end();
+    }
   }
-  t_.group_end();
 }
 
 void StepDriver::step(long k) {
-  const size_t pi = static_cast<size_t>(k % phases());
-  const Phase& p = sched_.phases[pi];
+  const int pi = static_cast<int>(k % phases());
+  const int g = gen_of(k);
+  const Phase& p = sched_.phases[static_cast<size_t>(pi)];
   if (!p.participates(t_.rank())) {
-    if (posts_phase(t_, p, t_.rank())) post_step_ops(p);  // relay only: no flow of its own to time
+    if (posts_phase(t_, p, t_.rank())) post_step_ops(p, pi, g);  // relay only: no flow of its own to time
     marks_.emplace_back(-1, -1);
   } else {
     int a = t_.mark();
-    if (opt_.graph && pi < graphs_.size() && graphs_[pi] >= 0)
-      t_.graph_launch(graphs_[pi]);
+    const size_t gi = static_cast<size_t>(g) * sched_.phases.size() + static_cast<size_t>(pi);
+    if (opt_.graph && gi < graphs_.size() && graphs_[gi] >= 0)
+      t_.graph_launch(graphs_[gi]);
     else
-      post_step_ops(p);
+      post_step_ops(p, pi, g);
     int b = t_.mark();
     marks_.emplace_back(a, b);
   }
@@ -613,15 +843,60 @@ void StepDriver::reset() {
   t_.clear_marks();
 }
 
-uint64_t StepDriver::verify_last() {
-  uint64_t bad = 0;
-  if (last_step_ >= 0 && verify_) {
-    const Phase& p = sched_.phases[static_cast<size_t>(last_step_ % phases())];
-    const RankOps& ops = p.ranks[static_cast<size_t>(t_.rank())];
-    for (size_t i = 0; i < ops.recv_from.size(); ++i)
-      bad += t_.verify(bufs_.recv_buf(static_cast<int>(i)), bytes_, payload_seed(ops.recv_from[i], bytes_, salt_)).mismatches;
+void StepDriver::poison() {
+  // Every rank drains first: with a push transport a peer writes into this
+  // rank's slots, and its writes are complete once this rank's receives are.
+  sync();
+  boot_.barrier();
+  if (verify_) {
+    t_.zero(bufs_.recv_base(), recv_bytes());
+    t_.sync();
   }
-  return boot_.allreduce_sum_u64(bad);
+  boot_.barrier();
+  const int me = t_.rank();
+  if (!skip_armed_ && fault_applies("skip", me, -1)) {
+    std::fprintf(stderr, "[p2p] injected fault: rank %d moves no payload in the steps after poison()\n", me);
+    skip_armed_ = true;
+    t_.set_discard(true);
+  }
+}
+
+StepVerifyReport StepDriver::verify_steps(long first, long count) {
+  if (skip_armed_) {
+    t_.set_discard(false);
+    skip_armed_ = false;
+  }
+  const int me = t_.rank();
+  uint64_t timed = 0, bad = 0;
+  std::map<int, std::pair<int, int>> last;  // slot -> (sender, message) of its last write in the range
+  for (long k = first; k < first + count; ++k) {
+    const int pi = static_cast<int>(k % phases());
+    const Phase& p = sched_.phases[static_cast<size_t>(pi)];
+    const RankOps& ops = p.ranks[static_cast<size_t>(me)];
+    timed += static_cast<uint64_t>(msgs_) * ops.recv_from.size();
+    for (int m = 0; m < msgs_; ++m)
+      for (size_t i = 0; i < ops.recv_from.size(); ++i)
+        last[slot_index(me, gen_of(k), pi, m, static_cast<int>(i))] = {ops.recv_from[i], m};
+  }
+  if (verify_)
+    for (const auto& kv : last)
+      bad += t_.verify(bufs_.recv_buf(kv.first), bytes_, msg_seed(kv.second.first, kv.second.second)).mismatches;
+  const uint64_t mine[4] = {bad, verify_ ? static_cast<uint64_t>(last.size()) : 0, timed, verify_ ? last.size() : 0};
+  std::vector<uint64_t> all(4 * static_cast<size_t>(boot_.size()));
+  boot_.allgather(mine, all.data(), sizeof(mine));
+  StepVerifyReport r;
+  for (int q = 0; q < boot_.size(); ++q) {
+    r.mismatches += all[4 * static_cast<size_t>(q)];
+    r.verified_msgs += all[4 * static_cast<size_t>(q) + 1];
+    r.timed_msgs += all[4 * static_cast<size_t>(q) + 2];
+    r.slots += all[4 * static_cast<size_t>(q) + 3];
+  }
+  return r;
+}
+
+uint64_t StepDriver::verify_last() {
+  if (last_step_ < 0) return boot_.allreduce_sum_u64(0);
+  return verify_steps(last_step_, 1).mismatches;
 }
 
 double StepDriver::bytes_sent_per_step(long k) const {
@@ -630,8 +905,11 @@ double StepDriver::bytes_sent_per_step(long k) const {
 }
 
 double StepDriver::job_bytes_per_step(long k) const {
-  const Phase& p = sched_.phases[static_cast<size_t>(k % static_cast<long>(sched_.phases.size()))];
-  return static_cast<double>(p.flows.size()) * static_cast<double>(bytes_) * msgs_;
+  return static_cast<double>(flows_per_step(k)) * static_cast<double>(bytes_) * msgs_;
+}
+
+int StepDriver::flows_per_step(long k) const {
+  return static_cast<int>(sched_.phases[static_cast<size_t>(k % static_cast<long>(sched_.phases.size()))].flows.size());
 }
 
 }  // namespace p2p

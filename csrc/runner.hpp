@@ -72,28 +72,44 @@ struct PhaseResult {
   uint64_t total_mismatches = 0;
 };
 
-// Send buffer + receive slots for one rank, sized for the largest message.
+// Send buffer + receive slots for one rank.  The slots are carved from one
+// receive arena (one allocation, one IPC export), `stride()` bytes apart, so
+// a step driver can hold thousands of them -- one per message of every timed
+// step -- within the 288 GB of HBM3E.
 class Buffers {
  public:
-  Buffers(Transport& t, size_t max_bytes, int recv_slots);
+  // `slot_bytes` per receive slot; the send buffer holds `send_bytes`
+  // (default: one message).
+  Buffers(Transport& t, size_t slot_bytes, int recv_slots, size_t send_bytes = 0);
   ~Buffers();
   Buffers(const Buffers&) = delete;
   Buffers& operator=(const Buffers&) = delete;
   void* send_buf() const { return send_; }
-  void* recv_buf(int slot) const { return recv_.at(static_cast<size_t>(slot)); }
-  size_t capacity() const { return cap_; }
-  int slots() const { return static_cast<int>(recv_.size()); }
+  void* send_at(size_t offset) const { return static_cast<char*>(send_) + offset; }
+  void* recv_buf(int slot) const;
+  void* recv_base() const { return recv_; }
+  size_t capacity() const { return cap_; }          // bytes per receive slot
+  size_t send_capacity() const { return send_cap_; }
+  size_t stride() const { return stride_; }
+  int slots() const { return nslots_; }
 
  private:
   Transport& t_;
   size_t cap_;
+  size_t send_cap_;
+  size_t stride_;
+  int nslots_;
   void* send_ = nullptr;
-  std::vector<void*> recv_;
+  void* recv_ = nullptr;
 };
 
 // Receive slot on `peer` that holds messages from `me` in `phase` (position
 // of `me` in the peer's recv list).
 int remote_slot(const Phase& phase, int me, int peer);
+// For each entry of `me`'s send list, the receive index on that peer: the
+// k-th send to a peer meets the k-th receive from `me` there (a phase may
+// hold several flows between the same two ranks, e.g. ring-bi with 2 ranks).
+std::vector<int> remote_slots(const Phase& phase, int me);
 
 // Posts one iteration (one group) of `phase` for this rank.
 void post_phase_iteration(Transport& t, const Phase& phase, size_t bytes, Buffers& bufs);
@@ -133,6 +149,32 @@ std::vector<LatencyResult> run_latency(Transport& t, Bootstrap& boot, size_t byt
 // run_latency; payloads are rounded up to 16 bytes (at most 64 KiB).
 std::vector<LatencyResult> run_device_latency(Transport& t, Bootstrap& boot, size_t bytes, int iters, int warmup);
 
+// ---- ring token chain: pipeline-parallel hop latency ----
+// Rank 0 sends a small message to rank 1; every rank forwards it to its
+// successor only after it has arrived from its predecessor (0 -> 1 -> ... ->
+// N-1 -> 0), `laps` times.  Unlike the concurrent ring phase (every rank
+// sends every iteration, which measures pipelined issue rate), each hop here
+// depends on the previous one, as a pipeline stage waits for its input.
+// Rank 0 times each lap (hipEvents / steady clock); hop = lap / N.
+struct RingLatencyResult {
+  int nranks = 0;
+  size_t bytes = 0;
+  int laps = 0;
+  Summary hop_us;  // lap time / nranks
+  Summary lap_us;
+  std::string method = "host";  // host: grouped send/recv through the transport; device: ring token kernel
+};
+
+// Host-posted chain: every lap is two groups per rank (rank 0: send, then
+// receive; the others: receive, then send), posted without host syncs, so on
+// a GPU transport the stream order makes each send wait for the preceding
+// receive.  Collective; n == 1 is the self send/recv.  Not meaningful on the
+// IPC pull engines (a pull does not wait for the sender).
+RingLatencyResult run_ring_latency(Transport& t, Bootstrap& boot, size_t bytes, int laps, int warmup, Buffers& bufs);
+// Device chain (Transport::device_ring_token, IPC): one wave per GPU spins
+// on its inbox and writes into its successor's; no host or runtime in the loop.
+RingLatencyResult run_device_ring_latency(Transport& t, Bootstrap& boot, size_t bytes, int laps, int warmup);
+
 // ---- transport fuzz (tests) ----
 // `rounds` groups of random messages (src, dst, size <= max_bytes; self
 // messages and repeated pairs included) drawn from `seed`, identical on every
@@ -143,12 +185,32 @@ std::vector<LatencyResult> run_device_latency(Transport& t, Bootstrap& boot, siz
 uint64_t fuzz_transport(Transport& t, Bootstrap& boot, int rounds, uint64_t seed, size_t max_bytes);
 
 // ---- step driver (used by bench.py): one phase per step, no host syncs ----
-// Step k posts `msgs` iterations of phase (k mod phases) with a timestamp
-// around them; nothing blocks until sync().  Per-step durations are read
-// after sync().
+// Step k posts `msgs` messages per flow of phase (k mod phases) with a
+// timestamp around them; nothing blocks until sync().  Per-step durations are
+// read after sync().
+//
+// Payload layout, so that verification covers the timed work:
+//   * the send buffer holds `msgs` regions; message m of every step is sent
+//     from region m, filled with its own PRNG stream (msg_seed(src, m));
+//   * every message of every step lands in its own receive slot: generation
+//     g = (k / phases) mod depth, then phase, message and receive index.
+//     With depth >= the laps of the timed steps, no timed delivery is
+//     overwritten, and verify_steps() checks each one against the stream of
+//     the region it was sent from;
+//   * poison() zeroes every slot after the warmup, so a slot passes only if
+//     a timed step wrote it.
 struct StepOptions {
   bool batch = false;  // all msgs of a step in ONE group (one launch) instead of one group per message
-  bool graph = false;  // capture each phase's step into a hipGraph (transports that support it)
+  bool graph = false;  // capture each (phase, generation) step into a hipGraph (transports that support it)
+  int depth = 1;       // receive generations requested (capped by recv_budget)
+  size_t recv_budget = 0;  // bytes of receive slots this rank may hold (0: a quarter of free memory)
+};
+
+struct StepVerifyReport {
+  uint64_t mismatches = 0;     // 32-bit words that differ, all ranks
+  uint64_t verified_msgs = 0;  // timed deliveries checked (the last one into each slot), all ranks
+  uint64_t timed_msgs = 0;     // timed deliveries in the range, all ranks
+  uint64_t slots = 0;          // receive slots checked, all ranks
 };
 
 class StepDriver {
@@ -161,11 +223,27 @@ class StepDriver {
   void sync();                  // wait for everything posted
   std::vector<double> step_ms();       // this rank's per-step durations since the last reset
   void reset();                 // forget recorded steps
-  uint64_t verify_last();       // mismatches in the receive slots of the last step's phase (collective)
+  // Collective, blocking, untimed: zero every receive slot of every rank and
+  // arm P2P_INJECT_FAULT=skip for the steps that follow.
+  void poison();
+  // Collective: checks every receive slot written by steps [first, first +
+  // count) against the payload of the message that wrote it last.
+  StepVerifyReport verify_steps(long first, long count);
+  uint64_t verify_last();       // mismatches in the receive slots of the last step (collective)
   double bytes_sent_per_step(long k) const;  // by THIS rank
   double job_bytes_per_step(long k) const;   // by all ranks
+  int flows_per_step(long k) const;          // directed flows of step k's phase
   const Schedule& schedule() const { return sched_; }
   int phases() const { return static_cast<int>(sched_.phases.size()); }
+  int depth() const { return depth_; }
+  int msgs() const { return msgs_; }
+  size_t recv_bytes() const { return bufs_.stride() * static_cast<size_t>(bufs_.slots()); }
+
+  // Receive slot on `rank` of message `msg` from its `i`-th sender in
+  // `phase`, generation `gen` (every rank computes every rank's layout).
+  int slot_index(int rank, int gen, int phase, int msg, int i) const;
+  uint64_t msg_seed(int src, int msg) const;
+  size_t region_offset(int msg) const;  // where message `msg` starts in the send buffer
 
  private:
   Transport& t_;
@@ -176,12 +254,17 @@ class StepDriver {
   bool verify_;
   uint64_t salt_;
   StepOptions opt_;
+  std::vector<std::vector<int>> phase_base_;  // [rank][phase]: first slot of the phase in generation 0
+  std::vector<int> gen_slots_;                // [rank]: slots per generation
+  int depth_;                                 // receive generations (the same on every rank)
   Buffers bufs_;
   std::vector<std::pair<int, int>> marks_;
-  std::vector<int> graphs_;  // per phase, when opt_.graph
+  std::vector<int> graphs_;  // per (generation, phase), when opt_.graph
   long last_step_ = -1;
+  bool skip_armed_ = false;
 
-  void post_step_ops(const Phase& p);
+  void post_step_ops(const Phase& p, int pi, int gen);
+  int gen_of(long k) const { return static_cast<int>((k / phases()) % depth_); }
 };
 
 }  // namespace p2p

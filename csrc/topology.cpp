@@ -4,12 +4,15 @@
 // fully connected point-to-point fabric the tournament / all-pairs schedules
 // are designed around (docs/DESIGN.md §1).  SURVEY.md §7.2 (bootstrap: xGMI
 // topology probe).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <string>
 #include <vector>
 
 #include "common.hpp"
+#include "provenance.hpp"
+#include "report.hpp"
 #include "topology.hpp"
 
 namespace p2p {
@@ -76,6 +79,31 @@ std::string topology_report() {
   }
   if (pairs) out += strfmt("  %d of %d ordered pairs are direct (1-hop) xGMI links\n", xgmi, pairs);
   return out;
+}
+
+// Path of the shared object that defines `sym` ("" if unknown).
+std::string library_of(const void* sym) {
+  Dl_info info{};
+  if (dladdr(sym, &info) && info.dli_fname) {
+    char real[4096];
+    if (realpath(info.dli_fname, real)) return real;
+    return info.dli_fname;
+  }
+  return "";
+}
+
+std::string hip_runtime_json() {
+  int rt = 0, drv = 0;
+  if (hipRuntimeGetVersion(&rt) != hipSuccess) rt = -1;
+  if (hipDriverGetVersion(&drv) != hipSuccess) drv = -1;
+  return strfmt("{\"runtime_version\":%d,\"driver_version\":%d,\"library\":\"%s\"}", rt, drv,
+                json_escape(library_of(reinterpret_cast<const void*>(&hipRuntimeGetVersion))).c_str());
+}
+
+std::string device_pci_id(int device) {
+  char pci[64] = {0};
+  if (hipDeviceGetPCIBusId(pci, sizeof(pci), device) != hipSuccess) return "";
+  return pci;
 }
 
 }  // namespace p2p

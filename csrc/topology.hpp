@@ -16,4 +16,7 @@ struct LinkInfo {
 std::vector<LinkInfo> probe_topology(int* ndev);
 std::string topology_report();
 
+// Path of the shared object that defines `sym` (dladdr; "" if unknown).
+std::string library_of(const void* sym);
+
 }  // namespace p2p

@@ -55,6 +55,12 @@ class Transport {
   virtual void send(const void* p, size_t bytes, int peer) = 0;
   virtual void recv(void* p, size_t bytes, int peer) = 0;
   virtual void group_end() = 0;
+  // A receive of the message the peer sends from `src_offset` bytes into its
+  // registered send buffer (the step driver gives every message of a step its
+  // own region there, so each carries its own payload).  One-sided pull
+  // transports read from that offset; two-sided ones match by order and
+  // ignore it.
+  virtual void recv_from(void* p, size_t bytes, int peer, size_t /*src_offset*/) { recv(p, bytes, peer); }
   // A send whose payload lands in receive slot `remote_slot` of the peer's
   // buffer set (the receiver's index of this sender in its recv list).  Push
   // transports need it to address the peer's memory; the rest ignore it.
@@ -70,7 +76,8 @@ class Transport {
   struct GroupFlow {
     int src = -1;
     int dst = -1;
-    int slot = 0;  // receive slot of the flow on dst
+    int slot = 0;           // receive slot of the flow on dst
+    size_t src_offset = 0;  // where the message starts in src's send buffer
   };
   virtual bool wants_group_flows() const { return false; }
   virtual void group_flows(const void* /*set_send*/, const std::vector<GroupFlow>& /*flows*/, size_t /*bytes*/) {}
@@ -84,12 +91,23 @@ class Transport {
   // Wait for all posted work (bounded by the transport's watchdog timeout).
   virtual void sync() = 0;
 
+  // A buffer set: one send buffer plus `nslots` receive slots of
+  // `slot_bytes`, `stride` bytes apart in one receive arena (slot i at
+  // recv + i * stride).  The number of slots may differ between ranks.
+  struct BufferSet {
+    void* send = nullptr;
+    size_t send_bytes = 0;
+    void* recv = nullptr;
+    size_t stride = 0;
+    size_t slot_bytes = 0;
+    int nslots = 0;
+  };
   // Collective: called by every rank, in the same order, right after it
   // allocated a buffer set (Buffers' constructor / destructor).  One-sided
-  // transports map the peers' send buffers here and route a receive into one
-  // of `recvs` to the same set's send buffer on the peer; two-sided ones
-  // (RCCL, host) ignore it.
-  virtual void register_buffers(void* /*send*/, const std::vector<void*>& /*recvs*/, size_t /*bytes*/) {}
+  // transports map the peers' send buffers (and, when they write remotely,
+  // receive arenas) here and route a receive into a slot of the set to the
+  // same set's send buffer on the peer; two-sided ones (RCCL, host) ignore it.
+  virtual void register_buffers(const BufferSet& /*set*/) {}
   virtual void unregister_buffers(void* /*send*/) {}
 
   // ---- graphs: record posted work once, replay it with one launch ----
@@ -111,10 +129,53 @@ class Transport {
   virtual bool supports_device_pingpong() const { return false; }
   virtual void pingpong_setup() {}
   virtual std::vector<double> device_pingpong(int /*peer*/, size_t /*bytes*/, int /*iters*/) { return {}; }
+  // Ring token chain on the device (after pingpong_setup()): every rank
+  // calls it with its predecessor and successor; rank `leader` injects the
+  // token and returns the `laps` lap times in microseconds (empty elsewhere).
+  // Each hop forwards only after the token arrived: a dependent chain.
+  virtual std::vector<double> device_ring_token(int /*pred*/, int /*succ*/, bool /*leader*/, size_t /*bytes*/,
+                                                int /*laps*/) {
+    return {};
+  }
 
   // ---- health ----
   // Non-empty when the transport saw an asynchronous error (e.g. a peer died).
   virtual std::string async_error() { return ""; }
+  // Seconds any one wait (sync, rendezvous, init) may take before the
+  // transport aborts; callers shrink it as a global deadline approaches.
+  virtual void set_timeout(double /*seconds*/) {}
+
+  // ---- fault injection (P2P_INJECT_FAULT=skip@<rank>) ----
+  // While set, this rank's transfers still run their protocol (so no peer
+  // hangs) but move no payload into the receive slots they name: receives
+  // land in a private sink, one-sided writers skip their copies.  It
+  // emulates a data plane that silently drops timed transfers; verification
+  // after timing must catch it.
+  void set_discard(bool on) { discard_ = on; }
+  bool discarding() const { return discard_; }
+
+ protected:
+  // Scratch of at least `bytes` that discarded receives land in (allocated
+  // with alloc(); the transport frees it in its destructor through
+  // release_discard_sink()).
+  void* discard_sink(size_t bytes) {
+    if (bytes > sink_bytes_) {
+      if (sink_) release(sink_);
+      sink_ = alloc(bytes);
+      sink_bytes_ = bytes;
+    }
+    return sink_;
+  }
+  void release_discard_sink() {
+    if (sink_) release(sink_);
+    sink_ = nullptr;
+    sink_bytes_ = 0;
+  }
+
+ private:
+  bool discard_ = false;
+  void* sink_ = nullptr;
+  size_t sink_bytes_ = 0;
 };
 
 struct TransportOptions {

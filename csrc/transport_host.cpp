@@ -30,10 +30,12 @@
 namespace p2p {
 
 void host_fill(void* p, size_t bytes, uint64_t seed) {
-  auto* w = static_cast<uint32_t*>(p);
-  size_t nw = bytes / 4;
-  for (size_t i = 0; i < nw; ++i) w[i] = prng_word(seed, i);
   auto* b = static_cast<uint8_t*>(p);
+  size_t nw = bytes / 4;
+  for (size_t i = 0; i < nw; ++i) {
+    const uint32_t w = prng_word(seed, i);
+    std::memcpy(b + 4 * i, &w, 4);  // any alignment
+  }
   for (size_t i = nw * 4; i < bytes; ++i) b[i] = prng_byte(seed, i);
 }
 
@@ -130,10 +132,12 @@ class HostTransport final : public Transport {
   }
 
   ~HostTransport() override {
+    release_discard_sink();
     for (int fd : fds_)
       if (fd >= 0) ::close(fd);
   }
 
+  void set_timeout(double seconds) override { timeout_ = seconds; }
   std::string name() const override { return "host"; }
   int rank() const override { return rank_; }
   int nranks() const override { return n_; }
@@ -161,7 +165,8 @@ class HostTransport final : public Transport {
   }
   void recv(void* p, size_t bytes, int peer) override {
     P2P_CHECK(peer >= 0 && peer < n_, "bad peer");
-    ops_.push_back({false, peer, static_cast<char*>(p), bytes});
+    // Injected skip fault: the bytes are read off the wire into a sink.
+    ops_.push_back({false, peer, static_cast<char*>(discarding() ? discard_sink(bytes) : p), bytes});
     if (!in_group_) run_ops();
   }
   void group_end() override {

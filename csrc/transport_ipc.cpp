@@ -1,7 +1,7 @@
 // IpcTransport: one-sided point-to-point over xGMI without RCCL.
 //
 // Every rank exports its send buffer with hipIpcGetMemHandle when the
-// buffers are created (register_send_buffer, collective); every peer maps it
+// buffers are created (register_buffers, collective); every peer maps it
 // with hipIpcOpenMemHandle.  A receive is then a *pull*: the receiver's GPU
 // reads the sender's send buffer directly over the xGMI link into its own
 // receive buffer.  A send moves nothing (the receiver does the work), which
@@ -204,47 +204,54 @@ class IpcTransport final : public Transport {
   // Buffer sets are registered collectively in the same order on every rank,
   // so "the same set" on a peer is the one with the same position.  A receive
   // into one of a set's receive slots pulls from that set's send buffer on the
-  // peer.
-  void register_buffers(void* send, const std::vector<void*>& recvs, size_t bytes) override {
+  // peer (at the message's offset).  Push / relay also map every peer's
+  // receive arena: one export per set, slot i at base + i * stride.
+  void register_buffers(const BufferSet& set) override {
     Export me{};
-    me.handle = handle_of(send);
-    me.bytes = bytes;
+    me.handle = handle_of(set.send);
+    me.bytes = set.send_bytes;
     me.host_hash = host_hash(real_hostname());
     me.device = device_;
     me.pid = static_cast<int32_t>(getpid());
     auto all = boot_.allgather_value(me);
     Registration reg;
-    reg.send = send;
-    reg.bytes = bytes;
-    reg.recvs = recvs;
+    reg.send = set.send;
+    reg.send_bytes = set.send_bytes;
+    reg.recv = set.recv;
+    reg.stride = set.stride;
+    reg.slot_bytes = set.slot_bytes;
+    reg.nslots = set.nslots;
     reg.peer_send.assign(static_cast<size_t>(n_), nullptr);
     for (int r = 0; r < n_; ++r) {
       if (r == rank_) {
-        reg.peer_send[static_cast<size_t>(r)] = send;
+        reg.peer_send[static_cast<size_t>(r)] = set.send;
         continue;
       }
       P2P_CHECK(all[static_cast<size_t>(r)].host_hash == me.host_hash,
                 strfmt("ipc transport is intra-node only: rank %d is on another host", r));
-      P2P_CHECK(all[static_cast<size_t>(r)].bytes == bytes, "ipc transport: buffer sets differ in size across ranks");
+      P2P_CHECK(all[static_cast<size_t>(r)].bytes == set.send_bytes,
+                "ipc transport: send buffers differ in size across ranks");
       void* mapped = nullptr;
       HIPCHECK(hipIpcOpenMemHandle(&mapped, all[static_cast<size_t>(r)].handle, hipIpcMemLazyEnablePeerAccess));
       reg.peer_send[static_cast<size_t>(r)] = mapped;
     }
     if (push_) {
       // The sender (or a relay) writes into the receiver's slot: map every
-      // peer's slots.  Every rank has the same number of slots per set.
-      reg.peer_recvs.assign(static_cast<size_t>(n_), std::vector<void*>(recvs.size(), nullptr));
-      for (size_t k = 0; k < recvs.size(); ++k) {
-        Export slot{};
-        slot.handle = handle_of(recvs[k]);
-        slot.bytes = bytes;
-        auto slots = boot_.allgather_value(slot);
-        for (int r = 0; r < n_; ++r) {
-          void* mapped = recvs[k];
-          if (r != rank_)
-            HIPCHECK(hipIpcOpenMemHandle(&mapped, slots[static_cast<size_t>(r)].handle, hipIpcMemLazyEnablePeerAccess));
-          reg.peer_recvs[static_cast<size_t>(r)][k] = mapped;
-        }
+      // peer's receive arena.  Slot counts may differ between ranks.
+      ArenaExport a{};
+      a.handle = handle_of(set.recv);
+      a.stride = set.stride;
+      a.nslots = set.nslots;
+      auto arenas = boot_.allgather_value(a);
+      reg.peer_recv.assign(static_cast<size_t>(n_), nullptr);
+      reg.peer_nslots.assign(static_cast<size_t>(n_), 0);
+      for (int r = 0; r < n_; ++r) {
+        P2P_CHECK(arenas[static_cast<size_t>(r)].stride == set.stride, "ipc transport: receive slots differ in size");
+        void* mapped = set.recv;
+        if (r != rank_)
+          HIPCHECK(hipIpcOpenMemHandle(&mapped, arenas[static_cast<size_t>(r)].handle, hipIpcMemLazyEnablePeerAccess));
+        reg.peer_recv[static_cast<size_t>(r)] = mapped;
+        reg.peer_nslots[static_cast<size_t>(r)] = arenas[static_cast<size_t>(r)].nslots;
       }
     }
     regs_.push_back(std::move(reg));
@@ -282,7 +289,7 @@ class IpcTransport final : public Transport {
     const Registration* reg = nullptr;
     for (const auto& r : regs_)
       if (r.send == set_send) reg = &r;
-    P2P_CHECK(reg && bytes <= reg->bytes, "ipc relay: flows of an unregistered buffer set");
+    P2P_CHECK(reg && bytes <= reg->slot_bytes, "ipc relay: flows of an unregistered buffer set");
     std::vector<std::pair<int, int>> pairs;
     pairs.reserve(flows.size());
     for (const auto& f : flows) pairs.emplace_back(f.src, f.dst);
@@ -290,13 +297,13 @@ class IpcTransport final : public Transport {
     for (size_t i = 0; i < flows.size(); ++i) {
       const GroupFlow& f = flows[i];
       if (f.src == f.dst) continue;  // self flows: the endpoint's send / recv copy locally
-      P2P_CHECK(f.slot >= 0 && f.slot < static_cast<int>(reg->recvs.size()), "ipc relay: bad receive slot");
-      char* slot = static_cast<char*>(reg->peer_recvs[static_cast<size_t>(f.dst)][static_cast<size_t>(f.slot)]);
+      P2P_CHECK(f.src_offset + bytes <= reg->send_bytes, "ipc relay: message outside the send buffer");
+      char* slot = remote_slot_ptr(*reg, f.dst, f.slot);
       for (const Stripe& st : plan[i]) {
         const int writer = st.via < 0 ? f.src : st.via;
         if (rank_ == writer) {
-          const char* src = static_cast<const char*>(reg->peer_send[static_cast<size_t>(f.src)]);
-          ops_.push_back({src + st.offset, slot + st.offset, st.bytes, true});
+          const char* src = static_cast<const char*>(reg->peer_send[static_cast<size_t>(f.src)]) + f.src_offset;
+          if (!discarding()) ops_.push_back({src + st.offset, slot + st.offset, st.bytes, true});
           push_sends_.push_back(f.dst);  // wait for its ready, raise its done
           if (st.via >= 0) {
             relayed_bytes_ += st.bytes;
@@ -314,34 +321,42 @@ class IpcTransport final : public Transport {
     P2P_CHECK(peer >= 0 && peer < n_, "bad peer");
     const Registration* reg = nullptr;
     for (const auto& r : regs_)
-      if (r.send == p && bytes <= r.bytes) reg = &r;
+      if (p >= r.send && static_cast<const char*>(p) + bytes <= static_cast<const char*>(r.send) + r.send_bytes &&
+          bytes <= r.slot_bytes)
+        reg = &r;
     P2P_CHECK(reg, "ipc transport sends only from a registered send buffer");
     if (!push_) return;  // nothing to move: the receiver pulls
-    P2P_CHECK(slot >= 0 && slot < static_cast<int>(reg->recvs.size()), "bad remote slot");
     if (take_covered(rank_, peer, slot)) return;  // posted by group_flows
-    ops_.push_back({p, reg->peer_recvs[static_cast<size_t>(peer)][static_cast<size_t>(slot)], bytes, peer != rank_});
+    char* dst = remote_slot_ptr(*reg, peer, slot);
+    // Injected skip fault: the rendezvous runs, the payload stays behind.
+    if (!discarding()) ops_.push_back({p, dst, bytes, peer != rank_});
     if (peer != rank_) push_sends_.push_back(peer);
     if (!in_group_) flush();
   }
-  void recv(void* p, size_t bytes, int peer) override {
+  void recv(void* p, size_t bytes, int peer) override { recv_from(p, bytes, peer, 0); }
+  void recv_from(void* p, size_t bytes, int peer, size_t src_offset) override {
     P2P_CHECK(peer >= 0 && peer < n_, "bad peer");
-    if (push_) {
-      int slot = -1;
-      for (const auto& r : regs_) {
-        auto it = std::find(r.recvs.begin(), r.recvs.end(), p);
-        if (bytes <= r.bytes && it != r.recvs.end()) slot = static_cast<int>(it - r.recvs.begin());
+    const Registration* reg = nullptr;
+    int slot = -1;
+    for (const auto& r : regs_) {
+      const int s = slot_of(r, p);
+      if (s >= 0 && bytes <= r.slot_bytes) {
+        reg = &r;
+        slot = s;
       }
-      P2P_CHECK(slot >= 0, "ipc transport receives only into a registered receive slot");
+    }
+    P2P_CHECK(reg, "ipc transport receives only into a registered receive slot");
+    if (push_) {
       if (take_covered(peer, rank_, slot)) return;  // posted by group_flows
       if (peer != rank_) push_recvs_.push_back(peer);  // a self receive is the self send's copy
       if (!in_group_) flush();
       return;
     }
-    const Registration* reg = nullptr;
-    for (const auto& r : regs_)
-      if (std::find(r.recvs.begin(), r.recvs.end(), p) != r.recvs.end()) reg = &r;
-    P2P_CHECK(reg && bytes <= reg->bytes, "ipc transport receives only into a registered receive slot");
-    ops_.push_back({reg->peer_send[static_cast<size_t>(peer)], p, bytes, peer != rank_});
+    P2P_CHECK(src_offset + bytes <= reg->send_bytes, "ipc transport: receive beyond the peer's send buffer");
+    // Injected skip fault: the pull is not issued.
+    if (!discarding())
+      ops_.push_back({static_cast<const char*>(reg->peer_send[static_cast<size_t>(peer)]) + src_offset, p, bytes,
+                      peer != rank_});
     if (!in_group_) flush();
   }
   void group_end() override {
@@ -411,39 +426,25 @@ class IpcTransport final : public Transport {
       HIPCHECK(hipIpcOpenMemHandle(&mapped, all[static_cast<size_t>(r)].handle, hipIpcMemLazyEnablePeerAccess));
       peer_pages_[static_cast<size_t>(r)] = mapped;
     }
-    seq_.assign(static_cast<size_t>(n_), 0);
+    sent_.assign(static_cast<size_t>(n_), 0);
+    recvd_.assign(static_cast<size_t>(n_), 0);
     HIPCHECK(hipMalloc(&ping_scratch_, kPingScratch));
     HIPCHECK(hipHostMalloc(&ping_host_, kPingScratch, hipHostMallocDefault));
     boot_.barrier();
   }
 
   std::vector<double> device_pingpong(int peer, size_t bytes, int iters) override {
-    P2P_CHECK(page_, "pingpong_setup() first");
     P2P_CHECK(peer >= 0 && peer < n_, "bad peer");
-    P2P_CHECK(iters >= 1 && iters <= kPingMaxIters, strfmt("device ping-pong: 1..%d iterations", kPingMaxIters));
-    P2P_CHECK(bytes <= kPingMaxBytes, strfmt("device ping-pong payload is at most %zu bytes", kPingMaxBytes));
-    const unsigned long long pay = std::max<size_t>(16, (bytes + 15) / 16 * 16);
-    auto slot = [&](void* page, int k) { return static_cast<unsigned char*>(page) + kPingSlot * static_cast<size_t>(k); };
-    auto* stamps = static_cast<unsigned long long*>(ping_scratch_);
-    auto* status = reinterpret_cast<unsigned int*>(stamps + kPingMaxIters + 1);
-    HIPCHECK(hipMemsetAsync(status, 0, 2 * sizeof(unsigned int), stream_));
-    dev::PingRole a{};
-    a.bytes = pay;
-    a.base = seq_[static_cast<size_t>(peer)];
-    a.iters = iters;
-    a.stamps = stamps;
-    a.status = status;
-    a.timeout_ticks = static_cast<unsigned long long>(std::min(timeout_, 30.0) * tick_hz_);
     const bool self = peer == rank_;
-    const bool lead = self || rank_ < peer;
-    a.leader = lead ? 1 : 0;
-    unsigned char* out = self ? slot(page_, rank_) : slot(peer_pages_[static_cast<size_t>(peer)], rank_);
-    unsigned char* in = self ? slot(page_, n_) : slot(page_, peer);
-    a.out_flag = reinterpret_cast<unsigned long long*>(out);
-    a.out_payload = out + kPingHeader;
-    a.in_flag = reinterpret_cast<const unsigned long long*>(in);
-    a.in_payload = in + kPingHeader;
+    dev::PingRole a = ping_role(bytes, iters);
+    a.leader = (self || rank_ < peer) ? 1 : 0;
     if (self) {
+      // Both waves on this GPU: a writes slot `rank`, the reply wave slot n.
+      a.base = a.in_base = sent_[static_cast<size_t>(rank_)];
+      a.out_flag = reinterpret_cast<unsigned long long*>(ping_slot(page_, rank_));
+      a.out_payload = ping_slot(page_, rank_) + kPingHeader;
+      a.in_flag = reinterpret_cast<const unsigned long long*>(ping_slot(page_, n_));
+      a.in_payload = ping_slot(page_, n_) + kPingHeader;
       dev::PingRole b = a;  // the reply wave: mirror image through slot n
       b.leader = 0;
       b.out_flag = const_cast<unsigned long long*>(a.in_flag);
@@ -451,25 +452,29 @@ class IpcTransport final : public Transport {
       b.in_flag = a.out_flag;
       b.in_payload = a.out_payload;
       dev::launch_pingpong(a, &b, stream_);
+      sent_[static_cast<size_t>(rank_)] += static_cast<unsigned long long>(iters);
     } else {
+      set_links(&a, peer, peer);
       dev::launch_pingpong(a, nullptr, stream_);
+      sent_[static_cast<size_t>(peer)] += static_cast<unsigned long long>(iters);
+      recvd_[static_cast<size_t>(peer)] += static_cast<unsigned long long>(iters);
     }
-    HIPCHECK(hipGetLastError());
-    HIPCHECK(hipMemcpyAsync(ping_host_, ping_scratch_, kPingScratch, hipMemcpyDeviceToHost, stream_));
-    sync();
-    const auto* host = static_cast<const unsigned long long*>(ping_host_);
-    const auto* st = reinterpret_cast<const unsigned int*>(host + kPingMaxIters + 1);
-    seq_[static_cast<size_t>(peer)] += static_cast<unsigned long long>(iters);
-    if (st[0] & 1u)
-      P2P_FATAL(strfmt("rank %d: device ping-pong with rank %d timed out (partner kernel never answered)", rank_, peer));
-    if (st[1])
-      P2P_FATAL(strfmt("rank %d: device ping-pong with rank %d: %u payloads arrived before their data", rank_, peer, st[1]));
-    std::vector<double> us;
-    if (lead)
-      for (int i = 0; i < iters; ++i)
-        us.push_back(static_cast<double>(host[static_cast<size_t>(i) + 1] - host[static_cast<size_t>(i)]) / tick_hz_ * 1e6 / 2.0);
-    return us;
+    return finish_ping(a.leader != 0, iters, 2.0, strfmt("device ping-pong with rank %d", peer));
   }
+
+  std::vector<double> device_ring_token(int pred, int succ, bool leader, size_t bytes, int laps) override {
+    P2P_CHECK(pred >= 0 && pred < n_ && succ >= 0 && succ < n_ && pred != rank_ && succ != rank_,
+              "ring token: predecessor and successor must be other ranks");
+    dev::PingRole a = ping_role(bytes, laps);
+    a.leader = leader ? 1 : 0;
+    set_links(&a, pred, succ);
+    dev::launch_pingpong(a, nullptr, stream_);
+    sent_[static_cast<size_t>(succ)] += static_cast<unsigned long long>(laps);
+    recvd_[static_cast<size_t>(pred)] += static_cast<unsigned long long>(laps);
+    return finish_ping(leader, laps, 1.0, strfmt("ring token (from %d, to %d)", pred, succ));
+  }
+
+  void set_timeout(double seconds) override { timeout_ = seconds; }
 
   void sync() override {
     double deadline = now_seconds() + timeout_;
@@ -493,22 +498,98 @@ class IpcTransport final : public Transport {
  private:
   struct Registration {
     void* send = nullptr;
-    size_t bytes = 0;
-    std::vector<void*> recvs;
+    size_t send_bytes = 0;
+    void* recv = nullptr;  // receive arena: slot i at recv + i * stride
+    size_t stride = 0;
+    size_t slot_bytes = 0;
+    int nslots = 0;
     std::vector<void*> peer_send;  // mapped send buffer of every rank (own one for self)
-    std::vector<std::vector<void*>> peer_recvs;  // push / relay: [rank][slot] mapped receive slots
+    std::vector<void*> peer_recv;  // push / relay: mapped receive arena of every rank
+    std::vector<int> peer_nslots;  // push / relay: slots in each rank's arena
   };
+  struct ArenaExport {
+    hipIpcMemHandle_t handle;
+    uint64_t stride;
+    int32_t nslots;
+  };
+
+  // Slot index of receive pointer p in reg's arena, -1 if it is not one.
+  static int slot_of(const Registration& reg, const void* p) {
+    const char* base = static_cast<const char*>(reg.recv);
+    const char* q = static_cast<const char*>(p);
+    if (q < base || reg.stride == 0) return -1;
+    const size_t off = static_cast<size_t>(q - base);
+    if (off % reg.stride || off / reg.stride >= static_cast<size_t>(reg.nslots)) return -1;
+    return static_cast<int>(off / reg.stride);
+  }
+  char* remote_slot_ptr(const Registration& reg, int peer, int slot) const {
+    P2P_CHECK(static_cast<size_t>(peer) < reg.peer_recv.size(), "ipc push: receive arenas are not mapped");
+    P2P_CHECK(slot >= 0 && slot < reg.peer_nslots[static_cast<size_t>(peer)],
+              strfmt("bad remote slot %d (rank %d has %d)", slot, peer, reg.peer_nslots[static_cast<size_t>(peer)]));
+    return static_cast<char*>(reg.peer_recv[static_cast<size_t>(peer)]) + reg.stride * static_cast<size_t>(slot);
+  }
+
+  // ---- device ping-pong / ring token helpers ----
+  unsigned char* ping_slot(void* page, int k) const {
+    return static_cast<unsigned char*>(page) + kPingSlot * static_cast<size_t>(k);
+  }
+  // A role with its timing buffers and bounds set; links and bases follow.
+  dev::PingRole ping_role(size_t bytes, int iters) {
+    P2P_CHECK(page_, "pingpong_setup() first");
+    P2P_CHECK(iters >= 1 && iters <= kPingMaxIters, strfmt("device ping-pong: 1..%d iterations", kPingMaxIters));
+    P2P_CHECK(bytes <= kPingMaxBytes, strfmt("device ping-pong payload is at most %zu bytes", kPingMaxBytes));
+    auto* stamps = static_cast<unsigned long long*>(ping_scratch_);
+    auto* status = reinterpret_cast<unsigned int*>(stamps + kPingMaxIters + 1);
+    HIPCHECK(hipMemsetAsync(status, 0, 2 * sizeof(unsigned int), stream_));
+    dev::PingRole a{};
+    a.bytes = std::max<size_t>(16, (bytes + 15) / 16 * 16);
+    a.iters = iters;
+    a.stamps = stamps;
+    a.status = status;
+    a.timeout_ticks = static_cast<unsigned long long>(std::min(timeout_, 30.0) * tick_hz_);
+    return a;
+  }
+  // Writes go to `to`'s inbox slot for this rank; waits read the slot `from`
+  // writes here.  Sequence bases: what this rank has written to `to` and
+  // read from `from` so far (flags are monotonic, never reset).
+  void set_links(dev::PingRole* a, int from, int to) {
+    unsigned char* out = ping_slot(peer_pages_[static_cast<size_t>(to)], rank_);
+    unsigned char* in = ping_slot(page_, from);
+    a->base = sent_[static_cast<size_t>(to)];
+    a->in_base = recvd_[static_cast<size_t>(from)];
+    a->out_flag = reinterpret_cast<unsigned long long*>(out);
+    a->out_payload = out + kPingHeader;
+    a->in_flag = reinterpret_cast<const unsigned long long*>(in);
+    a->in_payload = in + kPingHeader;
+  }
+  // Waits for the kernel, checks its status words, and returns the leader's
+  // per-iteration times in microseconds divided by `div` (empty elsewhere).
+  std::vector<double> finish_ping(bool leader, int iters, double div, const std::string& what) {
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(ping_host_, ping_scratch_, kPingScratch, hipMemcpyDeviceToHost, stream_));
+    sync();
+    const auto* host = static_cast<const unsigned long long*>(ping_host_);
+    const auto* st = reinterpret_cast<const unsigned int*>(host + kPingMaxIters + 1);
+    if (st[0] & 1u) P2P_FATAL(strfmt("rank %d: %s timed out (partner kernel never answered)", rank_, what.c_str()));
+    if (st[1]) P2P_FATAL(strfmt("rank %d: %s: %u payloads arrived before their data", rank_, what.c_str(), st[1]));
+    std::vector<double> us;
+    if (leader)
+      for (int i = 0; i < iters; ++i)
+        us.push_back(static_cast<double>(host[static_cast<size_t>(i) + 1] - host[static_cast<size_t>(i)]) / tick_hz_ * 1e6 /
+                     div);
+    return us;
+  }
 
   void close_registration(Registration& reg) {
     for (int r = 0; r < n_; ++r) {
       void*& m = reg.peer_send[static_cast<size_t>(r)];
       if (m && r != rank_) (void)hipIpcCloseMemHandle(m);
       m = nullptr;
-      if (static_cast<size_t>(r) < reg.peer_recvs.size())
-        for (void*& slot : reg.peer_recvs[static_cast<size_t>(r)]) {
-          if (slot && r != rank_) (void)hipIpcCloseMemHandle(slot);
-          slot = nullptr;
-        }
+      if (static_cast<size_t>(r) < reg.peer_recv.size()) {
+        void*& a = reg.peer_recv[static_cast<size_t>(r)];
+        if (a && r != rank_) (void)hipIpcCloseMemHandle(a);
+        a = nullptr;
+      }
     }
   }
 
@@ -756,7 +837,7 @@ class IpcTransport final : public Transport {
   static constexpr int kPingMaxIters = 100000;
   void* page_ = nullptr;
   std::vector<void*> peer_pages_;
-  std::vector<unsigned long long> seq_;
+  std::vector<unsigned long long> sent_, recvd_;  // ping messages written to / read from each rank
   double tick_hz_ = 1e8;
   static constexpr size_t kPingScratch = sizeof(unsigned long long) * (kPingMaxIters + 1) + 64;
   void* ping_scratch_ = nullptr;  // device: stamps[kPingMaxIters + 1], status[2]

@@ -49,6 +49,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <thread>
 #include <vector>
 
@@ -56,6 +57,9 @@
 #include "common.hpp"
 #include "hip_check.hpp"
 #include "kernels.hpp"
+#include "provenance.hpp"
+#include "report.hpp"
+#include "topology.hpp"
 #include "transport.hpp"
 #include "units.hpp"
 
@@ -158,6 +162,10 @@ class RcclTransport final : public Transport {
       for (auto& ch : r.handles)
         if (ch.first) ncclCommDeregister(ch.first, ch.second);
     reg_sets_.clear();
+    try {
+      release_discard_sink();
+    } catch (const std::exception&) {
+    }
     for (void* p : nccl_alloc_) ncclMemFree(p);
     nccl_alloc_.clear();
     for (auto& c : comms_)
@@ -214,16 +222,16 @@ class RcclTransport final : public Transport {
   // communicator (ncclCommRegister), which lets RCCL move point-to-point
   // messages between registered user buffers without its staging FIFOs
   // where it supports that.  An experiment knob (profiles/r1_comms/).
-  void register_buffers(void* send, const std::vector<void*>& recvs, size_t bytes) override {
+  void register_buffers(const BufferSet& set) override {
     if (!register_) return;
     RegSet r;
-    r.send = send;
-    std::vector<void*> all{send};
-    all.insert(all.end(), recvs.begin(), recvs.end());
+    r.send = set.send;
+    const std::pair<void*, size_t> all[2] = {{set.send, set.send_bytes},
+                                             {set.recv, set.stride * static_cast<size_t>(set.nslots)}};
     for (auto c : comms_)
-      for (void* p : all) {
+      for (const auto& pb : all) {
         void* h = nullptr;
-        nccl_ok(ncclCommRegister(c, p, bytes, &h), "ncclCommRegister");
+        nccl_ok(ncclCommRegister(c, pb.first, pb.second, &h), "ncclCommRegister");
         r.handles.emplace_back(c, h);
       }
     reg_sets_.push_back(std::move(r));
@@ -283,7 +291,8 @@ class RcclTransport final : public Transport {
   void recv(void* p, size_t bytes, int peer) override {
     const int j = pick(&recv_seq_, peer, bytes);
     hipStream_t s = j == 0 && recv_stream_ ? recv_stream_ : cstreams_[static_cast<size_t>(j)];
-    char* c = static_cast<char*>(p);
+    // Injected skip fault: the receive completes into a private sink.
+    char* c = static_cast<char*>(discarding() ? discard_sink(bytes) : p);
     do {
       size_t n = chunk_of(bytes);
       issue({j, false, c, n, peer, s});
@@ -429,6 +438,8 @@ class RcclTransport final : public Transport {
       }
     }
   }
+
+  void set_timeout(double seconds) override { timeout_ = seconds; }
 
   std::string async_error() override {
     for (auto c : comms_) {
@@ -622,6 +633,15 @@ class RcclTransport final : public Transport {
 
 std::unique_ptr<Transport> make_rccl_transport(Bootstrap& boot, const TransportOptions& opt) {
   return std::make_unique<RcclTransport>(boot, opt);
+}
+
+std::string rccl_runtime_json() {
+  int ver = 0;
+  if (ncclGetVersion(&ver) != ncclSuccess) ver = -1;
+  // The RCCL that runs is the one the loader resolved, which inside a torch
+  // process is torch's own (Makefile RUNTIME): name it by path.
+  return strfmt("{\"version\":%d,\"version_string\":\"%d.%d.%d\",\"library\":\"%s\"}", ver, ver / 10000,
+                (ver / 100) % 100, ver % 100, json_escape(library_of(reinterpret_cast<const void*>(&ncclGetVersion))).c_str());
 }
 
 bool rccl_transport_available() {

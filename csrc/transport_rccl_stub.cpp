@@ -28,3 +28,12 @@ std::vector<LinkInfo> probe_topology(int* ndev) {
 }
 std::string topology_report() { return "GPU link topology: not available in this host-only build\n"; }
 }  // namespace p2p
+
+// Provenance stubs for host-only builds: no GPU runtime in the process.
+#include "provenance.hpp"
+
+namespace p2p {
+std::string hip_runtime_json() { return "null"; }
+std::string rccl_runtime_json() { return "null"; }
+std::string device_pci_id(int) { return ""; }
+}  // namespace p2p

@@ -113,9 +113,11 @@ class ShmTransport final : public Transport {
   }
 
   ~ShmTransport() override {
+    release_discard_sink();
     if (base_) ::munmap(base_, bytes_);
   }
 
+  void set_timeout(double seconds) override { timeout_ = seconds; }
   std::string name() const override { return "shm"; }
   int rank() const override { return rank_; }
   int nranks() const override { return n_; }
@@ -143,7 +145,8 @@ class ShmTransport final : public Transport {
   }
   void recv(void* p, size_t bytes, int peer) override {
     P2P_CHECK(peer >= 0 && peer < n_, "bad peer");
-    ops_.push_back({false, peer, static_cast<char*>(p), bytes});
+    // Injected skip fault: the bytes are read off the wire into a sink.
+    ops_.push_back({false, peer, static_cast<char*>(discarding() ? discard_sink(bytes) : p), bytes});
     if (!in_group_) run_ops();
   }
   void group_end() override {

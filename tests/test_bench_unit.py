@@ -8,21 +8,23 @@ import bench  # noqa: E402
 
 
 def test_posting_candidates_default_rccl():
-    # W = 7: one communicator per-message and batched, four communicators batched.
-    assert bench.posting_candidates("rccl", -1, -1, 7) == [(1, 0), (1, 1), (4, 1)]
+    # One communicator per-message and batched, four communicators batched.
+    assert bench.posting_candidates("rccl", -1, -1) == [(1, 0), (1, 1), (4, 1)]
 
 
 def test_posting_candidates_fixed_and_other_transports():
-    assert bench.posting_candidates("rccl", 4, -1, 7) == [(4, 1)]
-    assert bench.posting_candidates("rccl", 1, 1, 7) == [(1, 1)]
-    assert bench.posting_candidates("ipc", -1, -1, 7) == [(1, 0), (1, 1)]
-    assert bench.posting_candidates("host", 4, 0, 7) == [(1, 0)]
+    assert bench.posting_candidates("rccl", 4, -1) == [(4, 1)]
+    assert bench.posting_candidates("rccl", 1, 1) == [(1, 1)]
+    assert bench.posting_candidates("rccl", -1, 1) == [(1, 1), (4, 1)]
+    assert bench.posting_candidates("ipc", -1, -1) == [(1, 0), (1, 1)]
+    assert bench.posting_candidates("host", 4, 0) == [(1, 0)]
 
 
-def test_posting_candidates_short_warmup_keeps_the_last():
-    assert bench.posting_candidates("rccl", -1, -1, 2) == [(4, 1)]
-    assert bench.posting_candidates("rccl", -1, -1, 1) == [(4, 1)]
-    assert bench.posting_candidates("shm", -1, -1, 0) == [(1, 1)]
+def test_tuning_steps_are_whole_laps():
+    # N = 8: 7 rounds, one lap covers every cell; N = 1 / 2: one round, 4 steps.
+    assert bench.tuning_steps(7) == 7
+    assert bench.tuning_steps(3) == 6
+    assert bench.tuning_steps(1) == 4
 
 
 def test_first_comms():
@@ -31,8 +33,34 @@ def test_first_comms():
     assert bench.first_comms("ipc", 4) == 1
 
 
+def test_headline_value_is_the_mean_cell():
+    # 8 ranks, 4 pairs x 2 directions = 8 flows per step, 20 steps of 8 x 32 MiB
+    # per flow, 2 s: aggregate = all bytes / 2 s; value = aggregate / 8.
+    per_flow = 8 * (32 << 20)
+    job = 20 * 8 * per_flow
+    value, aggregate = bench.headline_stats(job, 20 * 8, 20, 2.0)
+    assert abs(aggregate - job / 2.0 / 1e9) < 1e-9
+    assert abs(value - aggregate / 8) < 1e-9
+    # One GPU: one self flow per step, value == aggregate.
+    v1, a1 = bench.headline_stats(20 * per_flow, 20, 20, 0.5)
+    assert v1 == a1
+
+
+def test_cell_matrix_takes_the_longer_endpoint():
+    flows = {0: [(0, 1), (1, 0)], 1: [(0, 1), (1, 0)]}
+    all_ms = [[1.0, 2.0], [4.0, 1.0]]  # rank 0 / rank 1 per-step ms
+    m, samples, cells = bench.cell_matrix(2, [0, 1], lambda k: flows[k], all_ms, 1e6)
+    # step 0: max(1, 4) = 4 ms -> 0.25 GB/s; step 1: max(2, 1) = 2 ms -> 0.5 GB/s
+    assert cells[(0, 1)] == [0.25, 0.5] and m[0][1] == 0.375 and samples[0][1] == 2
+    assert samples[0][0] == 0 and m[1][1] == 0.0
+
+
+def test_pick_depth_covers_the_timed_steps():
+    assert bench.pick_depth(20, 7) == 3 and bench.pick_depth(20, 1) == 20 and bench.pick_depth(1, 7) == 1
+
+
 def test_bench_help_lists_transports():
     args = bench.parse_args([])
-    assert args.transport == "rccl" and args.comms == -1 and args.isolate == 1
+    assert args.transport == "rccl" and args.comms == -1 and args.isolate == 1 and args.deadline == 300.0
     for t in ("ipc:relay", "shm"):
         assert bench.parse_args(["--transport", t]).transport == t

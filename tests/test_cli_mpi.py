@@ -94,6 +94,42 @@ def test_corruption_detected(mpirun, host_build):
     assert "VERIFICATION FAILED" in out.stderr
 
 
+def test_skipped_transfers_detected(mpirun, host_build):
+    """P2P_INJECT_FAULT=skip@1: rank 1's receives silently move no payload in
+    the timed iterations (the protocol still runs).  The warmup delivered the
+    payload already, so the slots are poisoned again before timing: exit 2."""
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    for transport in ("host", "shm"):
+        out = run(mpirun, exe, 3, ["--transport", transport, "--mode", "pair,tournament", "--size", "64K", "-n", "3",
+                                   "-w", "2", "--verify", "--no-compat"], env={"P2P_INJECT_FAULT": "skip@1"})
+        assert out.returncode == 2, (transport, out.stderr[-2000:])
+        assert "VERIFICATION FAILED" in out.stderr and "moves no payload" in out.stderr
+    ok = run(mpirun, exe, 3, ["--transport", "shm", "--mode", "pair", "--size", "64K", "-n", "3", "-w", "2",
+                              "--verify", "--no-compat"])
+    assert ok.returncode == 0, ok.stderr[-2000:]
+
+
+def test_json_provenance_and_ring_token(mpirun, host_build, tmp_path):
+    """--json starts with the provenance record (knobs, runtime, every rank's
+    device and the links between them); --mode ring --latency adds the
+    dependent ring token chain."""
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    js = tmp_path / "r.json"
+    out = run(mpirun, exe, 3, ["--transport", "shm", "--mode", "ring", "--size", "16K", "-n", "2", "--latency",
+                               "--latency-iters", "60", "--json", str(js), "--no-compat"],
+              env={"NCCL_PROTO": "Simple"})
+    assert out.returncode == 0, out.stderr[-2000:]
+    recs = [json.loads(l) for l in js.read_text().splitlines()]
+    prov = recs[0]
+    assert prov["type"] == "provenance" and prov["env"]["NCCL_PROTO"] == "Simple"
+    assert "GPU_MAX_HW_QUEUES" in prov["env"] and "rccl" in prov["runtime"]
+    assert [d["rank"] for d in prov["rank_devices"]] == [0, 1, 2] and len(prov["rank_links"]) == 3
+    ring = [r for r in recs if r["type"] == "ring_latency"]
+    assert len(ring) == 1 and ring[0]["nranks"] == 3 and ring[0]["laps"] == 20
+    assert 0 < ring[0]["hop_us"]["p50"] <= ring[0]["lap_us"]["p50"]
+    assert "ring token latency: 3 rank(s)" in out.stdout
+
+
 def test_dead_rank_does_not_hang(mpirun, host_build):
     exe = os.path.join(host_build, "p2p_matrix_host")
     out = run(mpirun, exe, 3, ["--transport", "host", "--size", "64K", "-n", "3"],
@@ -131,14 +167,19 @@ def test_resume_and_trace(mpirun, host_build, tmp_path):
     base = ["--transport", "host", "--sizes", "4K,64K", "-n", "2", "--no-compat", "--json", str(js)]
     first = run(mpirun, exe, 2, base + ["--mode", "pair,ring", "--trace", str(tr)])
     assert first.returncode == 0, first.stderr
-    assert len(js.read_text().splitlines()) == 8  # (pair, ring) x (uni, bi) x 2 sizes
+
+    def runs():
+        return [json.loads(l) for l in js.read_text().splitlines() if json.loads(l)["type"] == "run"]
+
+    assert len(runs()) == 8  # (pair, ring) x (uni, bi) x 2 sizes
     trace = json.loads(tr.read_text())
     xs = [e for e in trace["traceEvents"] if e["ph"] == "X"]
     assert {e["tid"] for e in xs} == {0, 1} and all(e["dur"] >= 0 for e in xs)
     again = run(mpirun, exe, 2, base + ["--mode", "pair,ring,allpairs", "--resume", "-v"])
     assert again.returncode == 0, again.stderr
-    lines = js.read_text().splitlines()
-    assert len(lines) == 10  # only the 2 allpairs runs were added
+    assert len(runs()) == 10  # only the 2 allpairs runs were added
+    # Every invocation records its provenance first (the resume appended one).
+    assert sum(1 for l in js.read_text().splitlines() if json.loads(l)["type"] == "provenance") == 2
     assert again.stderr.count("resume: skipping") == 8
 
 

@@ -139,6 +139,41 @@ def test_corruption_detected_on_gpu(exe):
     assert "VERIFICATION FAILED" in out.stderr
 
 
+@pytest.mark.parametrize("engine", ["kernel", "push"])
+def test_skipped_transfers_detected_on_gpu(exe, engine):
+    """P2P_INJECT_FAULT=skip@1: rank 1 moves no payload in the timed
+    iterations (pull: its copies are not issued; push: its writes into rank
+    0's slots are not issued, the flags still flow, so nothing hangs).  The
+    warmup delivered everything, so only the poisoning before timing catches
+    it: exit 2.  The same run without the fault passes."""
+    base = [MPIRUN, "-n", "2", exe, "--transport", "ipc", "--ipc-engine", engine, "--device", "0", "--mode",
+            "pair,tournament", "--size", "1M", "-n", "3", "-w", "2", "--verify", "--no-compat", "--timeout", "60"]
+    out = subprocess.run(base, capture_output=True, text=True, timeout=300,
+                         env=dict(os.environ, P2P_INJECT_FAULT="skip@1"))
+    assert out.returncode == 2, out.stderr[-3000:]
+    assert "VERIFICATION FAILED" in out.stderr
+    ok = subprocess.run(base, capture_output=True, text=True, timeout=300)
+    assert ok.returncode == 0, ok.stderr[-3000:]
+
+
+def test_ring_token_chain_on_one_gpu(exe, tmp_path):
+    """--mode ring with --latency and --device-latency, 4 processes on one GPU:
+    the dependent token chain 0 -> 1 -> 2 -> 3 -> 0, host-posted through the
+    push engine's rendezvous and as the one-wave device kernel."""
+    js = tmp_path / "r.json"
+    out = subprocess.run([MPIRUN, "-n", "4", exe, "--transport", "ipc", "--ipc-engine", "push", "--device", "0",
+                          "--mode", "ring", "--dir", "uni", "--size", "64K", "-n", "2", "--no-compat", "--latency",
+                          "--device-latency", "--latency-iters", "200", "--json", str(js), "--timeout", "60"],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    ring = {r["method"]: r for r in (json.loads(l) for l in js.read_text().splitlines()) if r["type"] == "ring_latency"}
+    assert set(ring) == {"host", "device"}, ring
+    for r in ring.values():
+        assert r["nranks"] == 4 and r["laps"] == 50
+        assert 0 < r["hop_us"]["p50"] and abs(r["lap_us"]["p50"] / r["hop_us"]["p50"] - 4) < 0.5, r
+    assert ring["device"]["hop_us"]["p50"] < ring["host"]["hop_us"]["p50"]
+
+
 def test_bench_two_ranks_ipc_push():
     """bench.py with the push engine as the headline transport (rendezvous +
     remote writes), graphs off by construction."""
@@ -179,7 +214,7 @@ def test_bench_emulated_node(nranks):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nranks),
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", str(nranks),
            "--steps", "14", "--warmup", "7", "--transport", "ipc", "--device", "0", "--sweep-max", "64M",
-           "--latency-iters", "100",
+           "--latency-iters", "100", "--deadline", "560",
            # Child processes for the comparisons would double the processes
            # on the one GPU (8 ranks + 8 children + pytest > the box's 16):
            # isolate them only with 4 ranks.
@@ -204,6 +239,14 @@ def test_bench_emulated_node(nranks):
     relay = ipc["relay"]
     assert relay["verify_mismatches"] == 0 and relay["value_gbs"] > 0, relay
     assert [p["mismatches"] for p in relay["pair_0_1"]] == [0, 0], relay
+    # Every timed delivery verified; value is the mean cell (per flow and
+    # direction) and agrees with the matrix of per-step GPU times.
+    assert r["verify_coverage"] == 1.0 and ipc["verify_coverage"] == 1.0
+    assert abs(r["aggregate_gbs"] - r["flows_per_step"] * r["value"]) < 0.01 * r["aggregate_gbs"]
+    assert 0.5 < r["value"] / r["matrix_gbs_mean"] < 1.5, (r["value"], r["matrix_gbs_mean"])
+    assert r["extras"]["ring_hop"]["hop_us_p50"] > 0 and ipc["device_ring_hop_p50_us"] > 0
+    links = r["provenance"]["rank_links"]
+    assert all(links[a][b] == "same-gpu" for a in range(nranks) for b in range(nranks))
 
 
 @pytest.mark.parametrize("engine", ["kernel", "sdma", "push", "relay"])

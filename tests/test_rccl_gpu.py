@@ -71,6 +71,60 @@ def test_step_driver(native, session):
     assert d.job_bytes_per_step(0) == 4 * (8 << 20)
 
 
+def test_step_driver_verifies_every_timed_step(native):
+    """Every message of every timed step in its own slot: after poison() the
+    timed steps refill all of them (coverage 1.0), one or four communicators."""
+    for transport in ("rccl", "rccl:4"):
+        s = native.Session(0, 1, device=0, transport=transport, timeout_s=120)
+        d = native.StepDriver(s, "self", "bi", (4 << 20) + 64, 6, True, True, False, depth=5, salt=3)
+        assert d.depth == 5 and d.recv_bytes >= 5 * 6 * ((4 << 20) + 64)
+        d.connect()
+        d.run_steps(0, 2)
+        d.sync()
+        d.poison()
+        d.run_steps(2, 5)
+        d.sync()
+        v = d.verify_steps(2, 5)
+        assert v["mismatches"] == 0 and v["timed_msgs"] == 30 and v["verified_msgs"] == 30, v
+        d.poison()  # nothing ran since: every slot fails
+        z = d.verify_steps(2, 5)
+        assert z["mismatches"] == z["slots"] * (((4 << 20) + 64) // 4), z
+        del d, s
+
+
+def test_skip_fault_is_caught_rccl():
+    """P2P_INJECT_FAULT=skip@0 on the RCCL transport: the timed receives land
+    in a sink (the collective still completes); both the run engine and the
+    step driver report every timed delivery as missing."""
+    code = ("import json\n"
+            "from test_nccl_p2p_amd import require_native\n"
+            "nat = require_native()\n"
+            "s = nat.Session(0, 1, device=0, transport='rccl', timeout_s=60)\n"
+            "r = json.loads(s.run(mode='self', dir='uni', bytes=1 << 20, iters=4, warmup=2, verify=True))\n"
+            "print('RUN', r['phases'][0]['mismatches'])\n"
+            "d = nat.StepDriver(s, 'self', 'bi', 1 << 20, 2, True, True, False, depth=3)\n"
+            "d.connect(); d.run_steps(0, 2); d.sync(); d.poison(); d.run_steps(2, 3); d.sync()\n"
+            "print('STEPS', d.verify_steps(2, 3)['mismatches'])\n")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT,
+                         env=dict(__import__("os").environ, P2P_INJECT_FAULT="skip@0"))
+    assert out.returncode == 0, out.stderr[-3000:]
+    words = (1 << 20) // 4
+    assert "RUN %d" % words in out.stdout and "STEPS %d" % (3 * 2 * words) in out.stdout, out.stdout
+
+
+def test_ring_latency_and_provenance(native, session):
+    r = json.loads(session.ring_latency(8, 100, 10, False))
+    assert r["nranks"] == 1 and r["laps"] == 100 and 0 < r["hop_us"]["p50"] < 1000
+    # One runtime for every entry point: the RCCL / HIP this process runs are
+    # the files torch loaded (Makefile RUNTIME=torch, build/rt).
+    rt = json.loads(native.runtime_json())
+    maps = open("/proc/self/maps").read()
+    assert rt["rccl"]["library"] in maps and rt["hip"]["library"] in maps, rt
+    assert rt["visible_devices"] >= 1
+    p = json.loads(session.provenance(0))
+    assert p["rank_devices"][0]["pci"] and p["rank_links"] == [["same-gpu"]] and "GPU_MAX_HW_QUEUES" in p["env"]
+
+
 def test_message_larger_than_4gib(session):
     """size_t counts: the reference's `int msg_size` cannot express this."""
     r = json.loads(session.run(mode="self", dir="uni", bytes=(5 << 30) + 16, iters=2, warmup=1, verify=True))

@@ -55,6 +55,12 @@ def test_bench_cpu_two_ranks(native):
     # The untimed transport comparison runs in a child process per rank.
     cmp_ = r["ipc_transport"]
     assert cmp_["transport"] == "host" and cmp_["verify_mismatches"] == 0 and cmp_["value_gbs"] > 0, cmp_
+    # Every timed delivery was verified; provenance is recorded.
+    assert r["verify_coverage"] == 1.0 and r["verify_detail"]["timed_msgs"] == 4 * 2 * 2
+    prov = r["provenance"]
+    assert "GPU_MAX_HW_QUEUES" in prov["env"] and prov["runtime"]["rccl"]["library"]
+    assert [d["rank"] for d in prov["rank_devices"]] == [0, 1] and len(prov["rank_links"]) == 2
+    assert r["extras"]["ring_hop"]["hop_us_p50"] > 0 and r["matrix_samples"] == [[0, 4], [4, 0]]
 
 
 def test_bench_comparison_failure_is_isolated(native):
@@ -87,14 +93,14 @@ def test_bench_drops_a_failing_posting_candidate(native):
 
 
 def test_bench_drops_a_candidate_failing_in_warmup(native):
-    """The same when the candidate connects but its warmup steps fail."""
+    """The same when the candidate connects but its tuning lap fails."""
     out = torchrun(2, ["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "4", "--transport", "host",
                        "--size", "64K", "--msgs", "2", "--latency-iters", "10", "--sweep", "0", "--extras", "0",
-                       "--ref-iters", "0", "--ipc-extra", "0"], env={"P2P_BENCH_FAIL_CANDIDATE": "1,1,warmup"})
+                       "--ref-iters", "0", "--ipc-extra", "0"], env={"P2P_BENCH_FAIL_CANDIDATE": "1,1,tuning"})
     assert out.returncode == 0, out.stderr[-3000:]
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert r["value"] > 0 and r["posting"]["batch"] is False
-    assert r["posting"]["dropped"]["comms1_batch"] in ("injected warmup failure", "failed on another rank")
+    assert r["posting"]["dropped"]["comms1_batch"] in ("injected tuning failure", "failed on another rank")
 
 
 
@@ -116,5 +122,53 @@ def test_bench_untimed_budget_skips_sections(native):
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert r["value"] > 0 and r["p50_latency_us"] > 0
     assert r["reference_semantics"] is None and r["ipc_transport"] is None
-    assert set(r["untimed_skipped"]) >= {"reference_semantics", "allpairs_1g", "ring_256m", "ring_hop_8b",
+    assert set(r["untimed_skipped"]) >= {"reference_semantics", "allpairs_1g", "ring_256m", "ring_hop",
                                          "pair_sweep_0_1", "host"}, r["untimed_skipped"]
+
+
+def test_bench_value_is_the_mean_cell(native):
+    """value is the mean per-flow, per-direction rate from the wall clock; it
+    agrees with the matrix built from per-step GPU (here host) timelines, and
+    aggregate_gbs is the sum over the flows of a step."""
+    out = torchrun(4, ["bench.py", "--gpus", "4", "--steps", "9", "--warmup", "3", "--transport", "shm",
+                       "--size", "4M", "--msgs", "2", "--latency-iters", "10", "--sweep", "0", "--extras", "0",
+                       "--ref-iters", "0", "--ipc-extra", "0", "--batch", "1"])
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert r["flows_per_step"] == 4 and abs(r["aggregate_gbs"] - 4 * r["value"]) < 0.01 * r["aggregate_gbs"]
+    assert r["matrix_cells"] == "12/12" and all(r["matrix_samples"][i][j] == 3 for i in range(4) for j in range(4)
+                                                if i != j)
+    assert 0.6 < r["value"] / r["matrix_gbs_mean"] < 1.4, (r["value"], r["matrix_gbs_mean"])
+    assert r["verify_mismatches"] == 0 and r["verify_coverage"] == 1.0 and r["recv_slot_generations"] == 3
+
+
+def test_bench_skipped_transfers_fail_verification(native):
+    """P2P_INJECT_FAULT=skip@1: rank 1's transport silently moves no payload in
+    the timed steps.  The warmup had delivered everything, so only poisoning
+    after the warmup plus one slot per timed message can catch it: exit 3."""
+    out = torchrun(2, ["bench.py", "--gpus", "2", "--steps", "3", "--warmup", "2", "--transport", "host",
+                       "--size", "64K", "--msgs", "2", "--latency-iters", "10", "--sweep", "0", "--extras", "0",
+                       "--ref-iters", "0", "--ipc-extra", "0"], env={"P2P_INJECT_FAULT": "skip@1"})
+    assert out.returncode != 0
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    # rank 1 receives 3 steps x 2 messages of 16K words, all left poisoned.
+    assert r["verify_mismatches"] == 3 * 2 * (64 << 10) // 4, r["verify_detail"]
+
+
+def test_bench_deadline_with_a_hung_section(native):
+    """A rank that stops responding inside an untimed section: the others' waits
+    are bounded by the time left, and at the deadline the watchdog prints the
+    headline with the section reported; nothing waits for the driver's kill."""
+    import time as _time
+
+    t0 = _time.monotonic()
+    out = torchrun(4, ["bench.py", "--gpus", "4", "--steps", "3", "--warmup", "2", "--transport", "host",
+                       "--size", "64K", "--msgs", "1", "--latency-iters", "10", "--sweep", "0", "--ipc-extra", "0",
+                       "--deadline", "40"], env={"P2P_BENCH_HANG": "latency@3"}, timeout=150)
+    wall = _time.monotonic() - t0
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stderr[-3000:]
+    r = json.loads(lines[0])
+    assert r["value"] > 0 and r["deadline_hit"] is True
+    assert "latency" in (r["section_errors"] or {}), r["section_errors"]
+    assert wall < 40 + 30, wall
