@@ -1,0 +1,249 @@
+#!/usr/bin/env python3
+"""One-command tuning sweep of the xGMI pair cell.
+
+Runs the pair cell 0 -> 1 (uni) and 0 <-> 1 (bi) at 32 MiB and 1 GiB through
+build/p2p_matrix under every setting that can move a single xGMI link:
+
+  rccl rows   --comms 1, 2, 4, 8 (messages spread over K communicators / streams)
+              NCCL_NCHANNELS_PER_PEER, NCCL_P2P_NVL_CHUNKSIZE / NCCL_P2P_NET_CHUNKSIZE,
+              NCCL_PROTO, RCCL_P2P_BATCH_ENABLE / RCCL_P2P_BATCH_THRESHOLD
+  ipc rows    --ipc-engine kernel (one-sided pull by the gfx950 copy kernel),
+              sdma, push, relay (stripes through idle third GPUs, N >= 3)
+
+Every row runs with --verify (a mismatch fails the row and ends the sweep: the
+GPU is never driven again after a failure), and every row's cell GB/s, p50 per
+message and the environment it ran under are written to <out>/rows.jsonl.
+<out>/summary.json names the winning setting per (direction, size) and the
+gain over the default (RCCL, one communicator, no knobs).
+
+It measures a link, so it needs N >= 2 GPUs and refuses N = 1.  ``--emulate``
+validates the whole script without a second GPU: ranks share GPU 0 through
+the IPC transport (``--emulate ipc``; the RCCL rows are skipped because RCCL
+refuses two ranks on one GPU) or run on the CPU host transport
+(``--emulate host``, build/p2p_matrix_host).  The reference has no tuning at
+all: it inherits whatever NCCL_* the shell has (p2p_matrix.cc:126-131).
+
+    python scripts/xgmi_pair_sweep.py --np 8 --out gpurun_out/xgmi_sweep
+    python scripts/xgmi_pair_sweep.py --np 2 --emulate ipc --sizes 4M,32M
+    python scripts/xgmi_pair_sweep.py --np 2 --emulate host --sizes 64K
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shlex
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from test_nccl_p2p_amd.utils import rccl_env  # noqa: E402
+MPIRUN = os.environ.get("P2P_MPIRUN", "/opt/conda/bin/mpirun")
+
+# RCCL knobs that act on point-to-point traffic within a node.  Each entry is
+# applied on top of the default environment at --comms 1, then the best knob
+# set is re-run at the best communicator count.
+RCCL_KNOBS = [
+    {"NCCL_NCHANNELS_PER_PEER": "2"},
+    {"NCCL_NCHANNELS_PER_PEER": "8"},
+    {"NCCL_NCHANNELS_PER_PEER": "16", "NCCL_MIN_P2P_NCHANNELS": "16"},
+    {"NCCL_NCHANNELS_PER_PEER": "32", "NCCL_MIN_P2P_NCHANNELS": "32", "NCCL_MAX_P2P_NCHANNELS": "64"},
+    {"NCCL_P2P_NVL_CHUNKSIZE": "524288"},
+    {"NCCL_P2P_NVL_CHUNKSIZE": "2097152"},
+    {"NCCL_P2P_NET_CHUNKSIZE": "2097152"},
+    {"NCCL_PROTO": "Simple"},
+    {"NCCL_PROTO": "LL128"},
+    {"RCCL_P2P_BATCH_ENABLE": "1"},
+    {"RCCL_P2P_BATCH_ENABLE": "1", "RCCL_P2P_BATCH_THRESHOLD": "1048576"},
+]
+COMMS = [1, 2, 4, 8]
+IPC_ENGINES = ["kernel", "sdma", "push", "relay"]
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--np", type=int, default=0, help="ranks (default: visible GPUs)")
+    ap.add_argument("--sizes", default="32M,1G")
+    ap.add_argument("--dirs", default="uni,bi")
+    ap.add_argument("--iters", default="auto")
+    ap.add_argument("--out", default="gpurun_out/xgmi_sweep")
+    ap.add_argument("--emulate", choices=["", "ipc", "host"], default="",
+                    help="validate without a second GPU: ranks share GPU 0 (ipc) or use the CPU (host)")
+    ap.add_argument("--rows", default="rccl,knobs,ipc", help="row groups to run: rccl, knobs, ipc")
+    ap.add_argument("--budget", type=float, default=900.0, help="seconds for the whole sweep; rows that would "
+                    "start after it is spent are listed as skipped")
+    ap.add_argument("--row-timeout", type=float, default=180.0)
+    ap.add_argument("--dry-run", action="store_true", help="print the rows and exit")
+    return ap.parse_args(argv)
+
+
+def visible_gpus() -> int:
+    # Device count without initialising the GPU (no HIP call in this process).
+    vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")
+    if vis:
+        return len([v for v in vis.split(",") if v.strip()])
+    try:
+        return len([d for d in os.listdir("/dev/dri") if d.startswith("renderD")])
+    except OSError:
+        return 0
+
+
+def plan_rows(args, np_):
+    """Every (name, transport args, env) row of the sweep, in run order."""
+    groups = set(args.rows.split(","))
+    rows = []
+    rccl_ok = args.emulate == ""
+    if "rccl" in groups and rccl_ok:
+        for k in COMMS:
+            rows.append({"name": "rccl-comms%d" % k, "args": ["--transport", "rccl", "--comms", str(k)], "env": {}})
+    if "knobs" in groups and rccl_ok:
+        for i, env in enumerate(RCCL_KNOBS):
+            name = "rccl-" + "-".join("%s=%s" % (k.replace("NCCL_", "").replace("RCCL_", "").lower(), v)
+                                      for k, v in env.items())
+            rows.append({"name": name, "args": ["--transport", "rccl", "--comms", "1"], "env": env, "knob": True})
+    if "ipc" in groups and args.emulate != "host":
+        for eng in IPC_ENGINES:
+            if eng == "relay" and np_ < 3:
+                continue  # relay needs a third GPU to route through
+            a = ["--transport", "ipc", "--ipc-engine", eng]
+            rows.append({"name": "ipc-" + eng, "args": a, "env": {"P2P_IPC_POOL": "4G"} if eng == "relay" else {}})
+    if args.emulate == "host":
+        rows.append({"name": "host", "args": ["--transport", "host"], "env": {}})
+    return rows
+
+
+def cell_result(js_path, dirs):
+    """{(dir, bytes): {...}} for the 0-1 cell of every pair run in the file."""
+    out = {}
+    for line in open(js_path):
+        rec = json.loads(line)
+        if rec.get("type") != "run" or rec.get("dir") not in dirs:
+            continue
+        for ph in rec["phases"]:
+            if (ph["row"], ph["col"]) != (0, 1):
+                continue
+            flows = ph["flows"]
+            gbs = [f["gbs"] for f in flows]
+            out[(rec["dir"], rec["bytes"])] = {
+                "cell_gbs": sum(gbs),  # bi: both directions, like the reference's bi matrix
+                "per_dir_gbs": sum(gbs) / len(gbs),
+                "p50_us": max(f["iter_us"]["p50"] for f in flows),
+                "mismatches": ph["mismatches"],
+                "iters": rec["iters"],
+            }
+    return out
+
+
+def run_row(args, row, np_, exe, tag):
+    js = os.path.join(args.out, "%s.json" % tag)
+    if os.path.exists(js):
+        os.remove(js)
+    cmd = [MPIRUN, "-n", str(np_), exe, "--mode", "pair", "--cells", "0-1", "--dir", "both", "--sizes", args.sizes,
+           "-n", args.iters, "--verify", "--no-compat", "--json", js, "--timeout", str(int(args.row_timeout))]
+    cmd += row["args"]
+    if args.emulate == "ipc":
+        cmd += ["--device", "0"]
+    env = dict(os.environ, **row["env"])
+    t0 = time.time()
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=args.row_timeout + 30)
+        rc, err = r.returncode, r.stderr
+    except subprocess.TimeoutExpired:
+        rc, err = 124, "row timed out"
+    rec = {"name": row["name"], "env": row["env"], "args": row["args"], "rc": rc, "seconds": round(time.time() - t0, 2),
+           "cmd": " ".join(shlex.quote(c) for c in cmd)}
+    if rc == 0:
+        res = cell_result(js, set(args.dirs.split(",")))
+        rec["cells"] = {"%s/%d" % k: v for k, v in sorted(res.items())}
+        bad = sum(v["mismatches"] for v in res.values())
+        if bad or not res:
+            rec["rc"] = 2
+            rec["error"] = "verify mismatches %d" % bad if bad else "no 0-1 cell in the output"
+    else:
+        rec["error"] = err[-1500:]
+    return rec
+
+
+def summarize(rows, dirs, sizes_seen):
+    base = next((r for r in rows if r["name"] == "rccl-comms1" and r["rc"] == 0), None)
+    if base is None:
+        base = next((r for r in rows if r["rc"] == 0), None)
+    best = {}
+    for r in rows:
+        if r["rc"] != 0:
+            continue
+        for key, c in r["cells"].items():
+            if key not in best or c["cell_gbs"] > best[key]["cell_gbs"]:
+                best[key] = {"row": r["name"], "env": r["env"], "args": r["args"], "cell_gbs": c["cell_gbs"],
+                             "p50_us": c["p50_us"]}
+    for key, b in best.items():
+        if base and key in base["cells"]:
+            b["baseline_row"] = base["name"]
+            b["baseline_gbs"] = base["cells"][key]["cell_gbs"]
+            b["gain"] = round(b["cell_gbs"] / base["cells"][key]["cell_gbs"], 4)
+    return best
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    np_ = args.np or (2 if args.emulate else visible_gpus())
+    if np_ < 2:
+        print("xgmi_pair_sweep: needs N >= 2 ranks on distinct GPUs (found %d); a 1-GPU box has no xGMI link. "
+              "Use --emulate ipc|host to validate the script." % np_, file=sys.stderr)
+        return 1
+    exe = os.path.join(ROOT, "build", "p2p_matrix_host" if args.emulate == "host" else "p2p_matrix")
+    rows = plan_rows(args, np_)
+    if args.dry_run:
+        for r in rows:
+            print(r["name"], " ".join(r["args"]), " ".join("%s=%s" % kv for kv in r["env"].items()))
+        return 0
+    if not args.emulate and visible_gpus() < np_:
+        print("xgmi_pair_sweep: %d ranks but %d visible GPUs" % (np_, visible_gpus()), file=sys.stderr)
+        return 1
+    if not os.path.exists(exe):
+        print("xgmi_pair_sweep: %s not built (make)" % exe, file=sys.stderr)
+        return 1
+    os.makedirs(args.out, exist_ok=True)
+    t_end = time.time() + args.budget
+    done, skipped, failed = [], [], None
+    with open(os.path.join(args.out, "rows.jsonl"), "w") as f:
+        for i, row in enumerate(rows):
+            if failed is not None or time.time() + 5 > t_end:
+                skipped.append(row["name"])
+                continue
+            rec = run_row(args, row, np_, exe, "row%02d" % i)
+            f.write(json.dumps(rec) + "\n")
+            f.flush()
+            done.append(rec)
+            cells = " ".join("%s %.1f" % (k, v["cell_gbs"]) for k, v in rec.get("cells", {}).items())
+            print("%-40s rc=%d %6.1fs %s" % (rec["name"], rec["rc"], rec["seconds"], cells or rec.get("error", "")[-200:]),
+                  flush=True)
+            if rec["rc"] != 0:
+                failed = rec["name"]  # never keep driving the GPU after a failure
+        # Best knob set at the best communicator count (knobs ran at --comms 1).
+        knob_rows = [r for r in done if r["rc"] == 0 and any(r["name"] == x["name"] and x.get("knob") for x in rows)]
+        comm_rows = [r for r in done if r["rc"] == 0 and r["name"].startswith("rccl-comms")]
+        if failed is None and knob_rows and comm_rows and time.time() + 5 < t_end:
+            key = sorted(comm_rows[0]["cells"])[-1]
+            bk = max(knob_rows, key=lambda r: r["cells"].get(key, {}).get("cell_gbs", 0))
+            bc = max(comm_rows, key=lambda r: r["cells"].get(key, {}).get("cell_gbs", 0))
+            if bc["name"] != "rccl-comms1":
+                combo = {"name": bk["name"] + "+" + bc["name"].split("-")[1], "env": bk["env"],
+                         "args": ["--transport", "rccl"] + bc["args"][2:]}
+                rec = run_row(args, combo, np_, exe, "combo")
+                f.write(json.dumps(rec) + "\n")
+                done.append(rec)
+                print("%-40s rc=%d %6.1fs" % (rec["name"], rec["rc"], rec["seconds"]), flush=True)
+    summary = {"np": np_, "emulate": args.emulate or None, "sizes": args.sizes, "dirs": args.dirs,
+               "base_env": rccl_env.capture(), "rows_run": len(done), "rows_skipped": skipped, "failed_row": failed,
+               "best": summarize(done, args.dirs, args.sizes)}
+    with open(os.path.join(args.out, "summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    print(json.dumps({"best": summary["best"], "failed_row": failed, "rows_skipped": skipped}))
+    return 2 if failed else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

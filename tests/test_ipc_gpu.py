@@ -37,7 +37,7 @@ def test_two_ranks_all_modes(exe, tmp_path, engine):
 
 
 def _device_latency(out_json):
-    lines = [json.loads(l) for l in out_json.read_text().splitlines() if '"latency"' in l]
+    lines = [json.loads(l) for l in outjson.read_text().splitlines() if '"latency"' in l]
     dev = [l for l in lines if l.get("method") == "device"]
     assert len(dev) == 1
     return dev[0]
@@ -272,3 +272,19 @@ def test_cli_fuzz_four_ranks(exe, engine):
                           "--timeout", "60"], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     assert "all verified" in out.stdout
+
+
+def test_xgmi_pair_sweep_emulated():
+    """scripts/xgmi_pair_sweep.py end to end on one GPU: two ranks share GPU 0
+    through the IPC engines (RCCL rows need distinct GPUs); every row verified
+    and a winner per (direction, size) written."""
+    import tempfile
+    out_dir = tempfile.mkdtemp(prefix="xgmi_sweep_")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "xgmi_pair_sweep.py"), "--np", "2",
+                          "--emulate", "ipc", "--sizes", "4M,32M", "--out", out_dir, "--budget", "150",
+                          "--row-timeout", "60"], capture_output=True, text=True, timeout=200)
+    assert out.returncode == 0, out.stderr[-3000:] + out.stdout[-3000:]
+    s = json.loads(open(os.path.join(out_dir, "summary.json")).read())
+    assert s["failed_row"] is None and s["rows_run"] == 3 and not s["rows_skipped"], s
+    assert set(s["best"]) == {"uni/4194304", "uni/33554432", "bi/4194304", "bi/33554432"}
+    assert all(b["cell_gbs"] > 10 for b in s["best"].values()), s["best"]

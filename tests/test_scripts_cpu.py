@@ -1,0 +1,41 @@
+"""CPU checks of the operator scripts: the xGMI pair sweep runs end to end on
+the host transport (emulated ranks) and refuses a 1-GPU box."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+SWEEP = os.path.join(ROOT, "scripts", "xgmi_pair_sweep.py")
+
+
+def test_pair_sweep_refuses_one_rank():
+    out = subprocess.run([sys.executable, SWEEP, "--np", "1"], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 1 and "N >= 2" in out.stderr
+
+
+def test_pair_sweep_dry_run_lists_every_knob():
+    out = subprocess.run([sys.executable, SWEEP, "--np", "8", "--dry-run"], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    txt = out.stdout
+    for want in ("--comms 8", "NCCL_NCHANNELS_PER_PEER", "NCCL_P2P_NVL_CHUNKSIZE", "NCCL_P2P_NET_CHUNKSIZE",
+                 "NCCL_PROTO", "RCCL_P2P_BATCH_ENABLE", "--ipc-engine sdma", "--ipc-engine push",
+                 "--ipc-engine relay"):
+        assert want in txt, want
+
+
+@pytest.mark.mpi
+def test_pair_sweep_host_emulation(mpirun, host_build, tmp_path):
+    out = subprocess.run([sys.executable, SWEEP, "--np", "2", "--emulate", "host", "--sizes", "64K,1M",
+                          "--out", str(tmp_path)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr + out.stdout
+    s = json.loads((tmp_path / "summary.json").read_text())
+    assert s["failed_row"] is None and s["rows_run"] == 1
+    assert set(s["best"]) == {"uni/65536", "uni/1048576", "bi/65536", "bi/1048576"}
+    for b in s["best"].values():
+        assert b["cell_gbs"] > 0 and b["gain"] == 1.0
+    rows = [json.loads(l) for l in (tmp_path / "rows.jsonl").read_text().splitlines()]
+    assert all(c["mismatches"] == 0 for r in rows for c in r["cells"].values())
