@@ -66,7 +66,7 @@ RESERVE_S = 15.0  # kept free at the end of the deadline for the JSON line and t
 
 
 def log(*a):
-    print(*a, file=sys.stderr, flush=True)
+    print("[%7.1fs]" % (time.monotonic() - T0), *a, file=sys.stderr, flush=True)
 
 
 def claim_stdout() -> int:
@@ -223,15 +223,19 @@ def steps_through(nat, isess, args, mode, size, batch, transport, deadline=None)
         phases = len(nat.schedule(mode, "bi", n))
         idrv = nat.StepDriver(isess, mode, "bi", size, args.msgs, not args.no_verify, bool(batch), False,
                               depth=pick_depth(args.steps, phases), salt=2)
+        say = (lambda m: log("bench: %s: %s" % (transport, m))) if isess.rank == 0 else (lambda m: None)
         idrv.connect()
+        say("connected (%d receive generations)" % idrv.depth)
         idrv.run_steps(0, args.warmup)
         idrv.sync()
         idrv.poison()
         isess.barrier()
+        say("warm")
         i0 = time.perf_counter()
         idrv.run_steps(args.warmup, args.steps)
         idrv.sync()
         isess.barrier()
+        say("timed steps done")
         ielapsed = isess.allreduce_max(time.perf_counter() - i0)
         steps = range(args.warmup, args.warmup + args.steps)
         value, aggregate = headline_stats(sum(idrv.job_bytes_per_step(k) for k in steps),
@@ -286,6 +290,8 @@ def child_main(args) -> int:
     env = dist_env()
     device = env.local_rank if args.device is None else args.device
     size = nat.parse_size(args.size)
+    if env.rank == 0:
+        log("bench: child %s started" % args.child)
     try:
         sess = nat.Session(env.rank, env.world, host=env.master_addr, port=args.child_port, device=device,
                            transport=args.child, timeout_s=min(90.0, args.timeout))
@@ -294,6 +300,7 @@ def child_main(args) -> int:
     except Exception as e:
         out = {"error": str(e)[:300], "transport": args.child}
     if env.rank == 0:
+        log("bench: child %s done" % args.child)
         with open(args.child_out, "w") as f:
             json.dump(out, f)
     return 0

@@ -100,6 +100,14 @@ class IpcTransport final : public Transport {
     tick_hz_ = khz * 1e3;
     if (const char* pc = std::getenv("P2P_IPC_POOL")) pool_cap_ = std::strcmp(pc, "0") ? parse_size(pc) : 0;
     if (const char* ir = std::getenv("P2P_INJECT_EXPORT_REFUSALS")) inject_refusals_ = std::atoi(ir);
+    // HIP 7.0's hipIpcOpenMemHandle never returns for a block whose size mod
+    // 4 GiB is 2 GiB or more (scripts/ipc_open_probe.hip: 2 and 3.75 and 7 GiB
+    // hang, 2 GiB - 2 MiB, 4, 4 GiB + 2 MiB and 5 GiB open in 0.1 s; HIP 7.2
+    // opens them all).  Exported blocks are sized around it on such runtimes.
+    int hip_rt = 0;
+    if (hipRuntimeGetVersion(&hip_rt) != hipSuccess) hip_rt = 0;
+    size_fix_ = hip_rt < 70200000;
+    if (const char* sf = std::getenv("P2P_IPC_SIZE_FIX")) size_fix_ = std::atoi(sf) != 0;
     if (push_) setup_sync_pages();
   }
 
@@ -150,7 +158,9 @@ class IpcTransport final : public Transport {
   // allocation churn between runs.
   void* alloc(size_t bytes) override {
     constexpr size_t kGrain = size_t{2} << 20;
-    const size_t size = (std::max<size_t>(bytes, 1) + kGrain - 1) / kGrain * kGrain;
+    size_t size = (std::max<size_t>(bytes, 1) + kGrain - 1) / kGrain * kGrain;
+    constexpr size_t k4G = size_t{4} << 30;
+    if (size_fix_ && size % k4G >= k4G / 2) size = (size / k4G + 1) * k4G;  // see size_fix_
     for (auto it = pool_.begin(); it != pool_.end(); ++it)
       if (it->second.size == size) {
         void* p = it->first;
@@ -207,6 +217,9 @@ class IpcTransport final : public Transport {
   // peer (at the message's offset).  Push / relay also map every peer's
   // receive arena: one export per set, slot i at base + i * stride.
   void register_buffers(const BufferSet& set) override {
+    if (debug_)
+      std::fprintf(stderr, "ipc rank %d: register send %zu B, arena %d x %zu B\n", rank_, set.send_bytes, set.nslots,
+                   set.stride);
     Export me{};
     me.handle = handle_of(set.send);
     me.bytes = set.send_bytes;
@@ -234,6 +247,7 @@ class IpcTransport final : public Transport {
       void* mapped = nullptr;
       HIPCHECK(hipIpcOpenMemHandle(&mapped, all[static_cast<size_t>(r)].handle, hipIpcMemLazyEnablePeerAccess));
       reg.peer_send[static_cast<size_t>(r)] = mapped;
+      if (debug_) std::fprintf(stderr, "ipc rank %d: mapped send buffer of rank %d\n", rank_, r);
     }
     if (push_) {
       // The sender (or a relay) writes into the receiver's slot: map every
@@ -252,6 +266,7 @@ class IpcTransport final : public Transport {
           HIPCHECK(hipIpcOpenMemHandle(&mapped, arenas[static_cast<size_t>(r)].handle, hipIpcMemLazyEnablePeerAccess));
         reg.peer_recv[static_cast<size_t>(r)] = mapped;
         reg.peer_nslots[static_cast<size_t>(r)] = arenas[static_cast<size_t>(r)].nslots;
+        if (debug_) std::fprintf(stderr, "ipc rank %d: mapped receive arena of rank %d\n", rank_, r);
       }
     }
     regs_.push_back(std::move(reg));
@@ -817,6 +832,7 @@ class IpcTransport final : public Transport {
     pool_bytes_ = 0;
   }
   size_t pool_cap_ = size_t{32} << 30;
+  bool size_fix_ = true;  // round exported blocks so size mod 4 GiB < 2 GiB (HIP < 7.2 IPC import hang)
   int inject_refusals_ = 0;
   std::vector<std::pair<void*, Block>> pool_;  // released, kept for reuse
   size_t pool_bytes_ = 0;

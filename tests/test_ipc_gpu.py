@@ -288,3 +288,17 @@ def test_xgmi_pair_sweep_emulated():
     assert s["failed_row"] is None and s["rows_run"] == 3 and not s["rows_skipped"], s
     assert set(s["best"]) == {"uni/4194304", "uni/33554432", "bi/4194304", "bi/33554432"}
     assert all(b["cell_gbs"] > 10 for b in s["best"].values()), s["best"]
+
+
+def test_push_arena_between_2_and_4_gib():
+    """A push receive arena of 2.5 GiB (80 slots of 32 MiB): HIP 7.0's
+    hipIpcOpenMemHandle never returns for a block whose size mod 4 GiB is
+    2 GiB or more; the transport sizes its exported blocks around that
+    (scripts/ipc_open_probe.hip)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "tests/scripts/step_probe.py", "ipc:push", "tournament",
+           "32M", "8", "10", "12"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=120, cwd=ROOT,
+                         env=dict(os.environ, P2P_FUZZ_DEVICE="0", P2P_FUZZ_TIMEOUT="30"))
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert out.stderr.count("'mismatches': 0, 'verified_msgs': 72") == 2, out.stderr[-3000:]
