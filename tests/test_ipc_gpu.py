@@ -37,7 +37,7 @@ def test_two_ranks_all_modes(exe, tmp_path, engine):
 
 
 def _device_latency(out_json):
-    lines = [json.loads(l) for l in outjson.read_text().splitlines() if '"latency"' in l]
+    lines = [json.loads(l) for l in out_json.read_text().splitlines() if '"latency"' in l]
     dev = [l for l in lines if l.get("method") == "device"]
     assert len(dev) == 1
     return dev[0]
