@@ -301,4 +301,7 @@ def test_push_arena_between_2_and_4_gib():
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=120, cwd=ROOT,
                          env=dict(os.environ, P2P_FUZZ_DEVICE="0", P2P_FUZZ_TIMEOUT="30"))
     assert out.returncode == 0, out.stderr[-3000:]
-    assert out.stderr.count("'mismatches': 0, 'verified_msgs': 72") == 2, out.stderr[-3000:]
+    # 10 receive generations x 16 messages: every slot of the arena written and verified.
+    assert out.stderr.count("driver (depth 10, 2684354560 receive bytes)") == 2, out.stderr[-3000:]
+    assert out.stderr.count("'mismatches': 0, 'verified_msgs': 160, 'timed_msgs': 192, 'slots': 160") == 2, \
+        out.stderr[-3000:]
