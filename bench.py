@@ -561,9 +561,9 @@ def main(argv=None) -> int:
         "data": "synthetic (device PRNG-filled payloads, one stream per message; every timed delivery verified on "
                 "the device after timing)",
         "config": {
-            "model": "p2p_matrix: %s %s %s, %s x %d msgs/step"
+            "model": "p2p_matrix: %s %s, %s x %d msgs/step"
                      % ("RCCL ncclSend/ncclRecv" if headline_transport == "rccl" else headline_transport + " transport",
-                        mode, "self send/recv (uni)" if mode == "self" else "bidirectional",
+                        "self send/recv (uni)" if mode == "self" else mode + " bidirectional",
                         nat.format_size(size), args.msgs),
             "global_batch": args.msgs * n,
             "seq_len": size,
@@ -654,10 +654,11 @@ def main(argv=None) -> int:
         for p in lat["pairs"]:  # a < b; the ping-pong's one-way time holds for both directions
             lat_matrix[p["a"]][p["b"]] = lat_matrix[p["b"]][p["a"]] = round(p["one_way_us"]["p50"], 3)
         p50s = [p["one_way_us"]["p50"] for p in lat["pairs"]]
-        return statistics.median(p50s) if p50s else None
+        return float(statistics.median(p50s)) if p50s else None
 
     p50 = section("latency", latency, budgeted=False)
-    reporter.update(p50_latency_us=round(p50, 3) if isinstance(p50, float) else None, latency_p50_us_matrix=lat_matrix)
+    reporter.update(p50_latency_us=round(float(p50), 3) if isinstance(p50, (int, float)) else None,
+                    latency_p50_us_matrix=lat_matrix)
 
     # The reference's own methodology on one communicator, for comparison
     # (serial ordered pairs, host clock, one stream sync per message, no

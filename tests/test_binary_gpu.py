@@ -62,7 +62,13 @@ def test_bench_contract_single_gpu():
     assert len(lines) == 1
     r = json.loads(lines[0])
     assert r["n_gpus"] == 1 and r["steps"] == 6 and r["value"] > 10
-    assert r["verify_mismatches"] == 0 and r["transport"] == "rccl"
+    assert r["verify_mismatches"] == 0 and r["transport"] == "rccl" and r["verify_coverage"] == 1.0
+    # The posting the tuning laps chose is never slower than one communicator.
+    t = r["posting"]["tuning_ms_per_step"]
+    chosen = "comms%d_%s" % (r["posting"]["rccl_comms"], "batch" if r["posting"]["batch"] else "per_message")
+    assert t[chosen] <= min(v for k, v in t.items() if k.startswith("comms1_")), t
+    assert r["posting"]["rccl_comms"] == 4, t  # four communicators: ~2x one on the self path
+    assert isinstance(r["p50_latency_us"], float) and r["p50_latency_us"] > 0
 
 
 def test_topology_probe(exe):
