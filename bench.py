@@ -95,13 +95,17 @@ def first_comms(transport: str, comms: int) -> int:
     return comms if transport == "rccl" and comms > 0 else 1
 
 
-def posting_candidates(transport: str, comms: int, batch: int):
+def posting_candidates(transport: str, comms: int, batch: int, n: int = 1):
     """(communicators, batch) pairs the tuning laps time against each other.
 
-    comms: > 0 fixed, -1 = RCCL picks between 1 and 4 (other transports: 1).
-    batch: 1 one group per step, 0 one group per message, -1 = both (K = 1
-    only: with several communicators per-message groups cannot overlap)."""
-    comms_choices = ([comms] if comms > 0 else [1, 4]) if transport == "rccl" else [1]
+    comms: > 0 fixed, -1 = RCCL picks: between 1 and 4 on one GPU (measured:
+    2, 3, 6 and 8 are slower there, profiles/r2_step_shape/), between 1, 2, 4
+    and 8 across GPUs, where no measurement has fixed the count for an xGMI
+    link yet (other transports: 1).  batch: 1 one group per step, 0 one group
+    per message, -1 = both (K = 1 only: with several communicators
+    per-message groups cannot overlap)."""
+    auto = [1, 4] if n == 1 else [1, 2, 4, 8]
+    comms_choices = ([comms] if comms > 0 else auto) if transport == "rccl" else [1]
     batch_choices = [batch] if batch >= 0 else [0, 1]
     return [(c, b) for c in comms_choices for b in batch_choices if c == 1 or b == 1 or len(batch_choices) == 1]
 
@@ -433,11 +437,12 @@ def main(argv=None) -> int:
         budget = 256 << 20
 
     # ---- posting selection: one untimed lap of the schedule per candidate --
-    # (one group per step vs one per message; RCCL: one communicator vs four
-    # whose send/recv kernels run side by side), timed by the slowest rank,
+    # (one group per step vs one per message; RCCL: one communicator vs
+    # several whose send/recv kernels run side by side, posting_candidates),
+    # timed by the slowest rank,
     # before the W warmup steps of the chosen one.
     state["section"] = "tuning"
-    choices = posting_candidates(args.transport, args.comms, args.batch)
+    choices = posting_candidates(args.transport, args.comms, args.batch, n)
     c0 = first_comms(args.transport, args.comms)
     sessions = {c0: sess}
 
@@ -480,6 +485,13 @@ def main(argv=None) -> int:
                 if agree(err is None):
                     tuning[(c, b)] = sess.allreduce_max(w) / tune_k
                     del d
+                    # Only the best communicator count so far, the headline
+                    # session and the single communicator (kept for the
+                    # reference-method comparison) stay open.
+                    best_c = min(tuning, key=tuning.get)[0]
+                    for cc in [cc for cc in sessions if cc not in (c0, 1, best_c)]:
+                        if not any(cc == c2 for (c2, _) in choices[i + 1:]):
+                            del sessions[cc]
                     continue
             if not droppable:
                 raise RuntimeError(err or "the first posting candidate failed on another rank")

@@ -6,7 +6,12 @@ build/p2p_matrix under every setting that can move a single xGMI link:
 
   rccl rows   --comms 1, 2, 4, 8 (messages spread over K communicators / streams)
               NCCL_NCHANNELS_PER_PEER, NCCL_P2P_NVL_CHUNKSIZE / NCCL_P2P_NET_CHUNKSIZE,
-              NCCL_PROTO, RCCL_P2P_BATCH_ENABLE / RCCL_P2P_BATCH_THRESHOLD
+              NCCL_PROTO, RCCL_P2P_BATCH_ENABLE / RCCL_P2P_BATCH_THRESHOLD,
+              NCCL_P2P_READ_ENABLE (peer reads vs writes over the link),
+              P2P_RCCL_REGISTER=1|2 (user buffers registered with every
+              communicator / allocated by ncclMemAlloc: RCCL may then move
+              data straight between the user buffers instead of through its
+              staging FIFO, csrc/transport_rccl.cpp)
   ipc rows    --ipc-engine kernel (one-sided pull by the gfx950 copy kernel),
               sdma, push, relay (stripes through idle third GPUs, N >= 3)
 
@@ -57,6 +62,10 @@ RCCL_KNOBS = [
     {"NCCL_PROTO": "LL128"},
     {"RCCL_P2P_BATCH_ENABLE": "1"},
     {"RCCL_P2P_BATCH_ENABLE": "1", "RCCL_P2P_BATCH_THRESHOLD": "1048576"},
+    {"NCCL_P2P_READ_ENABLE": "0"},
+    {"NCCL_P2P_READ_ENABLE": "1"},
+    {"P2P_RCCL_REGISTER": "1"},
+    {"P2P_RCCL_REGISTER": "2"},
 ]
 COMMS = [1, 2, 4, 8]
 IPC_ENGINES = ["kernel", "sdma", "push", "relay"]
@@ -100,7 +109,7 @@ def plan_rows(args, np_):
             rows.append({"name": "rccl-comms%d" % k, "args": ["--transport", "rccl", "--comms", str(k)], "env": {}})
     if "knobs" in groups and rccl_ok:
         for i, env in enumerate(RCCL_KNOBS):
-            name = "rccl-" + "-".join("%s=%s" % (k.replace("NCCL_", "").replace("RCCL_", "").lower(), v)
+            name = "rccl-" + "-".join("%s=%s" % (k.replace("P2P_", "").replace("NCCL_", "").replace("RCCL_", "").lower(), v)
                                       for k, v in env.items())
             rows.append({"name": name, "args": ["--transport", "rccl", "--comms", "1"], "env": env, "knob": True})
     if "ipc" in groups and args.emulate != "host":

@@ -10,6 +10,9 @@ import bench  # noqa: E402
 def test_posting_candidates_default_rccl():
     # One communicator per-message and batched, four communicators batched.
     assert bench.posting_candidates("rccl", -1, -1) == [(1, 0), (1, 1), (4, 1)]
+    # Across GPUs the communicator count for one xGMI link is open: 1, 2, 4, 8.
+    assert bench.posting_candidates("rccl", -1, -1, 8) == [(1, 0), (1, 1), (2, 1), (4, 1), (8, 1)]
+    assert bench.posting_candidates("rccl", 4, -1, 8) == [(4, 1)]
 
 
 def test_posting_candidates_fixed_and_other_transports():
