@@ -344,7 +344,8 @@ def parse_args(argv=None):
                          "generations, and so verify_coverage")
     ap.add_argument("--json-out", default=None, help="also write the result line to this file")
     ap.add_argument("--ipc-extra", type=int, default=1,
-                    help="1: also run the tournament steps through the IPC transport (N > 1, after the timed region)")
+                    help="1: also run the timed steps through the IPC engines (pull, push, sdma; relay from N = 3) "
+                         "after the timed region, untimed by the contract, each in a child process per rank")
     ap.add_argument("--extras", type=int, default=1,
                     help="1: also measure all-pairs 1 GiB, ring 256 MiB and the ring token hop after the timed "
                          "region (N > 1)")
@@ -832,8 +833,10 @@ def main(argv=None) -> int:
     # rendezvous engine that writes into the receiver's slot ("push"), the
     # SDMA copy engines pulling instead of CUs ("sdma"), and multi-path push
     # with two-hop relays through GPUs whose links are idle ("relay").
+    # With one GPU the same engines run the self step (the GPU copies to
+    # itself through its own mapping), next to RCCL's self copy.
     ipc = None
-    if n > 1 and args.ipc_extra and extra_transport:
+    if args.ipc_extra and extra_transport:
         runs = [(extra_transport, None)]
         if extra_transport == "ipc":
             runs += [("ipc:push", "push"), ("ipc:sdma", "sdma")] + ([("ipc:relay", "relay")] if n > 2 else [])
@@ -860,6 +863,8 @@ def main(argv=None) -> int:
                 continue
             if transport in engines:
                 r["engine"] = engines[transport]
+            if isinstance(r.get("value_gbs"), (int, float)) and value > 0:
+                r["ratio_to_headline"] = round(r["value_gbs"] / value, 3)
             if key is None:
                 ipc = r
             elif ipc is not None:

@@ -69,6 +69,12 @@ def test_bench_contract_single_gpu():
     assert t[chosen] <= min(v for k, v in t.items() if k.startswith("comms1_")), t
     assert r["posting"]["rccl_comms"] == 4, t  # four communicators: ~2x one on the self path
     assert isinstance(r["p50_latency_us"], float) and r["p50_latency_us"] > 0
+    # The hand-written data plane runs the same self step after the timed
+    # region: pull, push and SDMA engines, all verified.
+    ipc = r["ipc_transport"]
+    assert ipc["verify_mismatches"] == 0 and ipc["value_gbs"] > 0, ipc
+    assert ipc["push"]["verify_mismatches"] == 0 and ipc["sdma"]["verify_mismatches"] == 0, ipc
+    assert 0 < ipc["device_pingpong_p50_us"] < 50, ipc
 
 
 def test_topology_probe(exe):
