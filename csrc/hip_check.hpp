@@ -5,6 +5,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <cstring>
+
 #include "common.hpp"
 
 #define HIPCHECK(cmd)                                                                            \
@@ -12,3 +15,23 @@
     hipError_t e_ = (cmd);                                                                       \
     if (e_ != hipSuccess) P2P_FATAL(::p2p::strfmt("HIP error in %s: %s", #cmd, hipGetErrorString(e_))); \
   } while (0)
+
+namespace p2p {
+
+// Flags of the events that only timestamp the stream (Transport::mark).  A
+// default event's record ends in a system-scope release: the L2 writes back
+// every dirty line before the event reads "recorded", which after a bulk copy
+// is ~10 us of idle GPU per mark (two marks per bench step: 10.5 us gaps
+// between steps in the IPC trace, profiles/r2_mark_fence/).  Timing needs no
+// fence -- the host never reads payload through these events, and stream
+// order, not the event, orders the work -- so marks skip it
+// (hipEventDisableSystemFence).  P2P_MARK_FENCE=system restores the default.
+inline unsigned timing_event_flags() {
+  static const unsigned flags = [] {
+    const char* e = std::getenv("P2P_MARK_FENCE");
+    return (e && std::strcmp(e, "system") == 0) ? unsigned{hipEventDefault} : unsigned{hipEventDisableSystemFence};
+  }();
+  return flags;
+}
+
+}  // namespace p2p

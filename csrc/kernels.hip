@@ -20,6 +20,8 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -575,6 +577,10 @@ struct CopyArgs {
   uint32_t block_begin[kMaxCopyOps + 1];
   uint32_t coherent;  // bit i: op i moves between GPUs (system-coherent accesses)
   int nops;
+  // Workgroup -> op lookup: > 0 every op has this many blocks (one division);
+  // 0 binary search of block_begin; -1 the linear scan (A/B only,
+  // P2P_COPY_LOOKUP=linear).
+  int32_t uniform;
 };
 
 // gfx940+ cache-policy bits of a buffer access: sc0 | sc1 = system scope.
@@ -586,10 +592,24 @@ constexpr int kSystemCoherent = 1 | 16;
 constexpr int kRsrcFlags = 0x00020000;  // raw buffer descriptor word 3 for gfx950
 
 __global__ __launch_bounds__(kBlock) void multi_copy_kernel(const CopyArgs a) {
-  // Workgroup -> op: block ranges are contiguous per op; the scan is over at
-  // most kMaxCopyOps wave-uniform values.
+  // Workgroup -> op: block ranges are contiguous per op.  Every workgroup
+  // moves a single 4 KiB chunk, so this lookup is on its critical path: a
+  // linear scan of up to 16 dependent scalar loads cost 6% at 16 ops x 32 MiB
+  // (2.95 vs 3.14 TB/s, profiles/r2_copy_lookup/); equal-sized ops (every
+  // bench step) take one division, others a 4-step binary search.
   int op = 0;
-  while (op + 1 < a.nops && blockIdx.x >= a.block_begin[op + 1]) ++op;
+  if (a.uniform > 0) {
+    op = min(static_cast<int>(blockIdx.x / static_cast<uint32_t>(a.uniform)), a.nops - 1);
+  } else if (a.uniform == 0) {
+    int lo = 0, hi = a.nops - 1;  // largest op with block_begin[op] <= blockIdx.x
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (blockIdx.x >= a.block_begin[mid]) lo = mid; else hi = mid - 1;
+    }
+    op = lo;
+  } else {
+    while (op + 1 < a.nops && blockIdx.x >= a.block_begin[op + 1]) ++op;
+  }
   const uint32_t b = blockIdx.x - a.block_begin[op];
   const uint32_t nb = a.block_begin[op + 1] - a.block_begin[op];
   const uint4* __restrict__ s = a.src[op];
@@ -654,6 +674,14 @@ void launch_copy_group(const CopyOp* ops, int cnt, hipStream_t stream, int max_b
     acc += static_cast<uint32_t>(std::min(share, need[i]));
   }
   a.block_begin[cnt] = acc;
+  a.uniform = static_cast<int32_t>(a.block_begin[1] - a.block_begin[0]);
+  for (int i = 1; i < cnt; ++i)
+    if (a.block_begin[i + 1] - a.block_begin[i] != static_cast<uint32_t>(a.uniform)) a.uniform = 0;
+  static const bool linear = [] {
+    const char* e = std::getenv("P2P_COPY_LOOKUP");
+    return e && std::strcmp(e, "linear") == 0;
+  }();
+  if (linear) a.uniform = -1;
   multi_copy_kernel<<<acc, kBlock, 0, stream>>>(a);
   HIP_OK(hipGetLastError());
 }

@@ -14,6 +14,7 @@
 
 #include <memory>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "app.hpp"
@@ -290,9 +291,9 @@ PYBIND11_MODULE(_p2pcore, m) {
       .def_property_readonly("recv_bytes", [](PyStepDriver& s) { return s.d().recv_bytes(); })
       .def("connect", [](PyStepDriver& s) { s.d().connect(); }, py::call_guard<py::gil_scoped_release>())
       .def("step", [](PyStepDriver& s, long k) { s.d().step(k); }, py::call_guard<py::gil_scoped_release>())
-      .def("run_steps", [](PyStepDriver& s, long first, long count) {
-            for (long k = first; k < first + count; ++k) s.d().step(k);
-          }, py::call_guard<py::gil_scoped_release>())
+      .def("run_steps", [](PyStepDriver& s, long first, long count) { s.d().run_steps(first, count); },
+           py::call_guard<py::gil_scoped_release>(),
+           "Enqueue steps [first, first+count); consecutive steps share their boundary timestamp.")
       .def("sync", [](PyStepDriver& s) { s.d().sync(); }, py::call_guard<py::gil_scoped_release>())
       .def("step_ms", [](PyStepDriver& s) { return s.d().step_ms(); })
       .def("reset", [](PyStepDriver& s) { s.d().reset(); })
@@ -332,6 +333,15 @@ PYBIND11_MODULE(_p2pcore, m) {
       py::arg("coherent") = false,
       "The IPC transport's gfx950 copy kernel on one (dst, src) pair (coherent: the cross-GPU form with "
       "system-scope sc0 sc1 buffer loads and stores).");
+  m.def("copy_many", [](const std::vector<std::tuple<uintptr_t, uintptr_t, size_t>>& ops, uintptr_t stream,
+                        bool coherent) {
+        std::vector<dev::CopyOp> v;
+        for (const auto& o : ops)
+          v.push_back({reinterpret_cast<const void*>(std::get<1>(o)), reinterpret_cast<void*>(std::get<0>(o)),
+                       std::get<2>(o), coherent});
+        dev::launch_multi_copy(v.data(), static_cast<int>(v.size()), as_stream(stream));
+      }, py::arg("ops"), py::arg("stream") = 0, py::arg("coherent") = false,
+      "The copy kernel over several (dst, src, bytes) ops, as the IPC transport launches a group's receives.");
   m.def("fill_geometry", [](size_t bytes) {
     auto g = dev::fill_geometry(bytes);
     return py::make_tuple(g.grid, g.block, g.lds_bytes);

@@ -220,6 +220,10 @@ class StepDriver {
   ~StepDriver();
   void connect();               // warm every phase once (collective, blocking)
   void step(long k);            // enqueue step k
+  // Enqueue steps [first, first + count): consecutive steps share their
+  // boundary mark (step k's end is step k + 1's start), so a step costs one
+  // timestamp event instead of two (each is a barrier packet on the queue).
+  void run_steps(long first, long count);
   void sync();                  // wait for everything posted
   std::vector<double> step_ms();       // this rank's per-step durations since the last reset
   void reset();                 // forget recorded steps
@@ -262,6 +266,9 @@ class StepDriver {
   std::vector<int> graphs_;  // per (generation, phase), when opt_.graph
   long last_step_ = -1;
   bool skip_armed_ = false;
+  int chain_mark_ = -1;  // run_steps: the previous step's end mark, the next one's start
+
+  void step_impl(long k, bool chain);
 
   void post_step_ops(const Phase& p, int pi, int gen);
   int gen_of(long k) const { return static_cast<int>((k / phases()) % depth_); }

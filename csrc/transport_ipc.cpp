@@ -384,7 +384,7 @@ class IpcTransport final : public Transport {
   int mark() override {
     if (next_event_ == static_cast<int>(events_.size())) {
       hipEvent_t ev;
-      HIPCHECK(hipEventCreate(&ev));
+      HIPCHECK(hipEventCreateWithFlags(&ev, timing_event_flags()));
       events_.push_back(ev);
     }
     HIPCHECK(hipEventRecord(events_[static_cast<size_t>(next_event_)], stream_));

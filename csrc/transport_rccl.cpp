@@ -343,7 +343,7 @@ class RcclTransport final : public Transport {
     const size_t m = static_cast<size_t>(next_event_);
     if (m == events_.size()) {
       hipEvent_t ev;
-      HIPCHECK(hipEventCreate(&ev));
+      HIPCHECK(hipEventCreateWithFlags(&ev, timing_event_flags()));
       events_.push_back(ev);
       side_ev_.emplace_back(cstreams_.size(), nullptr);
       side_rec_.emplace_back(cstreams_.size(), 0);
@@ -354,7 +354,7 @@ class RcclTransport final : public Transport {
     for (size_t j = 0; j < cstreams_.size(); ++j) {
       side_rec_[m][j] = 0;
       if (j < pending_.size() && pending_[j]) {
-        if (!side_ev_[m][j]) HIPCHECK(hipEventCreate(&side_ev_[m][j]));
+        if (!side_ev_[m][j]) HIPCHECK(hipEventCreateWithFlags(&side_ev_[m][j], timing_event_flags()));
         HIPCHECK(hipEventRecord(side_ev_[m][j], cstreams_[j]));
         side_rec_[m][j] = 1;
         pending_[j] = false;

@@ -696,8 +696,13 @@ TEST(test_step_driver_verifies_timed_steps) {
       for (long k = 0; k < 2; ++k) d.step(k);  // warmup
       d.sync();
       d.poison();
-      for (long k = 2; k < 2 + steps; ++k) d.step(k);
+      d.run_steps(2, steps);  // chained marks: one per step boundary
       d.sync();
+      {
+        auto ms = d.step_ms();
+        EXPECT(ms.size() == static_cast<size_t>(2 + steps));
+        for (double v : ms) EXPECT(v >= 0);
+      }
       StepVerifyReport r = d.verify_steps(2, steps);
       EXPECT(r.mismatches == 0);
       // 4 ranks x 1 sender x 3 messages per step.
