@@ -118,8 +118,9 @@ def _timed_tbs(fn, nbytes, reps=5):
 
 def test_kernel_bandwidth_floors(native):
     """Performance floors at 1 GiB, about 80% of the profiled rates
-    (profiles/r1_final/kernel_bench.txt: fill 6.99, lds8 verify 6.20, copy
-    3.13 TB/s; the measured HBM roof is 6.29): a kernel regression fails the
+    (profiles/r1_final/kernel_bench.txt: fill 6.99, lds8 verify 6.20;
+    profiles/r2_copy_nt/kernel_bench.txt: copy 3.31 TB/s with non-temporal
+    accesses; the measured HBM roof is 6.29): a kernel regression fails the
     GPU tier instead of passing it at a third of its speed."""
     nbytes = 1 << 30
     buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
@@ -135,7 +136,7 @@ def test_kernel_bandwidth_floors(native):
     print("fill %.2f  verify-lds8 %.2f  copy %.2f TB/s" % (fill_tbs, lds8_tbs, copy_tbs))
     assert fill_tbs > 5.5, fill_tbs
     assert lds8_tbs > 5.0, lds8_tbs
-    assert copy_tbs > 2.5, copy_tbs  # payload bytes (read once + written once)
+    assert copy_tbs > 2.65, copy_tbs  # payload bytes (read once + written once)
 
 
 def test_fill_verify_beyond_16gib():
