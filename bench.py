@@ -349,6 +349,8 @@ def parse_args(argv=None):
     ap.add_argument("--extras", type=int, default=1,
                     help="1: also measure all-pairs 1 GiB, ring 256 MiB and the ring token hop after the timed "
                          "region (N > 1)")
+    ap.add_argument("--allpairs-size", default="1G", help="message size of the all-pairs extra (BASELINE config 4: 1 GiB)")
+    ap.add_argument("--ring-size", default="256M", help="message size of the ring extra (BASELINE config 5: 256 MiB)")
     ap.add_argument("--sweep", type=int, default=1,
                     help="1: also sweep the single pair 0 -> 1 over 4 KiB .. --sweep-max (N > 1, after the timed region)")
     ap.add_argument("--sweep-max", default="4G", help="largest message of the pair sweep")
@@ -730,8 +732,10 @@ def main(argv=None) -> int:
         if env.rank == 0:
             log("bench: all-pairs / ring extras")
         extras = {}
-        for name, mode_x, dir_x, nbytes, iters in (("allpairs_1g", "allpairs", "bi", 1 << 30, 4),
-                                                   ("ring_256m", "ring", "uni", 256 << 20, 8)):
+        # Keyed by the BASELINE config names; the sizes can be lowered for
+        # CPU rehearsals (all-pairs holds N - 1 receive slots per rank).
+        for name, mode_x, dir_x, nbytes, iters in (("allpairs_1g", "allpairs", "bi", nat.parse_size(args.allpairs_size), 4),
+                                                   ("ring_256m", "ring", "uni", nat.parse_size(args.ring_size), 8)):
             v = section(name, lambda: concurrent_config(mode_x, dir_x, nbytes, iters), 5.0)
             if v is not None:
                 extras[name] = v

@@ -172,3 +172,32 @@ def test_bench_deadline_with_a_hung_section(native):
     assert r["value"] > 0 and r["deadline_hit"] is True
     assert "latency" in (r["section_errors"] or {}), r["section_errors"]
     assert wall < 40 + 30, wall
+
+
+def test_bench_eight_ranks_with_the_driver_step_counts(native):
+    """The driver's N = 8 invocation shape (20 timed steps after 5 warmup,
+    every untimed section on) over the shared-memory transport: the tuning
+    laps cover all 7 tournament rounds, every off-diagonal cell is sampled,
+    every timed delivery is verified, and no section is skipped or fails.
+    The extras' sizes are lowered to fit the CPU container (all-pairs holds
+    7 receive slots per rank)."""
+    out = torchrun(8, ["bench.py", "--gpus", "8", "--steps", "20", "--warmup", "5", "--transport", "shm",
+                       "--size", "256K", "--msgs", "4", "--sweep-max", "4M", "--ref-iters", "8",
+                       "--latency-iters", "50", "--allpairs-size", "16M", "--ring-size", "4M"], timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 8 and r["matrix_cells"] == "56/56"
+    assert all(r["matrix_samples"][s][d] >= 2 for s in range(8) for d in range(8) if s != d), r["matrix_samples"]
+    assert "7 round(s)" in r["posting"]["selection"]
+    assert r["verify_mismatches"] == 0 and r["verify_coverage"] == 1.0
+    assert r["untimed_skipped"] is None and r.get("section_errors") is None
+    ex = r["extras"]
+    assert ex["allpairs_1g"]["bytes"] == 16 << 20 and ex["allpairs_1g"]["mismatches"] == 0
+    assert ex["ring_256m"]["mismatches"] == 0 and ex["ring_hop"]["hop_us_p50"] > 0
+    assert len(ex["pair_sweep_0_1"]) == 6
+    assert r["reference_semantics"]["cell_gbs_mean"] > 0
+    assert r["ipc_transport"]["verify_mismatches"] == 0
+    lat = r["latency_p50_us_matrix"]
+    assert all(lat[a][b] > 0 for a in range(8) for b in range(8) if a != b)
