@@ -346,6 +346,8 @@ def parse_args(argv=None):
     ap.add_argument("--ipc-extra", type=int, default=1,
                     help="1: also run the timed steps through the IPC engines (pull, push, sdma; relay from N = 3) "
                          "after the timed region, untimed by the contract, each in a child process per rank")
+    ap.add_argument("--ipc-engines", default="pull,push,sdma,relay",
+                    help="engines of the IPC comparison, in this order (relay only from N = 3)")
     ap.add_argument("--extras", type=int, default=1,
                     help="1: also measure all-pairs 1 GiB, ring 256 MiB and the ring token hop after the timed "
                          "region (N > 1)")
@@ -844,6 +846,8 @@ def main(argv=None) -> int:
         runs = [(extra_transport, None)]
         if extra_transport == "ipc":
             runs += [("ipc:push", "push"), ("ipc:sdma", "sdma")] + ([("ipc:relay", "relay")] if n > 2 else [])
+            wanted = [e.strip() for e in args.ipc_engines.split(",") if e.strip()]
+            runs = [(t, k) for (t, k) in runs if (k or "pull") in wanted]
         engines = {"ipc": "gfx950 multi-copy kernel, one-sided pull over hipIpc mappings",
                    "ipc:push": "ready/done flags + gfx950 multi-copy kernel writing into the peer's slot",
                    "ipc:sdma": "one-sided pull by the SDMA copy engines (hipMemcpyAsync per receive)",
@@ -870,9 +874,9 @@ def main(argv=None) -> int:
             if isinstance(r.get("value_gbs"), (int, float)) and value > 0:
                 r["ratio_to_headline"] = round(r["value_gbs"] / value, 3)
             if key is None:
-                ipc = r
-            elif ipc is not None:
-                ipc[key] = r
+                ipc = dict(r, **(ipc or {}))
+            else:
+                ipc = dict(ipc or {}, **{key: r})
             reporter.update(ipc_transport=ipc)
 
     reporter.update(untimed_skipped=skipped or None, section_errors=errors or None)
