@@ -260,6 +260,12 @@ def steps_through(nat, isess, args, mode, size, batch, transport, deadline=None)
             dl = json.loads(isess.device_latency(nat.parse_size(args.latency_size), args.latency_iters,
                                                  min(100, args.latency_iters)))
             out["device_pingpong_p50_us"] = round(statistics.median(p["one_way_us"]["p50"] for p in dl["pairs"]), 3)
+            # BASELINE config 3's latency matrix at the fabric floor: one-way
+            # p50 per pair (symmetric; self on the diagonal at N = 1).
+            dm = [[0.0] * n for _ in range(n)]
+            for p in dl["pairs"]:
+                dm[p["a"]][p["b"]] = dm[p["b"]][p["a"]] = round(p["one_way_us"]["p50"], 3)
+            out["device_latency_p50_us_matrix"] = dm
             if n > 1:
                 rl = json.loads(isess.ring_latency(nat.parse_size(args.latency_size), 100, 10, True))
                 out["device_ring_hop_p50_us"] = round(rl["hop_us"]["p50"], 3)

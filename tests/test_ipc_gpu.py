@@ -236,6 +236,8 @@ def test_bench_emulated_node(nranks):
     assert ipc["verify_mismatches"] == 0 and ipc["push"]["verify_mismatches"] == 0, ipc
     assert ipc["sdma"]["verify_mismatches"] == 0 and ipc["sdma"]["value_gbs"] > 0, ipc
     assert ipc["device_pingpong_p50_us"] > 0
+    dm = ipc["device_latency_p50_us_matrix"]
+    assert all(dm[a][b] > 0 and dm[a][b] == dm[b][a] for a in range(nranks) for b in range(nranks) if a != b), dm
     relay = ipc["relay"]
     assert relay["verify_mismatches"] == 0 and relay["value_gbs"] > 0, relay
     assert [p["mismatches"] for p in relay["pair_0_1"]] == [0, 0], relay
