@@ -90,9 +90,31 @@ class RcclTransport final : public Transport {
       HIPCHECK(hipEventCreateWithFlags(&join_, hipEventDisableTiming));
     }
     if (const char* mi = std::getenv("P2P_RCCL_MAIN_IDLE")) main_idle_ = ncomms > 1 && std::atoi(mi) != 0;
+    // P2P_RCCL_CU_MASK=contig|stride (experiment): every communicator's
+    // stream gets its own 1/K of the CUs (contiguous mask bits, or every K-th
+    // bit), so the K concurrent send/recv kernels do not compete for CUs; the
+    // main stream (fill / verify) stays unmasked, so communicator 0 moves to
+    // a stream of its own as with P2P_RCCL_MAIN_IDLE.
+    int cu_mask_mode = 0;
+    if (const char* cm = std::getenv("P2P_RCCL_CU_MASK"))
+      cu_mask_mode = std::strcmp(cm, "contig") == 0 ? 1 : std::strcmp(cm, "stride") == 0 ? 2 : 0;
+    if (ncomms == 1) cu_mask_mode = 0;
+    if (cu_mask_mode) main_idle_ = true;
+    int ncus = 0;
+    HIPCHECK(hipDeviceGetAttribute(&ncus, hipDeviceAttributeMultiprocessorCount, device_));
     for (int j = 0; j < ncomms; ++j) {
       hipStream_t s = stream_;
-      if (j > 0 || main_idle_) HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      if (cu_mask_mode) {
+        std::vector<uint32_t> mask(static_cast<size_t>((ncus + 31) / 32), 0u);
+        for (int c = 0; c < ncus; ++c) {
+          const int owner = cu_mask_mode == 1 ? c * ncomms / ncus : c % ncomms;
+          if (owner == j) mask[static_cast<size_t>(c / 32)] |= 1u << (c % 32);
+        }
+        HIPCHECK(hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(mask.size()), mask.data()));
+        cu_masked_ = true;
+      } else if (j > 0 || main_idle_) {
+        HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      }
       cstreams_.push_back(s);
       hipEvent_t ev = nullptr;
       if (ncomms > 1) HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -144,6 +166,7 @@ class RcclTransport final : public Transport {
     desc_ = strfmt("hip:%d %s (%s, %d CUs, %.0f GiB, pci %s) rccl %d", device_, prop.name, prop.gcnArchName,
                    prop.multiProcessorCount, static_cast<double>(prop.totalGlobalMem) / (1ull << 30), pci, ver);
     if (ncomms > 1) desc_ += strfmt(" x%d comms", ncomms);
+    if (cu_masked_) desc_ += cu_mask_mode == 1 ? " cu-mask:contig" : " cu-mask:stride";
   }
 
   ~RcclTransport() override {
@@ -597,6 +620,7 @@ class RcclTransport final : public Transport {
   std::vector<hipStream_t> cstreams_;  // stream of each communicator (cstreams_[0] == stream_ unless main_idle_)
   std::vector<hipEvent_t> cjoin_;      // per communicator with a side stream: joins it into stream_
   bool main_idle_ = false;             // P2P_RCCL_MAIN_IDLE=1: communicator 0 on a side stream too
+  bool cu_masked_ = false;             // P2P_RCCL_CU_MASK: communicator streams own disjoint CU sets
   hipEvent_t fork_ = nullptr;          // recorded on stream_ when a stale side stream is first used
   bool forked_ = false;                // fork_ covers the main stream's latest buffer work
   std::vector<bool> stale_;            // side stream j has not waited for the latest buffer work
