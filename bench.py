@@ -364,6 +364,10 @@ def parse_args(argv=None):
     ap.add_argument("--sweep-max", default="4G", help="largest message of the pair sweep")
     ap.add_argument("--ref-iters", type=int, default=128,
                     help="iterations per cell of the reference-methodology comparison (0 = skip)")
+    ap.add_argument("--fallback", type=int, default=1,
+                    help="1: should the RCCL headline fail (setup, connection, stalled transfer), time the same steps "
+                         "through the IPC data plane and say so in headline_fallback; 0: report the error only")
+    ap.add_argument("--fallback-to", default="ipc", help=argparse.SUPPRESS)  # tests: host -> shm
     ap.add_argument("--isolate", type=int, default=1,
                     help="1: run each untimed transport comparison in a child process per rank (a fault there "
                          "cannot take the headline down); 0: in this process (halves the processes per GPU)")
@@ -429,147 +433,192 @@ def main(argv=None) -> int:
         return bool(t.item())
 
     size = nat.parse_size(args.size)
-    headline = args.transport + (":%d" % args.comms if args.transport == "rccl" and args.comms > 1 else "")
-    sess = create_session(headline, device=device, timeout_s=args.timeout)
-    if env.rank == 0:
-        log("bench: %d rank(s), %s, %s" % (n, sess.transport, sess.device_desc))
     mode = "self" if n == 1 else args.mode
-    provenance = json.loads(sess.provenance(device if use_gpu else -1))
-    provenance.pop("type", None)
 
-    # Receive-slot budget: every message of every timed step gets its own
-    # slot, up to this much memory per rank (ranks sharing a GPU split it).
-    budget = 0 if args.recv_budget.strip() in ("", "0") else nat.parse_size(args.recv_budget)
-    if budget == 0 and use_gpu:
-        free_b, _ = torch.cuda.mem_get_info(device)
-        same_gpu = sum(1 for d in provenance.get("rank_devices", []) if d["device"] == device) or 1
-        budget = int(0.4 * free_b / same_gpu)
-    elif budget == 0:
-        budget = 256 << 20
+    def measure(transport):
+        """Posting selection, then the W warmup and K timed steps of the headline
+        through `transport`; returns what the report needs."""
+        headline = transport + (":%d" % args.comms if transport == "rccl" and args.comms > 1 else "")
+        sess = create_session(headline, device=device, timeout_s=args.timeout)
+        if env.rank == 0:
+            log("bench: %d rank(s), %s, %s" % (n, sess.transport, sess.device_desc))
+        # Test hook: P2P_BENCH_FAIL_HEADLINE=<transport> fails the headline
+        # through that transport on every rank, as a communicator that cannot
+        # be set up does.
+        if os.environ.get("P2P_BENCH_FAIL_HEADLINE") == transport:
+            raise RuntimeError("injected headline failure")
+        provenance = json.loads(sess.provenance(device if use_gpu else -1))
+        provenance.pop("type", None)
 
-    # ---- posting selection: one untimed lap of the schedule per candidate --
-    # (one group per step vs one per message; RCCL: one communicator vs
-    # several whose send/recv kernels run side by side, posting_candidates),
-    # timed by the slowest rank,
-    # before the W warmup steps of the chosen one.
-    state["section"] = "tuning"
-    choices = posting_candidates(args.transport, args.comms, args.batch, n)
-    c0 = first_comms(args.transport, args.comms)
-    sessions = {c0: sess}
+        # Receive-slot budget: every message of every timed step gets its own
+        # slot, up to this much memory per rank (ranks sharing a GPU split it).
+        budget = 0 if args.recv_budget.strip() in ("", "0") else nat.parse_size(args.recv_budget)
+        if budget == 0 and use_gpu:
+            free_b, _ = torch.cuda.mem_get_info(device)
+            same_gpu = sum(1 for d in provenance.get("rank_devices", []) if d["device"] == device) or 1
+            budget = int(0.4 * free_b / same_gpu)
+        elif budget == 0:
+            budget = 256 << 20
 
-    def session_for(c):
-        if c not in sessions:
-            # A candidate that stalls is aborted and dropped after --timeout.
-            sessions[c] = create_session("rccl:%d" % c if c > 1 else "rccl", device=device, timeout_s=args.timeout)
-        return sessions[c]
+        # ---- posting selection: one untimed lap of the schedule per candidate --
+        # (one group per step vs one per message; RCCL: one communicator vs
+        # several whose send/recv kernels run side by side, posting_candidates),
+        # timed by the slowest rank,
+        # before the W warmup steps of the chosen one.
+        state["section"] = "tuning"
+        choices = posting_candidates(transport, args.comms, args.batch, n)
+        c0 = first_comms(transport, args.comms)
+        sessions = {c0: sess}
 
-    tuning, failed = {}, {}
-    phases = len(nat.schedule(mode, "bi", n))
-    tune_k = tuning_steps(phases) * args.tune_laps
-    if args.tune_laps > 0 and len(choices) > 1:
-        for i, (c, b) in enumerate(choices):
-            key = "comms%d_%s" % (c, "batch" if b else "per_message")
-            # The headline session's first candidate must work; anything else
-            # (another communicator count, another posting) may be dropped.
-            droppable = i > 0 or c != c0
-            d, err = None, None
-            try:
-                d = nat.StepDriver(session_for(c), mode, "bi", size, args.msgs, False, bool(b), bool(args.graph))
-                d.connect()
-                # Test hook: P2P_BENCH_FAIL_CANDIDATE="<comms>,<batch>" fails
-                # that candidate on the last rank only.
-                if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d" % (c, b) and env.rank == n - 1:
-                    raise RuntimeError("injected candidate failure")
-            except Exception as e:  # noqa: BLE001 -- reported, and the candidate is skipped everywhere
-                err = str(e)[:200]
-            if agree(err is None):
-                barrier()
-                w0 = time.perf_counter()
+        def session_for(c):
+            if c not in sessions:
+                # A candidate that stalls is aborted and dropped after --timeout.
+                sessions[c] = create_session("rccl:%d" % c if c > 1 else "rccl", device=device, timeout_s=args.timeout)
+            return sessions[c]
+
+        tuning, failed = {}, {}
+        phases = len(nat.schedule(mode, "bi", n))
+        tune_k = tuning_steps(phases) * args.tune_laps
+        if args.tune_laps > 0 and len(choices) > 1:
+            for i, (c, b) in enumerate(choices):
+                key = "comms%d_%s" % (c, "batch" if b else "per_message")
+                # The headline session's first candidate must work; anything else
+                # (another communicator count, another posting) may be dropped.
+                droppable = i > 0 or c != c0
+                d, err = None, None
                 try:
-                    d.run_steps(0, tune_k)
-                    d.sync()
-                    if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d,tuning" % (c, b) and env.rank == n - 1:
-                        raise RuntimeError("injected tuning failure")
-                except Exception as e:  # noqa: BLE001 -- same agreement as above
+                    d = nat.StepDriver(session_for(c), mode, "bi", size, args.msgs, False, bool(b), bool(args.graph))
+                    d.connect()
+                    # Test hook: P2P_BENCH_FAIL_CANDIDATE="<comms>,<batch>" fails
+                    # that candidate on the last rank only.
+                    if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d" % (c, b) and env.rank == n - 1:
+                        raise RuntimeError("injected candidate failure")
+                except Exception as e:  # noqa: BLE001 -- reported, and the candidate is skipped everywhere
                     err = str(e)[:200]
-                w = time.perf_counter() - w0
                 if agree(err is None):
-                    tuning[(c, b)] = sess.allreduce_max(w) / tune_k
-                    del d
-                    # Only the best communicator count so far, the headline
-                    # session and the single communicator (kept for the
-                    # reference-method comparison) stay open.
-                    best_c = min(tuning, key=tuning.get)[0]
-                    for cc in [cc for cc in sessions if cc not in (c0, 1, best_c)]:
-                        if not any(cc == c2 for (c2, _) in choices[i + 1:]):
-                            del sessions[cc]
-                    continue
-            if not droppable:
-                raise RuntimeError(err or "the first posting candidate failed on another rank")
-            failed[key] = err or "failed on another rank"
-            log("bench: posting candidate %s dropped: %s" % ((c, b), failed[key]))
-            del d
-            if c != c0 and not any(cc == c for (cc, _) in tuning):
-                sessions.pop(c, None)
-        comms, batch = min(tuning, key=tuning.get)
-        reason = "fastest of %d candidate(s) over %d untimed step(s) each (%s lap(s) of %d round(s)), slowest rank's " \
-                 "clock" % (len(tuning), tune_k, args.tune_laps, phases)
-    else:
-        comms, batch = choices[0]
-        reason = "single candidate" if len(choices) == 1 else "no tuning laps (--tune-laps 0): first candidate"
-    sess = session_for(comms)
-    # A single-communicator session stays for the reference-method comparison
-    # (the reference uses one communicator); other candidates are closed.
-    ref_sess = sessions.get(1)
-    for c in list(sessions):
-        if c not in (comms, 1):
-            del sessions[c]
+                    barrier()
+                    w0 = time.perf_counter()
+                    try:
+                        d.run_steps(0, tune_k)
+                        d.sync()
+                        if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d,tuning" % (c, b) and env.rank == n - 1:
+                            raise RuntimeError("injected tuning failure")
+                    except Exception as e:  # noqa: BLE001 -- same agreement as above
+                        err = str(e)[:200]
+                    w = time.perf_counter() - w0
+                    if agree(err is None):
+                        tuning[(c, b)] = sess.allreduce_max(w) / tune_k
+                        del d
+                        # Only the best communicator count so far, the headline
+                        # session and the single communicator (kept for the
+                        # reference-method comparison) stay open.
+                        best_c = min(tuning, key=tuning.get)[0]
+                        for cc in [cc for cc in sessions if cc not in (c0, 1, best_c)]:
+                            if not any(cc == c2 for (c2, _) in choices[i + 1:]):
+                                del sessions[cc]
+                        continue
+                if not droppable:
+                    raise RuntimeError(err or "the first posting candidate failed on another rank")
+                failed[key] = err or "failed on another rank"
+                log("bench: posting candidate %s dropped: %s" % ((c, b), failed[key]))
+                del d
+                if c != c0 and not any(cc == c for (cc, _) in tuning):
+                    sessions.pop(c, None)
+            comms, batch = min(tuning, key=tuning.get)
+            reason = "fastest of %d candidate(s) over %d untimed step(s) each (%s lap(s) of %d round(s)), slowest rank's " \
+                     "clock" % (len(tuning), tune_k, args.tune_laps, phases)
+        else:
+            comms, batch = choices[0]
+            reason = "single candidate" if len(choices) == 1 else "no tuning laps (--tune-laps 0): first candidate"
+        sess = session_for(comms)
+        # A single-communicator session stays for the reference-method comparison
+        # (the reference uses one communicator); other candidates are closed.
+        ref_sess = sessions.get(1)
+        for c in list(sessions):
+            if c not in (comms, 1):
+                del sessions[c]
 
-    # ---- the headline driver: W warmup steps, poison, K timed steps -------
-    state["section"] = "headline"
-    phases = len(nat.schedule(mode, "bi", n))
-    drv = nat.StepDriver(sess, mode, "bi", size, args.msgs, not args.no_verify, bool(batch), bool(args.graph),
-                         depth=pick_depth(args.steps, phases), recv_budget=budget, salt=1)
-    drv.connect()
-    drv.run_steps(0, args.warmup)
-    drv.sync()
-    drv.poison()  # untimed: every receive slot zeroed; a slot passes verification only if a timed step wrote it
-    gpu_sync()
-    drv.reset()
+        # ---- the headline driver: W warmup steps, poison, K timed steps -------
+        state["section"] = "headline"
+        phases = len(nat.schedule(mode, "bi", n))
+        drv = nat.StepDriver(sess, mode, "bi", size, args.msgs, not args.no_verify, bool(batch), bool(args.graph),
+                             depth=pick_depth(args.steps, phases), recv_budget=budget, salt=1)
+        drv.connect()
+        drv.run_steps(0, args.warmup)
+        drv.sync()
+        drv.poison()  # untimed: every receive slot zeroed; a slot passes verification only if a timed step wrote it
+        gpu_sync()
+        drv.reset()
 
-    barrier()
-    gpu_sync()
-    barrier()
-    t0 = time.perf_counter()
-    drv.run_steps(args.warmup, args.steps)
-    drv.sync()
-    gpu_sync()
-    barrier()
-    t1 = time.perf_counter()
-    elapsed = sess.allreduce_max(t1 - t0)
+        barrier()
+        gpu_sync()
+        barrier()
+        t0 = time.perf_counter()
+        drv.run_steps(args.warmup, args.steps)
+        drv.sync()
+        gpu_sync()
+        barrier()
+        t1 = time.perf_counter()
+        elapsed = sess.allreduce_max(t1 - t0)
 
-    steps = list(range(args.warmup, args.warmup + args.steps))
-    job_bytes = sum(drv.job_bytes_per_step(k) for k in steps)
-    flows_total = sum(drv.flows_per_step(k) for k in steps)
-    value, aggregate = headline_stats(job_bytes, flows_total, args.steps, elapsed)
+        steps = list(range(args.warmup, args.warmup + args.steps))
+        job_bytes = sum(drv.job_bytes_per_step(k) for k in steps)
+        flows_total = sum(drv.flows_per_step(k) for k in steps)
+        value, aggregate = headline_stats(job_bytes, flows_total, args.steps, elapsed)
 
-    # Per-step GPU durations of every rank -> per-cell bandwidth.
-    my_ms = drv.step_ms()
-    all_ms = [None] * n
-    if n > 1:
-        dist.all_gather_object(all_ms, my_ms)
-    else:
-        all_ms = [my_ms]
-    matrix, samples, cells = cell_matrix(n, steps, drv.phase_flows, all_ms, size * args.msgs)
-    offdiag = [matrix[s][d] for (s, d) in cells if s != d or n == 1]
-    expected = n * (n - 1) if n > 1 else 1
+        # Per-step GPU durations of every rank -> per-cell bandwidth.
+        my_ms = drv.step_ms()
+        all_ms = [None] * n
+        if n > 1:
+            dist.all_gather_object(all_ms, my_ms)
+        else:
+            all_ms = [my_ms]
+        matrix, samples, cells = cell_matrix(n, steps, drv.phase_flows, all_ms, size * args.msgs)
+        offdiag = [matrix[s][d] for (s, d) in cells if s != d or n == 1]
+        expected = n * (n - 1) if n > 1 else 1
 
-    vr = drv.verify_steps(args.warmup, args.steps) if not args.no_verify else None
-    mismatches = vr["mismatches"] if vr else -1
-    depth, recv_bytes = drv.depth, drv.recv_bytes
-    # Everything below is untimed; release the timed driver's buffers first so
-    # the comparisons run on the same memory footprint as the timed steps did.
-    del drv
+        vr = drv.verify_steps(args.warmup, args.steps) if not args.no_verify else None
+        mismatches = vr["mismatches"] if vr else -1
+        depth, recv_bytes = drv.depth, drv.recv_bytes
+        # Everything below is untimed; release the timed driver's buffers first so
+        # the comparisons run on the same memory footprint as the timed steps did.
+        del drv
+        return {"sess": sess, "ref_sess": ref_sess, "sessions": sessions, "provenance": provenance, "comms": comms, "batch": batch, "failed": failed, "reason": reason, "tuning": tuning, "elapsed": elapsed, "steps": steps, "flows_total": flows_total, "value": value, "aggregate": aggregate, "my_ms": my_ms, "matrix": matrix, "samples": samples, "cells": cells, "offdiag": offdiag, "expected": expected, "vr": vr, "mismatches": mismatches, "depth": depth, "recv_bytes": recv_bytes}
+
+    # The headline.  Should RCCL itself fail on this node (communicator setup,
+    # a peer connection, a stalled transfer: every wait is bounded by --timeout
+    # and aborts the communicators), the same steps run through the
+    # hand-written IPC data plane instead and the line says so
+    # (headline_fallback); with --fallback 0, or if that fails too, the line
+    # carries the error and value null.
+    fallback = None
+    transport_used = args.transport
+    try:
+        h = measure(args.transport)
+    except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+        err = str(e)[:300]
+        log("bench: headline through %s failed: %s" % (args.transport, err))
+        # The failure is collective (a communicator that cannot be set up or a
+        # stalled transfer times out on every rank): all ranks meet here first.
+        agree(False)
+        to = args.fallback_to
+        if not (args.fallback and args.transport in ("rccl", "host") and to != args.transport
+                and (use_gpu or to in ("host", "shm"))):
+            reporter.emit(error="headline failed: " + err, transport=args.transport)
+            return 5
+        fallback = {"from": args.transport, "to": to, "error": err}
+        transport_used = to
+        state["section"] = "fallback"
+        try:
+            h = measure(to)
+        except Exception as e2:  # noqa: BLE001
+            log("bench: fallback headline failed: %s" % e2)
+            reporter.emit(error="headline failed: %s; fallback through ipc failed: %s" % (err, str(e2)[:300]),
+                          transport=args.transport, headline_fallback=fallback)
+            return 5
+    (sess, ref_sess, sessions, provenance, comms, batch, failed, reason, tuning, elapsed, steps, flows_total, value,
+     aggregate, my_ms, matrix, samples, cells, offdiag, expected, vr, mismatches, depth, recv_bytes) = (
+        h[k] for k in ("sess", "ref_sess", "sessions", "provenance", "comms", "batch", "failed", "reason", "tuning", "elapsed", "steps", "flows_total", "value", "aggregate", "my_ms", "matrix", "samples", "cells", "offdiag", "expected", "vr", "mismatches", "depth", "recv_bytes"))
 
     step_ms_med = statistics.median(my_ms) if my_ms else 0.0
     headline_transport = sess.transport
@@ -629,6 +678,7 @@ def main(argv=None) -> int:
         "extras": None,
         "ipc_transport": None,
         "untimed_skipped": None,
+        "headline_fallback": fallback,
         "note": ("n_gpus=1 has no inter-GPU link: value is RCCL's on-GPU self send/recv copy (HBM-bound), the "
                  "diagonal the reference prints as 0.00. From n_gpus=2 every step is one tournament round of disjoint "
                  "pairs, each pair on its own xGMI link; value is the mean per-link, per-direction cell rate and "
@@ -800,7 +850,7 @@ def main(argv=None) -> int:
 
     # (with --transport host the same code path runs on the CPU transport, for tests)
     extra_transport = {"rccl": "ipc", "ipc": "ipc", "ipc:push": "ipc", "ipc:relay": "ipc", "host": "host",
-                       "shm": "host"}.get(args.transport)
+                       "shm": "host"}.get(transport_used)
 
     def isolated(transport):
         """steps_through() for `transport` in a child process per rank.  The

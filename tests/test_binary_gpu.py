@@ -123,3 +123,16 @@ def test_bench_drops_a_failing_communicator_candidate():
         r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
         assert r["posting"]["rccl_comms"] == 1 and "injected" in r["posting"]["dropped"]["comms4_batch"]
         assert r["verify_mismatches"] == 0 and r["value"] > 10
+
+
+def test_bench_headline_falls_back_to_ipc():
+    """Should RCCL fail on the node (injected on every rank), the timed steps
+    run through the IPC data plane and the line names the fallback."""
+    out = subprocess.run([sys.executable, "bench.py", "--steps", "4", "--warmup", "2", "--latency-iters", "20",
+                          "--ref-iters", "8", "--ipc-extra", "0"],
+                         capture_output=True, text=True, timeout=600, cwd=ROOT,
+                         env=dict(os.environ, P2P_BENCH_FAIL_HEADLINE="rccl"))
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert r["transport"] == "ipc" and r["headline_fallback"]["from"] == "rccl", r.get("headline_fallback")
+    assert r["verify_mismatches"] == 0 and r["verify_coverage"] == 1.0 and r["value"] > 10

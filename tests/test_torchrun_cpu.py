@@ -201,3 +201,24 @@ def test_bench_eight_ranks_with_the_driver_step_counts(native):
     assert r["ipc_transport"]["verify_mismatches"] == 0
     lat = r["latency_p50_us_matrix"]
     assert all(lat[a][b] > 0 for a in range(8) for b in range(8) if a != b)
+
+
+def test_bench_headline_fallback(native):
+    """A headline transport that cannot be set up (P2P_BENCH_FAIL_HEADLINE,
+    as an RCCL communicator that fails on every rank) is replaced by the
+    fallback data plane (host -> shm here; rccl -> ipc on GPUs), and the line
+    says so; with --fallback 0 the line carries the error and value null."""
+    args = ["bench.py", "--gpus", "2", "--steps", "3", "--warmup", "2", "--transport", "host", "--size", "256K",
+            "--msgs", "2", "--latency-iters", "20", "--sweep", "0", "--extras", "0", "--ref-iters", "0",
+            "--ipc-extra", "0", "--fallback-to", "shm"]
+    out = torchrun(2, args, env={"P2P_BENCH_FAIL_HEADLINE": "host"})
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert r["transport"] == "shm" and r["value"] > 0 and r["verify_mismatches"] == 0
+    assert r["headline_fallback"] == {"from": "host", "to": "shm", "error": "injected headline failure"}
+    out = torchrun(2, args + ["--fallback", "0"], env={"P2P_BENCH_FAIL_HEADLINE": "host"})
+    assert out.returncode != 0, out.stderr[-3000:]  # torchrun reports the ranks' exit status 5 as 1
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    r = json.loads(lines[0])
+    assert r["value"] is None and "injected headline failure" in r["error"]
