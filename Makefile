@@ -71,7 +71,7 @@ gpu: $(BUILD)/p2p_matrix
 	ln -sf $(BUILD)/p2p_matrix p2p_matrix
 host: $(BUILD)/p2p_matrix_host $(BUILD)/p2p_host_tests
 ext: $(EXT)
-tools: $(BUILD)/fill_probe $(BUILD)/ipc_export_probe
+tools: $(BUILD)/fill_probe $(BUILD)/copy_probe $(BUILD)/ipc_export_probe
 
 $(BUILD)/gpu $(BUILD)/host $(BUILD)/asan:
 	mkdir -p $@
@@ -131,6 +131,10 @@ $(EXT): $(GPU_OBJS) $(BUILD)/gpu/pymodule.o $(RT_STAMP)
 
 # Grid-shape probe (scripts/fill_probe.hip): standalone, no framework code.
 $(BUILD)/fill_probe: scripts/fill_probe.hip | $(BUILD)/gpu
+	$(HIPCC) --offload-arch=$(ARCH) -O3 $< -o $@
+
+# Copy cache-policy / shape probe (scripts/copy_probe.hip): standalone.
+$(BUILD)/copy_probe: scripts/copy_probe.hip | $(BUILD)/gpu
 	$(HIPCC) --offload-arch=$(ARCH) -O3 $< -o $@
 
 $(BUILD)/ipc_export_probe: scripts/ipc_export_probe.hip | $(BUILD)/gpu
