@@ -293,10 +293,19 @@ PhaseResult run_phase(Transport& t, Bootstrap& boot, const Phase& phase, size_t 
       t.sync();
       my_seconds = t.elapsed_ms(m0, marks.back()) / 1e3;
       if (cfg.samples) {
-        int prev = m0;
-        for (int m : marks) {
-          iter_samples.push_back(t.elapsed_ms(prev, m) * 1e3);
-          prev = m;
+        // With K messages in flight on K streams (t.concurrency()), one mark
+        // to the next is a completion frontier, often 0 when a later message
+        // finished first: a sample then spans K marks and is divided by K
+        // (per-message time over a round of one message per stream).
+        const size_t k = static_cast<size_t>(std::max(1, t.concurrency()));
+        if (marks.size() < k) {
+          iter_samples.push_back(t.elapsed_ms(m0, marks.back()) * 1e3 / static_cast<double>(marks.size()));
+        } else {
+          int prev = m0;
+          for (size_t i = k - 1; i < marks.size(); i += k) {
+            iter_samples.push_back(t.elapsed_ms(prev, marks[i]) * 1e3 / static_cast<double>(k));
+            prev = marks[i];
+          }
         }
       }
     }

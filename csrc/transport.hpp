@@ -88,6 +88,11 @@ class Transport {
   // Milliseconds between two marks; only valid after sync().
   virtual double elapsed_ms(int from, int to) = 0;
   virtual void clear_marks() = 0;
+  // Consecutive messages that may run side by side on independent streams
+  // (RCCL with K communicators: K).  Marks then record completion frontiers
+  // of overlapping messages, so per-message samples are taken over rounds of
+  // this many marks (run_phase).
+  virtual int concurrency() const { return 1; }
   // Wait for all posted work (bounded by the transport's watchdog timeout).
   virtual void sync() = 0;
 

@@ -129,6 +129,15 @@ class RcclTransport final : public Transport {
     HIPCHECK(hipMalloc(&acc_, dev::verify_accum_bytes()));
     HIPCHECK(hipHostMalloc(&acc_host_, sizeof(dev::VerifyAccum), hipHostMallocDefault));
 
+    // P2P_RCCL_DISTINCT_HOSTS=1 (tests on one GPU): every rank tells RCCL it
+    // is on a host of its own (NCCL_HOSTID, read when RCCL first hashes the
+    // host), so several ranks may share one GPU -- RCCL refuses duplicate GPUs
+    // on one host -- and talk over its network transport (sockets, e.g.
+    // NCCL_SOCKET_IFNAME=lo).  Not xGMI: this exercises the multi-rank RCCL
+    // paths (communicators, schedules, ordering across K communicators) where
+    // only one GPU is available.
+    if (const char* dh = std::getenv("P2P_RCCL_DISTINCT_HOSTS"); dh && std::atoi(dh) != 0)
+      setenv("NCCL_HOSTID", strfmt("p2p-emulated-host-%d", rank_).c_str(), 1);
     // RCCL prints a version banner to stdout on first use; send it to stderr
     // so stdout keeps the reference's output (P2P_RCCL_BANNER=1 keeps it).
     const char* banner = std::getenv("P2P_RCCL_BANNER");
@@ -462,6 +471,7 @@ class RcclTransport final : public Transport {
     }
   }
 
+  int concurrency() const override { return static_cast<int>(comms_.size()); }
   void set_timeout(double seconds) override { timeout_ = seconds; }
 
   std::string async_error() override {

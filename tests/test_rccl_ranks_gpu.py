@@ -1,0 +1,74 @@
+"""RCCL itself with several ranks on the one GPU of a test box.
+
+RCCL refuses two ranks on one GPU of one host ("Duplicate GPU detected"), so
+P2P_RCCL_DISTINCT_HOSTS=1 makes every rank claim a host of its own
+(NCCL_HOSTID) and RCCL connects the ranks through its socket network
+transport on loopback.  The bytes do not cross xGMI, but every multi-rank
+RCCL code path does run: communicator setup across ranks, K communicators
+with the (count + src + dst) routing and the sorted launch order, the
+tournament / ring / all-pairs schedules, the ring token chain, the latency
+matrix, and bench.py's N-rank flow with its communicator candidates.  This is
+what the driver's multi-GPU run executes, minus the link.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import MPIRUN, ROOT, ensure_built, free_port
+
+pytestmark = [pytest.mark.gpu]
+
+ENV = dict(os.environ, P2P_RCCL_DISTINCT_HOSTS="1", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+
+
+@pytest.fixture(scope="module")
+def exe():
+    ensure_built("gpu")
+    return os.path.join(ROOT, "build", "p2p_matrix")
+
+
+@pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
+@pytest.mark.parametrize("comms", ["1", "4"])
+def test_cli_four_rccl_ranks_every_mode(exe, tmp_path, comms):
+    js = tmp_path / "r.json"
+    out = subprocess.run([MPIRUN, "-n", "4", exe, "--device", "0", "--mode", "pair,tournament,ring,allpairs",
+                          "--size", "4M", "-n", "4", "--comms", comms, "--verify", "--latency", "--latency-iters", "30",
+                          "--json", str(js), "--timeout", "60"],
+                         capture_output=True, text=True, timeout=300, env=ENV)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "verification: OK" in out.stdout
+    assert out.stdout.startswith("Evaluating the Uni-Directional NCCL P2P Bandwidth (Gbps)")
+    recs = [json.loads(l) for l in js.read_text().splitlines()]
+    prov = [r for r in recs if r["type"] == "provenance"][0]
+    assert prov["env"]["NCCL_HOSTID"].startswith("p2p-emulated-host-")
+    assert "ring token latency: 4 rank(s)" in out.stdout
+
+
+def test_bench_four_rccl_ranks(tmp_path):
+    """bench.py's whole N = 4 flow through RCCL: the five posting candidates
+    (1 communicator per message / batched, 2, 4 and 8 communicators), the
+    tournament steps with every delivery verified, and every untimed section."""
+    out_json = tmp_path / "b.json"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "4", "--device", "0", "--size", "4M",
+           "--msgs", "8", "--sweep-max", "16M", "--allpairs-size", "16M", "--ring-size", "8M", "--ref-iters", "8",
+           "--latency-iters", "30", "--ipc-extra", "0", "--timeout", "60", "--json-out", str(out_json)]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=ROOT, env=ENV)
+    progress = "\n".join(l for l in out.stderr.splitlines() if "bench:" in l or "fatal" in l or "Error" in l)
+    assert out.returncode == 0, progress[-3000:]
+    r = json.loads(out_json.read_text())
+    assert r["transport"] == "rccl" and r["headline_fallback"] is None
+    assert r["verify_mismatches"] == 0 and r["verify_coverage"] == 1.0 and r["matrix_cells"] == "12/12"
+    tuned = r["posting"]["tuning_ms_per_step"]
+    assert set(tuned) == {"comms1_per_message", "comms1_batch", "comms2_batch", "comms4_batch", "comms8_batch"}, tuned
+    assert r["untimed_skipped"] is None and r.get("section_errors") is None
+    ex = r["extras"]
+    assert ex["allpairs_1g"]["mismatches"] == 0 and ex["ring_256m"]["mismatches"] == 0
+    assert ex["ring_hop"]["hop_us_p50"] > 0
+    assert all(p["mismatches"] == 0 and p["iter_us_p50"] > 0 for p in ex["pair_sweep_0_1"]), ex["pair_sweep_0_1"]
+    lat = r["latency_p50_us_matrix"]
+    assert all(lat[a][b] > 0 for a in range(4) for b in range(4) if a != b)
+    assert r["reference_semantics"]["cell_gbs_mean"] > 0
