@@ -300,7 +300,7 @@ def child_main(args) -> int:
 
     nat = require_native()
     env = dist_env()
-    device = env.local_rank if args.device is None else args.device
+    device = default_device(env.local_rank) if args.device is None else args.device
     size = nat.parse_size(args.size)
     if env.rank == 0:
         log("bench: child %s started" % args.child)
@@ -387,6 +387,14 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
+def default_device(local_rank: int) -> int:
+    """LOCAL_RANK, modulo the visible GPUs: a launcher that gives each rank
+    one visible GPU (HIP_VISIBLE_DEVICES per process) leaves every rank on
+    its device 0.  torch.cuda.device_count() does not initialise the GPU."""
+    count = torch.cuda.device_count()
+    return local_rank % count if count > 0 else local_rank
+
+
 def hang_requested(section: str, rank: int) -> bool:
     """Test hook: P2P_BENCH_HANG="<section>@<rank>" makes that rank stop
     responding inside that untimed section."""
@@ -409,7 +417,7 @@ def main(argv=None) -> int:
         log("bench: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, env.world))
     n = env.world
     use_gpu = args.transport not in ("host", "shm")
-    device = env.local_rank if args.device is None else args.device
+    device = default_device(env.local_rank) if args.device is None else args.device
     if use_gpu:
         torch.cuda.set_device(device)
     reporter = Reporter(env.rank, real_stdout, args.json_out)

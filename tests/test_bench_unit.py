@@ -67,3 +67,12 @@ def test_bench_help_lists_transports():
     assert args.transport == "rccl" and args.comms == -1 and args.isolate == 1 and args.deadline == 300.0
     for t in ("ipc:relay", "shm"):
         assert bench.parse_args(["--transport", t]).transport == t
+
+
+def test_default_device_wraps_to_the_visible_gpus(monkeypatch):
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 8)
+    assert [bench.default_device(r) for r in (0, 3, 7)] == [0, 3, 7]
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 1)  # one visible GPU per process
+    assert [bench.default_device(r) for r in (0, 3, 7)] == [0, 0, 0]
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 0)  # CPU transports
+    assert bench.default_device(5) == 5
