@@ -83,6 +83,21 @@ def claim_stdout() -> int:
 
 
 def free_port() -> int:
+    """A free port below Linux's ephemeral range (32768-60999), so that no
+    outgoing connection takes it before the child process binds it."""
+    import random
+
+    rng = random.Random()
+    for _ in range(256):
+        port = rng.randrange(20000, 32000)
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", port))
+            return port
+        except OSError:
+            continue
+        finally:
+            s.close()
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]

@@ -45,22 +45,28 @@ def mpirun():
 
 def free_port() -> int:
     """A port P with P and P + 1 both free: torchrun's store takes P and the
-    native TCP bootstrap listens on MASTER_PORT + 1 (csrc/bootstrap.cpp)."""
+    native TCP bootstrap listens on MASTER_PORT + 1 (csrc/bootstrap.cpp).
+
+    Drawn at random below Linux's ephemeral range (32768-60999): a port the
+    kernel handed out for bind(0) is also what outgoing connections use, so
+    between this check and the launcher's bind another process's client
+    socket could take it (EADDRINUSE in the GPU tier)."""
+    import random
     import socket
 
-    for _ in range(64):
-        s = socket.socket()
-        s.bind(("127.0.0.1", 0))
-        p = s.getsockname()[1]
-        s.close()
-        if p >= 65535:
-            continue
-        t = socket.socket()
+    rng = random.Random()
+    for _ in range(256):
+        p = rng.randrange(20000, 32000)
+        socks = []
         try:
-            t.bind(("127.0.0.1", p + 1))
+            for q in (p, p + 1):
+                t = socket.socket()
+                socks.append(t)
+                t.bind(("127.0.0.1", q))
             return p
         except OSError:
             continue
         finally:
-            t.close()
-    return p
+            for t in socks:
+                t.close()
+    raise RuntimeError("no free port pair in 20000-32000")
