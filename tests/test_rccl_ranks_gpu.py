@@ -72,3 +72,29 @@ def test_bench_four_rccl_ranks(tmp_path):
     lat = r["latency_p50_us_matrix"]
     assert all(lat[a][b] > 0 for a in range(4) for b in range(4) if a != b)
     assert r["reference_semantics"]["cell_gbs_mean"] > 0
+
+
+@pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
+def test_cli_four_rccl_ranks_reference_method(exe):
+    """The reference's own methodology through RCCL across ranks: serial
+    ordered pairs, host clock, a stream sync per message, sends on s_0 and
+    receives on s_1 (p2p_matrix.cc:141-267), compat matrices on stdout."""
+    out = subprocess.run([MPIRUN, "-n", "4", exe, "--device", "0", "--reference", "--size", "4M", "-n", "8", "--verify",
+                          "--timeout", "60"], capture_output=True, text=True, timeout=300, env=ENV)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "timing=wallclock warmup=0" in out.stdout and "verification: OK" in out.stdout
+    assert "Evaluating the Bi-Directional NCCL P2P Bandwidth (Gbps)" in out.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
+@pytest.mark.parametrize("comms", ["1", "4"])
+def test_cli_four_rccl_ranks_fuzz(exe, comms):
+    """Random message groups across 4 RCCL ranks (random pairs incl. self,
+    repeated peers, 1 B .. 4 MiB), every message verified; with 4
+    communicators this checks that both ends route every message to the same
+    communicator whatever the group's shape."""
+    out = subprocess.run([MPIRUN, "-n", "4", exe, "--device", "0", "--mode", "self", "--size", "4M", "-n", "1",
+                          "--comms", comms, "--fuzz", "60", "--no-compat", "--timeout", "60"],
+                         capture_output=True, text=True, timeout=300, env=ENV)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "all verified" in out.stdout
