@@ -15,21 +15,27 @@ build/p2p_matrix under every setting that can move a single xGMI link:
   ipc rows    --ipc-engine kernel (one-sided pull by the gfx950 copy kernel),
               sdma, push, relay (stripes through idle third GPUs, N >= 3)
 
-Every row runs with --verify (a mismatch fails the row and ends the sweep: the
-GPU is never driven again after a failure), and every row's cell GB/s, p50 per
-message and the environment it ran under are written to <out>/rows.jsonl.
+Every row runs with --verify.  A row whose data does not verify (rc 2: a
+setting under which RCCL delivers wrong bytes) is recorded as corrupt, never
+wins, and the sweep goes on; any other failure (crash, hang, timeout) ends the
+sweep, so the GPU is never driven again after a fault.  Every row's cell GB/s,
+p50 per message and the environment it ran under are written to
+<out>/rows.jsonl.
 <out>/summary.json names the winning setting per (direction, size) and the
 gain over the default (RCCL, one communicator, no knobs).
 
 It measures a link, so it needs N >= 2 GPUs and refuses N = 1.  ``--emulate``
 validates the whole script without a second GPU: ranks share GPU 0 through
-the IPC transport (``--emulate ipc``; the RCCL rows are skipped because RCCL
-refuses two ranks on one GPU) or run on the CPU host transport
-(``--emulate host``, build/p2p_matrix_host).  The reference has no tuning at
+the IPC transport (``--emulate ipc``; the RCCL rows are skipped), through RCCL
+itself (``--emulate rccl``: every rank claims a host of its own,
+P2P_RCCL_DISTINCT_HOSTS=1, and RCCL links them over its socket transport on
+loopback; every row runs, the GB/s are not xGMI's) or run on the CPU host
+transport (``--emulate host``, build/p2p_matrix_host).  The reference has no tuning at
 all: it inherits whatever NCCL_* the shell has (p2p_matrix.cc:126-131).
 
     python scripts/xgmi_pair_sweep.py --np 8 --out gpurun_out/xgmi_sweep
     python scripts/xgmi_pair_sweep.py --np 2 --emulate ipc --sizes 4M,32M
+    python scripts/xgmi_pair_sweep.py --np 3 --emulate rccl --sizes 4M
     python scripts/xgmi_pair_sweep.py --np 2 --emulate host --sizes 64K
 """
 from __future__ import annotations
@@ -46,6 +52,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from test_nccl_p2p_amd.utils import rccl_env  # noqa: E402
 MPIRUN = os.environ.get("P2P_MPIRUN", "/opt/conda/bin/mpirun")
+# --emulate rccl: one host id per rank, so RCCL accepts ranks sharing GPU 0
+# (csrc/transport_rccl.cpp) and connects them through loopback sockets.
+EMULATE_RCCL_ENV = {"P2P_RCCL_DISTINCT_HOSTS": "1", "NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1"}
 
 # RCCL knobs that act on point-to-point traffic within a node.  Each entry is
 # applied on top of the default environment at --comms 1, then the best knob
@@ -78,8 +87,9 @@ def parse_args(argv=None):
     ap.add_argument("--dirs", default="uni,bi")
     ap.add_argument("--iters", default="auto")
     ap.add_argument("--out", default="gpurun_out/xgmi_sweep")
-    ap.add_argument("--emulate", choices=["", "ipc", "host"], default="",
-                    help="validate without a second GPU: ranks share GPU 0 (ipc) or use the CPU (host)")
+    ap.add_argument("--emulate", choices=["", "ipc", "rccl", "host"], default="",
+                    help="validate without a second GPU: ranks share GPU 0 (ipc; rccl over RCCL's socket transport) "
+                         "or use the CPU (host)")
     ap.add_argument("--rows", default="rccl,knobs,ipc", help="row groups to run: rccl, knobs, ipc")
     ap.add_argument("--budget", type=float, default=900.0, help="seconds for the whole sweep; rows that would "
                     "start after it is spent are listed as skipped")
@@ -103,7 +113,7 @@ def plan_rows(args, np_):
     """Every (name, transport args, env) row of the sweep, in run order."""
     groups = set(args.rows.split(","))
     rows = []
-    rccl_ok = args.emulate == ""
+    rccl_ok = args.emulate in ("", "rccl")
     if "rccl" in groups and rccl_ok:
         for k in COMMS:
             rows.append({"name": "rccl-comms%d" % k, "args": ["--transport", "rccl", "--comms", str(k)], "env": {}})
@@ -152,9 +162,11 @@ def run_row(args, row, np_, exe, tag):
     cmd = [MPIRUN, "-n", str(np_), exe, "--mode", "pair", "--cells", "0-1", "--dir", "both", "--sizes", args.sizes,
            "-n", args.iters, "--verify", "--no-compat", "--json", js, "--timeout", str(int(args.row_timeout))]
     cmd += row["args"]
-    if args.emulate == "ipc":
+    if args.emulate in ("ipc", "rccl"):
         cmd += ["--device", "0"]
     env = dict(os.environ, **row["env"])
+    if args.emulate == "rccl":
+        env.update(EMULATE_RCCL_ENV)
     t0 = time.time()
     try:
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=args.row_timeout + 30)
@@ -216,7 +228,7 @@ def main(argv=None) -> int:
         return 1
     os.makedirs(args.out, exist_ok=True)
     t_end = time.time() + args.budget
-    done, skipped, failed = [], [], None
+    done, skipped, failed, corrupt = [], [], None, []
     with open(os.path.join(args.out, "rows.jsonl"), "w") as f:
         for i, row in enumerate(rows):
             if failed is not None or time.time() + 5 > t_end:
@@ -229,7 +241,9 @@ def main(argv=None) -> int:
             cells = " ".join("%s %.1f" % (k, v["cell_gbs"]) for k, v in rec.get("cells", {}).items())
             print("%-40s rc=%d %6.1fs %s" % (rec["name"], rec["rc"], rec["seconds"], cells or rec.get("error", "")[-200:]),
                   flush=True)
-            if rec["rc"] != 0:
+            if rec["rc"] == 2:
+                corrupt.append(rec["name"])  # wrong bytes under this setting: a finding, not a fault
+            elif rec["rc"] != 0:
                 failed = rec["name"]  # never keep driving the GPU after a failure
         # Best knob set at the best communicator count (knobs ran at --comms 1).
         knob_rows = [r for r in done if r["rc"] == 0 and any(r["name"] == x["name"] and x.get("knob") for x in rows)]
@@ -247,11 +261,12 @@ def main(argv=None) -> int:
                 print("%-40s rc=%d %6.1fs" % (rec["name"], rec["rc"], rec["seconds"]), flush=True)
     summary = {"np": np_, "emulate": args.emulate or None, "sizes": args.sizes, "dirs": args.dirs,
                "base_env": rccl_env.capture(), "rows_run": len(done), "rows_skipped": skipped, "failed_row": failed,
+               "corrupt_rows": corrupt,
                "best": summarize(done, args.dirs, args.sizes)}
     with open(os.path.join(args.out, "summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
-    print(json.dumps({"best": summary["best"], "failed_row": failed, "rows_skipped": skipped}))
-    return 2 if failed else 0
+    print(json.dumps({"best": summary["best"], "failed_row": failed, "corrupt_rows": corrupt, "rows_skipped": skipped}))
+    return 2 if failed or corrupt else 0
 
 
 if __name__ == "__main__":
