@@ -40,3 +40,15 @@ def test_pair_sweep_host_emulation(mpirun, host_build, tmp_path):
         assert b["cell_gbs"] > 0 and b["gain"] == 1.0
     rows = [json.loads(l) for l in (tmp_path / "rows.jsonl").read_text().splitlines()]
     assert all(c["mismatches"] == 0 for r in rows for c in r["cells"].values())
+
+
+@pytest.mark.mpi
+def test_pair_sweep_records_a_corrupt_row_and_goes_on(mpirun, host_build, tmp_path):
+    """A row whose bytes fail verification (here injected) is a finding, not a
+    fault: it is listed in corrupt_rows, never wins, and the script exits 2."""
+    out = subprocess.run([sys.executable, SWEEP, "--np", "2", "--emulate", "host", "--sizes", "64K",
+                          "--out", str(tmp_path)], capture_output=True, text=True, timeout=300,
+                         env=dict(os.environ, P2P_INJECT_FAULT="corrupt@1"))
+    assert out.returncode == 2, out.stderr + out.stdout
+    s = json.loads((tmp_path / "summary.json").read_text())
+    assert s["failed_row"] is None and s["corrupt_rows"] == ["host"] and s["best"] == {}
