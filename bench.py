@@ -606,7 +606,11 @@ def main(argv=None) -> int:
         # Everything below is untimed; release the timed driver's buffers first so
         # the comparisons run on the same memory footprint as the timed steps did.
         del drv
-        return {"sess": sess, "ref_sess": ref_sess, "sessions": sessions, "provenance": provenance, "comms": comms, "batch": batch, "failed": failed, "reason": reason, "tuning": tuning, "elapsed": elapsed, "steps": steps, "flows_total": flows_total, "value": value, "aggregate": aggregate, "my_ms": my_ms, "matrix": matrix, "samples": samples, "cells": cells, "offdiag": offdiag, "expected": expected, "vr": vr, "mismatches": mismatches, "depth": depth, "recv_bytes": recv_bytes}
+        return dict(sess=sess, ref_sess=ref_sess, sessions=sessions, provenance=provenance, comms=comms, batch=batch,
+                    failed=failed, reason=reason, tuning=tuning, elapsed=elapsed, steps=steps,
+                    flows_total=flows_total, value=value, aggregate=aggregate, my_ms=my_ms, matrix=matrix,
+                    samples=samples, cells=cells, offdiag=offdiag, expected=expected, vr=vr, mismatches=mismatches,
+                    depth=depth, recv_bytes=recv_bytes)
 
     # The headline.  Should RCCL itself fail on this node (communicator setup,
     # a peer connection, a stalled transfer: every wait is bounded by --timeout
@@ -616,10 +620,14 @@ def main(argv=None) -> int:
     # carries the error and value null.
     fallback = None
     transport_used = args.transport
+    err = None
     try:
         h = measure(args.transport)
     except Exception as e:  # noqa: BLE001 -- reported in the JSON line
         err = str(e)[:300]
+    # Outside the except block the failed attempt's frames are released, and
+    # with them its sessions (aborted communicators, their streams, buffers).
+    if err is not None:
         log("bench: headline through %s failed: %s" % (args.transport, err))
         # The failure is collective (a communicator that cannot be set up or a
         # stalled transfer times out on every rank): all ranks meet here first.
@@ -632,16 +640,22 @@ def main(argv=None) -> int:
         fallback = {"from": args.transport, "to": to, "error": err}
         transport_used = to
         state["section"] = "fallback"
+        err2 = None
         try:
             h = measure(to)
         except Exception as e2:  # noqa: BLE001
-            log("bench: fallback headline failed: %s" % e2)
-            reporter.emit(error="headline failed: %s; fallback through ipc failed: %s" % (err, str(e2)[:300]),
+            err2 = str(e2)[:300]
+        if err2 is not None:
+            log("bench: fallback headline failed: %s" % err2)
+            reporter.emit(error="headline failed: %s; fallback through %s failed: %s" % (err, to, err2),
                           transport=args.transport, headline_fallback=fallback)
             return 5
     (sess, ref_sess, sessions, provenance, comms, batch, failed, reason, tuning, elapsed, steps, flows_total, value,
      aggregate, my_ms, matrix, samples, cells, offdiag, expected, vr, mismatches, depth, recv_bytes) = (
-        h[k] for k in ("sess", "ref_sess", "sessions", "provenance", "comms", "batch", "failed", "reason", "tuning", "elapsed", "steps", "flows_total", "value", "aggregate", "my_ms", "matrix", "samples", "cells", "offdiag", "expected", "vr", "mismatches", "depth", "recv_bytes"))
+        h.pop(k) for k in ("sess", "ref_sess", "sessions", "provenance", "comms", "batch", "failed", "reason",
+                           "tuning", "elapsed", "steps", "flows_total", "value", "aggregate", "my_ms", "matrix",
+                           "samples", "cells", "offdiag", "expected", "vr", "mismatches", "depth", "recv_bytes"))
+    del h  # the sessions are closed by the del before the comparisons below; nothing else may hold them
 
     step_ms_med = statistics.median(my_ms) if my_ms else 0.0
     headline_transport = sess.transport
