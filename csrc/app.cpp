@@ -90,6 +90,18 @@ output
       --dry-run          print the schedules and exit
       --topology         print the GPU link matrix (xGMI/PCIe, hops, peer access) and exit
   -v, --verbose          -h, --help      --version
+environment (recorded in every --json provenance record; docs/OUTPUT.md)
+  P2P_RCCL_MAX_CHUNK=B   RCCL ops above B are posted as B-byte ops in one group [1G; 0 off]
+  P2P_RCCL_SPLIT_MIN=B   --comms: smaller messages stay on communicator 0       [1M]
+  P2P_RCCL_REGISTER=1|2  ncclCommRegister every buffer (2: + ncclMemAlloc)
+  P2P_RCCL_BLOCKING=1    blocking ncclCommInitRank instead of the polled non-blocking init
+  P2P_RCCL_DISTINCT_HOSTS=1  one NCCL_HOSTID per rank: RCCL ranks may share a GPU (tests,
+                         over RCCL's socket transport, e.g. NCCL_SOCKET_IFNAME=lo)
+  P2P_IPC_POOL=B         exported IPC buffers kept for reuse                     [32G]
+  P2P_BOOTSTRAP_PORT, P2P_BOOTSTRAP_TIMEOUT   TCP bootstrap port / receive deadline
+  P2P_HOSTNAME=name      hostname for the placement check (emulated hosts)
+  P2P_INJECT_FAULT=kind@rank[:phase]   corrupt | exit | hang | skip (tests)
+  P2P_ROCTX=1, P2P_LOG=1 roctx ranges; engine log on stderr
 )";
 }
 
