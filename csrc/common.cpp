@@ -119,12 +119,16 @@ Roctx& roctx() {
     const char* e = std::getenv("P2P_ROCTX");
     if (!e || std::atoi(e) == 0) return x;
     void* h = nullptr;
-    for (const char* lib : {"libroctx64.so", "libroctx64.so.4", "/opt/rocm/lib/libroctx64.so"}) {
+    // rocprofv3 (rocprofiler-sdk) records the markers of its own roctx
+    // library; the legacy roctracer libroctx64 is only a fallback for the
+    // older tools.
+    for (const char* lib : {"librocprofiler-sdk-roctx.so.1", "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1", "libroctx64.so",
+                            "libroctx64.so.4", "/opt/rocm/lib/libroctx64.so"}) {
       h = dlopen(lib, RTLD_NOW | RTLD_GLOBAL);
       if (h) break;
     }
     if (!h) {
-      std::fprintf(stderr, "[p2p] P2P_ROCTX=1 but libroctx64 could not be loaded; tracing disabled\n");
+      std::fprintf(stderr, "[p2p] P2P_ROCTX=1 but no roctx library could be loaded; tracing disabled\n");
       return x;
     }
     x.push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
