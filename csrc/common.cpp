@@ -125,7 +125,10 @@ Roctx& roctx() {
     for (const char* lib : {"librocprofiler-sdk-roctx.so.1", "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1", "libroctx64.so",
                             "libroctx64.so.4", "/opt/rocm/lib/libroctx64.so"}) {
       h = dlopen(lib, RTLD_NOW | RTLD_GLOBAL);
-      if (h) break;
+      if (h) {
+        std::fprintf(stderr, "[p2p] roctx ranges via %s\n", lib);
+        break;
+      }
     }
     if (!h) {
       std::fprintf(stderr, "[p2p] P2P_ROCTX=1 but no roctx library could be loaded; tracing disabled\n");
