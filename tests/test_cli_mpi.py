@@ -187,8 +187,8 @@ def test_roctx_library_for_rocprofv3(host_build):
     """P2P_ROCTX=1 loads rocprofiler-sdk's roctx (the one rocprofv3
     --marker-trace records; profiles/r2_tracing/), not the legacy one."""
     exe = os.path.join(host_build, "p2p_matrix_host")
-    out = subprocess.run([exe, "--mode", "self", "--size", "64K", "-n", "2", "--no-compat"], capture_output=True,
-                         text=True, timeout=60, env=dict(os.environ, P2P_ROCTX="1"))
+    out = subprocess.run([exe, "--transport", "host", "--mode", "self", "--size", "64K", "-n", "2", "--no-compat"],
+                         capture_output=True, text=True, timeout=60, env=dict(os.environ, P2P_ROCTX="1"))
     assert out.returncode == 0, out.stderr
     assert "roctx ranges via librocprofiler-sdk-roctx" in out.stderr, out.stderr
 
