@@ -693,12 +693,23 @@ void launch_copy_group(const CopyOp* ops, int cnt, hipStream_t stream, int max_b
 
 uint64_t copy_blocks(size_t bytes) { return std::max<uint64_t>(1, (bytes / 16 + kBlockVecs - 1) / kBlockVecs); }
 
+// Ops per launch: kMaxCopyOps, or fewer with P2P_COPY_MAX_OPS (A/B only).
+int copy_max_ops() {
+  static const int m = [] {
+    const char* e = std::getenv("P2P_COPY_MAX_OPS");
+    const int v = e ? std::atoi(e) : kMaxCopyOps;
+    return std::max(1, std::min(kMaxCopyOps, v));
+  }();
+  return m;
+}
+
 }  // namespace
 
 void launch_multi_copy(const CopyOp* ops, int nops, hipStream_t stream, int max_blocks) {
+  const int max_ops = copy_max_ops();
   if (max_blocks > 0) {  // explicit grid cap (grid-shape experiments): the ops share it
-    for (int first = 0; first < nops; first += kMaxCopyOps)
-      launch_copy_group(ops + first, std::min(kMaxCopyOps, nops - first), stream, max_blocks);
+    for (int first = 0; first < nops; first += max_ops)
+      launch_copy_group(ops + first, std::min(max_ops, nops - first), stream, max_blocks);
     return;
   }
   // Full grids only: ops above 4 GiB are split into 4 GiB pieces and pieces
@@ -720,7 +731,7 @@ void launch_multi_copy(const CopyOp* ops, int nops, hipStream_t stream, int max_
   while (i < pieces.size()) {
     size_t j = i;
     uint64_t blocks = 0;
-    while (j < pieces.size() && j - i < static_cast<size_t>(kMaxCopyOps) &&
+    while (j < pieces.size() && j - i < static_cast<size_t>(max_ops) &&
            (j == i || blocks + copy_blocks(pieces[j].bytes) <= kMaxGrid))
       blocks += copy_blocks(pieces[j++].bytes);
     launch_copy_group(pieces.data() + i, static_cast<int>(j - i), stream, 0);

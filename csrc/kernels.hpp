@@ -94,7 +94,7 @@ struct CopyOp {
   size_t bytes;
   bool coherent = false;
 };
-constexpr int kMaxCopyOps = 16;
+constexpr int kMaxCopyOps = 32;  // ops per launch (one bit each in CopyArgs::coherent)
 void launch_multi_copy(const CopyOp* ops, int nops, hipStream_t stream, int max_blocks = 0);
 
 // ---- device-initiated ping-pong (pingpong.hip) ----
