@@ -87,33 +87,53 @@ def _get(r: dict, *path, fmt: str = "%.1f") -> str:
     return fmt % v if isinstance(v, (int, float)) else str(v)
 
 
+def _aggregate(r: dict) -> float:
+    """All flows together, GB/s: `aggregate_gbs` (round 2 on), or `value` in
+    lines written while `value` was the aggregate (round 1)."""
+    return r["aggregate_gbs"] if r.get("aggregate_gbs") is not None else r["value"]
+
+
+def _ring_hop(r: dict) -> str:
+    ex = r.get("extras") or {}
+    if (ex.get("ring_hop") or {}).get("hop_us_p50") is not None:
+        return "%.2f" % ex["ring_hop"]["hop_us_p50"]
+    return _get(r, "extras", "ring_hop_8b", "iter_us_p50", fmt="%.2f")
+
+
 def scaling_table(results: Iterable[dict]) -> str:
-    """Markdown table of bench.py lines (one per GPU count): aggregate GB/s,
-    per-GPU GB/s, matrix min/mean, p50 latency, efficiency vs N=2 (the first
-    point where xGMI links are involved; N=1 is the self path), and the
-    untimed comparisons the line carries: the reference's methodology on the
-    same communicator, all-pairs aggregate, and the IPC pull / push engines."""
-    rows = sorted(results, key=lambda r: r["n_gpus"])
+    """Markdown table of bench.py lines (one per GPU count): `value` (the
+    mean cell of the matrix, GB/s per direction), aggregate and per-GPU GB/s,
+    the cell rate kept relative to N = 2 (weak scaling: per-GPU work is fixed,
+    so an ideal fabric keeps every cell's rate; N = 1 is the on-GPU self path
+    and has no link), matrix min / mean, p50 latency, and the untimed
+    comparisons the line carries: the reference's methodology on the same
+    communicator, all-pairs aggregate, the ring token hop, the IPC engines and
+    the device ping-pong."""
+    rows = sorted((r for r in results if r.get("value") is not None), key=lambda r: r["n_gpus"])
     base = next((r for r in rows if r["n_gpus"] == 2), None)
-    out = ["| GPUs | aggregate GB/s | per-GPU GB/s | RCCL comms | matrix min / mean GB/s | p50 latency us "
-           "| eff. vs 2 GPUs | reference-method cell GB/s | all-pairs 1 GiB aggregate GB/s "
-           "| ring hop 8 B us | IPC pull / push / SDMA / relay GB/s | relay pair 0->1 GB/s | device ping-pong us |",
-           "|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
+    out = ["| GPUs | value: mean cell GB/s | aggregate GB/s | per-GPU GB/s | cell rate vs 2 GPUs | RCCL comms "
+           "| matrix min / mean GB/s | p50 latency us | reference-method cell GB/s | all-pairs 1 GiB aggregate GB/s "
+           "| ring hop 8 B us | IPC pull / push / SDMA / relay GB/s | relay pair 0->1 GB/s | device ping-pong us "
+           "| headline fallback |",
+           "|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
     for r in rows:
         eff = ""
-        if base and r["n_gpus"] >= 2:
-            eff = "%.1f%%" % (100.0 * r["value"] / r["n_gpus"] / (base["value"] / 2))
+        if base and r["n_gpus"] >= 2 and base["value"]:
+            eff = "%.1f%%" % (100.0 * r["value"] / base["value"])
         relay = (r.get("ipc_transport") or {}).get("relay") or {}
         relay_pair = (relay.get("pair_0_1") or [{}])[0]
-        out.append("| %d | %.1f | %.1f | %s | %s / %s | %s | %s | %s | %s | %s | %s / %s / %s / %s | %s | %s |" % (
-            r["n_gpus"], r["value"], r["value"] / r["n_gpus"], _get(r, "posting", "rccl_comms", fmt="%d"),
+        agg = _aggregate(r)
+        fb = r.get("headline_fallback")
+        out.append("| %d | %.1f | %.1f | %.1f | %s | %s | %s / %s | %s | %s | %s | %s | %s / %s / %s / %s | %s | %s | %s |" % (
+            r["n_gpus"], r["value"], agg, agg / r["n_gpus"], eff, _get(r, "posting", "rccl_comms", fmt="%d"),
             r.get("matrix_gbs_min"), r.get("matrix_gbs_mean"),
-            r.get("p50_latency_us"), eff, _get(r, "reference_semantics", "cell_gbs_mean"),
-            _get(r, "extras", "allpairs_1g", "aggregate_gbs"), _get(r, "extras", "ring_hop_8b", "iter_us_p50"),
+            r.get("p50_latency_us"), _get(r, "reference_semantics", "cell_gbs_mean"),
+            _get(r, "extras", "allpairs_1g", "aggregate_gbs"), _ring_hop(r),
             _get(r, "ipc_transport", "value_gbs"),
             _get(r, "ipc_transport", "push", "value_gbs"), _get(r, "ipc_transport", "sdma", "value_gbs"),
             _get(r, "ipc_transport", "relay", "value_gbs"), relay_pair.get("gbs", "-"),
-            _get(r, "ipc_transport", "device_pingpong_p50_us", fmt="%.2f")))
+            _get(r, "ipc_transport", "device_pingpong_p50_us", fmt="%.2f"),
+            "%s -> %s" % (fb["from"], fb["to"]) if fb else "-"))
     return "\n".join(out)
 
 

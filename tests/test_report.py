@@ -27,24 +27,38 @@ def test_parse_roundtrip():
 
 
 def test_scaling_table():
-    rows = [{"n_gpus": 1, "value": 1000.0}, {"n_gpus": 2, "value": 100.0, "matrix_gbs_min": 50},
-            {"n_gpus": 4, "value": 200.0}]
+    """Round-2 lines: value = mean cell, aggregate_gbs = all flows; the cell
+    rate is compared with N = 2 (weak scaling keeps it constant)."""
+    rows = [{"n_gpus": 1, "value": 1000.0, "aggregate_gbs": 1000.0},
+            {"n_gpus": 2, "value": 100.0, "aggregate_gbs": 200.0, "matrix_gbs_min": 50},
+            {"n_gpus": 4, "value": 90.0, "aggregate_gbs": 360.0}]
     t = scaling_table(rows)
-    assert "| 4 | 200.0 | 50.0 |" in t and "100.0%" in t
+    assert "| 4 | 90.0 | 360.0 | 90.0 | 90.0% |" in t and "| 2 | 100.0 | 200.0 | 100.0 | 100.0% |" in t
+    assert "| 1 | 1000.0 | 1000.0 | 1000.0 |  |" in t
+
+
+def test_scaling_table_round1_lines():
+    """Round-1 lines carried the aggregate in value and no aggregate_gbs."""
+    t = scaling_table([{"n_gpus": 2, "value": 100.0}, {"n_gpus": 4, "value": 200.0}])
+    assert "| 4 | 200.0 | 200.0 | 50.0 | 200.0% |" in t
 
 
 def test_scaling_table_comparisons_and_cli(tmp_path, capsys):
     from test_nccl_p2p_amd.utils.report import main
-    rows = [{"metric": "m", "n_gpus": 2, "value": 100.0, "reference_semantics": {"cell_gbs_mean": 40.0},
-             "extras": {"allpairs_1g": {"aggregate_gbs": 300.0}},
+    rows = [{"metric": "m", "n_gpus": 2, "value": 100.0, "aggregate_gbs": 200.0,
+             "reference_semantics": {"cell_gbs_mean": 40.0},
+             "extras": {"allpairs_1g": {"aggregate_gbs": 300.0}, "ring_hop": {"hop_us_p50": 3.25}},
              "posting": {"rccl_comms": 4},
              "ipc_transport": {"value_gbs": 110.0, "device_pingpong_p50_us": 1.5, "push": {"value_gbs": 120.0},
                                "relay": {"value_gbs": 150.0, "pair_0_1": [{"bytes": 1, "gbs": 250.5}]}}},
-            {"metric": "m", "n_gpus": 8, "value": 380.0, "ipc_transport": {"error": "x"}}]
+            {"metric": "m", "n_gpus": 8, "value": 95.0, "aggregate_gbs": 760.0, "ipc_transport": {"error": "x"},
+             "headline_fallback": {"from": "rccl", "to": "ipc", "error": "e"}},
+            {"metric": "m", "n_gpus": 4, "value": None, "error": "headline failed"}]
     t = scaling_table(rows)
-    assert "| 2 | 100.0 | 50.0 | 4 |" in t
-    assert "| 40.0 | 300.0 | - | 110.0 / 120.0 / - / 150.0 | 250.5 | 1.50 |" in t
-    assert "| 8 | 380.0 | 47.5 | - |" in t and "95.0%" in t and "- / - / - / - | - |" in t
+    assert "| 2 | 100.0 | 200.0 | 100.0 | 100.0% | 4 |" in t
+    assert "| 40.0 | 300.0 | 3.25 | 110.0 / 120.0 / - / 150.0 | 250.5 | 1.50 | - |" in t
+    assert "| 8 | 95.0 | 760.0 | 95.0 | 95.0% | - |" in t and "- / - / - / - | - | - | rccl -> ipc |" in t
+    assert not any(l.startswith("| 4 |") for l in t.splitlines())  # a line without a value is left out
     files = []
     for r in rows:
         f = tmp_path / ("BENCH_%d.json" % r["n_gpus"])
@@ -52,4 +66,4 @@ def test_scaling_table_comparisons_and_cli(tmp_path, capsys):
         files.append(str(f))
     assert main(files) == 0
     out = capsys.readouterr().out
-    assert "== scaling" in out and "| 8 | 380.0 |" in out.split("== scaling")[1]
+    assert "== scaling" in out and "| 8 | 95.0 |" in out.split("== scaling")[1]
