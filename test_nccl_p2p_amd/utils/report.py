@@ -126,8 +126,8 @@ def scaling_table(results: Iterable[dict]) -> str:
         fb = r.get("headline_fallback")
         out.append("| %d | %.1f | %.1f | %.1f | %s | %s | %s / %s | %s | %s | %s | %s | %s / %s / %s / %s | %s | %s | %s |" % (
             r["n_gpus"], r["value"], agg, agg / r["n_gpus"], eff, _get(r, "posting", "rccl_comms", fmt="%d"),
-            r.get("matrix_gbs_min"), r.get("matrix_gbs_mean"),
-            r.get("p50_latency_us"), _get(r, "reference_semantics", "cell_gbs_mean"),
+            _get(r, "matrix_gbs_min", fmt="%.2f"), _get(r, "matrix_gbs_mean", fmt="%.2f"),
+            _get(r, "p50_latency_us", fmt="%.2f"), _get(r, "reference_semantics", "cell_gbs_mean"),
             _get(r, "extras", "allpairs_1g", "aggregate_gbs"), _ring_hop(r),
             _get(r, "ipc_transport", "value_gbs"),
             _get(r, "ipc_transport", "push", "value_gbs"), _get(r, "ipc_transport", "sdma", "value_gbs"),
