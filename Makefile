@@ -25,7 +25,7 @@ HIPFLAGS  := $(CXXSTD) $(OPT) $(WARN) -fPIC --offload-arch=$(ARCH) -Icsrc
 HOSTFLAGS := $(CXXSTD) $(OPT) $(WARN) -fPIC -Icsrc -pthread
 
 CORE      := common units stats schedule routing bootstrap transport_host transport_shm runner report provenance app
-GPU_OBJS  := $(addprefix $(BUILD)/gpu/,$(addsuffix .o,$(CORE) transport_rccl transport_ipc topology) kernels.o pingpong.o)
+GPU_OBJS  := $(addprefix $(BUILD)/gpu/,$(addsuffix .o,$(CORE) transport_rccl transport_ipc topology stream_gate) kernels.o pingpong.o)
 HOST_OBJS := $(addprefix $(BUILD)/host/,$(addsuffix .o,$(CORE) transport_rccl_stub))
 
 # MPICH lives in /opt/conda; putting /opt/conda/lib on the rpath would pull in

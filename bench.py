@@ -352,6 +352,9 @@ def parse_args(argv=None):
     ap.add_argument("--device", type=int, default=None, help="GPU index (default LOCAL_RANK)")
     ap.add_argument("--latency-iters", type=int, default=300)
     ap.add_argument("--latency-size", default="8")
+    ap.add_argument("--latency-preposted", type=int, default=16,
+                    help="also time the ping-pong posted this many exchanges at a time behind a stream gate "
+                         "(GPU-timeline latency, p50_latency_preposted_us; 0 = off)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--batch", type=int, default=-1,
                     help="1: all msgs of a step in one group (one launch); 0: one group per message; "
@@ -697,6 +700,8 @@ def main(argv=None) -> int:
         "matrix_samples": samples,
         "latency_p50_us_matrix": lat_matrix,
         "p50_latency_us": None,
+        "p50_latency_preposted_us": None,
+        "latency_preposted_p50_us_matrix": None,
         "latency_bytes": nat.parse_size(args.latency_size),
         "per_gpu_gbs": round(aggregate / n, 3),
         "rank0_step_ms_p50": round(step_ms_med, 4),
@@ -774,6 +779,26 @@ def main(argv=None) -> int:
     p50 = section("latency", latency, budgeted=False)
     reporter.update(p50_latency_us=round(float(p50), 3) if isinstance(p50, (int, float)) else None,
                     latency_p50_us_matrix=lat_matrix)
+
+    # The same ping-pong pre-posted: batches of exchanges wait behind a stream
+    # gate on every rank and run back to back once all are posted, so the
+    # samples are the operation's GPU-timeline latency without the host's
+    # posting rate (which the host-posted number above includes, and which
+    # varies from host to host).
+    pre_matrix = [[0.0] * n for _ in range(n)]
+
+    def latency_preposted():
+        lat = json.loads(sess.latency(nat.parse_size(args.latency_size), args.latency_iters,
+                                      min(50, args.latency_iters), args.latency_preposted))
+        for p in lat["pairs"]:
+            pre_matrix[p["a"]][p["b"]] = pre_matrix[p["b"]][p["a"]] = round(p["one_way_us"]["p50"], 3)
+        p50s = [p["one_way_us"]["p50"] for p in lat["pairs"]]
+        return {"p50": float(statistics.median(p50s)) if p50s else None, "method": lat["method"]}
+
+    if args.latency_preposted > 0:
+        pre = section("latency_preposted", latency_preposted, budgeted=False)
+        if isinstance(pre, dict) and pre.get("p50") is not None and pre.get("method") == "preposted":
+            reporter.update(p50_latency_preposted_us=round(pre["p50"], 3), latency_preposted_p50_us_matrix=pre_matrix)
 
     # The reference's own methodology on one communicator, for comparison
     # (serial ordered pairs, host clock, one stream sync per message, no

@@ -54,6 +54,10 @@ timing
       --device-latency   add a device-initiated ping-pong matrix (--transport ipc:
                          one wave per GPU writes into the peer's memory, no host
                          or runtime in the loop)
+      --latency-preposted B  also the ping-pong posted B exchanges at a time behind a
+                         stream gate (GPU transports), released together: the
+                         operation's GPU-timeline latency without the host's posting
+                         rate in it                                          [off]
       --latency-size S   [8]      --latency-iters N   [1000]
       --fuzz N           data-integrity stress: N groups of random messages (random
                          pairs incl. self, sizes 1 B .. the largest --size, at most
@@ -157,7 +161,7 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
     };
     // Options taking a value check it before use.
     static const char* kValued[] = {"-m", "--mode", "-d", "--dir", "-b", "--size", "--sizes", "-n", "--iters", "-w",
-                                    "--warmup", "--timing", "--latency-size", "--latency-iters", "--verify-impl",
+                                    "--warmup", "--timing", "--latency-size", "--latency-iters", "--latency-preposted", "--verify-impl",
                                     "--transport", "--ipc-engine", "--bootstrap", "--device", "--timeout", "--min-gbs", "--json",
                                     "--csv", "--trace", "--cells", "--comms", "--fuzz"};
     for (const char* v : kValued)
@@ -212,6 +216,9 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
       cfg->latency = true;
     } else if (a == "--device-latency") {
       cfg->device_latency = true;
+    } else if (a == "--latency-preposted") {
+      cfg->latency_preposted = std::atoi(next().c_str());
+      cfg->latency = true;
     } else if (a == "--fuzz") {
       cfg->fuzz_rounds = std::atoi(next().c_str());
     } else if (a == "--latency-size") {
@@ -444,6 +451,9 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
     }
   }
   if (cfg.latency) res.latency = run_latency(*t, boot, cfg.latency_bytes, cfg.latency_iters, std::min(cfg.latency_iters, 100), bufs);
+  if (cfg.latency && cfg.latency_preposted > 0)
+    res.preposted_latency = run_latency(*t, boot, cfg.latency_bytes, cfg.latency_iters, std::min(cfg.latency_iters, 100),
+                                        bufs, cfg.latency_preposted);
   if (cfg.device_latency)
     res.device_latency = run_device_latency(*t, boot, cfg.latency_bytes, cfg.latency_iters, std::min(cfg.latency_iters, 100));
   // Ring mode: also the dependent token chain (pipeline-parallel hop latency).
@@ -476,6 +486,7 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
       if (t->name() != "host" && t->name() != "shm") std::fprintf(out, "%s", topology_report().c_str());
       for (const auto& rec : res.runs) print_extended(out, rec, n);
       print_latency(out, res.latency, n);
+      print_latency(out, res.preposted_latency, n);
       print_latency(out, res.device_latency, n);
       for (const auto& rl : res.ring_latency) print_ring_latency(out, rl);
       if (cfg.fuzz_rounds > 0)
@@ -485,6 +496,7 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
                               : "all verified");
     }
     if (js.is_open() && !res.latency.empty()) js << latency_to_json(res.latency, n) << "\n";
+    if (js.is_open() && !res.preposted_latency.empty()) js << latency_to_json(res.preposted_latency, n) << "\n";
     if (js.is_open() && !res.device_latency.empty()) js << latency_to_json(res.device_latency, n) << "\n";
     for (const auto& rl : res.ring_latency)
       if (js.is_open()) js << ring_latency_to_json(rl) << "\n";

@@ -30,6 +30,7 @@ struct AppConfig {
   size_t target_bytes = 4ull << 30;
   bool latency = false;
   bool device_latency = false;   // ping-pong kernel matrix (one-sided transports)
+  int latency_preposted = 0;     // > 0: ping-pong also posted in batches of this many behind a stream gate
   int fuzz_rounds = 0;           // --fuzz N: N groups of random verified messages (data-integrity stress)
   size_t latency_bytes = 8;
   int latency_iters = 1000;
@@ -67,6 +68,7 @@ struct AppResult {
   std::vector<RunRecord> runs;
   std::vector<LatencyResult> latency;
   std::vector<LatencyResult> device_latency;
+  std::vector<LatencyResult> preposted_latency;
   std::vector<RingLatencyResult> ring_latency;  // --mode ring with --latency / --device-latency
   uint64_t mismatches = 0;
   int slow_flows = 0;  // flows under --min-gbs

@@ -97,9 +97,9 @@ class Session {
     return run_to_json(rec, world());
   }
 
-  std::string latency(size_t bytes, int iters, int warmup) {
+  std::string latency(size_t bytes, int iters, int warmup, int preposted) {
     Buffers bufs(*t_, std::max<size_t>(bytes, 16), 1);
-    auto lat = run_latency(*t_, *boot_, bytes, iters, warmup, bufs);
+    auto lat = run_latency(*t_, *boot_, bytes, iters, warmup, bufs, preposted);
     return latency_to_json(lat, world());
   }
 
@@ -248,7 +248,9 @@ PYBIND11_MODULE(_p2pcore, m) {
       .def("device_latency", &Session::device_latency, py::arg("bytes") = 8, py::arg("iters") = 1000,
            py::arg("warmup") = 100, py::call_guard<py::gil_scoped_release>())
       .def("latency", &Session::latency, py::arg("bytes") = 8, py::arg("iters") = 1000, py::arg("warmup") = 100,
-           py::call_guard<py::gil_scoped_release>())
+           py::arg("preposted") = 0, py::call_guard<py::gil_scoped_release>(),
+           "Ping-pong matrix (collective).  preposted=B: exchanges posted B at a time behind a stream gate and "
+           "released together (GPU-timeline latency; host-posted where the transport has no gate).")
       .def("fuzz", &Session::fuzz, py::arg("rounds") = 20, py::arg("seed") = 1, py::arg("max_bytes") = size_t{4} << 20,
            py::call_guard<py::gil_scoped_release>(),
            "Random groups of verified messages through the transport (collective); returns mismatching words.")

@@ -126,8 +126,9 @@ void print_latency(FILE* out, const std::vector<LatencyResult>& lat, int n) {
     p50s.push_back(l.one_way_us.p50);
   }
   std::fprintf(out, "\n== latency: %s messages, %s ==\n", format_size(lat[0].bytes).c_str(),
-               lat[0].method == "device" ? "device-initiated ping-pong (one wave per GPU, no host in the loop)"
-                                         : "ping-pong");
+               lat[0].method == "device"      ? "device-initiated ping-pong (one wave per GPU, no host in the loop)"
+               : lat[0].method == "preposted" ? "ping-pong pre-posted behind a stream gate (GPU timeline)"
+                                              : "ping-pong");
   print_matrix(out, "p50 one-way latency (us)", m, n, "%9.2f", n > 1);
   Summary s = summarize(p50s);
   std::fprintf(out, "  p50 over pairs: min %.2f  median %.2f  max %.2f us\n", s.min, s.p50, s.max);

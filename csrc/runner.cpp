@@ -400,11 +400,24 @@ void warm_connections(Transport& t, Bootstrap& boot, const Schedule& s, Buffers&
 
 // -------------------------------------------------------------- latency ----
 
-std::vector<LatencyResult> run_latency(Transport& t, Bootstrap& boot, size_t bytes, int iters, int warmup, Buffers& bufs) {
+std::vector<LatencyResult> run_latency(Transport& t, Bootstrap& boot, size_t bytes, int iters, int warmup, Buffers& bufs,
+                                       int preposted) {
   const int n = boot.size(), me = boot.rank();
   P2P_CHECK(bytes <= bufs.capacity() && bufs.slots() >= 1, "latency buffers too small");
   P2P_CHECK(iters >= 1, "latency iters must be >= 1");
   std::vector<LatencyResult> out;
+  // A transport without a gate (CPU) says so on its first arm: probe once,
+  // collectively, and fall back to host-posted samples everywhere.
+  bool gated = false;
+  if (preposted > 0) {
+    gated = t.gate_arm(1.0);
+    if (gated) {
+      t.gate_release();
+      t.sync();
+    }
+    gated = boot.allreduce_max(gated ? 0.0 : 1.0) == 0.0;
+  }
+  constexpr double kGateTimeoutS = 5.0;  // a gate opens by itself after this (never a hung stream)
 
   auto run_round = [&](int partner) -> Summary {
     const bool self = (partner == me);
@@ -429,7 +442,40 @@ std::vector<LatencyResult> run_latency(Transport& t, Bootstrap& boot, size_t byt
     }
     boot.barrier();
     std::vector<double> samples;
-    if (partner >= 0) {
+    auto sample = [&](const std::vector<int>& marks, size_t from) {
+      if (!lead) return;
+      for (size_t i = from; i < marks.size(); ++i) {
+        double us = t.elapsed_ms(marks[i - 1], marks[i]) * 1e3;
+        samples.push_back(self ? us : us / 2.0);
+      }
+    };
+    if (gated) {
+      // Batches of `batch` exchanges behind a gate on every rank; all ranks
+      // have posted theirs before any gate opens (barrier), so the batch runs
+      // with no host in the loop.  Every rank runs the same batches, active
+      // or not, so the barriers match.
+      const int batch = std::max(2, preposted);
+      for (int done = 0; done < iters; done += batch - 1) {
+        const int k = std::min(batch, iters - done + 1);
+        std::vector<int> marks;
+        if (partner >= 0) {
+          t.clear_marks();
+          P2P_CHECK(t.gate_arm(kGateTimeoutS), "stream gate unavailable");
+          marks.push_back(t.mark());
+          for (int i = 0; i < k; ++i) {
+            exchange();
+            marks.push_back(t.mark());
+          }
+        }
+        boot.barrier();  // every rank's batch is posted
+        if (partner >= 0) {
+          t.gate_release();
+          t.sync();
+          P2P_CHECK(!t.gate_timed_out(), "stream gate expired before its release (host stalled?)");
+          sample(marks, 2);  // marks[1]: the first exchange, which also waited for the partner's release
+        }
+      }
+    } else if (partner >= 0) {
       t.clear_marks();
       std::vector<int> marks;
       marks.push_back(t.mark());
@@ -438,11 +484,7 @@ std::vector<LatencyResult> run_latency(Transport& t, Bootstrap& boot, size_t byt
         marks.push_back(t.mark());
       }
       t.sync();
-      if (lead)
-        for (size_t i = 1; i < marks.size(); ++i) {
-          double us = t.elapsed_ms(marks[i - 1], marks[i]) * 1e3;
-          samples.push_back(self ? us : us / 2.0);
-        }
+      sample(marks, 1);
     }
     boot.barrier();
     return summarize(samples);
@@ -454,6 +496,7 @@ std::vector<LatencyResult> run_latency(Transport& t, Bootstrap& boot, size_t byt
     r.a = r.b = 0;
     r.bytes = bytes;
     r.one_way_us = s;
+    r.method = gated ? "preposted" : "host";
     out.push_back(r);
     return out;
   }
@@ -471,6 +514,7 @@ std::vector<LatencyResult> run_latency(Transport& t, Bootstrap& boot, size_t byt
       r.b = pr.second;
       r.bytes = bytes;
       r.one_way_us = all[static_cast<size_t>(pr.first)];
+      r.method = gated ? "preposted" : "host";
       out.push_back(r);
     }
   }

@@ -134,14 +134,24 @@ struct LatencyResult {
   int a = -1, b = -1;   // a < b; a == b for the self path
   size_t bytes = 0;
   Summary one_way_us;   // half round trip, microseconds
-  std::string method = "host";  // host: posted ping-pong through the transport; device: ping-pong kernel
+  // host: posted ping-pong through the transport; preposted: the same, posted
+  // in batches behind a stream gate (GPU timeline only); device: ping-pong kernel
+  std::string method = "host";
 };
 
 // Ping-pong over round-robin rounds (every unordered pair once; each round's
 // pairs run concurrently on disjoint xGMI links).  n == 1 measures the self
 // path (one grouped self send/recv per sample).
+//
+// preposted == 0: every exchange is posted as the previous one runs, so a
+// sample is max(operation time on the GPU, host posting time).  preposted =
+// B > 0 (transports with Transport::gate_arm): exchanges are posted B at a
+// time behind a stream gate on every rank and released together, so they run
+// back to back on the GPU and a sample is the operation's own GPU-timeline
+// time (the first exchange of each batch, which also absorbs the ranks'
+// release skew, is not sampled).  Transports without a gate fall back to 0.
 std::vector<LatencyResult> run_latency(Transport& t, Bootstrap& boot, size_t bytes, int iters, int warmup,
-                                       Buffers& bufs);
+                                       Buffers& bufs, int preposted = 0);
 
 // Device-initiated ping-pong (Transport::device_pingpong; the IPC transport):
 // one wave per GPU bounces a message through the peer's memory with no host

@@ -143,6 +143,17 @@ class Transport {
     return {};
   }
 
+  // ---- stream gate (pre-posted latency, run_latency with preposted > 0) ----
+  // gate_arm() enqueues a one-wave kernel that holds the stream carrying
+  // small messages until gate_release() (or `timeout_s`); what is posted in
+  // between then runs back to back on the GPU with no host in the loop, so
+  // per-message marks time the operation itself, not the host's posting rate.
+  // Returns false where there is nothing to gate (CPU transports).
+  // gate_timed_out() (after sync) reports a gate that expired instead.
+  virtual bool gate_arm(double /*timeout_s*/) { return false; }
+  virtual void gate_release() {}
+  virtual bool gate_timed_out() { return false; }
+
   // ---- health ----
   // Non-empty when the transport saw an asynchronous error (e.g. a peer died).
   virtual std::string async_error() { return ""; }

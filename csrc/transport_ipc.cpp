@@ -59,6 +59,7 @@
 #include "hip_check.hpp"
 #include "kernels.hpp"
 #include "routing.hpp"
+#include "stream_gate.hpp"
 #include "transport.hpp"
 #include "units.hpp"
 
@@ -416,6 +417,12 @@ class IpcTransport final : public Transport {
   // messages from rank r, slot n = replies of the self path), exported over
   // hipIpc so peers write into it directly.  Uncached device memory when the
   // runtime allows it, so the spinning wave reads HBM, not a stale line.
+  bool gate_arm(double timeout_s) override {
+    gate_.arm(stream_, timeout_s);
+    return true;
+  }
+  void gate_release() override { gate_.release(); }
+  bool gate_timed_out() override { return gate_.timed_out(); }
   bool supports_device_pingpong() const override { return true; }
   void pingpong_setup() override {
     if (page_) return;  // same state on every rank: they all set up together
@@ -757,6 +764,7 @@ class IpcTransport final : public Transport {
   RouteOptions route_opt_;
   int device_ = 0;
   hipStream_t stream_ = nullptr;
+  StreamGate gate_;
   std::vector<hipEvent_t> events_;
   int next_event_ = 0;
   std::vector<hipGraphExec_t> execs_;

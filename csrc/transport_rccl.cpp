@@ -59,6 +59,7 @@
 #include "kernels.hpp"
 #include "provenance.hpp"
 #include "report.hpp"
+#include "stream_gate.hpp"
 #include "topology.hpp"
 #include "transport.hpp"
 #include "units.hpp"
@@ -472,6 +473,14 @@ class RcclTransport final : public Transport {
   }
 
   int concurrency() const override { return static_cast<int>(comms_.size()); }
+  // Small messages (latency) run on communicator 0, on the main stream.
+  bool gate_arm(double timeout_s) override {
+    if (main_idle_) return false;
+    gate_.arm(stream_, timeout_s);
+    return true;
+  }
+  void gate_release() override { gate_.release(); }
+  bool gate_timed_out() override { return gate_.timed_out(); }
   void set_timeout(double seconds) override { timeout_ = seconds; }
 
   std::string async_error() override {
@@ -661,6 +670,7 @@ class RcclTransport final : public Transport {
   dev::VerifyImpl verify_impl_ = dev::VerifyImpl::Auto;
   std::string desc_;
   int hook_ = 0;
+  StreamGate gate_;
 };
 
 }  // namespace

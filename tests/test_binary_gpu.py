@@ -69,6 +69,7 @@ def test_bench_contract_single_gpu():
     assert t[chosen] <= min(v for k, v in t.items() if k.startswith("comms1_")), t
     assert r["posting"]["rccl_comms"] == 4, t  # four communicators: ~2x one on the self path
     assert isinstance(r["p50_latency_us"], float) and r["p50_latency_us"] > 0
+    assert 0 < r["p50_latency_preposted_us"] <= r["p50_latency_us"] * 1.2 + 1.0, r["p50_latency_preposted_us"]
     # The hand-written data plane runs the same self step after the timed
     # region: pull, push and SDMA engines, all verified.
     ipc = r["ipc_transport"]
@@ -136,3 +137,19 @@ def test_bench_headline_falls_back_to_ipc():
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert r["transport"] == "ipc" and r["headline_fallback"]["from"] == "rccl", r.get("headline_fallback")
     assert r["verify_mismatches"] == 0 and r["verify_coverage"] == 1.0 and r["value"] > 10
+
+
+@pytest.mark.parametrize("transport", ["rccl", "ipc"])
+def test_preposted_latency(exe, tmp_path, transport):
+    """--latency-preposted: the self ping-pong posted 16 at a time behind a
+    stream gate runs without the host in the loop, so its p50 is at most the
+    host-posted one's (plus noise)."""
+    js = tmp_path / "l.json"
+    out = subprocess.run([exe, "--transport", transport, "--mode", "self", "--size", "4K", "-n", "2",
+                          "--latency-preposted", "16", "--latency-iters", "400", "--no-compat", "--json", str(js)],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    recs = {r["method"]: r for r in (json.loads(l) for l in js.read_text().splitlines()) if r["type"] == "latency"}
+    host, pre = recs["host"]["pairs"][0]["one_way_us"], recs["preposted"]["pairs"][0]["one_way_us"]
+    assert 0 < pre["p50"] <= host["p50"] * 1.2 + 1.0, (pre, host)
+    assert "pre-posted behind a stream gate" in out.stdout

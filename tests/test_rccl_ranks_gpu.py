@@ -36,6 +36,7 @@ def test_cli_four_rccl_ranks_every_mode(exe, tmp_path, comms):
     js = tmp_path / "r.json"
     out = subprocess.run([MPIRUN, "-n", "4", exe, "--device", "0", "--mode", "pair,tournament,ring,allpairs",
                           "--size", "4M", "-n", "4", "--comms", comms, "--verify", "--latency", "--latency-iters", "30",
+                          "--latency-preposted", "8",
                           "--json", str(js), "--timeout", "60"],
                          capture_output=True, text=True, timeout=300, env=ENV)
     assert out.returncode == 0, out.stderr[-3000:]
@@ -45,6 +46,10 @@ def test_cli_four_rccl_ranks_every_mode(exe, tmp_path, comms):
     prov = [r for r in recs if r["type"] == "provenance"][0]
     assert prov["env"]["NCCL_HOSTID"].startswith("p2p-emulated-host-")
     assert "ring token latency: 4 rank(s)" in out.stdout
+    # The pre-posted ping-pong (stream gates on every rank, released together)
+    # ran through RCCL across ranks: every pair has samples.
+    pre = [r for r in recs if r["type"] == "latency" and r["method"] == "preposted"]
+    assert len(pre) == 1 and len(pre[0]["pairs"]) == 6 and all(p["one_way_us"]["p50"] > 0 for p in pre[0]["pairs"])
 
 
 def test_bench_four_rccl_ranks(tmp_path):
