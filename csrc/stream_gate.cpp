@@ -13,7 +13,9 @@ StreamGate::~StreamGate() {
 
 void StreamGate::arm(hipStream_t stream, double timeout_s) {
   if (!flag_) {
-    HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&flag_), 64, hipHostMallocDefault));
+    // Fine-grained (coherent) host memory: the gate's system-scope loads see the
+    // host's store without any cache maintenance.
+    HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&flag_), 64, hipHostMallocCoherent));
     __atomic_store_n(flag_, 0ull, __ATOMIC_RELEASE);
     HIPCHECK(hipMalloc(reinterpret_cast<void**>(&status_), sizeof(unsigned int)));
     HIPCHECK(hipMemsetAsync(status_, 0, sizeof(unsigned int), stream));
