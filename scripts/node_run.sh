@@ -1,0 +1,52 @@
+#!/bin/bash
+# Everything this framework measures on a multi-GPU MI355X node, in one command, each step time-limited and the
+# first failure ending the run (the GPUs are never driven again after a fault):
+#
+#   1. the multi-GPU test tier (tests/test_multi_gpu.py: RCCL across GPUs in every mode, 4 communicators, the IPC
+#      engines across xGMI, fuzz);
+#   2. the reference's own run line, `mpirun -n N ./p2p_matrix` (compat matrices, result.txt);
+#   3. the headline bench at N = 1, 2, 4, 8 and its scaling table (scripts/scaling.sh);
+#   4. the xGMI pair-cell tuning sweep (scripts/xgmi_pair_sweep.py).
+#
+#   bash scripts/node_run.sh [OUT_DIR] [--dry-run]
+set -uo pipefail
+cd "$(dirname "$0")/.."
+OUT=${1:-gpurun_out/node}
+DRY=0
+for a in "$@"; do [ "$a" = "--dry-run" ] && DRY=1; done
+[ "$OUT" = "--dry-run" ] && OUT=gpurun_out/node
+MPIRUN=${P2P_MPIRUN:-/opt/conda/bin/mpirun}
+NGPU=$(python3 -c "import torch; print(torch.cuda.device_count())")
+N=$(( NGPU < 8 ? NGPU : 8 ))
+[ "$DRY" = 1 ] && [ "$N" -lt 2 ] && N=8  # show the node commands anywhere
+
+step() {  # name, seconds, command...
+  local name=$1 secs=$2
+  shift 2
+  echo "== $name (limit ${secs}s): $*"
+  [ "$DRY" = 1 ] && return 0
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc" >> "$OUT/summary.txt"
+  if [ $rc -ne 0 ]; then
+    echo "node_run: $name failed (rc=$rc); stopping, see $OUT/$name.log" >&2
+    exit $rc
+  fi
+}
+
+if [ "$N" -lt 2 ] && [ "$DRY" = 0 ]; then
+  echo "node_run: needs >= 2 visible GPUs (found $NGPU); on one GPU use scripts/gpu_check.sh," \
+       "scripts/emulated_node.sh and scripts/rccl_emulated_node.sh" >&2
+  exit 1
+fi
+mkdir -p "$OUT"
+if [ "$DRY" = 0 ]; then
+  make -j16 all > "$OUT/build.log" 2>&1 || { echo "node_run: build failed, see $OUT/build.log" >&2; exit 1; }
+fi
+step multi_gpu_tests 1800 python3 -u -m pytest tests/test_multi_gpu.py -m gpu -x -v --timeout 900 --timeout-method thread
+step reference_run 600 "$MPIRUN" -n "$N" ./p2p_matrix
+[ "$DRY" = 0 ] && cp "$OUT/reference_run.log" "$OUT/result.txt"
+step scaling 3600 bash scripts/scaling.sh "$OUT/scaling.jsonl"
+step pair_sweep 1200 python3 scripts/xgmi_pair_sweep.py --np "$N" --out "$OUT/xgmi_sweep"
+[ "$DRY" = 0 ] && cat "$OUT/summary.txt"
+exit 0

@@ -52,3 +52,16 @@ def test_pair_sweep_records_a_corrupt_row_and_goes_on(mpirun, host_build, tmp_pa
     assert out.returncode == 2, out.stderr + out.stdout
     s = json.loads((tmp_path / "summary.json").read_text())
     assert s["failed_row"] is None and s["corrupt_rows"] == ["host"] and s["best"] == {}
+
+
+def test_node_run_dry_run_and_refusal():
+    """scripts/node_run.sh lists its four steps; without >= 2 GPUs it refuses
+    (one-GPU boxes have their own scripts)."""
+    script = os.path.join(ROOT, "scripts", "node_run.sh")
+    out = subprocess.run(["bash", script, "/tmp/p2p_node_dry", "--dry-run"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    for step in ("multi_gpu_tests", "reference_run", "scaling", "pair_sweep"):
+        assert "== %s" % step in out.stdout
+    assert "-n 8 ./p2p_matrix" in out.stdout
+    out = subprocess.run(["bash", script, "/tmp/p2p_node_real"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 1 and "needs >= 2 visible GPUs" in out.stderr
