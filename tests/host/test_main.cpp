@@ -646,6 +646,25 @@ TEST(test_wallclock_and_latency_host) {
   });
 }
 
+TEST(test_preposted_latency_batches) {
+  // Without a gate the pre-posted ping-pong falls back to host-posted samples;
+  // with one (faked on the CPU) it runs in batches whose first exchange is not
+  // sampled, and still yields exactly `iters` samples per pair.
+  for (int fake : {0, 1}) {
+    setenv("P2P_TEST_FAKE_GATE", fake ? "1" : "0", 1);
+    run_ranks(4, [&](Bootstrap& b, Transport& t) {
+      Buffers bufs(t, 64, 1);
+      auto lat = run_latency(t, b, 8, 37, 2, bufs, 8);
+      EXPECT(lat.size() == 6);
+      for (auto& l : lat) {
+        EXPECT(l.method == (fake ? "preposted" : "host"));
+        EXPECT(l.one_way_us.n == 37 && l.one_way_us.p50 > 0);
+      }
+    });
+  }
+  unsetenv("P2P_TEST_FAKE_GATE");
+}
+
 TEST(test_step_driver_host) {
   run_ranks(4, [&](Bootstrap& b, Transport& t) {
     StepDriver d(t, b, make_tournament_schedule(4, Direction::Bi), 8192, 2, true);
