@@ -56,6 +56,7 @@ import sys
 import tempfile
 import threading
 import time
+import types
 
 T0 = time.monotonic()  # the deadline counts from here (process start, give or take the interpreter)
 
@@ -420,78 +421,92 @@ def hang_requested(section: str, rank: int) -> bool:
     return bool(spec) and spec == "%s@%d" % (section, rank)
 
 
-def main(argv=None) -> int:
-    args = parse_args(argv)
-    if args.child:
-        return child_main(args)
-    real_stdout = claim_stdout()
-    from test_nccl_p2p_amd import require_native
-    from test_nccl_p2p_amd.parallel.session import create_session, init_control_plane
+class BenchRun:
+    """One rank of a bench.py run.  Every method is collective (all ranks
+    call it in the same order): the headline (posting selection, W warmup
+    and K timed steps, with the IPC fallback), then the untimed sections, all
+    under one deadline counted from process start."""
 
-    nat = require_native()
-    deadline = Deadline(args.deadline)
-    env = init_control_plane("gloo", timeout_s=max(60.0, args.deadline))
-    if args.gpus != env.world:
-        log("bench: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, env.world))
-    n = env.world
-    use_gpu = args.transport not in ("host", "shm")
-    device = default_device(env.local_rank) if args.device is None else args.device
-    if use_gpu:
-        torch.cuda.set_device(device)
-    reporter = Reporter(env.rank, real_stdout, args.json_out)
-    state = {"section": "setup", "skipped": [], "errors": {}}
-    start_watchdog(deadline, reporter, nat, state)
+    def __init__(self, args, real_stdout: int):
+        from test_nccl_p2p_amd import require_native
+        from test_nccl_p2p_amd.parallel.session import create_session, init_control_plane
 
-    def barrier():
-        if n > 1:
+        self.args = args
+        self.nat = require_native()
+        self.create_session = create_session
+        self.deadline = Deadline(args.deadline)
+        self.env = init_control_plane("gloo", timeout_s=max(60.0, args.deadline))
+        if args.gpus != self.env.world:
+            log("bench: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, self.env.world))
+        self.n = self.env.world
+        self.use_gpu = args.transport not in ("host", "shm")
+        self.device = default_device(self.env.local_rank) if args.device is None else args.device
+        if self.use_gpu:
+            torch.cuda.set_device(self.device)
+        self.reporter = Reporter(self.env.rank, real_stdout, args.json_out)
+        self.state = {"section": "setup", "skipped": [], "errors": {}}
+        start_watchdog(self.deadline, self.reporter, self.nat, self.state)
+        self.size = self.nat.parse_size(args.size)
+        self.mode = "self" if self.n == 1 else args.mode
+        self.h = None              # the headline's measurement (measure())
+        self.fallback = None       # headline_fallback of the JSON line
+        self.transport_used = args.transport
+        self.live = []             # sessions whose waits the untimed sections bound
+        self.untimed_t0 = None
+
+    # ---- collectives over the gloo control plane ---------------------------
+    def barrier(self):
+        if self.n > 1:
             dist.barrier()
 
-    def gpu_sync():
-        if use_gpu:
+    def gpu_sync(self):
+        if self.use_gpu:
             torch.cuda.synchronize()
 
-    def agree(ok: bool) -> bool:
+    def agree(self, ok: bool) -> bool:
         """True when every rank reports ok (the candidates are collective)."""
-        if n == 1:
+        if self.n == 1:
             return ok
         t = torch.tensor([1 if ok else 0], dtype=torch.int32)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         return bool(t.item())
 
-    size = nat.parse_size(args.size)
-    mode = "self" if n == 1 else args.mode
+    def log0(self, msg: str):
+        if self.env.rank == 0:
+            log(msg)
 
-    def measure(transport):
+    # ---- the headline -------------------------------------------------------
+    def measure(self, transport):
         """Posting selection, then the W warmup and K timed steps of the headline
         through `transport`; returns what the report needs."""
+        args, nat, n, mode, size = self.args, self.nat, self.n, self.mode, self.size
         headline = transport + (":%d" % args.comms if transport == "rccl" and args.comms > 1 else "")
-        sess = create_session(headline, device=device, timeout_s=args.timeout)
-        if env.rank == 0:
-            log("bench: %d rank(s), %s, %s" % (n, sess.transport, sess.device_desc))
+        sess = self.create_session(headline, device=self.device, timeout_s=args.timeout)
+        self.log0("bench: %d rank(s), %s, %s" % (n, sess.transport, sess.device_desc))
         # Test hook: P2P_BENCH_FAIL_HEADLINE=<transport> fails the headline
         # through that transport on every rank, as a communicator that cannot
         # be set up does.
         if os.environ.get("P2P_BENCH_FAIL_HEADLINE") == transport:
             raise RuntimeError("injected headline failure")
-        provenance = json.loads(sess.provenance(device if use_gpu else -1))
+        provenance = json.loads(sess.provenance(self.device if self.use_gpu else -1))
         provenance.pop("type", None)
 
         # Receive-slot budget: every message of every timed step gets its own
         # slot, up to this much memory per rank (ranks sharing a GPU split it).
         budget = 0 if args.recv_budget.strip() in ("", "0") else nat.parse_size(args.recv_budget)
-        if budget == 0 and use_gpu:
-            free_b, _ = torch.cuda.mem_get_info(device)
-            same_gpu = sum(1 for d in provenance.get("rank_devices", []) if d["device"] == device) or 1
+        if budget == 0 and self.use_gpu:
+            free_b, _ = torch.cuda.mem_get_info(self.device)
+            same_gpu = sum(1 for d in provenance.get("rank_devices", []) if d["device"] == self.device) or 1
             budget = int(0.4 * free_b / same_gpu)
         elif budget == 0:
             budget = 256 << 20
 
-        # ---- posting selection: one untimed lap of the schedule per candidate --
-        # (one group per step vs one per message; RCCL: one communicator vs
-        # several whose send/recv kernels run side by side, posting_candidates),
-        # timed by the slowest rank,
-        # before the W warmup steps of the chosen one.
-        state["section"] = "tuning"
+        # ---- posting selection: whole untimed laps of the schedule per
+        # candidate (one group per step vs one per message; RCCL: one
+        # communicator vs several whose send/recv kernels run side by side,
+        # posting_candidates), timed by the slowest rank, before the W warmup
+        # steps of the chosen one.
+        self.state["section"] = "tuning"
         choices = posting_candidates(transport, args.comms, args.batch, n)
         c0 = first_comms(transport, args.comms)
         sessions = {c0: sess}
@@ -499,7 +514,8 @@ def main(argv=None) -> int:
         def session_for(c):
             if c not in sessions:
                 # A candidate that stalls is aborted and dropped after --timeout.
-                sessions[c] = create_session("rccl:%d" % c if c > 1 else "rccl", device=device, timeout_s=args.timeout)
+                sessions[c] = self.create_session("rccl:%d" % c if c > 1 else "rccl", device=self.device,
+                                                  timeout_s=args.timeout)
             return sessions[c]
 
         tuning, failed = {}, {}
@@ -517,22 +533,23 @@ def main(argv=None) -> int:
                     d.connect()
                     # Test hook: P2P_BENCH_FAIL_CANDIDATE="<comms>,<batch>" fails
                     # that candidate on the last rank only.
-                    if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d" % (c, b) and env.rank == n - 1:
+                    if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d" % (c, b) and self.env.rank == n - 1:
                         raise RuntimeError("injected candidate failure")
                 except Exception as e:  # noqa: BLE001 -- reported, and the candidate is skipped everywhere
                     err = str(e)[:200]
-                if agree(err is None):
-                    barrier()
+                if self.agree(err is None):
+                    self.barrier()
                     w0 = time.perf_counter()
                     try:
                         d.run_steps(0, tune_k)
                         d.sync()
-                        if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d,tuning" % (c, b) and env.rank == n - 1:
+                        if (os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d,tuning" % (c, b)
+                                and self.env.rank == n - 1):
                             raise RuntimeError("injected tuning failure")
                     except Exception as e:  # noqa: BLE001 -- same agreement as above
                         err = str(e)[:200]
                     w = time.perf_counter() - w0
-                    if agree(err is None):
+                    if self.agree(err is None):
                         tuning[(c, b)] = sess.allreduce_max(w) / tune_k
                         del d
                         # Only the best communicator count so far, the headline
@@ -551,8 +568,8 @@ def main(argv=None) -> int:
                 if c != c0 and not any(cc == c for (cc, _) in tuning):
                     sessions.pop(c, None)
             comms, batch = min(tuning, key=tuning.get)
-            reason = "fastest of %d candidate(s) over %d untimed step(s) each (%s lap(s) of %d round(s)), slowest rank's " \
-                     "clock" % (len(tuning), tune_k, args.tune_laps, phases)
+            reason = "fastest of %d candidate(s) over %d untimed step(s) each (%s lap(s) of %d round(s)), slowest " \
+                     "rank's clock" % (len(tuning), tune_k, args.tune_laps, phases)
         else:
             comms, batch = choices[0]
             reason = "single candidate" if len(choices) == 1 else "no tuning laps (--tune-laps 0): first candidate"
@@ -565,25 +582,24 @@ def main(argv=None) -> int:
                 del sessions[c]
 
         # ---- the headline driver: W warmup steps, poison, K timed steps -------
-        state["section"] = "headline"
-        phases = len(nat.schedule(mode, "bi", n))
+        self.state["section"] = "headline"
         drv = nat.StepDriver(sess, mode, "bi", size, args.msgs, not args.no_verify, bool(batch), bool(args.graph),
                              depth=pick_depth(args.steps, phases), recv_budget=budget, salt=1)
         drv.connect()
         drv.run_steps(0, args.warmup)
         drv.sync()
         drv.poison()  # untimed: every receive slot zeroed; a slot passes verification only if a timed step wrote it
-        gpu_sync()
+        self.gpu_sync()
         drv.reset()
 
-        barrier()
-        gpu_sync()
-        barrier()
+        self.barrier()
+        self.gpu_sync()
+        self.barrier()
         t0 = time.perf_counter()
         drv.run_steps(args.warmup, args.steps)
         drv.sync()
-        gpu_sync()
-        barrier()
+        self.gpu_sync()
+        self.barrier()
         t1 = time.perf_counter()
         elapsed = sess.allreduce_max(t1 - t0)
 
@@ -601,335 +617,313 @@ def main(argv=None) -> int:
             all_ms = [my_ms]
         matrix, samples, cells = cell_matrix(n, steps, drv.phase_flows, all_ms, size * args.msgs)
         offdiag = [matrix[s][d] for (s, d) in cells if s != d or n == 1]
-        expected = n * (n - 1) if n > 1 else 1
 
         vr = drv.verify_steps(args.warmup, args.steps) if not args.no_verify else None
-        mismatches = vr["mismatches"] if vr else -1
         depth, recv_bytes = drv.depth, drv.recv_bytes
-        # Everything below is untimed; release the timed driver's buffers first so
-        # the comparisons run on the same memory footprint as the timed steps did.
+        # Everything after this is untimed; release the timed driver's buffers
+        # first so the comparisons run on the same memory footprint as the
+        # timed steps did.
         del drv
-        return dict(sess=sess, ref_sess=ref_sess, sessions=sessions, provenance=provenance, comms=comms, batch=batch,
-                    failed=failed, reason=reason, tuning=tuning, elapsed=elapsed, steps=steps,
-                    flows_total=flows_total, value=value, aggregate=aggregate, my_ms=my_ms, matrix=matrix,
-                    samples=samples, cells=cells, offdiag=offdiag, expected=expected, vr=vr, mismatches=mismatches,
-                    depth=depth, recv_bytes=recv_bytes)
+        return types.SimpleNamespace(
+            sess=sess, ref_sess=ref_sess, sessions=sessions, provenance=provenance, comms=comms, batch=batch,
+            failed=failed, reason=reason, tuning=tuning, elapsed=elapsed, flows_total=flows_total, value=value,
+            aggregate=aggregate, my_ms=my_ms, matrix=matrix, samples=samples, cells=cells, offdiag=offdiag,
+            expected=n * (n - 1) if n > 1 else 1, vr=vr, mismatches=vr["mismatches"] if vr else -1, depth=depth,
+            recv_bytes=recv_bytes)
 
-    # The headline.  Should RCCL itself fail on this node (communicator setup,
-    # a peer connection, a stalled transfer: every wait is bounded by --timeout
-    # and aborts the communicators), the same steps run through the
-    # hand-written IPC data plane instead and the line says so
-    # (headline_fallback); with --fallback 0, or if that fails too, the line
-    # carries the error and value null.
-    fallback = None
-    transport_used = args.transport
-    err = None
-    try:
-        h = measure(args.transport)
-    except Exception as e:  # noqa: BLE001 -- reported in the JSON line
-        err = str(e)[:300]
-    # Outside the except block the failed attempt's frames are released, and
-    # with them its sessions (aborted communicators, their streams, buffers).
-    if err is not None:
+    def headline(self):
+        """Measures the headline; should RCCL itself fail on this node
+        (communicator setup, a peer connection, a stalled transfer: every wait
+        is bounded by --timeout and aborts the communicators), the same steps
+        run through the hand-written IPC data plane instead and the line says
+        so (headline_fallback).  With --fallback 0, or if that fails too, the
+        line carries the error and value null; returns that exit status."""
+        args = self.args
+        err = None
+        try:
+            self.h = self.measure(args.transport)
+        except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+            err = str(e)[:300]
+        # Outside the except block the failed attempt's frames are released, and
+        # with them its sessions (aborted communicators, their streams, buffers).
+        if err is None:
+            return None
         log("bench: headline through %s failed: %s" % (args.transport, err))
         # The failure is collective (a communicator that cannot be set up or a
         # stalled transfer times out on every rank): all ranks meet here first.
-        agree(False)
+        self.agree(False)
         to = args.fallback_to
         if not (args.fallback and args.transport in ("rccl", "host") and to != args.transport
-                and (use_gpu or to in ("host", "shm"))):
-            reporter.emit(error="headline failed: " + err, transport=args.transport)
+                and (self.use_gpu or to in ("host", "shm"))):
+            self.reporter.emit(error="headline failed: " + err, transport=args.transport)
             return 5
-        fallback = {"from": args.transport, "to": to, "error": err}
-        transport_used = to
-        state["section"] = "fallback"
+        self.fallback = {"from": args.transport, "to": to, "error": err}
+        self.transport_used = to
+        self.state["section"] = "fallback"
         err2 = None
         try:
-            h = measure(to)
+            self.h = self.measure(to)
         except Exception as e2:  # noqa: BLE001
             err2 = str(e2)[:300]
-        if err2 is not None:
-            log("bench: fallback headline failed: %s" % err2)
-            reporter.emit(error="headline failed: %s; fallback through %s failed: %s" % (err, to, err2),
-                          transport=args.transport, headline_fallback=fallback)
-            return 5
-    (sess, ref_sess, sessions, provenance, comms, batch, failed, reason, tuning, elapsed, steps, flows_total, value,
-     aggregate, my_ms, matrix, samples, cells, offdiag, expected, vr, mismatches, depth, recv_bytes) = (
-        h.pop(k) for k in ("sess", "ref_sess", "sessions", "provenance", "comms", "batch", "failed", "reason",
-                           "tuning", "elapsed", "steps", "flows_total", "value", "aggregate", "my_ms", "matrix",
-                           "samples", "cells", "offdiag", "expected", "vr", "mismatches", "depth", "recv_bytes"))
-    del h  # the sessions are closed by the del before the comparisons below; nothing else may hold them
+        if err2 is None:
+            return None
+        log("bench: fallback headline failed: %s" % err2)
+        self.reporter.emit(error="headline failed: %s; fallback through %s failed: %s" % (err, to, err2),
+                           transport=args.transport, headline_fallback=self.fallback)
+        return 5
 
-    step_ms_med = statistics.median(my_ms) if my_ms else 0.0
-    headline_transport = sess.transport
-    lat_matrix = [[0.0] * n for _ in range(n)]
-    reporter.result = {
-        "metric": METRIC,
-        "value": round(value, 3),
-        "unit": "GB/s",
-        "n_gpus": n,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
-        "dtype": "uint8",
-        "data": "synthetic (device PRNG-filled payloads, one stream per message; every timed delivery verified on "
-                "the device after timing)",
-        "config": {
-            "model": "p2p_matrix: %s %s, %s x %d msgs/step"
-                     % ("RCCL ncclSend/ncclRecv" if headline_transport == "rccl" else headline_transport + " transport",
-                        "self send/recv (uni)" if mode == "self" else mode + " bidirectional",
-                        nat.format_size(size), args.msgs),
-            "global_batch": args.msgs * n,
-            "seq_len": size,
-            "parallelism": "p2p%d" % n,
-        },
-        "value_definition": "mean cell of the GB/s matrix: all flows' bytes / slowest rank's barrier-bracketed wall "
-                            "time / mean flows per step (per direction, 1 GB = 1e9 B)",
-        "aggregate_gbs": round(aggregate, 3),
-        "flows_per_step": round(flows_total / args.steps, 3),
-        "matrix_gbs_min": round(min(offdiag), 3) if offdiag else None,
-        "matrix_gbs_mean": round(statistics.mean(offdiag), 3) if offdiag else None,
-        "matrix_cells": "%d/%d" % (len(cells), expected),
-        # BASELINE config 3: the full N x N pairwise matrices (row = sender;
-        # GB/s per direction, median over steps, a cell's time = the longer of
-        # its endpoints'; p50 one-way latency, us).
-        "matrix_gbs": [[round(v, 2) for v in row] for row in matrix],
-        "matrix_samples": samples,
-        "latency_p50_us_matrix": lat_matrix,
-        "p50_latency_us": None,
-        "p50_latency_preposted_us": None,
-        "latency_preposted_p50_us_matrix": None,
-        "latency_bytes": nat.parse_size(args.latency_size),
-        "per_gpu_gbs": round(aggregate / n, 3),
-        "rank0_step_ms_p50": round(step_ms_med, 4),
-        "verify_mismatches": mismatches,
-        "verify_coverage": (round(vr["verified_msgs"] / vr["timed_msgs"], 4) if vr and vr["timed_msgs"] else None),
-        "verify_detail": vr,
-        "recv_slot_generations": depth,
-        "recv_slot_bytes_per_rank": recv_bytes,
-        "transport": headline_transport,
-        "posting": {"batch": bool(batch), "graph": bool(args.graph), "rccl_comms": comms, "dropped": failed or None,
-                    "selection": reason,
-                    "tuning_ms_per_step": {"comms%d_%s" % (c, "batch" if b else "per_message"): round(v * 1e3, 4)
-                                           for (c, b), v in tuning.items()} or None},
-        "provenance": provenance,
-        "reference_semantics": None,
-        "extras": None,
-        "ipc_transport": None,
-        "untimed_skipped": None,
-        "headline_fallback": fallback,
-        "note": ("n_gpus=1 has no inter-GPU link: value is RCCL's on-GPU self send/recv copy (HBM-bound), the "
-                 "diagonal the reference prints as 0.00. From n_gpus=2 every step is one tournament round of disjoint "
-                 "pairs, each pair on its own xGMI link; value is the mean per-link, per-direction cell rate and "
-                 "aggregate_gbs the whole fabric")
-                if n == 1 else
-                ("each step is one tournament round: %d disjoint pairs exchange in both directions, one xGMI link "
-                 "per pair; value = mean cell (per link and direction), aggregate_gbs = all pairs together" % (n // 2)),
-    }
-    if env.rank == 0:
-        log("bench: value %.2f GB/s per cell (aggregate %.2f GB/s), %.4f ms/step, verify %s" % (
-            value, aggregate, elapsed / args.steps * 1e3, vr))
+    def base_result(self) -> dict:
+        """The JSON line as far as the timed steps go; the untimed sections
+        fill in the rest (Reporter.update)."""
+        args, h, n, nat = self.args, self.h, self.n, self.nat
+        headline_transport = h.sess.transport
+        vr = h.vr
+        return {
+            "metric": METRIC,
+            "value": round(h.value, 3),
+            "unit": "GB/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(h.elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (round(h.value / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
+            "dtype": "uint8",
+            "data": "synthetic (device PRNG-filled payloads, one stream per message; every timed delivery verified "
+                    "on the device after timing)",
+            "config": {
+                "model": "p2p_matrix: %s %s, %s x %d msgs/step"
+                         % ("RCCL ncclSend/ncclRecv" if headline_transport == "rccl"
+                            else headline_transport + " transport",
+                            "self send/recv (uni)" if self.mode == "self" else self.mode + " bidirectional",
+                            nat.format_size(self.size), args.msgs),
+                "global_batch": args.msgs * n,
+                "seq_len": self.size,
+                "parallelism": "p2p%d" % n,
+            },
+            "value_definition": "mean cell of the GB/s matrix: all flows' bytes / slowest rank's barrier-bracketed "
+                                "wall time / mean flows per step (per direction, 1 GB = 1e9 B)",
+            "aggregate_gbs": round(h.aggregate, 3),
+            "flows_per_step": round(h.flows_total / args.steps, 3),
+            "matrix_gbs_min": round(min(h.offdiag), 3) if h.offdiag else None,
+            "matrix_gbs_mean": round(statistics.mean(h.offdiag), 3) if h.offdiag else None,
+            "matrix_cells": "%d/%d" % (len(h.cells), h.expected),
+            # BASELINE config 3: the full N x N pairwise matrices (row = sender;
+            # GB/s per direction, median over steps, a cell's time = the longer
+            # of its endpoints'; p50 one-way latency, us).
+            "matrix_gbs": [[round(v, 2) for v in row] for row in h.matrix],
+            "matrix_samples": h.samples,
+            "latency_p50_us_matrix": [[0.0] * n for _ in range(n)],
+            "p50_latency_us": None,
+            "p50_latency_preposted_us": None,
+            "latency_preposted_p50_us_matrix": None,
+            "latency_bytes": nat.parse_size(args.latency_size),
+            "per_gpu_gbs": round(h.aggregate / n, 3),
+            "rank0_step_ms_p50": round(statistics.median(h.my_ms) if h.my_ms else 0.0, 4),
+            "verify_mismatches": h.mismatches,
+            "verify_coverage": (round(vr["verified_msgs"] / vr["timed_msgs"], 4) if vr and vr["timed_msgs"] else None),
+            "verify_detail": vr,
+            "recv_slot_generations": h.depth,
+            "recv_slot_bytes_per_rank": h.recv_bytes,
+            "transport": headline_transport,
+            "posting": {"batch": bool(h.batch), "graph": bool(args.graph), "rccl_comms": h.comms,
+                        "dropped": h.failed or None, "selection": h.reason,
+                        "tuning_ms_per_step": {"comms%d_%s" % (c, "batch" if b else "per_message"): round(v * 1e3, 4)
+                                               for (c, b), v in h.tuning.items()} or None},
+            "provenance": h.provenance,
+            "reference_semantics": None,
+            "extras": None,
+            "ipc_transport": None,
+            "untimed_skipped": None,
+            "headline_fallback": self.fallback,
+            "note": ("n_gpus=1 has no inter-GPU link: value is RCCL's on-GPU self send/recv copy (HBM-bound), the "
+                     "diagonal the reference prints as 0.00. From n_gpus=2 every step is one tournament round of "
+                     "disjoint pairs, each pair on its own xGMI link; value is the mean per-link, per-direction cell "
+                     "rate and aggregate_gbs the whole fabric")
+                    if n == 1 else
+                    ("each step is one tournament round: %d disjoint pairs exchange in both directions, one xGMI link "
+                     "per pair; value = mean cell (per link and direction), aggregate_gbs = all pairs together"
+                     % (n // 2)),
+        }
 
     # ---- untimed sections: one deadline, waits shortened to the time left --
-    untimed_t0 = time.monotonic()
-    skipped, errors = state["skipped"], state["errors"]
-    live = [s for s in {id(x): x for x in (sess, ref_sess) if x is not None}.values()]
+    def budget_left(self) -> float:
+        return min(self.args.untimed_budget - (time.monotonic() - self.untimed_t0), self.deadline.left() - RESERVE_S)
 
-    def budget_left():
-        return min(args.untimed_budget - (time.monotonic() - untimed_t0), deadline.left() - RESERVE_S)
-
-    def section(name, fn, min_s=2.0, budgeted=True):
+    def section(self, name, fn, min_s=2.0, budgeted=True):
         """Runs one untimed section if every rank has time for it, with every
         wait of the live sessions bounded by the time left; an error is logged
         and returned in its place ({"error": ...}).  budgeted=False: only the
         deadline counts, not --untimed-budget (the headline's own latency)."""
-        left = budget_left() if budgeted else deadline.left() - RESERVE_S
-        if not agree(left > min_s):
-            skipped.append(name)
-            if env.rank == 0:
-                log("bench: no time left; skipping %s" % name)
+        left = self.budget_left() if budgeted else self.deadline.left() - RESERVE_S
+        if not self.agree(left > min_s):
+            self.state["skipped"].append(name)
+            self.log0("bench: no time left; skipping %s" % name)
             return None
-        for s in live:
-            s.set_timeout(max(1.0, min(args.timeout, left)))
-        state["section"] = name
-        if hang_requested(name, env.rank):
-            log("bench: injected hang in %s on rank %d" % (name, env.rank))
+        for s in self.live:
+            s.set_timeout(max(1.0, min(self.args.timeout, left)))
+        self.state["section"] = name
+        if hang_requested(name, self.env.rank):
+            log("bench: injected hang in %s on rank %d" % (name, self.env.rank))
             while True:
                 time.sleep(1)
         try:
             return fn()
         except Exception as e:  # noqa: BLE001 -- reported in the JSON
             log("bench: %s failed: %s" % (name, e))
-            errors[name] = str(e)[:300]
+            self.state["errors"][name] = str(e)[:300]
             return {"error": str(e)[:300]}
         finally:
-            state["section"] = None
+            self.state["section"] = None
 
-    def latency():
-        lat = json.loads(sess.latency(nat.parse_size(args.latency_size), args.latency_iters,
-                                      min(50, args.latency_iters)))
-        for p in lat["pairs"]:  # a < b; the ping-pong's one-way time holds for both directions
-            lat_matrix[p["a"]][p["b"]] = lat_matrix[p["b"]][p["a"]] = round(p["one_way_us"]["p50"], 3)
-        p50s = [p["one_way_us"]["p50"] for p in lat["pairs"]]
-        return float(statistics.median(p50s)) if p50s else None
+    def latency_sections(self):
+        """Host-posted ping-pong through the headline session, then the same
+        pre-posted: batches of exchanges wait behind a stream gate on every
+        rank and run back to back once all are posted, so those samples are
+        the operation's GPU-timeline latency without the host's posting rate."""
+        args, n, sess = self.args, self.n, self.h.sess
+        nbytes = self.nat.parse_size(args.latency_size)
 
-    p50 = section("latency", latency, budgeted=False)
-    reporter.update(p50_latency_us=round(float(p50), 3) if isinstance(p50, (int, float)) else None,
-                    latency_p50_us_matrix=lat_matrix)
+        def ping(preposted):
+            m = [[0.0] * n for _ in range(n)]
+            lat = json.loads(sess.latency(nbytes, args.latency_iters, min(50, args.latency_iters), preposted))
+            for p in lat["pairs"]:  # a < b; the ping-pong's one-way time holds for both directions
+                m[p["a"]][p["b"]] = m[p["b"]][p["a"]] = round(p["one_way_us"]["p50"], 3)
+            p50s = [p["one_way_us"]["p50"] for p in lat["pairs"]]
+            return {"p50": float(statistics.median(p50s)) if p50s else None, "matrix": m, "method": lat["method"]}
 
-    # The same ping-pong pre-posted: batches of exchanges wait behind a stream
-    # gate on every rank and run back to back once all are posted, so the
-    # samples are the operation's GPU-timeline latency without the host's
-    # posting rate (which the host-posted number above includes, and which
-    # varies from host to host).
-    pre_matrix = [[0.0] * n for _ in range(n)]
+        r = self.section("latency", lambda: ping(0), budgeted=False)
+        if isinstance(r, dict) and r.get("p50") is not None:
+            self.reporter.update(p50_latency_us=round(r["p50"], 3), latency_p50_us_matrix=r["matrix"])
+        if args.latency_preposted > 0:
+            r = self.section("latency_preposted", lambda: ping(args.latency_preposted), budgeted=False)
+            if isinstance(r, dict) and r.get("p50") is not None and r.get("method") == "preposted":
+                self.reporter.update(p50_latency_preposted_us=round(r["p50"], 3),
+                                     latency_preposted_p50_us_matrix=r["matrix"])
 
-    def latency_preposted():
-        lat = json.loads(sess.latency(nat.parse_size(args.latency_size), args.latency_iters,
-                                      min(50, args.latency_iters), args.latency_preposted))
-        for p in lat["pairs"]:
-            pre_matrix[p["a"]][p["b"]] = pre_matrix[p["b"]][p["a"]] = round(p["one_way_us"]["p50"], 3)
-        p50s = [p["one_way_us"]["p50"] for p in lat["pairs"]]
-        return {"p50": float(statistics.median(p50s)) if p50s else None, "method": lat["method"]}
+    def reference_section(self):
+        """The reference's own methodology on one communicator (serial ordered
+        pairs, host clock, one stream sync per message, no warmup,
+        p2p_matrix.cc:141-186), at the same message size.  With one GPU the
+        reference prints only the diagonal; its methodology is then applied to
+        the self cell, so the ratio still compares the two methods."""
+        args, n, h = self.args, self.n, self.h
 
-    if args.latency_preposted > 0:
-        pre = section("latency_preposted", latency_preposted, budgeted=False)
-        if isinstance(pre, dict) and pre.get("p50") is not None and pre.get("method") == "preposted":
-            reporter.update(p50_latency_preposted_us=round(pre["p50"], 3), latency_preposted_p50_us_matrix=pre_matrix)
+        def reference_semantics():
+            r = json.loads((h.ref_sess or h.sess).run(mode="pair" if n > 1 else "self", dir="uni", bytes=self.size,
+                                                      iters=args.ref_iters, warmup=0, timing="wallclock",
+                                                      verify=False, warm=False))
+            fl = [f["gbs"] for ph in r["phases"] for f in ph["flows"] if f["src"] != f["dst"] or n == 1]
+            mean = statistics.mean(fl) if fl else 0.0
+            return {"cell_gbs_min": round(min(fl), 3) if fl else None, "cell_gbs_mean": round(mean, 3),
+                    "iters": args.ref_iters, "size": self.size,
+                    "method": "reference semantics: serial ordered pairs, wall clock, stream sync per message, no "
+                              "warmup" + ("" if n > 1 else " (applied to the self cell)"),
+                    # Both are per-cell rates: ours from the pipelined timed
+                    # steps, the reference's from its serial cells.
+                    "value_ratio": round(h.value / mean, 3) if mean > 0 else None}
 
-    # The reference's own methodology on one communicator, for comparison
-    # (serial ordered pairs, host clock, one stream sync per message, no
-    # warmup, p2p_matrix.cc:141-186), at the same message size.  With one GPU
-    # the reference prints only the diagonal; its methodology is then applied
-    # to the self cell, so the ratio still compares the two methods.
-    def reference_semantics():
-        r = json.loads((ref_sess or sess).run(mode="pair" if n > 1 else "self", dir="uni", bytes=size,
-                                              iters=args.ref_iters, warmup=0, timing="wallclock", verify=False,
-                                              warm=False))
-        fl = [f["gbs"] for ph in r["phases"] for f in ph["flows"] if f["src"] != f["dst"] or n == 1]
-        mean = statistics.mean(fl) if fl else 0.0
-        return {"cell_gbs_min": round(min(fl), 3) if fl else None, "cell_gbs_mean": round(mean, 3),
-                "iters": args.ref_iters, "size": size,
-                "method": "reference semantics: serial ordered pairs, wall clock, stream sync per message, no warmup"
-                          + ("" if n > 1 else " (applied to the self cell)"),
-                # Both are per-cell rates: ours from the pipelined timed
-                # steps, the reference's from its serial cells.
-                "value_ratio": round(value / mean, 3) if mean > 0 else None}
+        if args.ref_iters > 0:
+            self.log0("bench: reference-semantics matrix")
+            self.reporter.update(reference_semantics=self.section("reference_semantics", reference_semantics, 5.0))
 
-    if args.ref_iters > 0:
-        if env.rank == 0:
-            log("bench: reference-semantics matrix")
-        reporter.update(reference_semantics=section("reference_semantics", reference_semantics, 5.0))
+    def extras_sections(self):
+        """The other BASELINE.json configs, measured after the timed region so
+        one driver run records them too: all-pairs concurrent exchange at 1 GiB
+        (bisection: every GPU drives all N-1 xGMI links at once), the ring
+        neighbour exchange at 256 MiB, the pipeline-parallel hop latency as a
+        dependent token chain 0 -> 1 -> ... -> N-1 -> 0, and the single-pair
+        (0 -> 1) bandwidth sweep 4 KiB -> 4 GiB (config 2; only cell (0, 1) is
+        scheduled, the other ranks just join the barriers)."""
+        args, n, nat, h = self.args, self.n, self.nat, self.h
+        if n == 1:
+            return
 
-    # The other BASELINE.json configs, measured after the timed region so one
-    # driver run records them too: all-pairs concurrent exchange at 1 GiB
-    # (bisection: every GPU drives all N-1 xGMI links at once), the ring
-    # neighbour exchange at 256 MiB, and the pipeline-parallel hop latency as
-    # a dependent token chain 0 -> 1 -> ... -> N-1 -> 0.
-    def concurrent_config(mode_x, dir_x, nbytes, iters):
-        r = json.loads(sess.run(mode=mode_x, dir=dir_x, bytes=nbytes, iters=iters, warmup=1, timing="events",
-                                verify=not args.no_verify, warm=True))
-        ph = r["phases"][0]
-        flows = [f["gbs"] for f in ph["flows"]]
-        p50s = [f["iter_us"]["p50"] for f in ph["flows"]]
-        return {"aggregate_gbs": round(ph["agg_gbs"], 2), "per_gpu_egress_gbs": round(ph["agg_gbs"] / n, 2),
-                "flow_gbs_min": round(min(flows), 2), "flow_gbs_mean": round(statistics.mean(flows), 2),
-                "iter_us_p50": round(statistics.median(p50s), 1), "bytes": nbytes, "iters": iters,
-                "mismatches": ph["mismatches"]}
+        def concurrent_config(mode_x, dir_x, nbytes, iters):
+            r = json.loads(h.sess.run(mode=mode_x, dir=dir_x, bytes=nbytes, iters=iters, warmup=1, timing="events",
+                                      verify=not args.no_verify, warm=True))
+            ph = r["phases"][0]
+            flows = [f["gbs"] for f in ph["flows"]]
+            p50s = [f["iter_us"]["p50"] for f in ph["flows"]]
+            return {"aggregate_gbs": round(ph["agg_gbs"], 2), "per_gpu_egress_gbs": round(ph["agg_gbs"] / n, 2),
+                    "flow_gbs_min": round(min(flows), 2), "flow_gbs_mean": round(statistics.mean(flows), 2),
+                    "iter_us_p50": round(statistics.median(p50s), 1), "bytes": nbytes, "iters": iters,
+                    "mismatches": ph["mismatches"]}
 
-    def ring_hop():
-        r = json.loads(sess.ring_latency(nat.parse_size(args.latency_size), 100, 10, False))
-        return {"hop_us_p50": round(r["hop_us"]["p50"], 3), "hop_us_p99": round(r["hop_us"]["p99"], 3),
-                "lap_us_p50": round(r["lap_us"]["p50"], 3), "laps": r["laps"], "bytes": r["bytes"],
-                "method": "dependent token chain 0 -> 1 -> ... -> N-1 -> 0, each hop forwards after its receive "
-                          "completed (grouped send/recv on the stream); hop = lap / N, rank 0's hipEvents"}
+        def ring_hop():
+            r = json.loads(h.sess.ring_latency(nat.parse_size(args.latency_size), 100, 10, False))
+            return {"hop_us_p50": round(r["hop_us"]["p50"], 3), "hop_us_p99": round(r["hop_us"]["p99"], 3),
+                    "lap_us_p50": round(r["lap_us"]["p50"], 3), "laps": r["laps"], "bytes": r["bytes"],
+                    "method": "dependent token chain 0 -> 1 -> ... -> N-1 -> 0, each hop forwards after its "
+                              "receive completed (grouped send/recv on the stream); hop = lap / N, rank 0's hipEvents"}
 
-    extras = None
-    if n > 1 and args.extras:
-        if env.rank == 0:
-            log("bench: all-pairs / ring extras")
-        extras = {}
-        # Keyed by the BASELINE config names; the sizes can be lowered for
-        # CPU rehearsals (all-pairs holds N - 1 receive slots per rank).
-        for name, mode_x, dir_x, nbytes, iters in (("allpairs_1g", "allpairs", "bi", nat.parse_size(args.allpairs_size), 4),
-                                                   ("ring_256m", "ring", "uni", nat.parse_size(args.ring_size), 8)):
-            v = section(name, lambda: concurrent_config(mode_x, dir_x, nbytes, iters), 5.0)
+        def pair_cell(session, nbytes, iters):
+            r = json.loads(session.run(mode="pair", dir="uni", bytes=nbytes, iters=iters, warmup=2, timing="events",
+                                       verify=not args.no_verify, warm=False, cells=[(0, 1)]))
+            fl = [f for ph in r["phases"] for f in ph["flows"]]
+            return fl[0] if fl else None
+
+        def pair_sweep():
+            sweep = []
+            for nbytes in [b for b in (4096 << (2 * k) for k in range(11)) if b <= nat.parse_size(args.sweep_max)]:
+                self.log0("bench: pair sweep %d B" % nbytes)
+                iters = max(4, min(200, (2 << 30) // nbytes))
+                f = pair_cell(h.sess, nbytes, iters)
+                if f:
+                    sweep.append({"bytes": nbytes, "iters": iters, "gbs": round(f["gbs"], 2),
+                                  "iter_us_p50": round(f["iter_us"]["p50"], 2), "mismatches": f.get("mismatches", -1)})
+            return sweep
+
+        def pair_one_comm():
+            # The same single pair on one communicator (what the sweep ran with
+            # K of them), at the bench's message size and 256 MiB.
+            return [{"bytes": nb, "gbs": round(f["gbs"], 2)}
+                    for nb in (self.size, 256 << 20) for f in [pair_cell(h.ref_sess, nb, 16)] if f]
+
+        extras = None
+        if args.extras:
+            self.log0("bench: all-pairs / ring extras")
+            extras = {}
+            # Keyed by the BASELINE config names; the sizes can be lowered for
+            # CPU rehearsals (all-pairs holds N - 1 receive slots per rank).
+            for name, mode_x, dir_x, nbytes, iters in (
+                    ("allpairs_1g", "allpairs", "bi", nat.parse_size(args.allpairs_size), 4),
+                    ("ring_256m", "ring", "uni", nat.parse_size(args.ring_size), 8)):
+                v = self.section(name, lambda: concurrent_config(mode_x, dir_x, nbytes, iters), 5.0)
+                if v is not None:
+                    extras[name] = v
+            v = self.section("ring_hop", ring_hop)
             if v is not None:
-                extras[name] = v
-        v = section("ring_hop", ring_hop)
-        if v is not None:
-            extras["ring_hop"] = v
-        reporter.update(extras=extras)
+                extras["ring_hop"] = v
+            self.reporter.update(extras=extras)
+        if args.sweep:
+            sw = self.section("pair_sweep_0_1", pair_sweep, 10.0)
+            if sw is not None:
+                extras = dict(extras or {}, pair_sweep_0_1=sw, pair_sweep_rccl_comms=h.comms)
+                if h.ref_sess is not None and h.ref_sess is not h.sess:
+                    oc = self.section("pair_0_1_one_comm", pair_one_comm)
+                    if oc is not None:
+                        extras["pair_0_1_one_comm"] = oc
+            self.reporter.update(extras=extras)
 
-    # BASELINE.json config 2: single-pair (0 -> 1) send/recv bandwidth sweep,
-    # 4 KiB -> 4 GiB in x4 steps, events-timed, uni-directional; only cell
-    # (0, 1) is scheduled, so the other ranks just join the barriers.
-    def pair_cell(session, nbytes, iters):
-        r = json.loads(session.run(mode="pair", dir="uni", bytes=nbytes, iters=iters, warmup=2, timing="events",
-                                   verify=not args.no_verify, warm=False, cells=[(0, 1)]))
-        fl = [f for ph in r["phases"] for f in ph["flows"]]
-        return fl[0] if fl else None
-
-    def pair_sweep():
-        sweep = []
-        for nbytes in [b for b in (4096 << (2 * k) for k in range(11)) if b <= nat.parse_size(args.sweep_max)]:
-            if env.rank == 0:
-                log("bench: pair sweep %d B" % nbytes)
-            iters = max(4, min(200, (2 << 30) // nbytes))
-            f = pair_cell(sess, nbytes, iters)
-            if f:
-                sweep.append({"bytes": nbytes, "iters": iters, "gbs": round(f["gbs"], 2),
-                              "iter_us_p50": round(f["iter_us"]["p50"], 2), "mismatches": f.get("mismatches", -1)})
-        return sweep
-
-    def pair_one_comm():
-        # The same single pair on one communicator (what the sweep ran with K
-        # of them), at the bench's message size and 256 MiB.
-        return [{"bytes": nb, "gbs": round(f["gbs"], 2)}
-                for nb in (size, 256 << 20) for f in [pair_cell(ref_sess, nb, 16)] if f]
-
-    if n > 1 and args.sweep:
-        sw = section("pair_sweep_0_1", pair_sweep, 10.0)
-        if sw is not None:
-            extras = dict(extras or {}, pair_sweep_0_1=sw, pair_sweep_rccl_comms=comms)
-            if ref_sess is not None and ref_sess is not sess:
-                oc = section("pair_0_1_one_comm", pair_one_comm)
-                if oc is not None:
-                    extras["pair_0_1_one_comm"] = oc
-        reporter.update(extras=extras)
-
-    # The same tournament steps through the hand-written data plane (IPC
-    # transport: one-sided pulls of hipIpc-mapped peer buffers by the gfx950
-    # copy kernel) on the same links, for comparison with RCCL.  Untimed by the
-    # contract; any error is reported in the JSON instead of failing the run.
-    # The comparisons below open sessions of their own; close the headline one
-    # first so they run alone, as the timed steps did.
-    live.clear()
-    del sess, ref_sess, sessions
-
-    # (with --transport host the same code path runs on the CPU transport, for tests)
-    extra_transport = {"rccl": "ipc", "ipc": "ipc", "ipc:push": "ipc", "ipc:relay": "ipc", "host": "host",
-                       "shm": "host"}.get(transport_used)
-
-    def isolated(transport):
+    def isolated(self, transport):
         """steps_through() for `transport` in a child process per rank.  The
-        comparisons drive the hand-written data plane (hipIpc mappings,
-        signal kernels, relays) across GPUs; if one of them faults or hangs
-        on some node, only the child dies, and the headline line still gets
-        printed with the error in its place."""
-        box = [free_port() if env.rank == 0 else None]
+        comparisons drive the hand-written data plane (hipIpc mappings, signal
+        kernels, relays) across GPUs; if one of them faults or hangs on some
+        node, only the child dies, and the headline line still gets printed
+        with the error in its place."""
+        args, n, rank = self.args, self.n, self.env.rank
+        box = [free_port() if rank == 0 else None]
         if n > 1:
             dist.broadcast_object_list(box, src=0)
-        out_path = os.path.join(tempfile.gettempdir(), "p2p_bench_child_%d_%d.json" % (box[0], env.rank))
-        limit = min(args.child_timeout, max(5.0, budget_left()))
+        out_path = os.path.join(tempfile.gettempdir(), "p2p_bench_child_%d_%d.json" % (box[0], rank))
+        limit = min(args.child_timeout, max(5.0, self.budget_left()))
         cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(n), "--steps", str(args.steps),
-               "--warmup", str(args.warmup), "--size", args.size, "--msgs", str(args.msgs), "--mode", mode,
+               "--warmup", str(args.warmup), "--size", args.size, "--msgs", str(args.msgs), "--mode", self.mode,
                "--latency-iters", str(args.latency_iters), "--latency-size", args.latency_size,
                "--child", transport, "--child-port", str(box[0]), "--child-out", out_path,
-               "--child-batch", str(int(batch)), "--timeout", str(max(5.0, min(args.timeout, limit)))]
+               "--child-batch", str(int(self.h.batch)), "--timeout", str(max(5.0, min(args.timeout, limit)))]
         if args.no_verify:
             cmd.append("--no-verify")
         if args.device is not None:
@@ -938,9 +932,9 @@ def main(argv=None) -> int:
             rc = subprocess.run(cmd, timeout=limit).returncode
         except subprocess.TimeoutExpired:
             rc = "timeout"
-        barrier()
+        self.barrier()
         res = None
-        if env.rank == 0:
+        if rank == 0:
             try:
                 with open(out_path) as f:
                     res = json.load(f)
@@ -952,15 +946,21 @@ def main(argv=None) -> int:
             pass
         return res
 
-    # The hand-written data plane on the same links: the gfx950 multi-copy
-    # kernel pulling from hipIpc-mapped peer buffers ("pull", one-sided), the
-    # rendezvous engine that writes into the receiver's slot ("push"), the
-    # SDMA copy engines pulling instead of CUs ("sdma"), and multi-path push
-    # with two-hop relays through GPUs whose links are idle ("relay").
-    # With one GPU the same engines run the self step (the GPU copies to
-    # itself through its own mapping), next to RCCL's self copy.
-    ipc = None
-    if args.ipc_extra and extra_transport:
+    def comparisons(self):
+        """The same tournament steps through the hand-written data plane on
+        the same links, untimed by the contract: the gfx950 multi-copy kernel
+        pulling from hipIpc-mapped peer buffers ("pull", one-sided), the
+        rendezvous engine that writes into the receiver's slot ("push"), the
+        SDMA copy engines pulling instead of CUs ("sdma"), and multi-path push
+        with two-hop relays through GPUs whose links are idle ("relay").  With
+        one GPU the same engines run the self step (the GPU copies to itself
+        through its own mapping), next to RCCL's self copy.  (With --transport
+        host the same code path runs on the CPU transport, for tests.)"""
+        args, n = self.args, self.n
+        extra_transport = {"rccl": "ipc", "ipc": "ipc", "ipc:push": "ipc", "ipc:relay": "ipc", "host": "host",
+                           "shm": "host"}.get(self.transport_used)
+        if not (args.ipc_extra and extra_transport):
+            return
         runs = [(extra_transport, None)]
         if extra_transport == "ipc":
             runs += [("ipc:push", "push"), ("ipc:sdma", "sdma")] + ([("ipc:relay", "relay")] if n > 2 else [])
@@ -971,21 +971,23 @@ def main(argv=None) -> int:
                    "ipc:sdma": "one-sided pull by the SDMA copy engines (hipMemcpyAsync per receive)",
                    "ipc:relay": "push over the direct link + two-hop stripes relayed through GPUs whose links are "
                                 "idle (routing.hpp)"}
+        value, batch = self.h.value, self.h.batch
 
         def compare(transport):
             if args.isolate:
-                return isolated(transport)
-            isess = create_session(transport, device=device, timeout_s=min(90.0, max(5.0, budget_left())))
+                return self.isolated(transport)
+            isess = self.create_session(transport, device=self.device,
+                                        timeout_s=min(90.0, max(5.0, self.budget_left())))
             try:
-                return steps_through(nat, isess, args, mode, size, batch, transport)
+                return steps_through(self.nat, isess, args, self.mode, self.size, batch, transport)
             finally:
                 del isess
 
+        ipc = None
         for transport, key in runs:
-            if env.rank == 0:
-                log("bench: %s comparison" % transport)
-            r = section(transport, lambda: compare(transport), 20.0)
-            if r is None or env.rank != 0:
+            self.log0("bench: %s comparison" % transport)
+            r = self.section(transport, lambda: compare(transport), 20.0)
+            if r is None or self.env.rank != 0:
                 continue
             if transport in engines:
                 r["engine"] = engines[transport]
@@ -995,20 +997,48 @@ def main(argv=None) -> int:
                 ipc = dict(r, **(ipc or {}))
             else:
                 ipc = dict(ipc or {}, **{key: r})
-            reporter.update(ipc_transport=ipc)
+            self.reporter.update(ipc_transport=ipc)
 
-    reporter.update(untimed_skipped=skipped or None, section_errors=errors or None)
-    if env.rank == 0:
-        log("bench: GB/s matrix (row=src, col=dst), median over steps:")
-        for r in range(n):
-            log("  " + " ".join("%8.2f" % matrix[r][c] for c in range(n)))
-    reporter.emit()
-    # The watchdog stays armed: should the teardown below hang, it ends the
-    # process at the deadline (the line is out already, so it exits 0).
-    barrier()
-    if n > 1 and dist.is_initialized():
-        dist.destroy_process_group()
-    return 0 if mismatches in (0, -1) else 3
+    def run(self) -> int:
+        rc = self.headline()
+        if rc is not None:
+            return rc
+        h = self.h
+        self.reporter.result = self.base_result()
+        self.log0("bench: value %.2f GB/s per cell (aggregate %.2f GB/s), %.4f ms/step, verify %s" % (
+            h.value, h.aggregate, h.elapsed / self.args.steps * 1e3, h.vr))
+
+        self.untimed_t0 = time.monotonic()
+        self.live = list({id(x): x for x in (h.sess, h.ref_sess) if x is not None}.values())
+        self.latency_sections()
+        self.reference_section()
+        self.extras_sections()
+        # The comparisons open sessions of their own; close the headline's
+        # first so they run alone, as the timed steps did.
+        self.live.clear()
+        h.sess = h.ref_sess = h.sessions = None
+        self.comparisons()
+
+        self.reporter.update(untimed_skipped=self.state["skipped"] or None,
+                             section_errors=self.state["errors"] or None)
+        if self.env.rank == 0:
+            log("bench: GB/s matrix (row=src, col=dst), median over steps:")
+            for r in range(self.n):
+                log("  " + " ".join("%8.2f" % h.matrix[r][c] for c in range(self.n)))
+        self.reporter.emit()
+        # The watchdog stays armed: should the teardown below hang, it ends the
+        # process at the deadline (the line is out already, so it exits 0).
+        self.barrier()
+        if self.n > 1 and dist.is_initialized():
+            dist.destroy_process_group()
+        return 0 if h.mismatches in (0, -1) else 3
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    if args.child:
+        return child_main(args)
+    return BenchRun(args, claim_stdout()).run()
 
 
 if __name__ == "__main__":
