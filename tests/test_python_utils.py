@@ -39,11 +39,11 @@ def test_report_cli(tmp_path, capsys):
     f = tmp_path / "result.txt"
     f.write_text(compat_matrix_text([[0, 8.0], [16.0, 0]], "uni") + compat_matrix_text([[0, 8.0], [8.0, 0]], "bi"))
     j = tmp_path / "bench.jsonl"
-    j.write_text(json.dumps({"metric": "m", "n_gpus": 2, "value": 100.0, "matrix_gbs_min": 50,
+    j.write_text(json.dumps({"metric": "m", "n_gpus": 2, "value": 50.0, "aggregate_gbs": 100.0, "matrix_gbs_min": 50,
                              "matrix_gbs_mean": 50, "p50_latency_us": 10}) + "\n")
     assert report_main([str(f), str(j)]) == 0
     out = capsys.readouterr().out
-    assert "bi: 2 ranks" in out and "| 2 | 100.0 | 50.0 |" in out
+    assert "bi: 2 ranks" in out and "| 2 | 50.0 | 100.0 | 50.0 |" in out
 
 
 def test_rccl_env_capture(monkeypatch):
