@@ -24,7 +24,7 @@ OPT       ?= -O3
 HIPFLAGS  := $(CXXSTD) $(OPT) $(WARN) -fPIC --offload-arch=$(ARCH) -Icsrc
 HOSTFLAGS := $(CXXSTD) $(OPT) $(WARN) -fPIC -Icsrc -pthread
 
-CORE      := common units stats schedule routing bootstrap transport_host transport_shm runner report provenance app
+CORE      := common units stats schedule routing bootstrap transport_host transport_shm runner step_driver report provenance app
 GPU_OBJS  := $(addprefix $(BUILD)/gpu/,$(addsuffix .o,$(CORE) transport_rccl transport_ipc topology stream_gate) kernels.o pingpong.o)
 HOST_OBJS := $(addprefix $(BUILD)/host/,$(addsuffix .o,$(CORE) transport_rccl_stub))
 
