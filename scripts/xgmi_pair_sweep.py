@@ -95,6 +95,8 @@ def parse_args(argv=None):
                     "start after it is spent are listed as skipped")
     ap.add_argument("--row-timeout", type=float, default=180.0)
     ap.add_argument("--dry-run", action="store_true", help="print the rows and exit")
+    ap.add_argument("--resume", action="store_true",
+                    help="keep the rows already in <out>/rows.jsonl (a killed sweep continues where it stopped)")
     return ap.parse_args(argv)
 
 
@@ -229,8 +231,26 @@ def main(argv=None) -> int:
     os.makedirs(args.out, exist_ok=True)
     t_end = time.time() + args.budget
     done, skipped, failed, corrupt = [], [], None, []
-    with open(os.path.join(args.out, "rows.jsonl"), "w") as f:
+    rows_path = os.path.join(args.out, "rows.jsonl")
+    kept = {}
+    if args.resume and os.path.exists(rows_path):
+        # Rows that finished (clean or corrupt) are kept; a row that crashed
+        # or timed out runs again.
+        for line in open(rows_path):
+            rec = json.loads(line)
+            if rec.get("rc") in (0, 2):
+                kept[rec["name"]] = rec
+    with open(rows_path, "w") as f:
+        for rec in kept.values():
+            f.write(json.dumps(rec) + "\n")
         for i, row in enumerate(rows):
+            if row["name"] in kept:
+                rec = kept[row["name"]]
+                done.append(rec)
+                if rec["rc"] == 2:
+                    corrupt.append(rec["name"])
+                print("%-40s kept from the previous run (rc=%d)" % (rec["name"], rec["rc"]), flush=True)
+                continue
             if failed is not None or time.time() + 5 > t_end:
                 skipped.append(row["name"])
                 continue

@@ -65,3 +65,16 @@ def test_node_run_dry_run_and_refusal():
     assert "-n 8 ./p2p_matrix" in out.stdout
     out = subprocess.run(["bash", script, "/tmp/p2p_node_real"], capture_output=True, text=True, timeout=120)
     assert out.returncode == 1 and "needs >= 2 visible GPUs" in out.stderr
+
+
+@pytest.mark.mpi
+def test_pair_sweep_resume_keeps_finished_rows(mpirun, host_build, tmp_path):
+    args = [sys.executable, SWEEP, "--np", "2", "--emulate", "host", "--sizes", "64K", "--out", str(tmp_path)]
+    first = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    assert first.returncode == 0, first.stderr + first.stdout
+    again = subprocess.run(args + ["--resume"], capture_output=True, text=True, timeout=300)
+    assert again.returncode == 0, again.stderr + again.stdout
+    assert "kept from the previous run" in again.stdout
+    rows = [json.loads(l) for l in (tmp_path / "rows.jsonl").read_text().splitlines()]
+    assert [r["name"] for r in rows] == ["host"]
+    assert json.loads((tmp_path / "summary.json").read_text())["rows_run"] == 1
