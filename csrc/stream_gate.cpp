@@ -39,6 +39,7 @@ bool StreamGate::timed_out() {
   if (!status_) return false;
   unsigned int st = 0;
   HIPCHECK(hipMemcpy(&st, status_, sizeof(st), hipMemcpyDeviceToHost));
+  if (st & 1u) HIPCHECK(hipMemset(status_, 0, sizeof(st)));  // report each expiry once
   return (st & 1u) != 0;
 }
 

@@ -17,7 +17,7 @@ class StreamGate {
   ~StreamGate();
   void arm(hipStream_t stream, double timeout_s);  // enqueue the gate kernel
   void release();                                  // let every armed gate pass
-  bool timed_out();                                // blocking: did any gate expire?
+  bool timed_out();  // blocking: did a gate expire since the last call?
 
  private:
   unsigned long long* flag_ = nullptr;  // host-pinned, written by the host only
