@@ -122,6 +122,19 @@ class Session {
     return "";
   }
 
+  // Test hook for the stream gate: arm one, release it or not, wait for the
+  // stream.  An unreleased gate must open by itself at its deadline.
+  std::string gate_probe(double timeout_s, bool release) {
+    const double t0 = now_seconds();
+    if (!t_->gate_arm(timeout_s)) return "{\"supported\":false}";
+    if (release) t_->gate_release();
+    t_->sync();
+    const double waited = now_seconds() - t0;
+    const bool expired = t_->gate_timed_out();
+    if (!release) t_->gate_release();  // keep the sequence consistent for later gates
+    return strfmt("{\"supported\":true,\"timed_out\":%s,\"seconds\":%.4f}", expired ? "true" : "false", waited);
+  }
+
   std::string device_latency(size_t bytes, int iters, int warmup) {
     return latency_to_json(run_device_latency(*t_, *boot_, bytes, iters, warmup), world());
   }
@@ -245,6 +258,8 @@ PYBIND11_MODULE(_p2pcore, m) {
       .def("run", &Session::run, py::arg("mode") = "pair", py::arg("dir") = "uni", py::arg("bytes") = 32u << 20,
            py::arg("iters") = 128, py::arg("warmup") = 8, py::arg("timing") = "events", py::arg("verify") = false,
            py::arg("warm") = true, py::arg("cells") = std::vector<std::pair<int, int>>{}, py::call_guard<py::gil_scoped_release>())
+      .def("gate_probe", &Session::gate_probe, py::arg("timeout_s") = 0.2, py::arg("release") = true,
+           py::call_guard<py::gil_scoped_release>())
       .def("device_latency", &Session::device_latency, py::arg("bytes") = 8, py::arg("iters") = 1000,
            py::arg("warmup") = 100, py::call_guard<py::gil_scoped_release>())
       .def("latency", &Session::latency, py::arg("bytes") = 8, py::arg("iters") = 1000, py::arg("warmup") = 100,

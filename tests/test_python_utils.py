@@ -73,3 +73,8 @@ def test_python_module_cli(native, argv):
     out = subprocess.run([sys.executable, "-m", "test_nccl_p2p_amd"] + argv, capture_output=True, text=True,
                          cwd=ROOT, timeout=120, env=dict(os.environ, RANK="0", WORLD_SIZE="1"))
     assert out.returncode == 0, out.stderr
+
+
+def test_gate_probe_unsupported_on_cpu(native):
+    sess = native.Session(0, 1, transport="host")
+    assert json.loads(sess.gate_probe(0.1, True)) == {"supported": False}

@@ -221,3 +221,18 @@ def test_self_copy_rate_floor(native, transport, floor):
     print("%s: %.1f GB/s" % (transport, gbs))
     del d, s
     assert gbs > floor, gbs
+
+
+@pytest.mark.parametrize("transport", ["rccl", "ipc"])
+def test_stream_gate_opens_at_its_deadline(native, transport):
+    """The pre-posted latency's stream gate: released, it opens at once; never
+    released, it opens by itself at its deadline and says so (a host that
+    dies between arming and releasing cannot hold the GPU)."""
+    sess = native.Session(0, 1, device=0, transport=transport)
+    r = json.loads(sess.gate_probe(5.0, True))
+    assert r["supported"] and not r["timed_out"] and r["seconds"] < 1.0, r
+    r = json.loads(sess.gate_probe(0.3, False))
+    assert r["supported"] and r["timed_out"] and 0.25 < r["seconds"] < 5.0, r
+    r = json.loads(sess.gate_probe(5.0, True))  # the next gate works normally
+    assert not r["timed_out"] and r["seconds"] < 1.0, r
+    del sess
