@@ -305,6 +305,13 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
     *exit_code = 1;
     return false;
   }
+  // Known before any rank starts: fail at the command line, not mid-run.
+  if (cfg->device_latency && cfg->transport != "ipc") {
+    std::fprintf(stderr, "p2p_matrix: --device-latency needs a one-sided transport (--transport ipc); %s has none\n",
+                 cfg->transport.c_str());
+    *exit_code = 1;
+    return false;
+  }
   return true;
 }
 
