@@ -6,7 +6,7 @@ import sys
 
 import pytest
 
-from conftest import MPIRUN, ROOT, ensure_built
+from conftest import MPIRUN, ROOT, ensure_built, free_port
 from test_nccl_p2p_amd.utils.report import parse_compat
 
 pytestmark = pytest.mark.gpu
@@ -153,3 +153,20 @@ def test_preposted_latency(exe, tmp_path, transport):
     host, pre = recs["host"]["pairs"][0]["one_way_us"], recs["preposted"]["pairs"][0]["one_way_us"]
     assert 0 < pre["p50"] <= host["p50"] * 1.2 + 1.0, (pre, host)
     assert "pre-posted behind a stream gate" in out.stdout
+
+
+def test_bench_real_rccl_failure_falls_back():
+    """A genuine RCCL failure, not an injected one: two ranks on the one GPU
+    with no --device, so RCCL refuses the duplicate GPU at communicator init
+    on both ranks; the timed steps run through the IPC data plane instead,
+    verified, and the line names the RCCL error."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2", "--steps", "6", "--warmup", "3",
+           "--size", "4M", "--msgs", "4", "--sweep", "0", "--extras", "0", "--ref-iters", "0", "--latency-iters", "20",
+           "--ipc-extra", "0", "--timeout", "60"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    fb = r["headline_fallback"]
+    assert r["transport"] == "ipc" and fb["from"] == "rccl" and "ncclCommInitRankConfig" in fb["error"], fb
+    assert r["verify_mismatches"] == 0 and r["verify_coverage"] == 1.0 and r["matrix_cells"] == "2/2"
