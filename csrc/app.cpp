@@ -328,13 +328,14 @@ void print_schedule(FILE* out, const Schedule& s) {
 
 }  // namespace
 
-int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result) {
-  if (cfg.verbose) set_log_level(cfg.verbose);
-  const int n = boot.size(), me = boot.rank();
-  const bool root = me == 0;
+namespace {
 
-  // Schedules: (mode, dir) pairs; Self and the concurrent all-pairs exchange
-  // have no meaningful uni/bi split, so they run once.
+// Schedules: (mode, dir) pairs; Self and the concurrent all-pairs exchange
+// have no meaningful uni/bi split, so they run once.  --cells: re-measure
+// only some (src, dst) cells of the pair schedule; the others stay in the
+// schedule as idle cells (barrier, reported 0.00), so the printed matrices
+// keep their shape.
+std::vector<Schedule> build_schedules(const AppConfig& cfg, int n) {
   std::vector<Schedule> scheds;
   for (Mode m : cfg.modes) {
     if (m == Mode::Self || m == Mode::AllPairs) {
@@ -343,66 +344,37 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
     }
     for (Direction d : cfg.dirs) scheds.push_back(make_schedule(m, d, n));
   }
-  // --cells: re-measure only some (src, dst) cells of the pair schedule; the
-  // others stay in the schedule as idle cells (barrier, reported 0.00), so the
-  // printed matrices keep their shape.
   if (!cfg.cells.empty())
     for (auto& s : scheds) restrict_cells(&s, cfg.cells, false);
   for (const auto& s : scheds) {
     std::string bad = validate(s);
     P2P_CHECK(bad.empty(), "invalid schedule " + s.name() + ": " + bad);
   }
-  if (cfg.dry_run) {
-    if (root)
-      for (const auto& s : scheds) print_schedule(out, s);
-    return 0;
-  }
-  if (cfg.topology_only) {
-    if (root) std::fprintf(out, "%s", topology_report().c_str());
-    return 0;
-  }
+  return scheds;
+}
 
-  Placement pl = check_placement(boot);
-  if (!pl.ok) P2P_FATAL("process placement check failed: " + pl.error);
+std::unique_ptr<Transport> open_transport(const AppConfig& cfg, Bootstrap& boot, const Placement& pl,
+                                          TransportOptions* topt) {
+  topt->device = cfg.device >= 0 ? cfg.device : pl.local_rank;
+  topt->timeout_s = cfg.timeout_s;
+  topt->verify_impl = cfg.verify_impl;
+  topt->ipc_engine = cfg.ipc_engine;
+  topt->two_streams = cfg.two_streams;
+  topt->rccl_comms = cfg.comms;
+  return cfg.transport == "host"  ? make_host_transport(boot, *topt)
+         : cfg.transport == "shm" ? make_shm_transport(boot, *topt)
+         : cfg.transport == "ipc" ? make_ipc_transport(boot, *topt)
+                                  : make_rccl_transport(boot, *topt);
+}
 
-  TransportOptions topt;
-  topt.device = cfg.device >= 0 ? cfg.device : pl.local_rank;
-  topt.timeout_s = cfg.timeout_s;
-  topt.verify_impl = cfg.verify_impl;
-  topt.ipc_engine = cfg.ipc_engine;
-  topt.two_streams = cfg.two_streams;
-  topt.rccl_comms = cfg.comms;
-  std::unique_ptr<Transport> t = cfg.transport == "host"  ? make_host_transport(boot, topt)
-                                 : cfg.transport == "shm" ? make_shm_transport(boot, topt)
-                                 : cfg.transport == "ipc" ? make_ipc_transport(boot, topt)
-                                                          : make_rccl_transport(boot, topt);
-
-  // Provenance (collective): the runtime, RCCL library and knobs, every
-  // rank's GPU and the links between them -- the first line of --json.
-  const bool gpu_transport = cfg.transport == "rccl" || cfg.transport == "ipc";
-  const std::string provenance =
-      cfg.json_path.empty() ? std::string() : provenance_json(boot, gpu_transport ? topt.device : -1);
-
-  size_t max_bytes = *std::max_element(cfg.sizes.begin(), cfg.sizes.end());
-  if (cfg.latency) max_bytes = std::max(max_bytes, cfg.latency_bytes);
-  int slots = 1;
-  for (const auto& s : scheds) slots = std::max(slots, s.max_recv_slots());
-  Buffers bufs(*t, max_bytes, slots);
-
-  // Connection warm-up outside any timed cell (the reference pays lazy p2p
-  // connection setup inside its first cells; --reference keeps that).
-  if (cfg.warm_connections)
-    for (const auto& s : scheds) warm_connections(*t, boot, s, bufs);
-
-  AppResult local;
-  AppResult& res = result ? *result : local;
-
-  // Checkpoint / resume: every finished run is appended to the JSON-lines
-  // file and flushed at once, so a killed sweep keeps what it measured;
-  // --resume skips the (mode, dir, size) runs already present in that file.
+// Checkpoint / resume: every finished run is appended to the JSON-lines file
+// and flushed at once, so a killed sweep keeps what it measured; --resume
+// skips the (mode, dir, size) runs already present in that file.  Returns the
+// skip mask (collective: rank 0 reads the file, every rank gets the mask).
+std::vector<uint8_t> open_results(const AppConfig& cfg, Bootstrap& boot, const std::vector<Schedule>& scheds,
+                                  const std::string& provenance, std::ofstream* js) {
   std::vector<uint8_t> skip(scheds.size() * cfg.sizes.size(), 0);
-  std::ofstream js;
-  if (root && !cfg.json_path.empty()) {
+  if (boot.rank() == 0 && !cfg.json_path.empty()) {
     if (cfg.resume) {
       std::ifstream in(cfg.json_path);
       std::vector<std::string> done;
@@ -415,13 +387,21 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
           skip[i * cfg.sizes.size() + j] = std::find(done.begin(), done.end(),
                                                      run_key(scheds[i].mode, scheds[i].dir, cfg.sizes[j])) != done.end();
     }
-    js.open(cfg.json_path, cfg.resume ? std::ios::app : std::ios::trunc);
-    P2P_CHECK(js.good(), "cannot write " + cfg.json_path);
-    js << provenance << "\n";
-    js.flush();
+    js->open(cfg.json_path, cfg.resume ? std::ios::app : std::ios::trunc);
+    P2P_CHECK(js->good(), "cannot write " + cfg.json_path);
+    *js << provenance << "\n";
+    js->flush();
   }
   if (!skip.empty()) boot.bcast(skip.data(), skip.size(), 0);
+  return skip;
+}
 
+// Every (schedule, size) run; rank 0 prints the reference-format matrices of
+// pair runs as their cells finish (the reference prints and flushes per cell).
+void run_all(const AppConfig& cfg, Transport& t, Bootstrap& boot, const std::vector<Schedule>& scheds,
+             const std::vector<uint8_t>& skip, Buffers& bufs, std::ofstream& js, FILE* out, AppResult& res) {
+  const int n = boot.size();
+  const bool root = boot.rank() == 0;
   bool printed_compat = false;
   for (size_t sj = 0; sj < scheds.size(); ++sj) {
     const Schedule& s = scheds[sj];
@@ -446,7 +426,7 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
         cp.begin(s.dir, printed_compat && s.dir == Direction::Uni && cfg.sizes.size() == 1);
         printed_compat = true;
       }
-      rec.phases = run_schedule(*t, boot, s, rec.cfg, bufs, [&](const PhaseResult& r) {
+      rec.phases = run_schedule(t, boot, s, rec.cfg, bufs, [&](const PhaseResult& r) {
         if (compat) cp.on_phase(r);
       });
       for (const auto& ph : rec.phases) res.mismatches += ph.total_mismatches;
@@ -457,20 +437,136 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
       res.runs.push_back(std::move(rec));
     }
   }
-  if (cfg.latency) res.latency = run_latency(*t, boot, cfg.latency_bytes, cfg.latency_iters, std::min(cfg.latency_iters, 100), bufs);
+}
+
+// Latency tables: host-posted and pre-posted ping-pong, the device ping-pong
+// (one-sided transports), and in ring mode the dependent token chain.
+void run_latencies(const AppConfig& cfg, Transport& t, Bootstrap& boot, Buffers& bufs, AppResult& res) {
+  const int n = boot.size();
+  const int warm = std::min(cfg.latency_iters, 100);
+  if (cfg.latency) res.latency = run_latency(t, boot, cfg.latency_bytes, cfg.latency_iters, warm, bufs);
   if (cfg.latency && cfg.latency_preposted > 0)
-    res.preposted_latency = run_latency(*t, boot, cfg.latency_bytes, cfg.latency_iters, std::min(cfg.latency_iters, 100),
-                                        bufs, cfg.latency_preposted);
-  if (cfg.device_latency)
-    res.device_latency = run_device_latency(*t, boot, cfg.latency_bytes, cfg.latency_iters, std::min(cfg.latency_iters, 100));
-  // Ring mode: also the dependent token chain (pipeline-parallel hop latency).
+    res.preposted_latency = run_latency(t, boot, cfg.latency_bytes, cfg.latency_iters, warm, bufs, cfg.latency_preposted);
+  if (cfg.device_latency) res.device_latency = run_device_latency(t, boot, cfg.latency_bytes, cfg.latency_iters, warm);
   if (std::find(cfg.modes.begin(), cfg.modes.end(), Mode::Ring) != cfg.modes.end()) {
     const int laps = std::max(1, cfg.latency_iters / std::max(1, n));
     if (cfg.latency)
-      res.ring_latency.push_back(run_ring_latency(*t, boot, cfg.latency_bytes, laps, std::min(laps, 20), bufs));
+      res.ring_latency.push_back(run_ring_latency(t, boot, cfg.latency_bytes, laps, std::min(laps, 20), bufs));
     if (cfg.device_latency)
-      res.ring_latency.push_back(run_device_ring_latency(*t, boot, cfg.latency_bytes, laps, std::min(laps, 20)));
+      res.ring_latency.push_back(run_device_ring_latency(t, boot, cfg.latency_bytes, laps, std::min(laps, 20)));
   }
+}
+
+// Rank 0: the extended tables after the reference matrices, and the JSON /
+// trace / CSV files.
+void write_reports(const AppConfig& cfg, const Transport& t, const Bootstrap& boot, const Placement& pl,
+                   const std::vector<char>& all_desc, size_t desc_len, const AppResult& res, uint64_t fuzz_bad,
+                   size_t fuzz_max, std::ofstream& js, FILE* out) {
+  const int n = boot.size();
+  if (cfg.extended) {
+    std::fprintf(out, "\n== p2p_matrix: %d rank(s), transport %s, bootstrap %s, %d host(s) ==\n", n, t.name().c_str(),
+                 boot.name().c_str(), pl.num_hosts);
+    for (int r = 0; r < n; ++r) std::fprintf(out, "  rank %d: %s\n", r, &all_desc[static_cast<size_t>(r) * desc_len]);
+    if (t.name() != "host" && t.name() != "shm") std::fprintf(out, "%s", topology_report().c_str());
+    for (const auto& rec : res.runs) print_extended(out, rec, n);
+    print_latency(out, res.latency, n);
+    print_latency(out, res.preposted_latency, n);
+    print_latency(out, res.device_latency, n);
+    for (const auto& rl : res.ring_latency) print_ring_latency(out, rl);
+    if (cfg.fuzz_rounds > 0)
+      std::fprintf(out, "\n== fuzz: %d groups of random messages (1 B .. %s, random pairs incl. self): %s ==\n",
+                   cfg.fuzz_rounds, format_size(fuzz_max).c_str(),
+                   fuzz_bad ? strfmt("%llu mismatching words", static_cast<unsigned long long>(fuzz_bad)).c_str()
+                            : "all verified");
+  }
+  if (js.is_open()) {
+    if (!res.latency.empty()) js << latency_to_json(res.latency, n) << "\n";
+    if (!res.preposted_latency.empty()) js << latency_to_json(res.preposted_latency, n) << "\n";
+    if (!res.device_latency.empty()) js << latency_to_json(res.device_latency, n) << "\n";
+    for (const auto& rl : res.ring_latency) js << ring_latency_to_json(rl) << "\n";
+    if (cfg.fuzz_rounds > 0)
+      js << strfmt("{\"type\":\"fuzz\",\"rounds\":%d,\"max_bytes\":%zu,\"mismatches\":%llu}", cfg.fuzz_rounds, fuzz_max,
+                   static_cast<unsigned long long>(fuzz_bad))
+         << "\n";
+  }
+  if (!cfg.trace_path.empty()) {
+    std::ofstream tr(cfg.trace_path);
+    P2P_CHECK(tr.good(), "cannot write " + cfg.trace_path);
+    tr << chrome_trace(res.runs, n) << "\n";
+  }
+  if (!cfg.csv_path.empty()) {
+    std::ofstream cs(cfg.csv_path);
+    P2P_CHECK(cs.good(), "cannot write " + cfg.csv_path);
+    cs << csv_header();
+    for (const auto& rec : res.runs) cs << run_to_csv(rec);
+  }
+  std::fflush(out);
+}
+
+// Link check (--min-gbs): every measured off-diagonal flow must reach the
+// threshold; the slow ones are named so a bad link or GPU can be found.
+int count_slow_flows(const AppConfig& cfg, const AppResult& res, bool root) {
+  int slow = 0;
+  if (cfg.min_gbs <= 0) return 0;
+  for (const auto& rec : res.runs)
+    for (const auto& ph : rec.phases)
+      for (const auto& f : ph.flows)
+        if (f.flow.src != f.flow.dst && f.gbs < cfg.min_gbs) {
+          ++slow;
+          if (root)
+            std::fprintf(stderr, "p2p_matrix: SLOW LINK: %d -> %d %.2f GB/s < %.2f (%s-%s, %s)\n", f.flow.src,
+                         f.flow.dst, f.gbs, cfg.min_gbs, mode_name(rec.mode), direction_name(rec.dir),
+                         format_size(rec.bytes).c_str());
+        }
+  return slow;
+}
+
+}  // namespace
+
+int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result) {
+  if (cfg.verbose) set_log_level(cfg.verbose);
+  const int n = boot.size();
+  const bool root = boot.rank() == 0;
+
+  const std::vector<Schedule> scheds = build_schedules(cfg, n);
+  if (cfg.dry_run) {
+    if (root)
+      for (const auto& s : scheds) print_schedule(out, s);
+    return 0;
+  }
+  if (cfg.topology_only) {
+    if (root) std::fprintf(out, "%s", topology_report().c_str());
+    return 0;
+  }
+
+  Placement pl = check_placement(boot);
+  if (!pl.ok) P2P_FATAL("process placement check failed: " + pl.error);
+  TransportOptions topt;
+  std::unique_ptr<Transport> t = open_transport(cfg, boot, pl, &topt);
+
+  // Provenance (collective): the runtime, RCCL library and knobs, every
+  // rank's GPU and the links between them -- the first line of --json.
+  const bool gpu_transport = cfg.transport == "rccl" || cfg.transport == "ipc";
+  const std::string provenance =
+      cfg.json_path.empty() ? std::string() : provenance_json(boot, gpu_transport ? topt.device : -1);
+
+  size_t max_bytes = *std::max_element(cfg.sizes.begin(), cfg.sizes.end());
+  if (cfg.latency) max_bytes = std::max(max_bytes, cfg.latency_bytes);
+  int slots = 1;
+  for (const auto& s : scheds) slots = std::max(slots, s.max_recv_slots());
+  Buffers bufs(*t, max_bytes, slots);
+
+  // Connection warm-up outside any timed cell (the reference pays lazy p2p
+  // connection setup inside its first cells; --reference keeps that).
+  if (cfg.warm_connections)
+    for (const auto& s : scheds) warm_connections(*t, boot, s, bufs);
+
+  AppResult local;
+  AppResult& res = result ? *result : local;
+  std::ofstream js;
+  const std::vector<uint8_t> skip = open_results(cfg, boot, scheds, provenance, &js);
+  run_all(cfg, *t, boot, scheds, skip, bufs, js, out, res);
+  run_latencies(cfg, *t, boot, bufs, res);
   uint64_t fuzz_bad = 0;
   size_t fuzz_max = 0;
   if (cfg.fuzz_rounds > 0) {
@@ -484,59 +580,9 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
   std::snprintf(mine, sizeof(mine), "%s", t->device_desc().c_str());
   std::vector<char> all_desc(static_cast<size_t>(n) * sizeof(mine));
   boot.allgather(mine, all_desc.data(), sizeof(mine));
+  if (root) write_reports(cfg, *t, boot, pl, all_desc, sizeof(mine), res, fuzz_bad, fuzz_max, js, out);
 
-  if (root) {
-    if (cfg.extended) {
-      std::fprintf(out, "\n== p2p_matrix: %d rank(s), transport %s, bootstrap %s, %d host(s) ==\n", n, t->name().c_str(),
-                   boot.name().c_str(), pl.num_hosts);
-      for (int r = 0; r < n; ++r) std::fprintf(out, "  rank %d: %s\n", r, &all_desc[static_cast<size_t>(r) * sizeof(mine)]);
-      if (t->name() != "host" && t->name() != "shm") std::fprintf(out, "%s", topology_report().c_str());
-      for (const auto& rec : res.runs) print_extended(out, rec, n);
-      print_latency(out, res.latency, n);
-      print_latency(out, res.preposted_latency, n);
-      print_latency(out, res.device_latency, n);
-      for (const auto& rl : res.ring_latency) print_ring_latency(out, rl);
-      if (cfg.fuzz_rounds > 0)
-        std::fprintf(out, "\n== fuzz: %d groups of random messages (1 B .. %s, random pairs incl. self): %s ==\n",
-                     cfg.fuzz_rounds, format_size(fuzz_max).c_str(),
-                     fuzz_bad ? strfmt("%llu mismatching words", static_cast<unsigned long long>(fuzz_bad)).c_str()
-                              : "all verified");
-    }
-    if (js.is_open() && !res.latency.empty()) js << latency_to_json(res.latency, n) << "\n";
-    if (js.is_open() && !res.preposted_latency.empty()) js << latency_to_json(res.preposted_latency, n) << "\n";
-    if (js.is_open() && !res.device_latency.empty()) js << latency_to_json(res.device_latency, n) << "\n";
-    for (const auto& rl : res.ring_latency)
-      if (js.is_open()) js << ring_latency_to_json(rl) << "\n";
-    if (js.is_open() && cfg.fuzz_rounds > 0)
-      js << strfmt("{\"type\":\"fuzz\",\"rounds\":%d,\"max_bytes\":%zu,\"mismatches\":%llu}", cfg.fuzz_rounds, fuzz_max,
-                   static_cast<unsigned long long>(fuzz_bad))
-         << "\n";
-    if (!cfg.trace_path.empty()) {
-      std::ofstream tr(cfg.trace_path);
-      P2P_CHECK(tr.good(), "cannot write " + cfg.trace_path);
-      tr << chrome_trace(res.runs, n) << "\n";
-    }
-    if (!cfg.csv_path.empty()) {
-      std::ofstream cs(cfg.csv_path);
-      P2P_CHECK(cs.good(), "cannot write " + cfg.csv_path);
-      cs << csv_header();
-      for (const auto& rec : res.runs) cs << run_to_csv(rec);
-    }
-    std::fflush(out);
-  }
-  // Link check (--min-gbs): every measured off-diagonal flow must reach the
-  // threshold; the slow ones are named so a bad link or GPU can be found.
-  if (cfg.min_gbs > 0)
-    for (const auto& rec : res.runs)
-      for (const auto& ph : rec.phases)
-        for (const auto& f : ph.flows)
-          if (f.flow.src != f.flow.dst && f.gbs < cfg.min_gbs) {
-            ++res.slow_flows;
-            if (root)
-              std::fprintf(stderr, "p2p_matrix: SLOW LINK: %d -> %d %.2f GB/s < %.2f (%s-%s, %s)\n", f.flow.src,
-                           f.flow.dst, f.gbs, cfg.min_gbs, mode_name(rec.mode), direction_name(rec.dir),
-                           format_size(rec.bytes).c_str());
-          }
+  res.slow_flows = count_slow_flows(cfg, res, root);
   boot.barrier();
   if (res.mismatches) {
     if (root) std::fprintf(stderr, "p2p_matrix: VERIFICATION FAILED: %llu mismatching words\n", static_cast<unsigned long long>(res.mismatches));
