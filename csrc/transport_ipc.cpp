@@ -729,18 +729,32 @@ class IpcTransport final : public Transport {
     } else if (ops_.size() == 1) {
       HIPCHECK(hipMemcpyAsync(ops_[0].dst, ops_[0].src, ops_[0].bytes, hipMemcpyDeviceToDevice, stream_));
     } else {
-      // Fork: every receive on its own stream so the copy engines overlap,
-      // then join back into the main stream.
-      ensure_side_streams(ops_.size());
+      // Fork: the receives round-robin over a few side streams so the copy
+      // engines overlap, then join back into the main stream.  A small pool
+      // (P2P_SDMA_STREAMS, default 4) rather than a stream per receive: more
+      // streams than the process's hardware queues only share queues, and
+      // every extra queue is one more for the GPU's scheduler to map.
+      const size_t k = std::min(ops_.size(), sdma_streams());
+      ensure_side_streams(k);
       HIPCHECK(hipEventRecord(fork_, stream_));
-      for (size_t i = 0; i < ops_.size(); ++i) {
-        HIPCHECK(hipStreamWaitEvent(side_[i], fork_, 0));
-        HIPCHECK(hipMemcpyAsync(ops_[i].dst, ops_[i].src, ops_[i].bytes, hipMemcpyDeviceToDevice, side_[i]));
-        HIPCHECK(hipEventRecord(side_done_[i], side_[i]));
-        HIPCHECK(hipStreamWaitEvent(stream_, side_done_[i], 0));
+      for (size_t j = 0; j < k; ++j) HIPCHECK(hipStreamWaitEvent(side_[j], fork_, 0));
+      for (size_t i = 0; i < ops_.size(); ++i)
+        HIPCHECK(hipMemcpyAsync(ops_[i].dst, ops_[i].src, ops_[i].bytes, hipMemcpyDeviceToDevice, side_[i % k]));
+      for (size_t j = 0; j < k; ++j) {
+        HIPCHECK(hipEventRecord(side_done_[j], side_[j]));
+        HIPCHECK(hipStreamWaitEvent(stream_, side_done_[j], 0));
       }
     }
     ops_.clear();
+  }
+
+  static size_t sdma_streams() {
+    static const size_t k = [] {
+      const char* e = std::getenv("P2P_SDMA_STREAMS");
+      const int v = e ? std::atoi(e) : 4;
+      return static_cast<size_t>(std::max(1, std::min(64, v)));
+    }();
+    return k;
   }
 
   void ensure_side_streams(size_t n) {
