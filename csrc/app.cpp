@@ -102,6 +102,7 @@ environment (recorded in every --json provenance record; docs/OUTPUT.md)
   P2P_RCCL_DISTINCT_HOSTS=1  one NCCL_HOSTID per rank: RCCL ranks may share a GPU (tests,
                          over RCCL's socket transport, e.g. NCCL_SOCKET_IFNAME=lo)
   P2P_IPC_POOL=B         exported IPC buffers kept for reuse                     [32G]
+  P2P_SDMA_STREAMS=K     --ipc-engine sdma: side streams the receives share      [4]
   P2P_BOOTSTRAP_PORT, P2P_BOOTSTRAP_TIMEOUT   TCP bootstrap port / receive deadline
   P2P_HOSTNAME=name      hostname for the placement check (emulated hosts)
   P2P_INJECT_FAULT=kind@rank[:phase]   corrupt | exit | hang | skip (tests)
