@@ -37,6 +37,11 @@ from process start (--deadline): each section's waits are shortened to the
 time left, sections that would not fit are skipped (untimed_skipped), and a
 watchdog prints the JSON line with what is done when the deadline passes.
 
+Should RCCL itself fail on every rank (a communicator that cannot be set up, a
+connection or transfer that stalls past --timeout), the same steps are timed
+through the hand-written IPC data plane and the line says so
+(headline_fallback); --fallback 0 reports the error with value null instead.
+
 Usage (driver contract):
   python bench.py --gpus 1 --steps K --warmup W
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N \\
