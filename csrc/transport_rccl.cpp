@@ -85,43 +85,7 @@ class RcclTransport final : public Transport {
     P2P_CHECK(ncomms >= 1 && ncomms <= kMaxComms, strfmt("rccl communicators per rank: 1..%d", kMaxComms));
     P2P_CHECK(ncomms == 1 || !opt.two_streams, "--two-streams (the reference layout) uses one communicator");
     HIPCHECK(hipSetDevice(device_));
-    HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    if (opt.two_streams) {
-      HIPCHECK(hipStreamCreateWithFlags(&recv_stream_, hipStreamNonBlocking));
-      HIPCHECK(hipEventCreateWithFlags(&join_, hipEventDisableTiming));
-    }
-    if (const char* mi = std::getenv("P2P_RCCL_MAIN_IDLE")) main_idle_ = ncomms > 1 && std::atoi(mi) != 0;
-    // P2P_RCCL_CU_MASK=contig|stride (experiment): every communicator's
-    // stream gets its own 1/K of the CUs (contiguous mask bits, or every K-th
-    // bit), so the K concurrent send/recv kernels do not compete for CUs; the
-    // main stream (fill / verify) stays unmasked, so communicator 0 moves to
-    // a stream of its own as with P2P_RCCL_MAIN_IDLE.
-    int cu_mask_mode = 0;
-    if (const char* cm = std::getenv("P2P_RCCL_CU_MASK"))
-      cu_mask_mode = std::strcmp(cm, "contig") == 0 ? 1 : std::strcmp(cm, "stride") == 0 ? 2 : 0;
-    if (ncomms == 1) cu_mask_mode = 0;
-    if (cu_mask_mode) main_idle_ = true;
-    int ncus = 0;
-    HIPCHECK(hipDeviceGetAttribute(&ncus, hipDeviceAttributeMultiprocessorCount, device_));
-    for (int j = 0; j < ncomms; ++j) {
-      hipStream_t s = stream_;
-      if (cu_mask_mode) {
-        std::vector<uint32_t> mask(static_cast<size_t>((ncus + 31) / 32), 0u);
-        for (int c = 0; c < ncus; ++c) {
-          const int owner = cu_mask_mode == 1 ? c * ncomms / ncus : c % ncomms;
-          if (owner == j) mask[static_cast<size_t>(c / 32)] |= 1u << (c % 32);
-        }
-        HIPCHECK(hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(mask.size()), mask.data()));
-        cu_masked_ = true;
-      } else if (j > 0 || main_idle_) {
-        HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-      }
-      cstreams_.push_back(s);
-      hipEvent_t ev = nullptr;
-      if (ncomms > 1) HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-      cjoin_.push_back(ev);
-    }
-    if (ncomms > 1) HIPCHECK(hipEventCreateWithFlags(&fork_, hipEventDisableTiming));
+    const int cu_mask_mode = open_streams(opt, ncomms);
     stale_.assign(static_cast<size_t>(ncomms), true);
     pending_.assign(static_cast<size_t>(ncomms), false);
     unjoined_.assign(static_cast<size_t>(ncomms), false);
@@ -129,54 +93,8 @@ class RcclTransport final : public Transport {
     recv_seq_.assign(static_cast<size_t>(n_), 0);
     HIPCHECK(hipMalloc(&acc_, dev::verify_accum_bytes()));
     HIPCHECK(hipHostMalloc(&acc_host_, sizeof(dev::VerifyAccum), hipHostMallocDefault));
-
-    // P2P_RCCL_DISTINCT_HOSTS=1 (tests on one GPU): every rank tells RCCL it
-    // is on a host of its own (NCCL_HOSTID, read when RCCL first hashes the
-    // host), so several ranks may share one GPU -- RCCL refuses duplicate GPUs
-    // on one host -- and talk over its network transport (sockets, e.g.
-    // NCCL_SOCKET_IFNAME=lo).  Not xGMI: this exercises the multi-rank RCCL
-    // paths (communicators, schedules, ordering across K communicators) where
-    // only one GPU is available.
-    if (const char* dh = std::getenv("P2P_RCCL_DISTINCT_HOSTS"); dh && std::atoi(dh) != 0)
-      setenv("NCCL_HOSTID", strfmt("p2p-emulated-host-%d", rank_).c_str(), 1);
-    // RCCL prints a version banner to stdout on first use; send it to stderr
-    // so stdout keeps the reference's output (P2P_RCCL_BANNER=1 keeps it).
-    const char* banner = std::getenv("P2P_RCCL_BANNER");
-    StdoutToStderr quiet(!(banner && std::atoi(banner)));
-    std::vector<ncclUniqueId> ids(static_cast<size_t>(ncomms));
-    std::memset(ids.data(), 0, sizeof(ncclUniqueId) * ids.size());
-    if (rank_ == 0)
-      for (auto& id : ids) nccl_ok(ncclGetUniqueId(&id), "ncclGetUniqueId");
-    boot.bcast(ids.data(), sizeof(ncclUniqueId) * ids.size(), 0);
-
-    if (const char* mc = std::getenv("P2P_RCCL_MAX_CHUNK")) max_chunk_ = std::strcmp(mc, "0") ? parse_size(mc) : 0;
-    if (const char* sm = std::getenv("P2P_RCCL_SPLIT_MIN")) split_min_ = parse_size(sm);
-    if (const char* rg = std::getenv("P2P_RCCL_REGISTER")) register_ = std::atoi(rg);
-    const char* blk = std::getenv("P2P_RCCL_BLOCKING");
-    nonblocking_ = opt.nonblocking_init && !(blk && std::atoi(blk));
-    comms_.assign(static_cast<size_t>(ncomms), nullptr);
-    hook_ = push_abort_hook([this](int) { abort_all(); });
-    // One communicator after the other, in the same order on every rank.
-    for (int j = 0; j < ncomms; ++j) {
-      if (nonblocking_) {
-        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-        cfg.blocking = 0;
-        ncclResult_t r = ncclCommInitRankConfig(&comms_[static_cast<size_t>(j)], n_, ids[static_cast<size_t>(j)], rank_, &cfg);
-        wait_ready(r, "ncclCommInitRankConfig");
-      } else {
-        nccl_ok(ncclCommInitRank(&comms_[static_cast<size_t>(j)], n_, ids[static_cast<size_t>(j)], rank_), "ncclCommInitRank");
-      }
-    }
-    hipDeviceProp_t prop;
-    HIPCHECK(hipGetDeviceProperties(&prop, device_));
-    char pci[64] = {0};
-    if (hipDeviceGetPCIBusId(pci, sizeof(pci), device_) != hipSuccess) pci[0] = 0;
-    int ver = 0;
-    ncclGetVersion(&ver);
-    desc_ = strfmt("hip:%d %s (%s, %d CUs, %.0f GiB, pci %s) rccl %d", device_, prop.name, prop.gcnArchName,
-                   prop.multiProcessorCount, static_cast<double>(prop.totalGlobalMem) / (1ull << 30), pci, ver);
-    if (ncomms > 1) desc_ += strfmt(" x%d comms", ncomms);
-    if (cu_masked_) desc_ += cu_mask_mode == 1 ? " cu-mask:contig" : " cu-mask:stride";
+    open_communicators(boot, opt, ncomms);
+    describe(ncomms, cu_mask_mode);
   }
 
   ~RcclTransport() override {
@@ -495,6 +413,104 @@ class RcclTransport final : public Transport {
   }
 
  private:
+  // Main stream (fill / verify), the optional reference receive stream, and
+  // one stream + join event per communicator.  Returns the CU-mask mode
+  // (0 off, 1 contig, 2 stride).
+  int open_streams(const TransportOptions& opt, int ncomms) {
+    HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    if (opt.two_streams) {
+      HIPCHECK(hipStreamCreateWithFlags(&recv_stream_, hipStreamNonBlocking));
+      HIPCHECK(hipEventCreateWithFlags(&join_, hipEventDisableTiming));
+    }
+    if (const char* mi = std::getenv("P2P_RCCL_MAIN_IDLE")) main_idle_ = ncomms > 1 && std::atoi(mi) != 0;
+    // P2P_RCCL_CU_MASK=contig|stride (experiment): every communicator's
+    // stream gets its own 1/K of the CUs (contiguous mask bits, or every K-th
+    // bit), so the K concurrent send/recv kernels do not compete for CUs; the
+    // main stream (fill / verify) stays unmasked, so communicator 0 moves to
+    // a stream of its own as with P2P_RCCL_MAIN_IDLE.
+    int cu_mask_mode = 0;
+    if (const char* cm = std::getenv("P2P_RCCL_CU_MASK"))
+      cu_mask_mode = std::strcmp(cm, "contig") == 0 ? 1 : std::strcmp(cm, "stride") == 0 ? 2 : 0;
+    if (ncomms == 1) cu_mask_mode = 0;
+    if (cu_mask_mode) main_idle_ = true;
+    int ncus = 0;
+    HIPCHECK(hipDeviceGetAttribute(&ncus, hipDeviceAttributeMultiprocessorCount, device_));
+    for (int j = 0; j < ncomms; ++j) {
+      hipStream_t s = stream_;
+      if (cu_mask_mode) {
+        std::vector<uint32_t> mask(static_cast<size_t>((ncus + 31) / 32), 0u);
+        for (int c = 0; c < ncus; ++c) {
+          const int owner = cu_mask_mode == 1 ? c * ncomms / ncus : c % ncomms;
+          if (owner == j) mask[static_cast<size_t>(c / 32)] |= 1u << (c % 32);
+        }
+        HIPCHECK(hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(mask.size()), mask.data()));
+        cu_masked_ = true;
+      } else if (j > 0 || main_idle_) {
+        HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      }
+      cstreams_.push_back(s);
+      hipEvent_t ev = nullptr;
+      if (ncomms > 1) HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      cjoin_.push_back(ev);
+    }
+    if (ncomms > 1) HIPCHECK(hipEventCreateWithFlags(&fork_, hipEventDisableTiming));
+    return cu_mask_mode;
+  }
+
+  // ncclUniqueIds from rank 0 through the bootstrap, then the communicators.
+  void open_communicators(Bootstrap& boot, const TransportOptions& opt, int ncomms) {
+    // P2P_RCCL_DISTINCT_HOSTS=1 (tests on one GPU): every rank tells RCCL it
+    // is on a host of its own (NCCL_HOSTID, read when RCCL first hashes the
+    // host), so several ranks may share one GPU -- RCCL refuses duplicate GPUs
+    // on one host -- and talk over its network transport (sockets, e.g.
+    // NCCL_SOCKET_IFNAME=lo).  Not xGMI: this exercises the multi-rank RCCL
+    // paths (communicators, schedules, ordering across K communicators) where
+    // only one GPU is available.
+    if (const char* dh = std::getenv("P2P_RCCL_DISTINCT_HOSTS"); dh && std::atoi(dh) != 0)
+      setenv("NCCL_HOSTID", strfmt("p2p-emulated-host-%d", rank_).c_str(), 1);
+    // RCCL prints a version banner to stdout on first use; send it to stderr
+    // so stdout keeps the reference's output (P2P_RCCL_BANNER=1 keeps it).
+    const char* banner = std::getenv("P2P_RCCL_BANNER");
+    StdoutToStderr quiet(!(banner && std::atoi(banner)));
+    std::vector<ncclUniqueId> ids(static_cast<size_t>(ncomms));
+    std::memset(ids.data(), 0, sizeof(ncclUniqueId) * ids.size());
+    if (rank_ == 0)
+      for (auto& id : ids) nccl_ok(ncclGetUniqueId(&id), "ncclGetUniqueId");
+    boot.bcast(ids.data(), sizeof(ncclUniqueId) * ids.size(), 0);
+
+    if (const char* mc = std::getenv("P2P_RCCL_MAX_CHUNK")) max_chunk_ = std::strcmp(mc, "0") ? parse_size(mc) : 0;
+    if (const char* sm = std::getenv("P2P_RCCL_SPLIT_MIN")) split_min_ = parse_size(sm);
+    if (const char* rg = std::getenv("P2P_RCCL_REGISTER")) register_ = std::atoi(rg);
+    const char* blk = std::getenv("P2P_RCCL_BLOCKING");
+    nonblocking_ = opt.nonblocking_init && !(blk && std::atoi(blk));
+    comms_.assign(static_cast<size_t>(ncomms), nullptr);
+    hook_ = push_abort_hook([this](int) { abort_all(); });
+    // One communicator after the other, in the same order on every rank.
+    for (int j = 0; j < ncomms; ++j) {
+      if (nonblocking_) {
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        ncclResult_t r = ncclCommInitRankConfig(&comms_[static_cast<size_t>(j)], n_, ids[static_cast<size_t>(j)], rank_, &cfg);
+        wait_ready(r, "ncclCommInitRankConfig");
+      } else {
+        nccl_ok(ncclCommInitRank(&comms_[static_cast<size_t>(j)], n_, ids[static_cast<size_t>(j)], rank_), "ncclCommInitRank");
+      }
+    }
+  }
+
+  void describe(int ncomms, int cu_mask_mode) {
+    hipDeviceProp_t prop;
+    HIPCHECK(hipGetDeviceProperties(&prop, device_));
+    char pci[64] = {0};
+    if (hipDeviceGetPCIBusId(pci, sizeof(pci), device_) != hipSuccess) pci[0] = 0;
+    int ver = 0;
+    ncclGetVersion(&ver);
+    desc_ = strfmt("hip:%d %s (%s, %d CUs, %.0f GiB, pci %s) rccl %d", device_, prop.name, prop.gcnArchName,
+                   prop.multiProcessorCount, static_cast<double>(prop.totalGlobalMem) / (1ull << 30), pci, ver);
+    if (ncomms > 1) desc_ += strfmt(" x%d comms", ncomms);
+    if (cu_masked_) desc_ += cu_mask_mode == 1 ? " cu-mask:contig" : " cu-mask:stride";
+  }
+
   static constexpr int kMaxComms = 8;
 
   // The main stream is about to touch payload buffers: side streams must wait
