@@ -37,6 +37,11 @@ from process start (--deadline): each section's waits are shortened to the
 time left, sections that would not fit are skipped (untimed_skipped), and a
 watchdog prints the JSON line with what is done when the deadline passes.
 
+At N = 2 on two distinct GPUs the time the deadline leaves after every other
+section goes to the xGMI pair-cell tuning sweep (scripts/xgmi_pair_sweep.py:
+RCCL communicator counts, the IPC engines, RCCL knobs; every row verified),
+recorded in xgmi_pair_sweep.
+
 Should RCCL itself fail on every rank (a communicator that cannot be set up, a
 connection or transfer that stalls past --timeout), the same steps are timed
 through the hand-written IPC data plane and the line says so
@@ -54,6 +59,8 @@ import argparse
 import json
 import math
 import os
+import shutil
+import signal
 import socket
 import statistics
 import subprocess
@@ -71,6 +78,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "pairwise P2P GB/s matrix (min/mean) + p50 latency at 1/2/4/8 MI355X"
 BASELINE_VALUE = None  # the reference publishes no numbers
 RESERVE_S = 15.0  # kept free at the end of the deadline for the JSON line and teardown
+HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def log(*a):
@@ -214,6 +222,32 @@ class Reporter:
             return True
 
 
+def run_child(state, cmd, timeout, **kw):
+    """Runs a child process in a session of its own, registered in
+    state["children"] while it runs, so that the watchdog (which ends this
+    process at the deadline) takes the child and everything it started down
+    with it; at `timeout` the same happens here.  Returns the exit status, or
+    "timeout"."""
+    proc = subprocess.Popen(cmd, start_new_session=True, **kw)
+    state.setdefault("children", []).append(proc)
+    try:
+        return proc.wait(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        kill_children(state, [proc])
+        return "timeout"
+    finally:
+        state["children"].remove(proc)
+
+
+def kill_children(state, procs=None):
+    for proc in list(procs if procs is not None else state.get("children", [])):
+        try:
+            os.killpg(proc.pid, signal.SIGKILL)
+        except (ProcessLookupError, PermissionError):
+            pass
+        proc.wait()
+
+
 def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> threading.Event:
     """At the deadline: print the JSON line with what is finished (the section
     still running is named), abort every RCCL communicator so its kernels exit,
@@ -231,6 +265,7 @@ def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> thread
         if state.get("section"):
             errors[state["section"]] = "deadline reached while running"
         reporter.emit(deadline_hit=True, untimed_skipped=state.get("skipped") or None, section_errors=errors or None)
+        kill_children(state)
         try:
             nat.run_abort_hooks()
         except Exception:  # noqa: BLE001 -- the process ends either way
@@ -404,6 +439,12 @@ def parse_args(argv=None):
                     help="seconds for all untimed sections after the timed steps (within --deadline)")
     ap.add_argument("--child-timeout", type=float, default=300.0,
                     help="seconds allowed to each untimed comparison process")
+    ap.add_argument("--xgmi-sweep", type=int, default=-1,
+                    help="the xGMI pair-cell tuning sweep (scripts/xgmi_pair_sweep.py: RCCL communicator counts, the "
+                         "IPC engines, RCCL knobs on cell 0 -> 1, every row verified) in the time left after the other "
+                         "sections: -1 at N = 2 on distinct GPUs, 1 at any N >= 2 (emulated where ranks share a GPU, "
+                         "on the CPU host transport for --transport host), 0 never")
+    ap.add_argument("--xgmi-sweep-sizes", default="32M,1G", help="message sizes of the pair sweep")
     ap.add_argument("--child", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--child-port", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--child-out", default=None, help=argparse.SUPPRESS)
@@ -740,6 +781,7 @@ class BenchRun:
             "reference_semantics": None,
             "extras": None,
             "ipc_transport": None,
+            "xgmi_pair_sweep": None,
             "untimed_skipped": None,
             "headline_fallback": self.fallback,
             "note": ("n_gpus=1 has no inter-GPU link: value is RCCL's on-GPU self send/recv copy (HBM-bound), the "
@@ -933,10 +975,7 @@ class BenchRun:
             cmd.append("--no-verify")
         if args.device is not None:
             cmd += ["--device", str(args.device)]
-        try:
-            rc = subprocess.run(cmd, timeout=limit).returncode
-        except subprocess.TimeoutExpired:
-            rc = "timeout"
+        rc = run_child(self.state, cmd, limit)
         self.barrier()
         res = None
         if rank == 0:
@@ -1004,6 +1043,81 @@ class BenchRun:
                 ipc = dict(ipc or {}, **{key: r})
             self.reporter.update(ipc_transport=ipc)
 
+    def xgmi_sweep_section(self):
+        """The xGMI pair-cell tuning sweep in whatever time
+        the deadline leaves: RCCL at 1, 2, 4 and 8 communicators, the IPC
+        engines, then RCCL's channel / chunk / protocol / batch / read knobs,
+        on cell 0 -> 1 (uni) and 0 <-> 1 (bi), every row verified; rows that do
+        not fit are listed as skipped.  Rank 0 runs it as a child job while the
+        other ranks wait at a barrier (their sessions are closed by then)."""
+        args, n = self.args, self.n
+        pcis = [d.get("pci") for d in (self.h.provenance or {}).get("rank_devices", [])]
+        distinct = len(pcis) == n and all(pcis) and len(set(pcis)) == n
+        on = args.xgmi_sweep if args.xgmi_sweep >= 0 else int(n == 2 and distinct and self.use_gpu)
+        if n < 2 or not on:
+            return
+        if not self.use_gpu:
+            emulate = "host"
+        elif distinct:
+            emulate = ""
+        else:
+            emulate = "rccl" if os.environ.get("P2P_RCCL_DISTINCT_HOSTS") == "1" else "ipc"
+
+        def sweep():
+            res = None
+            if self.env.rank == 0:
+                try:
+                    res = self.run_pair_sweep(emulate)
+                except Exception as e:  # noqa: BLE001 -- the other ranks wait at the barrier below
+                    res = {"error": str(e)[:300]}
+            self.barrier()
+            return res
+
+        r = self.section("xgmi_pair_sweep", sweep, 30.0)
+        if r is not None and self.env.rank == 0:
+            self.reporter.update(xgmi_pair_sweep=r)
+
+    def run_pair_sweep(self, emulate):
+        """scripts/xgmi_pair_sweep.py within the time left; returns its rows
+        (cell GB/s and p50 per direction and size; bi = both directions
+        summed, like the reference's bi matrix) and the winner per cell."""
+        args, n = self.args, self.n
+        budget = self.budget_left() - 15.0
+        out = tempfile.mkdtemp(prefix="p2p_xgmi_sweep_")
+        cmd = [sys.executable, os.path.join(HERE, "scripts", "xgmi_pair_sweep.py"), "--np", str(n), "--out", out,
+               "--sizes", args.xgmi_sweep_sizes, "--rows", "rccl,ipc,knobs", "--budget", "%.0f" % budget,
+               "--row-timeout", "%.0f" % min(90.0, budget)]
+        if emulate:
+            cmd += ["--emulate", emulate]
+        log("bench: xGMI pair sweep (%.0f s%s)" % (budget, ", emulated: " + emulate if emulate else ""))
+        t0 = time.monotonic()
+        try:
+            with open(os.path.join(out, "sweep.log"), "w") as lf:
+                rc = run_child(self.state, cmd, budget + 15.0, stdout=lf, stderr=subprocess.STDOUT)
+            res = {"rc": rc, "seconds": round(time.monotonic() - t0, 1), "budget_s": round(budget, 1),
+                   "emulated": emulate or None, "sizes": args.xgmi_sweep_sizes, "cell": "0 -> 1 (uni), 0 <-> 1 (bi)",
+                   "rows": {}}
+            rows_path = os.path.join(out, "rows.jsonl")
+            for line in (open(rows_path) if os.path.exists(rows_path) else []):
+                r = json.loads(line)
+                res["rows"][r["name"]] = dict(
+                    {"rc": r["rc"], "seconds": r.get("seconds")},
+                    **{k: {"cell_gbs": round(c["cell_gbs"], 2), "p50_us": round(c["p50_us"], 2)}
+                       for k, c in (r.get("cells") or {}).items()})
+            try:
+                with open(os.path.join(out, "summary.json")) as f:
+                    summary = json.load(f)
+                res["best"] = {k: {"row": b["row"], "cell_gbs": round(b["cell_gbs"], 2), "gain": b.get("gain")}
+                               for k, b in summary["best"].items()}
+                res.update(skipped=summary["rows_skipped"] or None, corrupt=summary["corrupt_rows"] or None,
+                           failed_row=summary["failed_row"])
+            except (OSError, ValueError, KeyError):
+                with open(os.path.join(out, "sweep.log")) as f:
+                    res["error"] = f.read()[-600:] or "the sweep wrote no summary"
+            return res
+        finally:
+            shutil.rmtree(out, ignore_errors=True)
+
     def run(self) -> int:
         rc = self.headline()
         if rc is not None:
@@ -1023,6 +1137,7 @@ class BenchRun:
         self.live.clear()
         h.sess = h.ref_sess = h.sessions = None
         self.comparisons()
+        self.xgmi_sweep_section()
 
         self.reporter.update(untimed_skipped=self.state["skipped"] or None,
                              section_errors=self.state["errors"] or None)

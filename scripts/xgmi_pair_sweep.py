@@ -44,6 +44,7 @@ import argparse
 import json
 import os
 import shlex
+import signal
 import subprocess
 import sys
 import time
@@ -90,7 +91,7 @@ def parse_args(argv=None):
     ap.add_argument("--emulate", choices=["", "ipc", "rccl", "host"], default="",
                     help="validate without a second GPU: ranks share GPU 0 (ipc; rccl over RCCL's socket transport) "
                          "or use the CPU (host)")
-    ap.add_argument("--rows", default="rccl,knobs,ipc", help="row groups to run: rccl, knobs, ipc")
+    ap.add_argument("--rows", default="rccl,knobs,ipc", help="row groups to run, in this order: rccl, knobs, ipc")
     ap.add_argument("--budget", type=float, default=900.0, help="seconds for the whole sweep; rows that would "
                     "start after it is spent are listed as skipped")
     ap.add_argument("--row-timeout", type=float, default=180.0)
@@ -112,24 +113,26 @@ def visible_gpus() -> int:
 
 
 def plan_rows(args, np_):
-    """Every (name, transport args, env) row of the sweep, in run order."""
-    groups = set(args.rows.split(","))
+    """Every (name, transport args, env) row of the sweep, in run order: the
+    row groups in the order --rows names them (a budgeted sweep runs the
+    groups it cares about most first)."""
     rows = []
     rccl_ok = args.emulate in ("", "rccl")
-    if "rccl" in groups and rccl_ok:
-        for k in COMMS:
-            rows.append({"name": "rccl-comms%d" % k, "args": ["--transport", "rccl", "--comms", str(k)], "env": {}})
-    if "knobs" in groups and rccl_ok:
-        for i, env in enumerate(RCCL_KNOBS):
-            name = "rccl-" + "-".join("%s=%s" % (k.replace("P2P_", "").replace("NCCL_", "").replace("RCCL_", "").lower(), v)
-                                      for k, v in env.items())
-            rows.append({"name": name, "args": ["--transport", "rccl", "--comms", "1"], "env": env, "knob": True})
-    if "ipc" in groups and args.emulate != "host":
-        for eng in IPC_ENGINES:
-            if eng == "relay" and np_ < 3:
-                continue  # relay needs a third GPU to route through
-            a = ["--transport", "ipc", "--ipc-engine", eng]
-            rows.append({"name": "ipc-" + eng, "args": a, "env": {"P2P_IPC_POOL": "4G"} if eng == "relay" else {}})
+    for group in [g.strip() for g in args.rows.split(",") if g.strip()]:
+        if group == "rccl" and rccl_ok:
+            for k in COMMS:
+                rows.append({"name": "rccl-comms%d" % k, "args": ["--transport", "rccl", "--comms", str(k)], "env": {}})
+        elif group == "knobs" and rccl_ok:
+            for env in RCCL_KNOBS:
+                name = "rccl-" + "-".join("%s=%s" % (k.replace("P2P_", "").replace("NCCL_", "").replace("RCCL_", "").lower(),
+                                                     v) for k, v in env.items())
+                rows.append({"name": name, "args": ["--transport", "rccl", "--comms", "1"], "env": env, "knob": True})
+        elif group == "ipc" and args.emulate != "host":
+            for eng in IPC_ENGINES:
+                if eng == "relay" and np_ < 3:
+                    continue  # relay needs a third GPU to route through
+                a = ["--transport", "ipc", "--ipc-engine", eng]
+                rows.append({"name": "ipc-" + eng, "args": a, "env": {"P2P_IPC_POOL": "4G"} if eng == "relay" else {}})
     if args.emulate == "host":
         rows.append({"name": "host", "args": ["--transport", "host"], "env": {}})
     return rows
@@ -157,12 +160,16 @@ def cell_result(js_path, dirs):
     return out
 
 
-def run_row(args, row, np_, exe, tag):
+def run_row(args, row, np_, exe, tag, t_end=None):
+    """One row as its own mpirun job, in a session of its own: on a timeout
+    the whole job (launcher, proxies, ranks) is killed, so no rank is left
+    driving a GPU.  t_end caps the row's time at the sweep's budget."""
     js = os.path.join(args.out, "%s.json" % tag)
     if os.path.exists(js):
         os.remove(js)
+    limit = args.row_timeout if t_end is None else max(5.0, min(args.row_timeout, t_end - time.time()))
     cmd = [MPIRUN, "-n", str(np_), exe, "--mode", "pair", "--cells", "0-1", "--dir", "both", "--sizes", args.sizes,
-           "-n", args.iters, "--verify", "--no-compat", "--json", js, "--timeout", str(int(args.row_timeout))]
+           "-n", args.iters, "--verify", "--no-compat", "--json", js, "--timeout", str(max(5, int(limit) - 5))]
     cmd += row["args"]
     if args.emulate in ("ipc", "rccl"):
         cmd += ["--device", "0"]
@@ -170,11 +177,18 @@ def run_row(args, row, np_, exe, tag):
     if args.emulate == "rccl":
         env.update(EMULATE_RCCL_ENV)
     t0 = time.time()
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                            start_new_session=True)
     try:
-        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=args.row_timeout + 30)
-        rc, err = r.returncode, r.stderr
+        _, err = proc.communicate(timeout=limit + 10)
+        rc = proc.returncode
     except subprocess.TimeoutExpired:
-        rc, err = 124, "row timed out"
+        try:
+            os.killpg(proc.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+        proc.communicate()
+        rc, err = 124, "row timed out after %.0f s" % limit
     rec = {"name": row["name"], "env": row["env"], "args": row["args"], "rc": rc, "seconds": round(time.time() - t0, 2),
            "cmd": " ".join(shlex.quote(c) for c in cmd)}
     if rc == 0:
@@ -228,6 +242,9 @@ def main(argv=None) -> int:
     if not os.path.exists(exe):
         print("xgmi_pair_sweep: %s not built (make)" % exe, file=sys.stderr)
         return 1
+    if not os.path.exists(MPIRUN):
+        print("xgmi_pair_sweep: no mpirun at %s (P2P_MPIRUN)" % MPIRUN, file=sys.stderr)
+        return 1
     os.makedirs(args.out, exist_ok=True)
     t_end = time.time() + args.budget
     done, skipped, failed, corrupt = [], [], None, []
@@ -251,10 +268,12 @@ def main(argv=None) -> int:
                     corrupt.append(rec["name"])
                 print("%-40s kept from the previous run (rc=%d)" % (rec["name"], rec["rc"]), flush=True)
                 continue
-            if failed is not None or time.time() + 5 > t_end:
+            # A row starts only if the longest row so far still fits.
+            longest = max([r["seconds"] for r in done if "seconds" in r] + [5.0])
+            if failed is not None or time.time() + longest > t_end:
                 skipped.append(row["name"])
                 continue
-            rec = run_row(args, row, np_, exe, "row%02d" % i)
+            rec = run_row(args, row, np_, exe, "row%02d" % i, t_end)
             f.write(json.dumps(rec) + "\n")
             f.flush()
             done.append(rec)
@@ -268,14 +287,15 @@ def main(argv=None) -> int:
         # Best knob set at the best communicator count (knobs ran at --comms 1).
         knob_rows = [r for r in done if r["rc"] == 0 and any(r["name"] == x["name"] and x.get("knob") for x in rows)]
         comm_rows = [r for r in done if r["rc"] == 0 and r["name"].startswith("rccl-comms")]
-        if failed is None and knob_rows and comm_rows and time.time() + 5 < t_end:
+        longest = max([r["seconds"] for r in done if "seconds" in r] + [5.0])
+        if failed is None and knob_rows and comm_rows and time.time() + longest < t_end:
             key = sorted(comm_rows[0]["cells"])[-1]
             bk = max(knob_rows, key=lambda r: r["cells"].get(key, {}).get("cell_gbs", 0))
             bc = max(comm_rows, key=lambda r: r["cells"].get(key, {}).get("cell_gbs", 0))
             if bc["name"] != "rccl-comms1":
                 combo = {"name": bk["name"] + "+" + bc["name"].split("-")[1], "env": bk["env"],
                          "args": ["--transport", "rccl"] + bc["args"][2:]}
-                rec = run_row(args, combo, np_, exe, "combo")
+                rec = run_row(args, combo, np_, exe, "combo", t_end)
                 f.write(json.dumps(rec) + "\n")
                 done.append(rec)
                 print("%-40s rc=%d %6.1fs" % (rec["name"], rec["rc"], rec["seconds"]), flush=True)

@@ -176,16 +176,23 @@ def test_ring_token_chain_on_one_gpu(exe, tmp_path):
 
 def test_bench_two_ranks_ipc_push():
     """bench.py with the push engine as the headline transport (rendezvous +
-    remote writes), graphs off by construction."""
+    remote writes), graphs off by construction; then the xGMI pair sweep in
+    the time left (--xgmi-sweep 1: ranks sharing the GPU, so its IPC rows run
+    emulated, each an mpirun job of build/p2p_matrix, verified)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2", "--steps", "6", "--warmup", "3",
-           "--transport", "ipc:push", "--device", "0", "--latency-iters", "50", "--sweep-max", "64M", "--ipc-extra", "0"]
+           "--transport", "ipc:push", "--device", "0", "--latency-iters", "50", "--sweep-max", "64M", "--ipc-extra", "0",
+           "--xgmi-sweep", "1", "--xgmi-sweep-sizes", "4M"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
     progress = "\n".join(l for l in out.stderr.splitlines() if "bench:" in l or "fatal" in l)
     assert out.returncode == 0, progress
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert r["n_gpus"] == 2 and r["verify_mismatches"] == 0 and r["matrix_cells"] == "2/2" and r["value"] > 0
     assert r["p50_latency_us"] > 0
+    sw = r["xgmi_pair_sweep"]
+    assert sw["emulated"] == "ipc" and sw["rc"] == 0, sw
+    assert sorted(sw["rows"]) == ["ipc-kernel", "ipc-push", "ipc-sdma"], sw
+    assert all(row["rc"] == 0 and row["bi/4194304"]["cell_gbs"] > 0 for row in sw["rows"].values()), sw
 
 
 def test_bench_two_ranks_ipc():

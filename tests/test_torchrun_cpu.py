@@ -7,7 +7,9 @@ import os
 import subprocess
 import sys
 
-from conftest import ROOT, free_port
+import pytest
+
+from conftest import MPIRUN, ROOT, free_port
 
 
 def torchrun(nproc, args, timeout=240, env=None):
@@ -61,6 +63,31 @@ def test_bench_cpu_two_ranks(native):
     assert "GPU_MAX_HW_QUEUES" in prov["env"] and prov["runtime"]["rccl"]["library"]
     assert [d["rank"] for d in prov["rank_devices"]] == [0, 1] and len(prov["rank_links"]) == 2
     assert r["extras"]["ring_hop"]["hop_us_p50"] > 0 and r["matrix_samples"] == [[0, 4], [4, 0]]
+    assert r["xgmi_pair_sweep"] is None  # auto: only at N = 2 on two distinct GPUs
+
+
+@pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
+def test_bench_runs_the_pair_sweep_in_the_time_left(native, host_build):
+    """--xgmi-sweep 1: after every other section rank 0 runs
+    scripts/xgmi_pair_sweep.py (here on the CPU host transport) in the time
+    the deadline leaves and the line carries its verified rows and winner;
+    without the option a CPU run skips it (auto: N = 2 on distinct GPUs)."""
+    out = torchrun(2, ["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--transport", "host",
+                       "--size", "64K", "--msgs", "1", "--latency-iters", "10", "--sweep", "0", "--extras", "0",
+                       "--ipc-extra", "0", "--xgmi-sweep", "1", "--xgmi-sweep-sizes", "64K"])
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    sw = r["xgmi_pair_sweep"]
+    assert sw["rc"] == 0 and sw["emulated"] == "host", sw
+    assert sw["rows"]["host"]["rc"] == 0 and sw["rows"]["host"]["uni/65536"]["cell_gbs"] > 0, sw
+    assert sw["best"]["bi/65536"]["row"] == "host" and sw["budget_s"] > 0
+    # A sweep that cannot run is an error in its field, not a failed bench.
+    out = torchrun(2, ["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--transport", "host",
+                       "--size", "64K", "--msgs", "1", "--latency-iters", "10", "--sweep", "0", "--extras", "0",
+                       "--ipc-extra", "0", "--xgmi-sweep", "1"], env={"P2P_MPIRUN": "/nonexistent/mpirun"})
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert r["xgmi_pair_sweep"]["rc"] == 1 and "no mpirun" in r["xgmi_pair_sweep"]["error"], r["xgmi_pair_sweep"]
 
 
 def test_bench_comparison_failure_is_isolated(native):
