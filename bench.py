@@ -1098,12 +1098,14 @@ class BenchRun:
                    "emulated": emulate or None, "sizes": args.xgmi_sweep_sizes, "cell": "0 -> 1 (uni), 0 <-> 1 (bi)",
                    "rows": {}}
             rows_path = os.path.join(out, "rows.jsonl")
-            for line in (open(rows_path) if os.path.exists(rows_path) else []):
-                r = json.loads(line)
-                res["rows"][r["name"]] = dict(
-                    {"rc": r["rc"], "seconds": r.get("seconds")},
-                    **{k: {"cell_gbs": round(c["cell_gbs"], 2), "p50_us": round(c["p50_us"], 2)}
-                       for k, c in (r.get("cells") or {}).items()})
+            if os.path.exists(rows_path):
+                with open(rows_path) as f:
+                    for line in f:
+                        r = json.loads(line)
+                        res["rows"][r["name"]] = dict(
+                            {"rc": r["rc"], "seconds": r.get("seconds")},
+                            **{k: {"cell_gbs": round(c["cell_gbs"], 2), "p50_us": round(c["p50_us"], 2)}
+                               for k, c in (r.get("cells") or {}).items()})
             try:
                 with open(os.path.join(out, "summary.json")) as f:
                     summary = json.load(f)
