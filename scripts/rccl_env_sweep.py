@@ -51,10 +51,11 @@ def main():
             print("config %s failed rc=%d: %s" % (cfg, r.returncode, r.stderr[-500:]), flush=True)
             break  # never keep driving the GPU after a failure
         row = {"env": cfg, "gbs": {}}
-        for line in open(js):
-            rec = json.loads(line)
-            if rec["type"] == "run":
-                row["gbs"][rec["bytes"]] = rec["gbs_mean"]
+        with open(js) as fh:
+            for line in fh:
+                rec = json.loads(line)
+                if rec["type"] == "run":
+                    row["gbs"][rec["bytes"]] = rec["gbs_mean"]
         table.append(row)
         print(json.dumps(row), flush=True)
     with open(os.path.join(a.out, "summary.json"), "w") as f:

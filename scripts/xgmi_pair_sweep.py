@@ -141,22 +141,23 @@ def plan_rows(args, np_):
 def cell_result(js_path, dirs):
     """{(dir, bytes): {...}} for the 0-1 cell of every pair run in the file."""
     out = {}
-    for line in open(js_path):
-        rec = json.loads(line)
-        if rec.get("type") != "run" or rec.get("dir") not in dirs:
-            continue
-        for ph in rec["phases"]:
-            if (ph["row"], ph["col"]) != (0, 1):
+    with open(js_path) as fh:
+        for line in fh:
+            rec = json.loads(line)
+            if rec.get("type") != "run" or rec.get("dir") not in dirs:
                 continue
-            flows = ph["flows"]
-            gbs = [f["gbs"] for f in flows]
-            out[(rec["dir"], rec["bytes"])] = {
-                "cell_gbs": sum(gbs),  # bi: both directions, like the reference's bi matrix
-                "per_dir_gbs": sum(gbs) / len(gbs),
-                "p50_us": max(f["iter_us"]["p50"] for f in flows),
-                "mismatches": ph["mismatches"],
-                "iters": rec["iters"],
-            }
+            for ph in rec["phases"]:
+                if (ph["row"], ph["col"]) != (0, 1):
+                    continue
+                flows = ph["flows"]
+                gbs = [f["gbs"] for f in flows]
+                out[(rec["dir"], rec["bytes"])] = {
+                    "cell_gbs": sum(gbs),  # bi: both directions, like the reference's bi matrix
+                    "per_dir_gbs": sum(gbs) / len(gbs),
+                    "p50_us": max(f["iter_us"]["p50"] for f in flows),
+                    "mismatches": ph["mismatches"],
+                    "iters": rec["iters"],
+                }
     return out
 
 
@@ -253,10 +254,11 @@ def main(argv=None) -> int:
     if args.resume and os.path.exists(rows_path):
         # Rows that finished (clean or corrupt) are kept; a row that crashed
         # or timed out runs again.
-        for line in open(rows_path):
-            rec = json.loads(line)
-            if rec.get("rc") in (0, 2):
-                kept[rec["name"]] = rec
+        with open(rows_path) as fh:
+            for line in fh:
+                rec = json.loads(line)
+                if rec.get("rc") in (0, 2):
+                    kept[rec["name"]] = rec
     with open(rows_path, "w") as f:
         for rec in kept.values():
             f.write(json.dumps(rec) + "\n")
