@@ -134,7 +134,29 @@ def scaling_table(results: Iterable[dict]) -> str:
             _get(r, "ipc_transport", "relay", "value_gbs"), relay_pair.get("gbs", "-"),
             _get(r, "ipc_transport", "device_pingpong_p50_us", fmt="%.2f"),
             "%s -> %s" % (fb["from"], fb["to"]) if fb else "-"))
+    for r in rows:
+        out += pair_sweep_lines(r)
     return "\n".join(out)
+
+
+def pair_sweep_lines(r: dict) -> List[str]:
+    """The winner per cell of a line's xGMI pair sweep (bench.py
+    --xgmi-sweep, on at N = 2): row, GB/s (bi: both directions) and the gain
+    over RCCL with one communicator and no knobs; corrupt and skipped rows."""
+    sw = r.get("xgmi_pair_sweep")
+    if not isinstance(sw, dict):
+        return []
+    head = "xGMI pair sweep, %d GPUs%s:" % (r["n_gpus"], " (emulated: %s)" % sw["emulated"] if sw.get("emulated") else "")
+    if not sw.get("best"):
+        return ["", head + " %s" % (sw.get("error") or "no verified row")[:200]]
+    out = ["", head]
+    for cell, b in sorted(sw["best"].items()):
+        gain = " (%.2fx RCCL, 1 communicator)" % b["gain"] if b.get("gain") else ""
+        out.append("- %s: %s %.2f GB/s%s" % (cell, b["row"], b["cell_gbs"], gain))
+    for key in ("corrupt", "skipped"):
+        if sw.get(key):
+            out.append("- %s rows: %s" % (key, ", ".join(sw[key])))
+    return out
 
 
 def summarize_compat(text: str) -> str:

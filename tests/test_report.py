@@ -67,3 +67,21 @@ def test_scaling_table_comparisons_and_cli(tmp_path, capsys):
     assert main(files) == 0
     out = capsys.readouterr().out
     assert "== scaling" in out and "| 8 | 95.0 |" in out.split("== scaling")[1]
+
+
+def test_scaling_table_pair_sweep():
+    """The N = 2 line's xGMI pair sweep: winner per cell with its gain over
+    RCCL on one communicator, corrupt and skipped rows."""
+    sw = {"rc": 2, "emulated": None, "best": {
+        "bi/33554432": {"row": "rccl-comms4", "cell_gbs": 201.5, "gain": 1.42},
+        "uni/1073741824": {"row": "ipc-push", "cell_gbs": 110.25, "gain": None}},
+        "corrupt": ["rccl-nchannels_per_peer=8"], "skipped": ["rccl-register=2"]}
+    t = scaling_table([{"n_gpus": 2, "value": 100.0, "aggregate_gbs": 200.0, "xgmi_pair_sweep": sw},
+                       {"n_gpus": 4, "value": 90.0, "aggregate_gbs": 360.0, "xgmi_pair_sweep": None}])
+    lines = t.splitlines()
+    assert "xGMI pair sweep, 2 GPUs:" in lines
+    assert "- bi/33554432: rccl-comms4 201.50 GB/s (1.42x RCCL, 1 communicator)" in lines
+    assert "- uni/1073741824: ipc-push 110.25 GB/s" in lines
+    assert "- corrupt rows: rccl-nchannels_per_peer=8" in lines and "- skipped rows: rccl-register=2" in lines
+    failed = scaling_table([{"n_gpus": 2, "value": 1.0, "xgmi_pair_sweep": {"rc": 1, "error": "no mpirun at x"}}])
+    assert "xGMI pair sweep, 2 GPUs: no mpirun at x" in failed
