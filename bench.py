@@ -1106,6 +1106,18 @@ class BenchRun:
                             {"rc": r["rc"], "seconds": r.get("seconds")},
                             **{k: {"cell_gbs": round(c["cell_gbs"], 2), "p50_us": round(c["p50_us"], 2)}
                                for k, c in (r.get("cells") or {}).items()})
+            # The best RCCL row per cell too: the setting the headline itself
+            # could use on this link (the IPC engines are a different data plane).
+            base = res["rows"].get("rccl-comms1", {})
+            best_rccl = {}
+            for name, row in res["rows"].items():
+                for cell, c in row.items():
+                    if name.startswith("rccl-") and row["rc"] == 0 and isinstance(c, dict) and (
+                            cell not in best_rccl or c["cell_gbs"] > best_rccl[cell]["cell_gbs"]):
+                        b0 = (base.get(cell) or {}).get("cell_gbs")
+                        best_rccl[cell] = {"row": name, "cell_gbs": c["cell_gbs"],
+                                           "gain": round(c["cell_gbs"] / b0, 4) if b0 else None}
+            res["best_rccl"] = best_rccl or None
             try:
                 with open(os.path.join(out, "summary.json")) as f:
                     summary = json.load(f)

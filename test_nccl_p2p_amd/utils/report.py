@@ -153,6 +153,10 @@ def pair_sweep_lines(r: dict) -> List[str]:
     for cell, b in sorted(sw["best"].items()):
         gain = " (%.2fx RCCL, 1 communicator)" % b["gain"] if b.get("gain") else ""
         out.append("- %s: %s %.2f GB/s%s" % (cell, b["row"], b["cell_gbs"], gain))
+    for cell, b in sorted((sw.get("best_rccl") or {}).items()):
+        if b["row"] != (sw["best"].get(cell) or {}).get("row"):
+            gain = " (%.2fx)" % b["gain"] if b.get("gain") else ""
+            out.append("- %s, best RCCL: %s %.2f GB/s%s" % (cell, b["row"], b["cell_gbs"], gain))
     for key in ("corrupt", "skipped"):
         if sw.get(key):
             out.append("- %s rows: %s" % (key, ", ".join(sw[key])))

@@ -75,13 +75,17 @@ def test_scaling_table_pair_sweep():
     sw = {"rc": 2, "emulated": None, "best": {
         "bi/33554432": {"row": "rccl-comms4", "cell_gbs": 201.5, "gain": 1.42},
         "uni/1073741824": {"row": "ipc-push", "cell_gbs": 110.25, "gain": None}},
-        "corrupt": ["rccl-nchannels_per_peer=8"], "skipped": ["rccl-register=2"]}
+        "corrupt": ["rccl-nchannels_per_peer=8"], "skipped": ["rccl-register=2"],
+        "best_rccl": {"bi/33554432": {"row": "rccl-comms4", "cell_gbs": 201.5, "gain": 1.42},
+                      "uni/1073741824": {"row": "rccl-proto=Simple", "cell_gbs": 70.0, "gain": 1.05}}}
     t = scaling_table([{"n_gpus": 2, "value": 100.0, "aggregate_gbs": 200.0, "xgmi_pair_sweep": sw},
                        {"n_gpus": 4, "value": 90.0, "aggregate_gbs": 360.0, "xgmi_pair_sweep": None}])
     lines = t.splitlines()
     assert "xGMI pair sweep, 2 GPUs:" in lines
     assert "- bi/33554432: rccl-comms4 201.50 GB/s (1.42x RCCL, 1 communicator)" in lines
     assert "- uni/1073741824: ipc-push 110.25 GB/s" in lines
+    assert "- uni/1073741824, best RCCL: rccl-proto=Simple 70.00 GB/s (1.05x)" in lines
+    assert not any(l.startswith("- bi/33554432, best RCCL") for l in lines)  # the overall winner already
     assert "- corrupt rows: rccl-nchannels_per_peer=8" in lines and "- skipped rows: rccl-register=2" in lines
     failed = scaling_table([{"n_gpus": 2, "value": 1.0, "xgmi_pair_sweep": {"rc": 1, "error": "no mpirun at x"}}])
     assert "xGMI pair sweep, 2 GPUs: no mpirun at x" in failed
