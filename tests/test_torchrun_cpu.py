@@ -90,6 +90,27 @@ def test_bench_runs_the_pair_sweep_in_the_time_left(native, host_build):
     assert r["xgmi_pair_sweep"]["rc"] == 1 and "no mpirun" in r["xgmi_pair_sweep"]["error"], r["xgmi_pair_sweep"]
 
 
+def test_bench_pair_sweep_row_that_hangs_is_killed(native, host_build, tmp_path):
+    """A sweep row that never ends (a launcher that hangs) is killed with its
+    whole job at the sweep's budget, the sweep stops there (failed_row), the
+    line is still printed, and nothing the row started is left running."""
+    import psutil
+    fake = tmp_path / "hanging_mpirun.sh"
+    fake.write_text("#!/bin/sh\nsleep 600\n")
+    fake.chmod(0o755)
+    out = torchrun(2, ["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--transport", "host",
+                       "--size", "64K", "--msgs", "1", "--latency-iters", "10", "--sweep", "0", "--extras", "0",
+                       "--ipc-extra", "0", "--xgmi-sweep", "1", "--xgmi-sweep-sizes", "64K", "--deadline", "75"],
+                   env={"P2P_MPIRUN": str(fake)})
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    sw = r["xgmi_pair_sweep"]
+    assert sw["failed_row"] == "host" and sw["rows"]["host"]["rc"] == 124, sw
+    assert not r.get("deadline_hit")
+    left = [p.pid for p in psutil.process_iter(["cmdline"]) if str(fake) in " ".join(p.info["cmdline"] or [])]
+    assert left == [], left
+
+
 def test_bench_comparison_failure_is_isolated(native):
     """A comparison process that dies or hangs (here: killed at its time
     limit) is reported in the JSON; the headline line is still printed."""
