@@ -126,3 +126,17 @@ def test_cli_fuzz_all_gpus(exe, args):
                          capture_output=True, text=True, timeout=900)
     assert out.returncode == 0, out.stderr[-3000:]
     assert "all verified" in out.stdout
+
+
+def test_bench_two_gpus_pair_sweep():
+    """The driver's N = 2 bench on two distinct GPUs: after the other sections
+    the time left goes to the xGMI pair sweep (on by default there), whose
+    rows cross the real link, every one verified."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2", "--steps", "14", "--warmup", "7"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    sw = r["xgmi_pair_sweep"]
+    assert sw["emulated"] is None and sw["rows"]["rccl-comms1"]["rc"] == 0, sw
+    assert sw["best"] and sw["best_rccl"], sw
