@@ -228,7 +228,11 @@ def run_child(state, cmd, timeout, **kw):
     process at the deadline) takes the child and everything it started down
     with it; at `timeout` the same happens here.  Returns the exit status, or
     "timeout"."""
-    proc = subprocess.Popen(cmd, start_new_session=True, **kw)
+    from test_nccl_p2p_amd.utils.proc import child_env
+
+    # A session of its own (one killpg takes the whole tree down), and
+    # P2P_PARENT_PID so the child dies with this process (utils/proc.py).
+    proc = subprocess.Popen(cmd, start_new_session=True, env=child_env(kw.pop("env", None)), **kw)
     state.setdefault("children", []).append(proc)
     try:
         return proc.wait(timeout=timeout)
@@ -350,6 +354,9 @@ def child_main(args) -> int:
     main).  Bootstraps its own native TCP star on --child-port (no
     torch.distributed: the parent's store is busy) and writes rank 0's result
     to --child-out."""
+    from test_nccl_p2p_amd.utils.proc import die_with_parent
+
+    die_with_parent()
     claim_stdout()
     from test_nccl_p2p_amd import require_native
     from test_nccl_p2p_amd.parallel.session import dist_env

@@ -52,6 +52,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from test_nccl_p2p_amd.utils import rccl_env  # noqa: E402
+from test_nccl_p2p_amd.utils.proc import die_with_parent, pdeathsig_prefix  # noqa: E402
 MPIRUN = os.environ.get("P2P_MPIRUN", "/opt/conda/bin/mpirun")
 # --emulate rccl: one host id per rank, so RCCL accepts ranks sharing GPU 0
 # (csrc/transport_rccl.cpp) and connects them through loopback sockets.
@@ -169,8 +170,11 @@ def run_row(args, row, np_, exe, tag, t_end=None):
     if os.path.exists(js):
         os.remove(js)
     limit = args.row_timeout if t_end is None else max(5.0, min(args.row_timeout, t_end - time.time()))
-    cmd = [MPIRUN, "-n", str(np_), exe, "--mode", "pair", "--cells", "0-1", "--dir", "both", "--sizes", args.sizes,
-           "-n", args.iters, "--verify", "--no-compat", "--json", js, "--timeout", str(max(5, int(limit) - 5))]
+    # setpriv --pdeathsig: the launcher dies with this script (bench.py starts
+    # the sweep as a child that dies with the bench, utils/proc.py).
+    cmd = pdeathsig_prefix() + [
+        MPIRUN, "-n", str(np_), exe, "--mode", "pair", "--cells", "0-1", "--dir", "both", "--sizes", args.sizes,
+        "-n", args.iters, "--verify", "--no-compat", "--json", js, "--timeout", str(max(5, int(limit) - 5))]
     cmd += row["args"]
     if args.emulate in ("ipc", "rccl"):
         cmd += ["--device", "0"]
@@ -225,6 +229,7 @@ def summarize(rows, dirs, sizes_seen):
 
 
 def main(argv=None) -> int:
+    die_with_parent()  # when started by bench.py (P2P_PARENT_PID)
     args = parse_args(argv)
     np_ = args.np or (2 if args.emulate else visible_gpus())
     if np_ < 2:

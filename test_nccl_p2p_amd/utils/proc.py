@@ -1,0 +1,51 @@
+"""Child processes that cannot outlive the run that started them.
+
+bench.py starts its untimed comparisons and the xGMI pair sweep as child jobs
+in sessions of their own, so that a timeout can kill a job's whole tree
+(launcher, proxies, ranks) with one killpg.  A session of its own also takes
+the child out of the launcher's process group, though: should the driver kill
+the bench (its process group) the child would keep driving a GPU.  The child
+therefore asks the kernel to kill it when its parent goes (PR_SET_PDEATHSIG),
+and checks that the parent it was started for is still the one it has, for
+the case where the parent died before the request took effect.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import signal
+
+PARENT_ENV = "P2P_PARENT_PID"
+_PR_SET_PDEATHSIG = 1
+
+
+def child_env(env=None) -> dict:
+    """The environment for a child that should die with this process."""
+    return dict(os.environ if env is None else env, **{PARENT_ENV: str(os.getpid())})
+
+
+def die_with_parent() -> bool:
+    """In a child started with child_env(): SIGKILL when the parent exits
+    (Linux; a no-op elsewhere or without the variable).  Exits at once if the
+    parent is already gone.  True when the request is in place."""
+    expected = os.environ.get(PARENT_ENV)
+    if not expected:
+        return False
+    try:
+        import ctypes
+
+        libc = ctypes.CDLL(None, use_errno=True)
+        if libc.prctl(_PR_SET_PDEATHSIG, int(signal.SIGKILL), 0, 0, 0) != 0:
+            return False
+    except (OSError, AttributeError):
+        return False
+    if os.getppid() != int(expected):
+        os._exit(1)
+    return True
+
+
+def pdeathsig_prefix() -> list:
+    """Command prefix giving a launched program the same guarantee
+    (util-linux setpriv), or [] where setpriv is missing."""
+    exe = shutil.which("setpriv")
+    return [exe, "--pdeathsig", "KILL"] if exe else []

@@ -78,3 +78,29 @@ def test_python_module_cli(native, argv):
 def test_gate_probe_unsupported_on_cpu(native):
     sess = native.Session(0, 1, transport="host")
     assert json.loads(sess.gate_probe(0.1, True)) == {"supported": False}
+
+
+def test_child_dies_with_its_parent():
+    """utils.proc: a child in a session of its own (out of reach of a kill of
+    its parent's process group) that called die_with_parent() is killed by
+    the kernel when its parent exits."""
+    import psutil
+    import time
+    child = ("from test_nccl_p2p_amd.utils.proc import die_with_parent; import time; "
+             "assert die_with_parent(); time.sleep(120)")
+    parent = ("import subprocess, sys, time; from test_nccl_p2p_amd.utils.proc import child_env; "
+              "p = subprocess.Popen([sys.executable, '-c', %r], env=child_env(), start_new_session=True, "
+              "stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL); "
+              "print(p.pid, flush=True); time.sleep(4)" % child)
+    out = subprocess.run([sys.executable, "-c", parent], capture_output=True, text=True, cwd=ROOT, timeout=60)
+    pid = int(out.stdout.split()[0])
+    for _ in range(100):
+        try:
+            if psutil.Process(pid).status() == psutil.STATUS_ZOMBIE:
+                break
+        except psutil.NoSuchProcess:
+            break
+        time.sleep(0.1)
+    else:
+        os.kill(pid, 9)
+        raise AssertionError("the child outlived its parent")
