@@ -641,6 +641,9 @@ class BenchRun:
         drv.connect()
         drv.run_steps(0, args.warmup)
         drv.sync()
+        chunking = None
+        if transport == "rccl" and not args.no_verify and args.warmup > 0:
+            chunking = self.verify_warmup(drv, [x for x in (sess, ref_sess) if x is not None])
         drv.poison()  # untimed: every receive slot zeroed; a slot passes verification only if a timed step wrote it
         self.gpu_sync()
         drv.reset()
@@ -682,7 +685,38 @@ class BenchRun:
             failed=failed, reason=reason, tuning=tuning, elapsed=elapsed, flows_total=flows_total, value=value,
             aggregate=aggregate, my_ms=my_ms, matrix=matrix, samples=samples, cells=cells, offdiag=offdiag,
             expected=n * (n - 1) if n > 1 else 1, vr=vr, mismatches=vr["mismatches"] if vr else -1, depth=depth,
-            recv_bytes=recv_bytes)
+            recv_bytes=recv_bytes, chunking=chunking)
+
+    def verify_warmup(self, drv, sessions):
+        """RCCL 2.26 delivers exactly half of a message whose share of one p2p
+        channel exceeds 16 MiB, silently; the transport posts messages in ops
+        under that for the channel counts it can know (transport_rccl.cpp),
+        but RCCL does not report how many channels it gives a remote peer.
+        So the warmup's deliveries are verified (collectively), and should
+        any word be wrong every session posts its messages as smaller ops
+        (16, 4, 1 MiB) and the warmup runs again, until it verifies.  Returns
+        what was seen and done (posting.chunking)."""
+        args = self.args
+        peer = (self.env.rank + 1) % self.n
+        bad = drv.verify_steps(0, args.warmup)["mismatches"]
+        out = {"max_chunk_bytes": sessions[0].max_chunk(peer), "warmup_mismatches": bad, "fallback": None}
+        tried = []
+        for c in (16 << 20, 4 << 20, 1 << 20):
+            if bad == 0:
+                break
+            current = sessions[0].max_chunk(peer)
+            if current and c >= current:
+                continue
+            self.log0("bench: %d wrong words in the warmup: messages now posted as ops of <= %d MiB" % (bad, c >> 20))
+            for s in sessions:
+                s.set_max_chunk(c)
+            drv.run_steps(0, args.warmup)
+            drv.sync()
+            bad = drv.verify_steps(0, args.warmup)["mismatches"]
+            tried.append({"max_chunk_bytes": c, "warmup_mismatches": bad})
+        if tried:
+            out.update(fallback=tried, max_chunk_bytes=sessions[0].max_chunk(peer))
+        return out
 
     def headline(self):
         """Measures the headline; should RCCL itself fail on this node
@@ -780,7 +814,7 @@ class BenchRun:
             "recv_slot_generations": h.depth,
             "recv_slot_bytes_per_rank": h.recv_bytes,
             "transport": headline_transport,
-            "posting": {"batch": bool(h.batch), "graph": bool(args.graph), "rccl_comms": h.comms,
+            "posting": {"batch": bool(h.batch), "graph": bool(args.graph), "rccl_comms": h.comms, "chunking": h.chunking,
                         "dropped": h.failed or None, "selection": h.reason,
                         "tuning_ms_per_step": {"comms%d_%s" % (c, "batch" if b else "per_message"): round(v * 1e3, 4)
                                                for (c, b), v in h.tuning.items()} or None},

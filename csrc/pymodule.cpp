@@ -153,6 +153,11 @@ class Session {
     boot_->set_timeout(seconds);
   }
 
+  // Largest op a message is posted as (RCCL: 16 MiB per p2p channel, see
+  // transport_rccl.cpp); set on every rank alike.
+  bool set_max_chunk(size_t bytes) { return t_->set_max_chunk(bytes); }
+  size_t max_chunk(int peer) const { return t_->max_chunk(peer); }
+
   // Collective: provenance_json() for this session's ranks.
   std::string provenance(int device) { return provenance_json(*boot_, device); }
 
@@ -274,6 +279,10 @@ PYBIND11_MODULE(_p2pcore, m) {
            "Dependent ring token chain 0 -> 1 -> ... -> 0 (collective); JSON with per-hop and per-lap times.")
       .def("set_timeout", &Session::set_timeout, py::arg("seconds"),
            "Bounds every later wait of the session (transport sync / rendezvous, bootstrap receives).")
+      .def("set_max_chunk", &Session::set_max_chunk, py::arg("bytes"),
+           "Posts messages to every peer as ops of at most `bytes` (0: unsplit); False where nothing is split. "
+           "Call it on every rank with the same value.")
+      .def("max_chunk", &Session::max_chunk, py::arg("peer"), "Largest op a message to `peer` is posted as (0: unsplit).")
       .def("provenance", &Session::provenance, py::arg("device") = -1, py::call_guard<py::gil_scoped_release>(),
            "Collective: runtime, RCCL library, knobs, every rank's GPU and the links between them (JSON).")
       .def("_unmatched_recv", &Session::unmatched_recv, py::arg("bytes") = size_t{1} << 20,

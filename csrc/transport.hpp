@@ -154,6 +154,13 @@ class Transport {
   virtual void gate_release() {}
   virtual bool gate_timed_out() { return false; }
 
+  // ---- message chunking (RCCL) ----
+  // Largest single op a message to a peer is posted as (0 = unsplit), and
+  // setting it for every peer (0 = no splitting); both ends must use the same
+  // value, so callers set it collectively.  false / 0 where nothing is split.
+  virtual bool set_max_chunk(size_t /*bytes*/) { return false; }
+  virtual size_t max_chunk(int /*peer*/) const { return 0; }
+
   // ---- health ----
   // Non-empty when the transport saw an asynchronous error (e.g. a peer died).
   virtual std::string async_error() { return ""; }

@@ -224,16 +224,24 @@ class RcclTransport final : public Transport {
       used_.resize(cstreams_.size(), false);
     }
   }
-  // Messages above max_chunk_ are posted as several back-to-back ops of at
-  // most max_chunk_ bytes inside the same group (matched in order on both
-  // sides).  On MI355X, RCCL 2.26/2.27 deliver only half of a single
-  // ncclSend/ncclRecv of >= 2 GiB (scripts/rccl_size_probe.py); 1 GiB chunks
-  // are exact and run at the same bandwidth.  P2P_RCCL_MAX_CHUNK=0 disables.
+  // Messages above the peer's chunk are posted as several back-to-back ops of
+  // at most that many bytes inside the same group (matched in order on both
+  // sides).  RCCL 2.26 on MI355X delivers exactly half of a send/recv whose
+  // share of one p2p channel exceeds 16 MiB: with its 64 p2p channels that
+  // is any message above 1 GiB (scripts/rccl_size_probe.py), with
+  // NCCL_MAX_P2P_NCHANNELS=1 / 2 / 4 / 8 anything above 16 / 32 / 64 / 128
+  // MiB (profiles/r2_rccl_channels/p2p_threshold/).  Chunks therefore stay
+  // at 16 MiB x channels: 64 channels (or fewer, as the NCCL_* channel knobs
+  // set) to this rank itself; to other ranks, whose per-peer channel count
+  // RCCL derives from the topology and does not report, 2 channels' worth
+  // (32 MiB, the bench's message size; bench.py halves it further should
+  // its warmup not verify).  P2P_RCCL_MAX_CHUNK=<bytes> sets every peer's,
+  // 0 disables splitting.
   void send(const void* p, size_t bytes, int peer) override {
     const int j = pick(&send_seq_, peer, bytes);
     const char* c = static_cast<const char*>(p);
     do {
-      size_t n = chunk_of(bytes);
+      size_t n = chunk_of(bytes, peer);
       issue({j, true, const_cast<char*>(c), n, peer, cstreams_[static_cast<size_t>(j)]});
       c += n;
       bytes -= n;
@@ -245,7 +253,7 @@ class RcclTransport final : public Transport {
     // Injected skip fault: the receive completes into a private sink.
     char* c = static_cast<char*>(discarding() ? discard_sink(bytes) : p);
     do {
-      size_t n = chunk_of(bytes);
+      size_t n = chunk_of(bytes, peer);
       issue({j, false, c, n, peer, s});
       c += n;
       bytes -= n;
@@ -392,6 +400,12 @@ class RcclTransport final : public Transport {
 
   int concurrency() const override { return static_cast<int>(comms_.size()); }
   // Small messages (latency) run on communicator 0, on the main stream.
+  bool set_max_chunk(size_t bytes) override {
+    self_chunk_ = peer_chunk_ = bytes;
+    return true;
+  }
+  size_t max_chunk(int peer) const override { return chunk_for(peer); }
+
   bool gate_arm(double timeout_s) override {
     if (main_idle_) return false;
     gate_.arm(stream_, timeout_s);
@@ -478,7 +492,10 @@ class RcclTransport final : public Transport {
       for (auto& id : ids) nccl_ok(ncclGetUniqueId(&id), "ncclGetUniqueId");
     boot.bcast(ids.data(), sizeof(ncclUniqueId) * ids.size(), 0);
 
-    if (const char* mc = std::getenv("P2P_RCCL_MAX_CHUNK")) max_chunk_ = std::strcmp(mc, "0") ? parse_size(mc) : 0;
+    self_chunk_ = kChunkPerChannel * static_cast<size_t>(p2p_channel_limit(64));
+    peer_chunk_ = kChunkPerChannel * static_cast<size_t>(p2p_channel_limit(2));
+    if (const char* mc = std::getenv("P2P_RCCL_MAX_CHUNK"))
+      self_chunk_ = peer_chunk_ = std::strcmp(mc, "0") ? parse_size(mc) : 0;
     if (const char* sm = std::getenv("P2P_RCCL_SPLIT_MIN")) split_min_ = parse_size(sm);
     if (const char* rg = std::getenv("P2P_RCCL_REGISTER")) register_ = std::atoi(rg);
     const char* blk = std::getenv("P2P_RCCL_BLOCKING");
@@ -648,9 +665,24 @@ class RcclTransport final : public Transport {
   hipStream_t recv_stream_ = nullptr;  // two-stream (reference) layout only
   hipEvent_t join_ = nullptr;
   bool recv_on_side_ = false;
-  size_t max_chunk_ = kDefaultMaxChunk;
-  static constexpr size_t kDefaultMaxChunk = size_t{1} << 30;
-  size_t chunk_of(size_t bytes) const { return (max_chunk_ && bytes > max_chunk_) ? max_chunk_ : bytes; }
+  // Message chunking (see send()): 16 MiB per RCCL p2p channel.
+  static constexpr size_t kChunkPerChannel = size_t{16} << 20;
+  size_t self_chunk_ = kChunkPerChannel * 64;
+  size_t peer_chunk_ = kChunkPerChannel * 2;
+  // `fallback` channels, or fewer where NCCL_MAX_P2P_NCHANNELS /
+  // NCCL_NCHANNELS_PER_PEER ask RCCL for fewer.
+  static int p2p_channel_limit(int fallback) {
+    int c = fallback;
+    for (const char* k : {"NCCL_MAX_P2P_NCHANNELS", "NCCL_NCHANNELS_PER_PEER"})
+      if (const char* v = std::getenv(k))
+        if (const int x = std::atoi(v); x > 0) c = std::min(c, x);
+    return c;
+  }
+  size_t chunk_for(int peer) const { return peer == rank_ ? self_chunk_ : peer_chunk_; }
+  size_t chunk_of(size_t bytes, int peer) const {
+    const size_t c = chunk_for(peer);
+    return (c && bytes > c) ? c : bytes;
+  }
   std::vector<ncclComm_t> comms_;      // comms_[0] on stream_
   std::vector<hipStream_t> cstreams_;  // stream of each communicator (cstreams_[0] == stream_ unless main_idle_)
   std::vector<hipEvent_t> cjoin_;      // per communicator with a side stream: joins it into stream_

@@ -126,6 +126,29 @@ def test_bench_drops_a_failing_communicator_candidate():
         assert r["verify_mismatches"] == 0 and r["value"] > 10
 
 
+def test_bench_chunks_around_rccl_half_delivery():
+    """RCCL 2.26 delivers exactly half of a send/recv whose share of one p2p
+    channel exceeds 16 MiB.  With one p2p channel (NCCL_MAX_P2P_NCHANNELS=1)
+    the transport posts the bench's 32 MiB messages as 16 MiB ops by itself;
+    with that turned off (P2P_RCCL_MAX_CHUNK=0) the bench's verified warmup
+    sees the loss, reposts as 16 MiB ops, and the timed steps verify."""
+    base = [sys.executable, "bench.py", "--steps", "4", "--warmup", "2", "--comms", "1", "--ipc-extra", "0",
+            "--ref-iters", "0", "--latency-iters", "20"]
+    runs = {}
+    for name, extra in (("transport", {}), ("fallback", {"P2P_RCCL_MAX_CHUNK": "0"})):
+        out = subprocess.run(base, capture_output=True, text=True, timeout=600, cwd=ROOT,
+                             env=dict(os.environ, NCCL_MAX_P2P_NCHANNELS="1", **extra))
+        assert out.returncode == 0, out.stderr[-3000:]
+        runs[name] = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+        assert runs[name]["verify_mismatches"] == 0 and runs[name]["verify_coverage"] == 1.0, runs[name]
+    ch = runs["transport"]["posting"]["chunking"]
+    assert ch == {"max_chunk_bytes": 16 << 20, "warmup_mismatches": 0, "fallback": None}, ch
+    ch = runs["fallback"]["posting"]["chunking"]
+    assert ch["warmup_mismatches"] > 0, ch
+    assert ch["fallback"] == [{"max_chunk_bytes": 16 << 20, "warmup_mismatches": 0}], ch
+    assert ch["max_chunk_bytes"] == 16 << 20
+
+
 def test_bench_headline_falls_back_to_ipc():
     """Should RCCL fail on the node (injected on every rank), the timed steps
     run through the IPC data plane and the line names the fallback."""
