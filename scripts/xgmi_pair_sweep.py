@@ -11,7 +11,10 @@ build/p2p_matrix under every setting that can move a single xGMI link:
               P2P_RCCL_REGISTER=1|2 (user buffers registered with every
               communicator / allocated by ncclMemAlloc: RCCL may then move
               data straight between the user buffers instead of through its
-              staging FIFO, csrc/transport_rccl.cpp)
+              staging FIFO, csrc/transport_rccl.cpp),
+              P2P_RCCL_MAX_CHUNK=1G (1 GiB ops instead of 32 MiB ones: RCCL
+              loses half of an op above 16 MiB per p2p channel, so this row
+              tells whether the link gets >= 64 channels)
   ipc rows    --ipc-engine kernel (one-sided pull by the gfx950 copy kernel),
               sdma, push, relay (stripes through idle third GPUs, N >= 3)
 
@@ -77,6 +80,10 @@ RCCL_KNOBS = [
     {"NCCL_P2P_READ_ENABLE": "1"},
     {"P2P_RCCL_REGISTER": "1"},
     {"P2P_RCCL_REGISTER": "2"},
+    # Ops of up to 1 GiB to the peer instead of the transport's 32 MiB: exact
+    # only if RCCL gives the link >= 64 p2p channels (16 MiB each); "corrupt"
+    # otherwise, which measures the channel count it does not report.
+    {"P2P_RCCL_MAX_CHUNK": "1G"},
 ]
 COMMS = [1, 2, 4, 8]
 IPC_ENGINES = ["kernel", "sdma", "push", "relay"]
