@@ -60,7 +60,6 @@ import json
 import math
 import os
 import shutil
-import signal
 import socket
 import statistics
 import subprocess
@@ -74,6 +73,8 @@ T0 = time.monotonic()  # the deadline counts from here (process start, give or t
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
+
+from test_nccl_p2p_amd.utils.proc import kill_children, run_child  # noqa: E402
 
 METRIC = "pairwise P2P GB/s matrix (min/mean) + p50 latency at 1/2/4/8 MI355X"
 BASELINE_VALUE = None  # the reference publishes no numbers
@@ -220,36 +221,6 @@ class Reporter:
                 with open(self.json_out, "w") as f:
                     f.write(line + "\n")
             return True
-
-
-def run_child(state, cmd, timeout, **kw):
-    """Runs a child process in a session of its own, registered in
-    state["children"] while it runs, so that the watchdog (which ends this
-    process at the deadline) takes the child and everything it started down
-    with it; at `timeout` the same happens here.  Returns the exit status, or
-    "timeout"."""
-    from test_nccl_p2p_amd.utils.proc import child_env
-
-    # A session of its own (one killpg takes the whole tree down), and
-    # P2P_PARENT_PID so the child dies with this process (utils/proc.py).
-    proc = subprocess.Popen(cmd, start_new_session=True, env=child_env(kw.pop("env", None)), **kw)
-    state.setdefault("children", []).append(proc)
-    try:
-        return proc.wait(timeout=timeout)
-    except subprocess.TimeoutExpired:
-        kill_children(state, [proc])
-        return "timeout"
-    finally:
-        state["children"].remove(proc)
-
-
-def kill_children(state, procs=None):
-    for proc in list(procs if procs is not None else state.get("children", [])):
-        try:
-            os.killpg(proc.pid, signal.SIGKILL)
-        except (ProcessLookupError, PermissionError):
-            pass
-        proc.wait()
 
 
 def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> threading.Event:

@@ -14,6 +14,7 @@ from __future__ import annotations
 import os
 import shutil
 import signal
+import subprocess
 
 PARENT_ENV = "P2P_PARENT_PID"
 _PR_SET_PDEATHSIG = 1
@@ -49,3 +50,29 @@ def pdeathsig_prefix() -> list:
     (util-linux setpriv), or [] where setpriv is missing."""
     exe = shutil.which("setpriv")
     return [exe, "--pdeathsig", "KILL"] if exe else []
+
+
+def run_child(state: dict, cmd, timeout: float, **kw):
+    """Runs `cmd` in a session of its own (one killpg takes its whole tree
+    down) with child_env(), registered in state["children"] while it runs so
+    that a watchdog can kill_children(state) before ending the process; at
+    `timeout` the same happens here.  Returns the exit status, or "timeout"."""
+    proc = subprocess.Popen(cmd, start_new_session=True, env=child_env(kw.pop("env", None)), **kw)
+    state.setdefault("children", []).append(proc)
+    try:
+        return proc.wait(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        kill_children(state, [proc])
+        return "timeout"
+    finally:
+        state["children"].remove(proc)
+
+
+def kill_children(state: dict, procs=None) -> None:
+    """SIGKILL to the sessions of `procs` (default: every registered child)."""
+    for proc in list(procs if procs is not None else state.get("children", [])):
+        try:
+            os.killpg(proc.pid, signal.SIGKILL)
+        except (ProcessLookupError, PermissionError):
+            pass
+        proc.wait()
