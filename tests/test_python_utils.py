@@ -80,6 +80,14 @@ def test_gate_probe_unsupported_on_cpu(native):
     assert json.loads(sess.gate_probe(0.1, True)) == {"supported": False}
 
 
+def test_chunking_is_rccl_only(native):
+    """Session.set_max_chunk / max_chunk: only the RCCL transport splits
+    messages (RCCL's 16 MiB-per-p2p-channel loss); the CPU transports report
+    nothing to split."""
+    sess = native.Session(0, 1, transport="host")
+    assert sess.set_max_chunk(16 << 20) is False and sess.max_chunk(0) == 0
+
+
 def test_child_dies_with_its_parent():
     """utils.proc: a child in a session of its own (out of reach of a kill of
     its parent's process group) that called die_with_parent() is killed by
