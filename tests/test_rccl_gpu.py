@@ -1,6 +1,7 @@
 """Tier T3: the RCCL transport on one MI355X (1-rank communicator: self
 send/recv through ncclGroupStart/End), through every engine entry point."""
 import json
+import os
 import subprocess
 import sys
 
@@ -199,6 +200,22 @@ def test_unmatched_receive_is_reported(transport):
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     assert "ERR: " in out.stdout and ("ncclGroupEnd failed" in out.stdout or "did not finish" in out.stdout), out.stdout
+
+
+def test_chunk_sizes_follow_the_channel_knobs():
+    """RCCL 2.26 loses half of an op above 16 MiB per p2p channel, so the
+    transport's largest op to itself is 16 MiB x RCCL's 64 p2p channels, or
+    fewer under NCCL_MAX_P2P_NCHANNELS (which RCCL caches per process: each
+    setting runs in a process of its own)."""
+    code = ("import test_nccl_p2p_amd as t; n = t.require_native(); "
+            "s = n.Session(0, 1, device=0, transport='rccl', timeout_s=60); "
+            "a = s.max_chunk(0); ok = s.set_max_chunk(8 << 20); print(a, ok, s.max_chunk(0))")
+    for env, want in (({}, 1 << 30), ({"NCCL_MAX_P2P_NCHANNELS": "4"}, 64 << 20),
+                      ({"P2P_RCCL_MAX_CHUNK": "0"}, 0)):
+        out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT,
+                             env=dict(os.environ, **env))
+        assert out.returncode == 0, out.stderr[-2000:]
+        assert out.stdout.split()[-3:] == [str(want), "True", str(8 << 20)], (env, out.stdout)
 
 
 @pytest.mark.parametrize("transport,floor", [("rccl", 800.0), ("rccl:4", 1800.0)])
