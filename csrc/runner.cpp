@@ -226,6 +226,48 @@ void maybe_inject_fault(Transport& t, Buffers& bufs, int rank, size_t phase_inde
 
 // ------------------------------------------------------------ run_phase ----
 
+namespace {
+
+// RCCL 2.26 delivers exactly half of an op whose share of one p2p channel
+// exceeds 16 MiB, and reports neither that nor how many channels it gives a
+// peer; the RCCL transport sizes its ops for the channel counts it can know
+// (transport_rccl.cpp).  With --verify the warmup's deliveries are checked
+// too: should any rank see a wrong word, every rank posts smaller ops (16,
+// 4, 1 MiB, the same on all: chunking must match on both ends of a message)
+// and warms up again, until the warmup verifies.  Transports that split
+// nothing (set_max_chunk false) are left as they are.
+void rechunk_until_warmup_verifies(Transport& t, Bootstrap& boot, const Phase& phase, const RunConfig& cfg,
+                                   Buffers& bufs, bool active) {
+  const int me = t.rank();
+  const int n = boot.size();
+  auto local_mismatches = [&]() -> uint64_t {
+    if (!active) return 0;
+    uint64_t bad = 0;
+    const RankOps& ops = phase.ranks[static_cast<size_t>(me)];
+    for (size_t i = 0; i < ops.recv_from.size(); ++i)
+      bad += t.verify(bufs.recv_buf(static_cast<int>(i)), cfg.bytes, payload_seed(ops.recv_from[i], cfg.bytes, cfg.salt))
+                 .mismatches;
+    return bad;
+  };
+  uint64_t bad = boot.allreduce_sum_u64(local_mismatches());
+  for (const size_t c : {size_t{16} << 20, size_t{4} << 20, size_t{1} << 20}) {
+    if (bad == 0) return;
+    const size_t cur = std::max(t.max_chunk(me), t.max_chunk((me + 1) % n));
+    if (cur != 0 && c >= cur) continue;
+    if (!t.set_max_chunk(c)) return;
+    if (me == 0)
+      std::fprintf(stderr, "[p2p] %s: %llu wrong words in the warmup; messages now posted as ops of <= %zu MiB\n",
+                   phase.label.c_str(), static_cast<unsigned long long>(bad), c >> 20);
+    if (active) {
+      for (int i = 0; i < cfg.warmup; ++i) post_phase_iteration(t, phase, cfg.bytes, bufs);
+      t.sync();
+    }
+    bad = boot.allreduce_sum_u64(local_mismatches());
+  }
+}
+
+}  // namespace
+
 PhaseResult run_phase(Transport& t, Bootstrap& boot, const Phase& phase, size_t phase_index, const RunConfig& cfg,
                       Buffers& bufs) {
   const int n = boot.size();
@@ -257,6 +299,7 @@ PhaseResult run_phase(Transport& t, Bootstrap& boot, const Phase& phase, size_t 
     t.sync();
   }
   if (cfg.verify && cfg.warmup > 0) {
+    rechunk_until_warmup_verifies(t, boot, phase, cfg, bufs, active);
     // The warmup delivered the payload already: poison the slots again (after
     // every rank drained its warmup), so the check after timing passes only
     // for data the timed iterations delivered.

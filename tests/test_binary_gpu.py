@@ -112,6 +112,20 @@ def test_cli_fuzz_rccl(exe, comms):
     assert "groups of random messages" in out.stdout and "all verified" in out.stdout
 
 
+def test_cli_rechunks_when_the_warmup_does_not_verify(exe):
+    """p2p_matrix --verify under RCCL's 16 MiB-per-p2p-channel loss (one
+    channel, the transport's own chunking off): the warmup's deliveries do
+    not verify, the run reposts as 16 MiB ops, and the timed iterations
+    verify; K = 1 and 4 communicators."""
+    env = dict(os.environ, NCCL_MAX_P2P_NCHANNELS="1", P2P_RCCL_MAX_CHUNK="0")
+    for comms in ("1", "4"):
+        out = subprocess.run([exe, "--mode", "self", "--sizes", "8M,32M", "-n", "4", "--verify", "--no-compat",
+                              "--comms", comms], capture_output=True, text=True, timeout=300, env=env)
+        assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+        assert "verification: OK" in out.stdout
+        assert "messages now posted as ops of <= 16 MiB" in out.stderr, out.stderr[-2000:]
+
+
 def test_bench_drops_a_failing_communicator_candidate():
     """If the 4-communicator candidate fails (injected), bench.py reports it
     in posting.dropped and times the single-communicator posting instead; with
