@@ -1098,7 +1098,7 @@ class BenchRun:
         out = tempfile.mkdtemp(prefix="p2p_xgmi_sweep_")
         cmd = [sys.executable, os.path.join(HERE, "scripts", "xgmi_pair_sweep.py"), "--np", str(n), "--out", out,
                "--sizes", args.xgmi_sweep_sizes, "--rows", "rccl,ipc,knobs", "--budget", "%.0f" % budget,
-               "--row-timeout", "%.0f" % min(90.0, budget)]
+               "--row-timeout", "%.0f" % min(float(os.environ.get("P2P_XGMI_SWEEP_ROW_TIMEOUT", 90)), budget)]
         if emulate:
             cmd += ["--emulate", emulate]
         log("bench: xGMI pair sweep (%.0f s%s)" % (budget, ", emulated: " + emulate if emulate else ""))

@@ -100,8 +100,8 @@ def test_bench_pair_sweep_row_that_hangs_is_killed(native, host_build, tmp_path)
     fake.chmod(0o755)
     out = torchrun(2, ["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--transport", "host",
                        "--size", "64K", "--msgs", "1", "--latency-iters", "10", "--sweep", "0", "--extras", "0",
-                       "--ipc-extra", "0", "--xgmi-sweep", "1", "--xgmi-sweep-sizes", "64K", "--deadline", "75"],
-                   env={"P2P_MPIRUN": str(fake)})
+                       "--ipc-extra", "0", "--xgmi-sweep", "1", "--xgmi-sweep-sizes", "64K", "--deadline", "120"],
+                   env={"P2P_MPIRUN": str(fake), "P2P_XGMI_SWEEP_ROW_TIMEOUT": "10"})
     assert out.returncode == 0, out.stderr[-3000:]
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     sw = r["xgmi_pair_sweep"]
