@@ -7,6 +7,10 @@
 // reference comments it out, :272).
 #include <mpi.h>
 
+#include <chrono>
+#include <cstdio>
+#include <thread>
+
 #include "bootstrap.hpp"
 #include "common.hpp"
 
@@ -56,7 +60,14 @@ class MpiBootstrap final : public Bootstrap {
     P2P_MPICHECK(MPI_Bcast(buf, static_cast<int>(bytes), MPI_BYTE, root, MPI_COMM_WORLD));
   }
   void barrier() override { P2P_MPICHECK(MPI_Barrier(MPI_COMM_WORLD)); }
-  void abort(int code) override { MPI_Abort(MPI_COMM_WORLD, code); }
+  void abort(int code) override {
+    // Give mpirun's I/O forwarding a moment to drain the error this rank just
+    // printed: MPI_Abort tears the job down at once, and under load the last
+    // stderr lines of the ranks could otherwise be lost.
+    std::fflush(nullptr);
+    std::this_thread::sleep_for(std::chrono::milliseconds(250));
+    MPI_Abort(MPI_COMM_WORLD, code);
+  }
 
  private:
   int rank_ = 0, size_ = 1;
