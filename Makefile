@@ -24,7 +24,7 @@ OPT       ?= -O3
 HIPFLAGS  := $(CXXSTD) $(OPT) $(WARN) -fPIC --offload-arch=$(ARCH) -Icsrc
 HOSTFLAGS := $(CXXSTD) $(OPT) $(WARN) -fPIC -Icsrc -pthread
 
-CORE      := common units stats schedule routing bootstrap transport_host transport_shm runner step_driver report provenance app
+CORE      := common units stats schedule routing bootstrap transport_host transport_shm runner step_driver report provenance app rccl_log
 GPU_OBJS  := $(addprefix $(BUILD)/gpu/,$(addsuffix .o,$(CORE) transport_rccl transport_ipc topology stream_gate) kernels.o pingpong.o)
 HOST_OBJS := $(addprefix $(BUILD)/host/,$(addsuffix .o,$(CORE) transport_rccl_stub))
 
@@ -71,7 +71,7 @@ gpu: $(BUILD)/p2p_matrix
 	ln -sf $(BUILD)/p2p_matrix p2p_matrix
 host: $(BUILD)/p2p_matrix_host $(BUILD)/p2p_host_tests
 ext: $(EXT)
-tools: $(BUILD)/fill_probe $(BUILD)/copy_probe $(BUILD)/ipc_export_probe
+tools: $(BUILD)/fill_probe $(BUILD)/copy_probe $(BUILD)/ipc_export_probe $(BUILD)/rccl_half_repro $(BUILD)/rccl_half_repro_rocm
 
 $(BUILD)/gpu $(BUILD)/host $(BUILD)/asan:
 	mkdir -p $@
@@ -119,8 +119,10 @@ $(BUILD)/p2p_matrix: $(GPU_OBJS) $(BUILD)/gpu/bootstrap_mpi.o $(BUILD)/gpu/main.
 $(BUILD)/p2p_matrix_host: $(HOST_OBJS) $(BUILD)/host/bootstrap_mpi.o $(BUILD)/host/main.o $(MPILIB)/.stamp
 	$(CXX_HOST) $(HOST_OBJS) $(BUILD)/host/bootstrap_mpi.o $(BUILD)/host/main.o -o $@ $(MPI_LINK) -pthread
 
+TEST_DATA := -DP2P_TEST_DATA='"$(abspath tests/data)"'
+
 $(BUILD)/p2p_host_tests: $(HOST_OBJS) tests/host/test_main.cpp $(HEADERS)
-	$(CXX_HOST) $(HOSTFLAGS) $(HOST_OBJS) tests/host/test_main.cpp -o $@
+	$(CXX_HOST) $(HOSTFLAGS) $(TEST_DATA) $(HOST_OBJS) tests/host/test_main.cpp -o $@
 
 $(BUILD)/gpu/pymodule.o: csrc/pymodule.cpp $(HEADERS) | $(BUILD)/gpu
 	$(HIPCC) $(HIPFLAGS) -fvisibility=hidden -I$(PY_INC) -I$(PYBIND) -c $< -o $@
@@ -140,6 +142,15 @@ $(BUILD)/copy_probe: scripts/copy_probe.hip | $(BUILD)/gpu
 $(BUILD)/ipc_export_probe: scripts/ipc_export_probe.hip | $(BUILD)/gpu
 	$(HIPCC) --offload-arch=$(ARCH) -O2 $< -o $@
 
+# Framework-free RCCL half-delivery reproducer (scripts/rccl_half_repro.cpp):
+# raw HIP + RCCL only, linked once against the RCCL every entry point uses
+# (build/rt) and once against /opt/rocm's.
+$(BUILD)/rccl_half_repro: scripts/rccl_half_repro.cpp $(RT_STAMP) | $(BUILD)/gpu
+	$(HIPCC) --offload-arch=$(ARCH) -O2 $(WARN) $< -o $@ $(BIN_RPATH) -L$(ROCM)/lib -lrccl
+
+$(BUILD)/rccl_half_repro_rocm: scripts/rccl_half_repro.cpp | $(BUILD)/gpu
+	$(HIPCC) --offload-arch=$(ARCH) -O2 $(WARN) $< -o $@ -Wl,-rpath,$(ROCM)/lib -L$(ROCM)/lib -lrccl
+
 # AddressSanitizer / UBSan on host code only (GPU sanitizers are not available):
 # the unit tests, and the MPI host binary that tests/test_host_unit.py runs as
 # a 3-rank job over the TCP transport.
@@ -149,7 +160,7 @@ asan: $(BUILD)/asan/p2p_host_tests $(BUILD)/asan/p2p_matrix_host
 	ASAN_OPTIONS=detect_leaks=1 $(BUILD)/asan/p2p_host_tests
 
 $(BUILD)/asan/p2p_host_tests: $(ASAN_SRCS) tests/host/test_main.cpp $(HEADERS) | $(BUILD)/asan
-	$(CXX_HOST) $(CXXSTD) $(WARN) $(ASAN) -Icsrc -pthread $(ASAN_SRCS) tests/host/test_main.cpp -o $@
+	$(CXX_HOST) $(CXXSTD) $(WARN) $(ASAN) $(TEST_DATA) -Icsrc -pthread $(ASAN_SRCS) tests/host/test_main.cpp -o $@
 
 $(BUILD)/asan/p2p_matrix_host: $(ASAN_SRCS) csrc/bootstrap_mpi.cpp csrc/main.cpp $(HEADERS) $(MPILIB)/.stamp | $(BUILD)/asan
 	$(CXX_HOST) $(CXXSTD) $(WARN) $(ASAN) -Icsrc $(MPI_INC) -pthread $(ASAN_SRCS) csrc/bootstrap_mpi.cpp csrc/main.cpp \

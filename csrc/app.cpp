@@ -1,6 +1,7 @@
 #include "app.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
@@ -9,6 +10,7 @@
 #include "bootstrap.hpp"
 #include "common.hpp"
 #include "provenance.hpp"
+#include "rccl_log.hpp"
 #include "report.hpp"
 #include "topology.hpp"
 #include "transport.hpp"
@@ -95,7 +97,12 @@ output
       --topology         print the GPU link matrix (xGMI/PCIe, hops, peer access) and exit
   -v, --verbose          -h, --help      --version
 environment (recorded in every --json provenance record; docs/OUTPUT.md)
-  P2P_RCCL_MAX_CHUNK=B   RCCL ops above B are posted as B-byte ops in one group [1G; 0 off]
+  P2P_RCCL_MAX_CHUNK=B   RCCL: messages above B are posted as B-byte ops in one group, every peer
+                         [16M x the p2p channels RCCL set up for the peer; 0 off]
+  P2P_RECHUNK=0          --verify: a warmup that does not verify is reported, not retried with
+                         smaller ops                                               [1]
+  P2P_VERIFY_BUDGET=B    --verify: bytes of receive generations (one per timed iteration)
+                         [free HBM / 4, <= 32G]
   P2P_RCCL_SPLIT_MIN=B   --comms: smaller messages stay on communicator 0       [1M]
   P2P_RCCL_REGISTER=1|2  ncclCommRegister every buffer (2: + ncclMemAlloc)
   P2P_RCCL_BLOCKING=1    blocking ncclCommInitRank instead of the polled non-blocking init
@@ -105,7 +112,7 @@ environment (recorded in every --json provenance record; docs/OUTPUT.md)
   P2P_SDMA_STREAMS=K     --ipc-engine sdma: side streams the receives share      [4]
   P2P_BOOTSTRAP_PORT, P2P_BOOTSTRAP_TIMEOUT   TCP bootstrap port / receive deadline
   P2P_HOSTNAME=name      hostname for the placement check (emulated hosts)
-  P2P_INJECT_FAULT=kind@rank[:phase]   corrupt | exit | hang | skip (tests)
+  P2P_INJECT_FAULT=kind@rank[:phase]   corrupt | exit | hang | skip | skip-some (tests)
   P2P_ROCTX=1, P2P_LOG=1 roctx ranges; engine log on stderr
 )";
 }
@@ -460,6 +467,9 @@ void run_latencies(const AppConfig& cfg, Transport& t, Bootstrap& boot, Buffers&
 
 // Rank 0: the extended tables after the reference matrices, and the JSON /
 // trace / CSV files.
+std::string links_to_json(const AppResult& res, int n);
+void print_transport_matrix(FILE* out, const AppResult& res, int n);
+
 void write_reports(const AppConfig& cfg, const Transport& t, const Bootstrap& boot, const Placement& pl,
                    const std::vector<char>& all_desc, size_t desc_len, const AppResult& res, uint64_t fuzz_bad,
                    size_t fuzz_max, std::ofstream& js, FILE* out) {
@@ -469,6 +479,7 @@ void write_reports(const AppConfig& cfg, const Transport& t, const Bootstrap& bo
                  boot.name().c_str(), pl.num_hosts);
     for (int r = 0; r < n; ++r) std::fprintf(out, "  rank %d: %s\n", r, &all_desc[static_cast<size_t>(r) * desc_len]);
     if (t.name() != "host" && t.name() != "shm") std::fprintf(out, "%s", topology_report().c_str());
+    print_transport_matrix(out, res, n);
     for (const auto& rec : res.runs) print_extended(out, rec, n);
     print_latency(out, res.latency, n);
     print_latency(out, res.preposted_latency, n);
@@ -481,6 +492,7 @@ void write_reports(const AppConfig& cfg, const Transport& t, const Bootstrap& bo
                             : "all verified");
   }
   if (js.is_open()) {
+    js << links_to_json(res, n) << "\n";
     if (!res.latency.empty()) js << latency_to_json(res.latency, n) << "\n";
     if (!res.preposted_latency.empty()) js << latency_to_json(res.preposted_latency, n) << "\n";
     if (!res.device_latency.empty()) js << latency_to_json(res.device_latency, n) << "\n";
@@ -504,11 +516,87 @@ void write_reports(const AppConfig& cfg, const Transport& t, const Bootstrap& bo
   std::fflush(out);
 }
 
+// Collective: every rank's per-peer transport classes, the GPU link types
+// between ranks and every rank's link report (AppResult).
+void collect_links(Transport& t, Bootstrap& boot, int device, AppResult& res) {
+  const int n = boot.size();
+  std::vector<std::string> mine = t.peer_transports();
+  mine.resize(static_cast<size_t>(n));
+  std::string packed;
+  for (const auto& tr : mine) packed += tr + "\n";
+  const auto rows = boot.allgather_string(packed);
+  res.transport_matrix.assign(static_cast<size_t>(n) * n, "");
+  for (int r = 0; r < n; ++r) {
+    size_t at = 0;
+    for (int p = 0; p < n; ++p) {
+      const size_t e = rows[static_cast<size_t>(r)].find('\n', at);
+      if (e == std::string::npos) break;
+      res.transport_matrix[static_cast<size_t>(r) * n + p] = rows[static_cast<size_t>(r)].substr(at, e - at);
+      at = e + 1;
+    }
+  }
+  res.link_matrix = rank_link_matrix(boot, device);
+  res.link_reports = boot.allgather_string(t.link_report());
+}
+
+// {"type":"links"}: transport class and GPU link per pair, and every rank's
+// link report (RCCL: p2p channels, per-peer transport and op limit).
+std::string links_to_json(const AppResult& res, int n) {
+  auto mat = [&](const std::vector<std::string>& m) {
+    std::string o = "[";
+    for (int a = 0; a < n; ++a) {
+      o += a ? ",[" : "[";
+      for (int b = 0; b < n; ++b) {
+        const size_t i = static_cast<size_t>(a) * n + b;
+        o += std::string(b ? "," : "") + "\"" + json_escape(i < m.size() ? m[i] : "") + "\"";
+      }
+      o += "]";
+    }
+    return o + "]";
+  };
+  std::string o = "{\"type\":\"links\",\"matrix_transport\":" + mat(res.transport_matrix) +
+                  ",\"rank_links\":" + mat(res.link_matrix) + ",\"ranks\":[";
+  for (size_t r = 0; r < res.link_reports.size(); ++r)
+    o += (r ? "," : "") + (res.link_reports[r].empty() ? std::string("null") : res.link_reports[r]);
+  return o + "]}";
+}
+
+// The transport class per pair, when the data plane reports one.
+void print_transport_matrix(FILE* out, const AppResult& res, int n) {
+  bool any = false;
+  for (const auto& tr : res.transport_matrix) any = any || !tr.empty();
+  if (!any) return;
+  std::fprintf(out, "\n== data-plane transport per pair (row = rank, col = peer; RCCL INFO log) ==\n      ");
+  for (int b = 0; b < n; ++b) std::fprintf(out, "%7d", b);
+  std::fprintf(out, "\n");
+  for (int a = 0; a < n; ++a) {
+    std::fprintf(out, "%6d", a);
+    for (int b = 0; b < n; ++b) {
+      const std::string& tr = res.transport_matrix[static_cast<size_t>(a) * n + b];
+      std::fprintf(out, "%7s", tr.empty() ? "-" : tr.c_str());
+    }
+    std::fprintf(out, "\n");
+  }
+}
+
 // Link check (--min-gbs): every measured off-diagonal flow must reach the
-// threshold; the slow ones are named so a bad link or GPU can be found.
+// threshold, and a pair whose GPUs share a direct xGMI link must have been
+// carried by RCCL's P2P transport (link_transport_mismatch: a silent SHM or
+// NET fallback reads as a slow link); the failing ones are named so a bad
+// link or GPU can be found.
 int count_slow_flows(const AppConfig& cfg, const AppResult& res, bool root) {
   int slow = 0;
   if (cfg.min_gbs <= 0) return 0;
+  const size_t n = static_cast<size_t>(std::sqrt(static_cast<double>(res.transport_matrix.size())) + 0.5);
+  if (n > 0 && res.link_matrix.size() == n * n)
+    for (size_t a = 0; a < n; ++a)
+      for (size_t b = 0; b < n; ++b)
+        if (a != b && link_transport_mismatch(res.link_matrix[a * n + b], res.transport_matrix[a * n + b])) {
+          ++slow;
+          if (root)
+            std::fprintf(stderr, "p2p_matrix: WRONG TRANSPORT: %zu -> %zu went over %s although the GPUs share a %s link\n",
+                         a, b, res.transport_matrix[a * n + b].c_str(), res.link_matrix[a * n + b].c_str());
+        }
   for (const auto& rec : res.runs)
     for (const auto& ph : rec.phases)
       for (const auto& f : ph.flows)
@@ -555,7 +643,19 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
   if (cfg.latency) max_bytes = std::max(max_bytes, cfg.latency_bytes);
   int slots = 1;
   for (const auto& s : scheds) slots = std::max(slots, s.max_recv_slots());
-  Buffers bufs(*t, max_bytes, slots);
+  // --verify: every timed iteration gets a receive generation of its own (its
+  // own send region, seed and receive slots), as many as the memory budget
+  // allows, so the check after timing covers each delivery, not only the last
+  // one into a slot (runner.hpp RunConfig::gens; verify_coverage in the output).
+  AppConfig run_cfg = cfg;
+  if (cfg.run.verify) {
+    int most_iters = std::max(cfg.run.iters, cfg.run.warmup);
+    if (cfg.iters_auto)
+      for (size_t b : cfg.sizes) most_iters = std::max(most_iters, auto_iters(b, cfg.target_bytes));
+    run_cfg.run.gens = verify_generations(*t, boot, max_bytes, slots, most_iters);
+  }
+  if (const char* rc = std::getenv("P2P_RECHUNK")) run_cfg.run.rechunk = std::atoi(rc) != 0;
+  Buffers bufs(*t, max_bytes, slots * run_cfg.run.gens, slot_stride_bytes(max_bytes) * static_cast<size_t>(run_cfg.run.gens));
 
   // Connection warm-up outside any timed cell (the reference pays lazy p2p
   // connection setup inside its first cells; --reference keeps that).
@@ -566,7 +666,7 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
   AppResult& res = result ? *result : local;
   std::ofstream js;
   const std::vector<uint8_t> skip = open_results(cfg, boot, scheds, provenance, &js);
-  run_all(cfg, *t, boot, scheds, skip, bufs, js, out, res);
+  run_all(run_cfg, *t, boot, scheds, skip, bufs, js, out, res);
   run_latencies(cfg, *t, boot, bufs, res);
   uint64_t fuzz_bad = 0;
   size_t fuzz_max = 0;
@@ -575,6 +675,10 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
     fuzz_bad = boot.allreduce_sum_u64(fuzz_transport(*t, boot, cfg.fuzz_rounds, 0xF022, fuzz_max));
     res.mismatches += fuzz_bad;
   }
+
+  // What the data plane set up per peer (RCCL: transports and channels from
+  // its INFO log), now that every connection the runs used exists.
+  collect_links(*t, boot, gpu_transport ? topt.device : -1, res);
 
   // Device descriptions of every rank, for the banner.
   char mine[256] = {0};

@@ -71,7 +71,14 @@ struct AppResult {
   std::vector<LatencyResult> preposted_latency;
   std::vector<RingLatencyResult> ring_latency;  // --mode ring with --latency / --device-latency
   uint64_t mismatches = 0;
-  int slow_flows = 0;  // flows under --min-gbs
+  int slow_flows = 0;  // flows under --min-gbs, or carried by the wrong transport (see count_slow_flows)
+  // After the runs (collective): per pair (row-major n x n) the transport
+  // class the data plane reached the peer through (Transport::peer_transports,
+  // "" unknown) and the GPU link type (provenance rank_links); each rank's
+  // Transport::link_report().
+  std::vector<std::string> transport_matrix;
+  std::vector<std::string> link_matrix;
+  std::vector<std::string> link_reports;
 };
 
 // Runs everything collectively; rank 0 prints to `out`.  Returns 0 on success,

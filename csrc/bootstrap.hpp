@@ -41,6 +41,19 @@ class Bootstrap {
     allgather(&v, out.data(), sizeof(T));
     return out;
   }
+  // Strings of any length, one per rank.
+  std::vector<std::string> allgather_string(const std::string& mine) {
+    const auto lens = allgather_value(static_cast<uint64_t>(mine.size()));
+    uint64_t most = 0;
+    for (uint64_t l : lens) most = l > most ? l : most;
+    std::string padded = mine;
+    padded.resize(static_cast<size_t>(most) + 1, '\0');
+    std::string all(padded.size() * lens.size(), '\0');
+    allgather(padded.data(), &all[0], padded.size());
+    std::vector<std::string> out;
+    for (size_t r = 0; r < lens.size(); ++r) out.push_back(all.substr(r * padded.size(), static_cast<size_t>(lens[r])));
+    return out;
+  }
   template <class T>
   std::vector<T> allgather_vector(const std::vector<T>& v) {  // equal lengths on all ranks
     std::vector<T> out(v.size() * static_cast<size_t>(size()));

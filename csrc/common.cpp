@@ -3,11 +3,13 @@
 #include <dlfcn.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdarg>
 #include <cstdlib>
 #include <mutex>
 #include <stdexcept>
+#include <thread>
 #include <vector>
 
 namespace p2p {
@@ -160,6 +162,20 @@ void trace_mark(const char* name) {
 double now_seconds() {
   using clk = std::chrono::steady_clock;
   return std::chrono::duration<double>(clk::now().time_since_epoch()).count();
+}
+
+void emulate_link_delay(const std::vector<size_t>& send_bytes, int me) {
+  static const double gbs = [] {
+    const char* v = std::getenv("P2P_EMULATE_LINK_GBS");
+    return v ? std::atof(v) : 0.0;
+  }();
+  if (gbs <= 0) return;
+  size_t most = 0;
+  for (size_t p = 0; p < send_bytes.size(); ++p)
+    if (static_cast<int>(p) != me) most = std::max(most, send_bytes[p]);
+  if (most == 0) return;
+  const double until = now_seconds() + static_cast<double>(most) / (gbs * 1e9);
+  while (now_seconds() < until) std::this_thread::sleep_for(std::chrono::microseconds(20));
 }
 
 StdoutToStderr::StdoutToStderr(bool enable) {

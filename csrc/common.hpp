@@ -14,6 +14,7 @@
 #include <functional>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 namespace p2p {
 
@@ -46,6 +47,14 @@ void set_log_level(int level);
 void logf(int level, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 
 double now_seconds();  // monotonic (steady_clock), unlike the reference's system_clock
+
+// Link-rate emulation for the CPU transports (P2P_EMULATE_LINK_GBS=<GB/s>, 0 or
+// unset: off).  A group waits, before it moves any byte, as long as its
+// busiest peer link would take at that rate (every peer its own full-duplex
+// link, as on xGMI; self copies are free), so a CPU rehearsal with scaled-down
+// sizes takes the time a node would (tests/test_torchrun_cpu.py).
+// `send_bytes[p]` = bytes this rank sends to rank p in the group.
+void emulate_link_delay(const std::vector<size_t>& send_bytes, int me);
 
 // roctx ranges (visible in rocprofv3 --marker-trace / roctracer timelines).
 // libroctx64 is dlopen'ed on first use and only when P2P_ROCTX=1, so nothing

@@ -1,6 +1,7 @@
 #include "provenance.hpp"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <utility>
@@ -65,40 +66,58 @@ std::string runtime_json() {
   return o + "]}";
 }
 
-std::string provenance_json(Bootstrap& boot, int device) {
-  struct RankDev {
-    int32_t device;
-    char pci[60];
-    uint64_t host;
-  };
+namespace {
+struct RankDev {
+  int32_t device;
+  char pci[60];
+  uint64_t host;
+};
+RankDev my_rank_dev(int device) {
   RankDev mine{};
   mine.device = device;
   std::snprintf(mine.pci, sizeof(mine.pci), "%s", device >= 0 ? device_pci_id(device).c_str() : "");
   mine.host = host_hash(real_hostname());
-  auto all = boot.allgather_value(mine);
-  const int n = boot.size();
+  return mine;
+}
+// Link between the GPUs of every two ranks, from this host's probe (ranks on
+// other hosts, or ranks without a GPU, read "n/a").
+std::vector<std::string> link_matrix(const std::vector<RankDev>& all, const RankDev& mine) {
+  const int n = static_cast<int>(all.size());
   int ndev = 0;
   auto links = probe_topology(&ndev);
+  std::vector<std::string> out(static_cast<size_t>(n) * static_cast<size_t>(n), "n/a");
+  for (int a = 0; a < n; ++a)
+    for (int b = 0; b < n; ++b) {
+      const int da = all[static_cast<size_t>(a)].device, db = all[static_cast<size_t>(b)].device;
+      const bool local = all[static_cast<size_t>(a)].host == mine.host && all[static_cast<size_t>(b)].host == mine.host;
+      if (local && da >= 0 && db >= 0 && da < ndev && db < ndev) {
+        const LinkInfo& li = links[static_cast<size_t>(da) * ndev + db];
+        out[static_cast<size_t>(a) * n + b] = da == db ? "same-gpu" : strfmt("%s/%d", li.type.c_str(), li.hops);
+      }
+    }
+  return out;
+}
+}  // namespace
+
+std::vector<std::string> rank_link_matrix(Bootstrap& boot, int device) {
+  const RankDev mine = my_rank_dev(device);
+  return link_matrix(boot.allgather_value(mine), mine);
+}
+
+std::string provenance_json(Bootstrap& boot, int device) {
+  const RankDev mine = my_rank_dev(device);
+  auto all = boot.allgather_value(mine);
+  const int n = boot.size();
   std::string o = "{\"type\":\"provenance\",\"runtime\":" + runtime_json() + ",\"env\":" + env_knobs_json() +
                   ",\"rank_devices\":[";
   for (int r = 0; r < n; ++r)
     o += strfmt("%s{\"rank\":%d,\"device\":%d,\"pci\":%s}", r ? "," : "", r, all[static_cast<size_t>(r)].device,
                 quoted(all[static_cast<size_t>(r)].pci).c_str());
-  // Link between the GPUs of every two ranks, from this host's probe (ranks
-  // on other hosts, or ranks without a GPU, read "n/a").
+  const auto lm = link_matrix(all, mine);
   o += "],\"rank_links\":[";
   for (int a = 0; a < n; ++a) {
     o += a ? ",[" : "[";
-    for (int b = 0; b < n; ++b) {
-      const int da = all[static_cast<size_t>(a)].device, db = all[static_cast<size_t>(b)].device;
-      std::string v = "n/a";
-      const bool local = all[static_cast<size_t>(a)].host == mine.host && all[static_cast<size_t>(b)].host == mine.host;
-      if (local && da >= 0 && db >= 0 && da < ndev && db < ndev) {
-        const LinkInfo& li = links[static_cast<size_t>(da) * ndev + db];
-        v = da == db ? "same-gpu" : strfmt("%s/%d", li.type.c_str(), li.hops);
-      }
-      o += (b ? "," : "") + quoted(v);
-    }
+    for (int b = 0; b < n; ++b) o += (b ? "," : "") + quoted(lm[static_cast<size_t>(a) * n + b]);
     o += "]";
   }
   return o + "]}";

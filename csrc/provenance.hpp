@@ -13,6 +13,7 @@
 #pragma once
 
 #include <string>
+#include <vector>
 
 namespace p2p {
 
@@ -29,6 +30,10 @@ std::string runtime_json();
 // Collective: runtime_json() + env_knobs_json() + every rank's device and the
 // rank-to-rank link types (device = this rank's GPU index, -1 for none).
 std::string provenance_json(Bootstrap& boot, int device);
+
+// Collective: the link type between every two ranks' GPUs (row-major n x n,
+// "XGMI/1", "PCIE/2", "same-gpu", "n/a"), as in provenance_json's rank_links.
+std::vector<std::string> rank_link_matrix(Bootstrap& boot, int device);
 
 // ---- pieces implemented per build (GPU: topology.cpp / transport_rccl.cpp;
 // host-only: transport_rccl_stub.cpp) ----

@@ -12,6 +12,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cstdlib>
 #include <memory>
 #include <string>
 #include <tuple>
@@ -86,7 +87,12 @@ class Session {
     cfg.timing = parse_timing(timing);
     cfg.verify = verify;
     cfg.salt = ++salt_;
-    Buffers bufs(*t_, bytes, std::max(1, s.max_recv_slots()));
+    const int slots = std::max(1, s.max_recv_slots());
+    // Verified runs: one receive generation per iteration, as far as memory
+    // allows (runner.hpp RunConfig::gens).
+    cfg.gens = verify ? verify_generations(*t_, *boot_, bytes, slots, std::max(iters, warmup)) : 1;
+    if (const char* rc = std::getenv("P2P_RECHUNK")) cfg.rechunk = std::atoi(rc) != 0;
+    Buffers bufs(*t_, bytes, slots * cfg.gens, slot_stride_bytes(bytes) * static_cast<size_t>(cfg.gens));
     if (warm) warm_connections(*t_, *boot_, s, bufs);
     RunRecord rec;
     rec.mode = s.mode;
@@ -154,9 +160,18 @@ class Session {
   }
 
   // Largest op a message is posted as (RCCL: 16 MiB per p2p channel, see
-  // transport_rccl.cpp); set on every rank alike.
-  bool set_max_chunk(size_t bytes) { return t_->set_max_chunk(bytes); }
+  // transport_rccl.cpp), capped on every rank alike.
+  bool set_chunk_cap(size_t bytes) { return t_->set_chunk_cap(bytes); }
   size_t max_chunk(int peer) const { return t_->max_chunk(peer); }
+
+  // Collective: every rank's Transport::link_report() as a JSON list (rank
+  // order; null where the transport has nothing to report).
+  std::string link_reports() {
+    const auto all = boot_->allgather_string(t_->link_report());
+    std::string o = "[";
+    for (size_t r = 0; r < all.size(); ++r) o += (r ? "," : "") + (all[r].empty() ? std::string("null") : all[r]);
+    return o + "]";
+  }
 
   // Collective: provenance_json() for this session's ranks.
   std::string provenance(int device) { return provenance_json(*boot_, device); }
@@ -279,10 +294,13 @@ PYBIND11_MODULE(_p2pcore, m) {
            "Dependent ring token chain 0 -> 1 -> ... -> 0 (collective); JSON with per-hop and per-lap times.")
       .def("set_timeout", &Session::set_timeout, py::arg("seconds"),
            "Bounds every later wait of the session (transport sync / rendezvous, bootstrap receives).")
-      .def("set_max_chunk", &Session::set_max_chunk, py::arg("bytes"),
-           "Posts messages to every peer as ops of at most `bytes` (0: unsplit); False where nothing is split. "
-           "Call it on every rank with the same value.")
+      .def("set_chunk_cap", &Session::set_chunk_cap, py::arg("bytes"),
+           "Caps the ops messages to every peer are posted as at `bytes` (0: lifts the cap, back to the limits the "
+           "transport derived per peer); False where nothing is split. Call it on every rank with the same value.")
       .def("max_chunk", &Session::max_chunk, py::arg("peer"), "Largest op a message to `peer` is posted as (0: unsplit).")
+      .def("link_reports", &Session::link_reports, py::call_guard<py::gil_scoped_release>(),
+           "Collective: what the data plane set up towards each peer, per rank (RCCL: p2p channels from its INFO log, "
+           "each peer's transport, the op limit in use); JSON list.")
       .def("provenance", &Session::provenance, py::arg("device") = -1, py::call_guard<py::gil_scoped_release>(),
            "Collective: runtime, RCCL library, knobs, every rank's GPU and the links between them (JSON).")
       .def("_unmatched_recv", &Session::unmatched_recv, py::arg("bytes") = size_t{1} << 20,
@@ -296,7 +314,13 @@ PYBIND11_MODULE(_p2pcore, m) {
            py::arg("depth") = 1, py::arg("recv_budget") = size_t{0}, py::arg("salt") = uint64_t{0},
            py::call_guard<py::gil_scoped_release>())
       .def("poison", [](PyStepDriver& s) { s.d().poison(); }, py::call_guard<py::gil_scoped_release>(),
-           "Collective: zero every receive slot (after the warmup, before the timed steps).")
+           "Collective: zero every receive slot (after the warmup, before the timed steps) and arm the skip faults.")
+      .def("clear", [](PyStepDriver& s) { s.d().clear(); }, py::call_guard<py::gil_scoped_release>(),
+           "Collective: zero every receive slot once every rank has drained (no fault armed).")
+      .def("recapture", [](PyStepDriver& s) { s.d().recapture(); }, py::call_guard<py::gil_scoped_release>(),
+           "Collective: record the step graphs again after the op sizes changed (no-op without graphs).")
+      .def_property_readonly("recaptures", [](PyStepDriver& s) { return s.d().recaptures(); })
+      .def_property_readonly("graphs", [](PyStepDriver& s) { return s.d().graphs(); })
       .def("verify_steps", [](PyStepDriver& s, long first, long count) {
             StepVerifyReport r;
             {

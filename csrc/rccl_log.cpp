@@ -1,0 +1,148 @@
+#include "rccl_log.hpp"
+
+#include <algorithm>
+#include <cctype>
+#include <cstdlib>
+#include <map>
+#include <set>
+#include <sstream>
+
+namespace p2p {
+namespace {
+
+// Integer right after `key` (spaces skipped) in `line`; -1 if absent.
+int int_after(const std::string& line, const std::string& key) {
+  size_t at = line.find(key);
+  if (at == std::string::npos) return -1;
+  at += key.size();
+  while (at < line.size() && line[at] == ' ') ++at;
+  if (at >= line.size() || !std::isdigit(static_cast<unsigned char>(line[at]))) return -1;
+  return std::atoi(line.c_str() + at);
+}
+
+// Integer ending right before position `end` (spaces skipped); -1 if none.
+int int_before(const std::string& line, size_t end) {
+  size_t e = end;
+  while (e > 0 && line[e - 1] == ' ') --e;
+  size_t b = e;
+  while (b > 0 && std::isdigit(static_cast<unsigned char>(line[b - 1]))) --b;
+  if (b == e) return -1;
+  return std::atoi(line.substr(b, e - b).c_str());
+}
+
+// "<int>[<int>]" at `at`; returns the rank, advances `at`.
+bool rank_dev(const std::string& s, size_t* at, int* rank) {
+  size_t i = *at;
+  while (i < s.size() && s[i] == ' ') ++i;
+  size_t b = i;
+  while (i < s.size() && std::isdigit(static_cast<unsigned char>(s[i]))) ++i;
+  if (i == b || i >= s.size() || s[i] != '[') return false;
+  *rank = std::atoi(s.substr(b, i - b).c_str());
+  size_t close = s.find(']', i);
+  if (close == std::string::npos) return false;
+  *at = close + 1;
+  return true;
+}
+
+std::string transport_class(const std::string& via) {
+  if (via.rfind("P2P", 0) == 0) return "P2P";
+  if (via.rfind("SHM", 0) == 0) return "SHM";
+  if (via.rfind("NET", 0) == 0 || via.rfind("COLLNET", 0) == 0) return "NET";
+  return via.substr(0, via.find('/'));
+}
+
+}  // namespace
+
+RcclInitInfo parse_rccl_init(const std::string& text) {
+  RcclInitInfo info;
+  std::istringstream in(text);
+  for (std::string line; std::getline(in, line);) {
+    if (line.find(" nNodes ") != std::string::npos && line.find(" nRanks ") != std::string::npos) {
+      info.nranks = int_after(line, " nRanks ");
+      info.nnodes = int_after(line, " nNodes ");
+    }
+    const size_t pp = line.find(" p2p channels per peer");
+    if (pp != std::string::npos) {
+      info.p2p_per_peer = int_before(line, pp);
+      const size_t pc = line.rfind(" p2p channels,", pp);
+      info.p2p_channels = pc == std::string::npos ? -1 : int_before(line, pc);
+    }
+  }
+  return info;
+}
+
+std::vector<RcclConnection> parse_rccl_connections(const std::string& text) {
+  std::vector<RcclConnection> out;
+  std::istringstream in(text);
+  for (std::string line; std::getline(in, line);) {
+    const size_t ch = line.find("Channel ");
+    const size_t via = line.find(" via ");
+    if (ch == std::string::npos || via == std::string::npos || via < ch) continue;
+    RcclConnection c;
+    size_t at = ch + 8;
+    c.channel = std::atoi(line.c_str() + at);
+    const size_t colon = line.find(" : ", at);
+    if (colon == std::string::npos || colon > via) continue;
+    at = colon + 3;
+    if (!rank_dev(line, &at, &c.src)) continue;
+    const size_t arrow = line.find("->", at);
+    if (arrow == std::string::npos || arrow > via) continue;
+    at = arrow + 2;
+    if (!rank_dev(line, &at, &c.dst)) continue;
+    size_t t = via + 5;
+    while (t < line.size() && line[t] == ' ') ++t;
+    size_t e = t;
+    while (e < line.size() && line[e] != ' ' && line[e] != '\r') ++e;
+    c.via = line.substr(t, e - t);
+    if (c.via.empty()) continue;
+    out.push_back(c);
+  }
+  return out;
+}
+
+std::vector<RcclPeerLink> rccl_peer_links(const std::vector<RcclConnection>& conns, int me, int nranks) {
+  std::vector<RcclPeerLink> out(static_cast<size_t>(std::max(nranks, 0)));
+  std::map<int, std::set<int>> send_ch, recv_ch;
+  for (int p = 0; p < nranks; ++p) {
+    out[static_cast<size_t>(p)].peer = p;
+    if (p == me) out[static_cast<size_t>(p)].transport = "self";
+  }
+  for (const auto& c : conns) {
+    int peer = -1;
+    bool send = false;
+    if (c.src == me && c.dst != me) {
+      peer = c.dst;
+      send = true;
+    } else if (c.dst == me && c.src != me) {
+      peer = c.src;
+    }
+    if (peer < 0 || peer >= nranks) continue;
+    (send ? send_ch : recv_ch)[peer].insert(c.channel);
+    auto& l = out[static_cast<size_t>(peer)];
+    if (l.via.empty()) {
+      l.via = c.via;
+      l.transport = transport_class(c.via);
+    }
+  }
+  for (auto& l : out) {
+    if (l.peer == me) continue;
+    auto s = send_ch.find(l.peer);
+    auto r = recv_ch.find(l.peer);
+    l.channels_connected = static_cast<int>(s != send_ch.end() ? s->second.size() : r != recv_ch.end() ? r->second.size() : 0);
+  }
+  return out;
+}
+
+int rccl_op_channels(const RcclInitInfo& info, bool net_peer, int net_per_peer) {
+  if (!info.found()) return 0;
+  int c = std::min(info.p2p_channels, info.p2p_per_peer);
+  if (net_peer && net_per_peer > 0) c = std::min(c, net_per_peer);
+  return std::max(c, 1);
+}
+
+bool link_transport_mismatch(const std::string& link, const std::string& transport) {
+  const bool direct_xgmi = link.rfind("XGMI/1", 0) == 0 && link.size() == 6;
+  return direct_xgmi && !transport.empty() && transport != "?" && transport != "P2P" && transport != "self";
+}
+
+}  // namespace p2p

@@ -1,0 +1,72 @@
+// What RCCL set up, read from its own INFO log (pure host code, unit-tested).
+//
+// RCCL reports neither how many p2p channels a send/recv to a peer is split
+// over nor which transport (P2P/IPC over xGMI, SHM, NET) carries it -- except
+// in its INFO log.  Both matter here:
+//   * RCCL 2.26 / 2.27 on MI355X deliver exactly the first half of an op whose
+//     share of one p2p channel exceeds 16 MiB, silently
+//     (scripts/rccl_half_repro.cpp, profiles/r3_rccl_half_repro/), so the
+//     transport posts messages as ops of at most 16 MiB x channels;
+//   * a pair that silently fell back from xGMI to SHM or NET would look like a
+//     slow link.
+// The transport points NCCL_DEBUG_FILE at a private file (when the user has not
+// set NCCL_DEBUG), reads it after each communicator's init and after the lazy
+// p2p connects, and records what it found (provenance.rccl_peers).
+#pragma once
+
+#include <string>
+#include <vector>
+
+namespace p2p {
+
+// From a communicator's init block.
+struct RcclInitInfo {
+  int nranks = -1;           // "comm 0x.. rank r nRanks N nNodes H localRanks L ..."
+  int nnodes = -1;
+  int p2p_channels = -1;     // "... %d p2p channels, %d p2p channels per peer"
+  int p2p_per_peer = -1;
+  bool found() const { return p2p_channels > 0 && p2p_per_peer > 0; }
+};
+
+// One connection line: "Channel 03/0 : 0[2] -> 1[5] [send] via NET/Socket/0".
+struct RcclConnection {
+  int channel = -1;
+  int src = -1;  // ranks
+  int dst = -1;
+  std::string via;  // first token after "via": "P2P/IPC/read", "NET/Socket/0", "SHM/direct/direct", ...
+};
+
+// The last init block in `text` (fields not seen stay -1).
+RcclInitInfo parse_rccl_init(const std::string& text);
+// Every connection line in `text`, in order.
+std::vector<RcclConnection> parse_rccl_connections(const std::string& text);
+
+// Per peer of rank `me`: the channels connected towards it (send lines
+// me -> peer; receive-side lines peer -> me where no send line exists) and
+// the transport class: "P2P" (xGMI / PCIe peer access through IPC), "SHM",
+// "NET", "self" (peer == me: RCCL copies inside the kernel and logs no
+// connection) or "" (not connected yet).
+struct RcclPeerLink {
+  int peer = -1;
+  int channels_connected = 0;
+  std::string transport;  // class, as above
+  std::string via;        // the full token of the first line seen
+};
+std::vector<RcclPeerLink> rccl_peer_links(const std::vector<RcclConnection>& conns, int me, int nranks);
+
+// Channels a send/recv to a peer is split over: min(p2p channels, per peer)
+// of the communicator, and for a peer RCCL reaches through its network
+// transport at most `net_per_peer` (NCCL_NCHANNELS_PER_NET_PEER, 2 by
+// default).  0 when the init block was not found.
+int rccl_op_channels(const RcclInitInfo& info, bool net_peer, int net_per_peer);
+
+// Link check (--min-gbs): a pair whose GPUs share a direct xGMI link
+// (`link` "XGMI/1", provenance rank_links) must be carried by RCCL's P2P
+// transport; a known transport of another class (SHM, NET) there is a silent
+// fallback that would read as a slow link.
+bool link_transport_mismatch(const std::string& link, const std::string& transport);
+
+// RCCL's half-delivery threshold: bytes of one op per p2p channel.
+constexpr size_t kRcclBytesPerChannel = size_t{16} << 20;
+
+}  // namespace p2p

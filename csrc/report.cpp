@@ -106,13 +106,23 @@ void print_extended(FILE* out, const RunRecord& rec, int n) {
       std::fprintf(out, "\n");
     }
   }
-  uint64_t bad = 0;
+  uint64_t bad = 0, timed = 0, checked = 0;
   bool verified = false;
   for (const auto& ph : rec.phases) {
     bad += ph.total_mismatches;
+    timed += ph.timed_msgs;
+    checked += ph.verified_msgs;
     for (const auto& f : ph.flows) verified |= f.verified;
   }
-  if (verified) std::fprintf(out, "  verification: %s (%llu mismatching words)\n", bad ? "FAILED" : "OK", static_cast<unsigned long long>(bad));
+  if (verified)
+    std::fprintf(out, "  verification: %s (%llu mismatching words; %llu of %llu timed deliveries checked)\n",
+                 bad ? "FAILED" : "OK", static_cast<unsigned long long>(bad), static_cast<unsigned long long>(checked),
+                 static_cast<unsigned long long>(timed));
+  // Phases whose warmup did not verify and were re-posted with smaller ops.
+  for (const auto& ph : rec.phases)
+    if (!ph.rechunked_to.empty())
+      std::fprintf(out, "  %s: warmup had %llu wrong words; timed as ops of <= %s\n", ph.label.c_str(),
+                   static_cast<unsigned long long>(ph.warmup_mismatches), format_size(ph.rechunked_to.back()).c_str());
   std::fflush(out);
 }
 
@@ -179,9 +189,19 @@ std::string run_to_json(const RunRecord& rec, int n) {
   auto gbs = flow_matrix_gbs(rec, n);
   MatrixSummary ms = summarize_offdiag(gbs, n);
   std::ostringstream o;
+  uint64_t timed = 0, checked = 0;
+  bool rechunked = false;
+  for (const auto& ph : rec.phases) {
+    timed += ph.timed_msgs;
+    checked += ph.verified_msgs;
+    rechunked = rechunked || !ph.rechunked_to.empty();
+  }
   o << "{\"type\":\"run\",\"mode\":\"" << mode_name(rec.mode) << "\",\"dir\":\"" << direction_name(rec.dir)
     << "\",\"bytes\":" << rec.bytes << ",\"iters\":" << rec.cfg.iters << ",\"warmup\":" << rec.cfg.warmup
-    << ",\"timing\":\"" << timing_name(rec.cfg.timing) << "\",\"nranks\":" << n
+    << ",\"timing\":\"" << timing_name(rec.cfg.timing) << "\",\"nranks\":" << n << ",\"verify\":"
+    << (rec.cfg.verify ? "true" : "false") << ",\"timed_msgs\":" << timed << ",\"verified_msgs\":" << checked
+    << ",\"verify_coverage\":" << (rec.cfg.verify && timed ? num(static_cast<double>(checked) / static_cast<double>(timed)) : "null")
+    << ",\"rechunked\":" << (rechunked ? "true" : "false")
     << ",\"gbs_matrix\":" << matrix_json(gbs, n) << ",\"p50_us_matrix\":" << matrix_json(flow_matrix_p50_us(rec, n), n)
     << ",\"gbs_min\":" << num(ms.min) << ",\"gbs_mean\":" << num(ms.mean) << ",\"gbs_max\":" << num(ms.max)
     << ",\"phases\":[";
@@ -191,7 +211,11 @@ std::string run_to_json(const RunRecord& rec, int n) {
     o << (first ? "" : ",") << "{\"label\":\"" << json_escape(ph.label) << "\",\"row\":" << ph.row << ",\"col\":" << ph.col
       << ",\"seconds_per_iter\":" << num(ph.seconds_per_iter) << ",\"agg_gbs\":" << num(ph.agg_gbs)
       << ",\"compat_gbps\":" << num(compat_cell_gbps(ph)) << ",\"wall_seconds\":" << num(ph.wall_seconds)
-      << ",\"mismatches\":" << ph.total_mismatches << ",\"flows\":[";
+      << ",\"mismatches\":" << ph.total_mismatches << ",\"generations\":" << ph.generations
+      << ",\"timed_msgs\":" << ph.timed_msgs << ",\"verified_msgs\":" << ph.verified_msgs << ",\"op_bytes\":" << ph.op_bytes
+      << ",\"warmup_mismatches\":" << ph.warmup_mismatches << ",\"rechunked_to\":[";
+    for (size_t i = 0; i < ph.rechunked_to.size(); ++i) o << (i ? "," : "") << ph.rechunked_to[i];
+    o << "],\"flows\":[";
     for (size_t i = 0; i < ph.flows.size(); ++i) {
       const auto& f = ph.flows[i];
       o << (i ? "," : "") << "{\"src\":" << f.flow.src << ",\"dst\":" << f.flow.dst << ",\"seconds\":" << num(f.seconds)

@@ -135,25 +135,93 @@ std::vector<Transport::GroupFlow> group_flow_list(const Phase& phase) {
 
 }  // namespace
 
-void post_phase_iteration(Transport& t, const Phase& phase, size_t bytes, Buffers& bufs) {
+void post_phase_iteration(Transport& t, const Phase& phase, size_t bytes, Buffers& bufs, int gen) {
   const RankOps& ops = phase.ranks[static_cast<size_t>(t.rank())];
   const std::vector<int> rs = remote_slots(phase, t.rank());
+  const int base = gen * std::max(1, phase.max_recv_slots());
+  const size_t off = slot_stride(bytes) * static_cast<size_t>(gen);
   t.group_begin();
-  if (t.wants_group_flows()) t.group_flows(bufs.send_buf(), group_flow_list(phase), bytes);
-  for (size_t j = 0; j < ops.send_to.size(); ++j) t.send_to_slot(bufs.send_buf(), bytes, ops.send_to[j], rs[j]);
-  for (size_t i = 0; i < ops.recv_from.size(); ++i) t.recv(bufs.recv_buf(static_cast<int>(i)), bytes, ops.recv_from[i]);
+  if (t.wants_group_flows()) {
+    std::vector<Transport::GroupFlow> flows = group_flow_list(phase);
+    for (auto& f : flows) {
+      f.slot += base;
+      f.src_offset = off;
+    }
+    t.group_flows(bufs.send_buf(), flows, bytes);
+  }
+  for (size_t j = 0; j < ops.send_to.size(); ++j) t.send_to_slot(bufs.send_at(off), bytes, ops.send_to[j], base + rs[j]);
+  for (size_t i = 0; i < ops.recv_from.size(); ++i)
+    t.recv_from(bufs.recv_buf(base + static_cast<int>(i)), bytes, ops.recv_from[i], off);
   t.group_end();
+}
+
+size_t slot_stride_bytes(size_t bytes) { return slot_stride(bytes); }
+
+uint64_t generation_seed(int src, size_t bytes, uint64_t salt, int gen) {
+  return payload_seed(src, bytes, gen == 0 ? salt : salt ^ (static_cast<uint64_t>(gen) << 40));
+}
+
+int verify_generations(Transport& t, Bootstrap& boot, size_t max_bytes, int slots, int iters) {
+  // One generation = a send region + `slots` receive slots.
+  const size_t per_gen = slot_stride(max_bytes) * static_cast<size_t>(std::max(1, slots) + 1);
+  size_t budget = size_t{256} << 20;
+  size_t free_b = 0, total_b = 0;
+  if (t.mem_info(&free_b, &total_b)) budget = std::min(free_b / 4, size_t{32} << 30);
+  if (const char* b = std::getenv("P2P_VERIFY_BUDGET")) budget = parse_size(b);
+  long g = std::max(1, iters);
+  g = std::min<long>(g, std::max<long>(1, static_cast<long>(budget / per_gen)));
+  return static_cast<int>(-boot.allreduce_max(-static_cast<double>(g)));
 }
 
 namespace {
 
-void prepare_payload(Transport& t, const Phase& phase, const RunConfig& cfg, Buffers& bufs) {
+// Generations a phase of `cfg` uses in `bufs`: cfg.gens, capped by the
+// iterations and by the send regions and receive slots the buffers hold (the
+// same on every rank: every rank allocates the same buffers).
+int phase_generations(const Phase& phase, const RunConfig& cfg, const Buffers& bufs) {
+  if (!cfg.verify) return 1;
+  const long per = std::max(1, phase.max_recv_slots());
+  long g = std::min<long>(std::max(1, cfg.gens), std::max(cfg.iters, cfg.warmup));
+  g = std::min<long>(g, bufs.slots() / per);
+  g = std::min<long>(g, static_cast<long>(bufs.send_capacity() / slot_stride(cfg.bytes)));
+  return static_cast<int>(std::max<long>(1, g));
+}
+
+void zero_slots(Transport& t, const Phase& phase, const RunConfig& cfg, Buffers& bufs, int gens) {
+  const RankOps& ops = phase.ranks[static_cast<size_t>(t.rank())];
+  const int per = std::max(1, phase.max_recv_slots());
+  for (int g = 0; g < gens; ++g)
+    for (size_t i = 0; i < ops.recv_from.size(); ++i) t.zero(bufs.recv_buf(g * per + static_cast<int>(i)), cfg.bytes);
+}
+
+void prepare_payload(Transport& t, const Phase& phase, const RunConfig& cfg, Buffers& bufs, int gens) {
   const RankOps& ops = phase.ranks[static_cast<size_t>(t.rank())];
   P2P_CHECK(cfg.bytes <= bufs.capacity(), "message larger than buffers");
   P2P_CHECK(static_cast<int>(ops.recv_from.size()) <= bufs.slots(), "not enough receive slots");
-  if (!ops.send_to.empty()) t.fill(bufs.send_buf(), cfg.bytes, payload_seed(t.rank(), cfg.bytes, cfg.salt));
-  if (cfg.verify)
-    for (size_t i = 0; i < ops.recv_from.size(); ++i) t.zero(bufs.recv_buf(static_cast<int>(i)), cfg.bytes);
+  if (!ops.send_to.empty())
+    for (int g = 0; g < gens; ++g)
+      t.fill(bufs.send_at(slot_stride(cfg.bytes) * static_cast<size_t>(g)), cfg.bytes,
+             generation_seed(t.rank(), cfg.bytes, cfg.salt, g));
+  if (cfg.verify) zero_slots(t, phase, cfg, bufs, gens);
+}
+
+// Wrong words in this rank's receive slots of generations [0, gens).
+uint64_t check_slots(Transport& t, const Phase& phase, const RunConfig& cfg, Buffers& bufs, int gens,
+                     std::vector<uint64_t>* per_slot = nullptr) {
+  const RankOps& ops = phase.ranks[static_cast<size_t>(t.rank())];
+  const int per = std::max(1, phase.max_recv_slots());
+  uint64_t bad = 0;
+  for (int g = 0; g < gens; ++g)
+    for (size_t i = 0; i < ops.recv_from.size(); ++i) {
+      VerifyResult v = t.verify(bufs.recv_buf(g * per + static_cast<int>(i)), cfg.bytes,
+                                generation_seed(ops.recv_from[i], cfg.bytes, cfg.salt, g));
+      bad += v.mismatches;
+      if (per_slot) {
+        (*per_slot)[2 * i] += v.mismatches;
+        if (g == 0) (*per_slot)[2 * i + 1] = v.checksum;
+      }
+    }
+  return bad;
 }
 
 // Fault injection for the failure-detection tests: P2P_INJECT_FAULT =
@@ -163,6 +231,9 @@ void prepare_payload(Transport& t, const Phase& phase, const RunConfig& cfg, Buf
 //   skip    — the rank's transport silently moves no payload during the
 //             timed iterations (Transport::set_discard; the protocol still
 //             runs, so nothing hangs): verification must report it, exit 2,
+//   skip-some — the same for every other timed iteration (the even ones):
+//             caught only because every iteration has its own receive
+//             generation (RunConfig::gens),
 //   exit    — the rank dies abruptly (peers must fail, not hang),
 //   hang    — the rank stops responding (peers' watchdogs must fire).
 struct FaultSpec {
@@ -204,7 +275,7 @@ namespace {
 
 void maybe_inject_fault(Transport& t, Buffers& bufs, int rank, size_t phase_index, size_t bytes) {
   const FaultSpec& f = fault_spec();
-  if (f.kind.empty() || f.kind == "skip" || f.rank != rank) return;
+  if (f.kind.empty() || f.kind == "skip" || f.kind == "skip-some" || f.rank != rank) return;
   if (f.phase >= 0 && static_cast<size_t>(f.phase) != phase_index) return;
   if (f.kind == "corrupt") {
     if (bufs.slots() > 0) {
@@ -229,41 +300,64 @@ void maybe_inject_fault(Transport& t, Buffers& bufs, int rank, size_t phase_inde
 namespace {
 
 // RCCL 2.26 delivers exactly half of an op whose share of one p2p channel
-// exceeds 16 MiB, and reports neither that nor how many channels it gives a
-// peer; the RCCL transport sizes its ops for the channel counts it can know
-// (transport_rccl.cpp).  With --verify the warmup's deliveries are checked
-// too: should any rank see a wrong word, every rank posts smaller ops (16,
-// 4, 1 MiB, the same on all: chunking must match on both ends of a message)
-// and warms up again, until the warmup verifies.  Transports that split
-// nothing (set_max_chunk false) are left as they are.
+// exceeds 16 MiB and reports no error; the RCCL transport sizes its ops from
+// the channels RCCL set up for each peer (transport_rccl.cpp).  With --verify
+// the warmup's deliveries are checked as a second line of defence: should any
+// rank see a wrong word, every rank caps its ops at 16, 4, then 1 MiB (the
+// same on all: chunking must match on both ends of a message), re-poisons its
+// slots once every rank has drained, and warms up again, until the warmup
+// verifies.  The cap lasts for this phase only (run_phase lifts it) and the
+// phase record keeps what happened (warmup_mismatches, rechunked_to).
+// Transports that split nothing (set_chunk_cap false) are left as they are.
 void rechunk_until_warmup_verifies(Transport& t, Bootstrap& boot, const Phase& phase, const RunConfig& cfg,
-                                   Buffers& bufs, bool active) {
+                                   Buffers& bufs, bool active, int gens, PhaseResult* res) {
   const int me = t.rank();
-  const int n = boot.size();
-  auto local_mismatches = [&]() -> uint64_t {
-    if (!active) return 0;
-    uint64_t bad = 0;
-    const RankOps& ops = phase.ranks[static_cast<size_t>(me)];
-    for (size_t i = 0; i < ops.recv_from.size(); ++i)
-      bad += t.verify(bufs.recv_buf(static_cast<int>(i)), cfg.bytes, payload_seed(ops.recv_from[i], cfg.bytes, cfg.salt))
-                 .mismatches;
-    return bad;
-  };
+  const int warm_gens = std::min(gens, cfg.warmup);
+  auto local_mismatches = [&]() -> uint64_t { return active ? check_slots(t, phase, cfg, bufs, warm_gens) : 0; };
   uint64_t bad = boot.allreduce_sum_u64(local_mismatches());
+  res->warmup_mismatches = bad;
+  if (!cfg.rechunk) return;
   for (const size_t c : {size_t{16} << 20, size_t{4} << 20, size_t{1} << 20}) {
     if (bad == 0) return;
-    const size_t cur = std::max(t.max_chunk(me), t.max_chunk((me + 1) % n));
-    if (cur != 0 && c >= cur) continue;
-    if (!t.set_max_chunk(c)) return;
+    // Agreed on every rank: each posts the same groups, so each must take the
+    // same branch.
+    const size_t cur = static_cast<size_t>(boot.allreduce_max(static_cast<double>(res->op_bytes ? res->op_bytes : cfg.bytes)));
+    if (c >= cur) continue;
+    if (!t.set_chunk_cap(c)) return;
+    res->rechunked_to.push_back(c);
+    res->op_bytes = c;
     if (me == 0)
       std::fprintf(stderr, "[p2p] %s: %llu wrong words in the warmup; messages now posted as ops of <= %zu MiB\n",
                    phase.label.c_str(), static_cast<unsigned long long>(bad), c >> 20);
+    boot.barrier();  // every rank drained its warmup (push writers too)
     if (active) {
-      for (int i = 0; i < cfg.warmup; ++i) post_phase_iteration(t, phase, cfg.bytes, bufs);
+      zero_slots(t, phase, cfg, bufs, gens);
+      t.sync();
+    }
+    boot.barrier();
+    if (active) {
+      for (int i = 0; i < cfg.warmup; ++i) post_phase_iteration(t, phase, cfg.bytes, bufs, i % gens);
       t.sync();
     }
     bad = boot.allreduce_sum_u64(local_mismatches());
   }
+}
+
+// Largest op this rank posts for the phase's messages (0: one op each).
+size_t phase_op_bytes(const Transport& t, const Phase& phase, size_t bytes) {
+  const RankOps& ops = phase.ranks[static_cast<size_t>(t.rank())];
+  size_t most = 0;
+  bool split = false;
+  auto see = [&](int peer) {
+    const size_t c = t.max_chunk(peer);
+    if (c && bytes > c) {
+      split = true;
+      most = std::max(most, c);
+    }
+  };
+  for (int p : ops.send_to) see(p);
+  for (int p : ops.recv_from) see(p);
+  return split ? most : 0;
 }
 
 }  // namespace
@@ -292,29 +386,49 @@ PhaseResult run_phase(Transport& t, Bootstrap& boot, const Phase& phase, size_t 
   // Relay ranks of a multi-path transport post (and time) the phase too; a
   // flow is still charged by its two endpoints only.
   const bool active = posts_phase(t, phase, me);
+  const int gens = phase_generations(phase, cfg, bufs);
+  res.generations = gens;
+  res.op_bytes = phase_op_bytes(t, phase, cfg.bytes);
+  // The ops a phase's messages are posted as: what the transport derived, or
+  // less after a warmup that did not verify (this phase only).
+  struct ChunkCap {
+    Transport& t;
+    bool set = false;
+    ~ChunkCap() {
+      if (set) t.set_chunk_cap(0);
+    }
+  } cap{t};
 
   if (active) {
-    prepare_payload(t, phase, cfg, bufs);
-    for (int i = 0; i < cfg.warmup; ++i) post_phase_iteration(t, phase, cfg.bytes, bufs);
+    prepare_payload(t, phase, cfg, bufs, gens);
+    for (int i = 0; i < cfg.warmup; ++i) post_phase_iteration(t, phase, cfg.bytes, bufs, i % gens);
     t.sync();
   }
   if (cfg.verify && cfg.warmup > 0) {
-    rechunk_until_warmup_verifies(t, boot, phase, cfg, bufs, active);
+    rechunk_until_warmup_verifies(t, boot, phase, cfg, bufs, active, gens, &res);
+    cap.set = !res.rechunked_to.empty();
     // The warmup delivered the payload already: poison the slots again (after
     // every rank drained its warmup), so the check after timing passes only
     // for data the timed iterations delivered.
     boot.barrier();
     if (active) {
-      const RankOps& ops = phase.ranks[static_cast<size_t>(me)];
-      for (size_t i = 0; i < ops.recv_from.size(); ++i) t.zero(bufs.recv_buf(static_cast<int>(i)), cfg.bytes);
+      zero_slots(t, phase, cfg, bufs, gens);
       t.sync();
     }
   }
   const bool skip = active && fault_applies("skip", me, static_cast<long>(phase_index));
+  const bool skip_some = active && fault_applies("skip-some", me, static_cast<long>(phase_index));
   if (skip) {
     std::fprintf(stderr, "[p2p] injected fault: rank %d moves no payload in the timed iterations\n", me);
     t.set_discard(true);
   }
+  if (skip_some)
+    std::fprintf(stderr, "[p2p] injected fault: rank %d moves no payload in every other timed iteration\n", me);
+  // Iteration i posts generation i mod gens; skip-some drops the even ones.
+  auto post = [&](int i) {
+    if (skip_some) t.set_discard(i % 2 == 0);
+    post_phase_iteration(t, phase, cfg.bytes, bufs, i % gens);
+  };
 
   double my_seconds = 0;
   std::vector<double> iter_samples;
@@ -329,7 +443,7 @@ PhaseResult run_phase(Transport& t, Bootstrap& boot, const Phase& phase, size_t 
       iter_samples.reserve(static_cast<size_t>(cfg.iters));
       for (int i = 0; i < cfg.iters; ++i) {
         double a = now_seconds();
-        post_phase_iteration(t, phase, cfg.bytes, bufs);
+        post(i);
         t.sync();
         iter_samples.push_back((now_seconds() - a) * 1e6);
       }
@@ -343,7 +457,7 @@ PhaseResult run_phase(Transport& t, Bootstrap& boot, const Phase& phase, size_t 
       std::vector<int> marks;
       marks.reserve(static_cast<size_t>(cfg.iters));
       for (int i = 0; i < cfg.iters; ++i) {
-        post_phase_iteration(t, phase, cfg.bytes, bufs);
+        post(i);
         if (cfg.samples || i + 1 == cfg.iters) marks.push_back(t.mark());
       }
       t.sync();
@@ -369,24 +483,30 @@ PhaseResult run_phase(Transport& t, Bootstrap& boot, const Phase& phase, size_t 
   }
   const double w1 = now_seconds();
   res.wall_seconds = w1 - w0;
-  if (skip) t.set_discard(false);
+  if (skip || skip_some) t.set_discard(false);
 
   if (active) maybe_inject_fault(t, bufs, me, phase_index, cfg.bytes);
 
   std::string err = t.async_error();
   if (!err.empty()) P2P_FATAL("transport reported an asynchronous error: " + err);
 
-  // Verification of every receive slot on this rank.
+  // Verification of every receive slot of every generation on this rank:
+  // per slot, the wrong words summed over generations and generation 0's
+  // checksum.
   const int maxslots = std::max(1, phase.max_recv_slots());
   std::vector<uint64_t> vr(static_cast<size_t>(maxslots) * 2, 0);
-  if (active && cfg.verify) {
-    const RankOps& ops = phase.ranks[static_cast<size_t>(me)];
-    for (size_t i = 0; i < ops.recv_from.size(); ++i) {
-      VerifyResult v = t.verify(bufs.recv_buf(static_cast<int>(i)), cfg.bytes, payload_seed(ops.recv_from[i], cfg.bytes, cfg.salt));
-      vr[2 * i] = v.mismatches;
-      vr[2 * i + 1] = v.checksum;
+  const int timed_gens = std::min(gens, cfg.iters);
+  uint64_t cover[2] = {0, 0};  // timed deliveries, verified deliveries (this rank)
+  if (active) {
+    const uint64_t nrecv = phase.ranks[static_cast<size_t>(me)].recv_from.size();
+    cover[0] = nrecv * static_cast<uint64_t>(cfg.iters);
+    if (cfg.verify) {
+      check_slots(t, phase, cfg, bufs, timed_gens, &vr);
+      cover[1] = nrecv * static_cast<uint64_t>(timed_gens);
     }
   }
+  res.timed_msgs = boot.allreduce_sum_u64(cover[0]);
+  res.verified_msgs = boot.allreduce_sum_u64(cover[1]);
 
   res.rank_seconds = boot.allgather_value(my_seconds);
   const double span[2] = {w0, w1};

@@ -41,6 +41,17 @@ struct RunConfig {
   bool verify = false;
   bool samples = true;       // record an event per iteration for the distribution
   uint64_t salt = 0;
+  // With verify: receive generations.  Iteration i (warmup and timed alike)
+  // sends from send region i mod G, filled with that generation's PRNG stream,
+  // into receive slots g * P + 0..P-1 (P = the phase's most receive slots on
+  // any rank), so up to G timed deliveries per slot are checked, not only the
+  // last one (run_phase caps G by the buffers; verify_generations() sizes it).
+  int gens = 1;
+  // With verify: a warmup that does not verify makes every rank post smaller
+  // ops (rechunk_until_warmup_verifies) -- the second line of defence against
+  // RCCL's half-delivery.  P2P_RECHUNK=0 turns it off, so the timed check
+  // reports the loss instead.
+  bool rechunk = true;
 };
 
 struct FlowResult {
@@ -70,6 +81,17 @@ struct PhaseResult {
   std::vector<double> host_end;      // timed region (seconds; one clock per host) -> --trace
   std::vector<FlowResult> flows;
   uint64_t total_mismatches = 0;
+  // Verification coverage (all ranks): timed deliveries, and those checked
+  // (one per receive slot and generation; G >= iters checks every one).
+  int generations = 1;
+  uint64_t timed_msgs = 0;
+  uint64_t verified_msgs = 0;
+  // Op size the phase's messages were posted as (largest over this rank's
+  // peers; 0 = one op per message) and what the warmup check saw: wrong words
+  // in the first warmup and the op sizes it had to fall back to.
+  size_t op_bytes = 0;
+  uint64_t warmup_mismatches = 0;
+  std::vector<size_t> rechunked_to;
 };
 
 // Send buffer + receive slots for one rank.  The slots are carved from one
@@ -111,8 +133,23 @@ int remote_slot(const Phase& phase, int me, int peer);
 // hold several flows between the same two ranks, e.g. ring-bi with 2 ranks).
 std::vector<int> remote_slots(const Phase& phase, int me);
 
-// Posts one iteration (one group) of `phase` for this rank.
-void post_phase_iteration(Transport& t, const Phase& phase, size_t bytes, Buffers& bufs);
+// Posts one iteration (one group) of `phase` for this rank, generation `gen`:
+// the payload comes from send region gen (slot_stride(bytes) apart) and lands
+// in receive slots gen * phase.max_recv_slots() + i.
+void post_phase_iteration(Transport& t, const Phase& phase, size_t bytes, Buffers& bufs, int gen = 0);
+
+// Receive generations for verified runs of messages up to `max_bytes` with
+// `slots` receive slots per iteration and up to `iters` iterations: as many as
+// P2P_VERIFY_BUDGET bytes of send regions + receive slots allow (default a
+// quarter of free device memory, at most 32 GiB; 256 MiB where the transport
+// cannot tell), agreed by every rank (collective).
+int verify_generations(Transport& t, Bootstrap& boot, size_t max_bytes, int slots, int iters);
+
+// Receive-slot / send-region stride for messages of `bytes` (4 KiB aligned).
+size_t slot_stride_bytes(size_t bytes);
+
+// PRNG stream of generation `gen` of a run's payload from `src`.
+uint64_t generation_seed(int src, size_t bytes, uint64_t salt, int gen);
 
 // Runs one phase on every rank (collective over `boot`).
 PhaseResult run_phase(Transport& t, Bootstrap& boot, const Phase& phase, size_t phase_index, const RunConfig& cfg,
@@ -237,9 +274,18 @@ class StepDriver {
   void sync();                  // wait for everything posted
   std::vector<double> step_ms();       // this rank's per-step durations since the last reset
   void reset();                 // forget recorded steps
-  // Collective, blocking, untimed: zero every receive slot of every rank and
-  // arm P2P_INJECT_FAULT=skip for the steps that follow.
+  // Collective, blocking, untimed: zero every receive slot of every rank once
+  // every rank has drained.
+  void clear();
+  // clear(), then arm P2P_INJECT_FAULT=skip (no payload) or skip-some (no
+  // payload in every other step) for the steps that follow.
   void poison();
+  // Collective: record the step graphs again (opt.graph), after the
+  // transport's op sizes changed (Transport::set_chunk_cap); a graph replays
+  // the ops it recorded.
+  void recapture();
+  int recaptures() const { return recaptures_; }
+  bool graphs() const { return opt_.graph; }
   // Collective: checks every receive slot written by steps [first, first +
   // count) against the payload of the message that wrote it last.
   StepVerifyReport verify_steps(long first, long count);
@@ -276,9 +322,12 @@ class StepDriver {
   std::vector<int> graphs_;  // per (generation, phase), when opt_.graph
   long last_step_ = -1;
   bool skip_armed_ = false;
+  bool skip_some_armed_ = false;
+  int recaptures_ = 0;
   int chain_mark_ = -1;  // run_steps: the previous step's end mark, the next one's start
 
   void step_impl(long k, bool chain);
+  void capture_graphs();
 
   void post_step_ops(const Phase& p, int pi, int gen);
   int gen_of(long k) const { return static_cast<int>((k / phases()) % depth_); }

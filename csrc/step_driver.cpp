@@ -80,7 +80,7 @@ StepDriver::StepDriver(Transport& t, Bootstrap& boot, Schedule sched, size_t byt
 }
 
 StepDriver::~StepDriver() {
-  if (skip_armed_) t_.set_discard(false);
+  if (skip_armed_ || skip_some_armed_) t_.set_discard(false);
 }
 
 int StepDriver::slot_index(int rank, int gen, int phase, int msg, int i) const {
@@ -110,20 +110,32 @@ void StepDriver::connect() {
   t_.sync();
   // Graph capture only records launches (no peer interaction), so it must
   // follow the warm-up that established every lazy connection.
-  if (opt_.graph && graphs_.empty()) {
-    for (int g = 0; g < depth_; ++g)
-      for (size_t pi = 0; pi < sched_.phases.size(); ++pi) {
-        const Phase& p = sched_.phases[pi];
-        if (!p.participates(t_.rank())) {
-          graphs_.push_back(-1);
-          continue;
-        }
-        t_.capture_begin();
-        post_step_ops(p, static_cast<int>(pi), g);
-        graphs_.push_back(t_.capture_end());
+  if (opt_.graph && graphs_.empty()) capture_graphs();
+}
+
+void StepDriver::capture_graphs() {
+  graphs_.clear();
+  for (int g = 0; g < depth_; ++g)
+    for (size_t pi = 0; pi < sched_.phases.size(); ++pi) {
+      const Phase& p = sched_.phases[pi];
+      if (!p.participates(t_.rank())) {
+        graphs_.push_back(-1);
+        continue;
       }
-    boot_.barrier();
-  }
+      t_.capture_begin();
+      post_step_ops(p, static_cast<int>(pi), g);
+      graphs_.push_back(t_.capture_end());
+    }
+  boot_.barrier();
+}
+
+void StepDriver::recapture() {
+  // A graph replays the ops it recorded, op sizes included: after the
+  // transport's chunking changed, the steps must be recorded again.
+  if (!opt_.graph) return;
+  sync();
+  capture_graphs();
+  ++recaptures_;
 }
 
 void StepDriver::post_step_ops(const Phase& p, int pi, int gen) {
@@ -175,6 +187,10 @@ void StepDriver::step_impl(long k, bool chain) {
   const int g = gen_of(k);
   const Phase& p = sched_.phases[static_cast<size_t>(pi)];
   if (!chain) chain_mark_ = -1;
+  // skip-some: every other step moves no payload (a graph replay would not
+  // honour the discard, so such steps are posted eagerly).
+  if (skip_some_armed_) t_.set_discard(k % 2 == 0);
+  const bool replay = opt_.graph && !skip_armed_ && !skip_some_armed_;
   if (!p.participates(t_.rank())) {
     if (posts_phase(t_, p, t_.rank())) post_step_ops(p, pi, g);  // relay only: no flow of its own to time
     marks_.emplace_back(-1, -1);
@@ -186,7 +202,7 @@ void StepDriver::step_impl(long k, bool chain) {
     // profiles/r2_mark_fence/).
     const int a = chain_mark_ >= 0 ? chain_mark_ : t_.mark();
     const size_t gi = static_cast<size_t>(g) * sched_.phases.size() + static_cast<size_t>(pi);
-    if (opt_.graph && gi < graphs_.size() && graphs_[gi] >= 0)
+    if (replay && gi < graphs_.size() && graphs_[gi] >= 0)
       t_.graph_launch(graphs_[gi]);
     else
       post_step_ops(p, pi, g);
@@ -215,7 +231,7 @@ void StepDriver::reset() {
   t_.clear_marks();
 }
 
-void StepDriver::poison() {
+void StepDriver::clear() {
   // Every rank drains first: with a push transport a peer writes into this
   // rank's slots, and its writes are complete once this rank's receives are.
   sync();
@@ -225,18 +241,26 @@ void StepDriver::poison() {
     t_.sync();
   }
   boot_.barrier();
+}
+
+void StepDriver::poison() {
+  clear();
   const int me = t_.rank();
   if (!skip_armed_ && fault_applies("skip", me, -1)) {
     std::fprintf(stderr, "[p2p] injected fault: rank %d moves no payload in the steps after poison()\n", me);
     skip_armed_ = true;
     t_.set_discard(true);
   }
+  if (!skip_some_armed_ && fault_applies("skip-some", me, -1)) {
+    std::fprintf(stderr, "[p2p] injected fault: rank %d moves no payload in every other step after poison()\n", me);
+    skip_some_armed_ = true;
+  }
 }
 
 StepVerifyReport StepDriver::verify_steps(long first, long count) {
-  if (skip_armed_) {
+  if (skip_armed_ || skip_some_armed_) {
     t_.set_discard(false);
-    skip_armed_ = false;
+    skip_armed_ = skip_some_armed_ = false;
   }
   const int me = t_.rank();
   uint64_t timed = 0, bad = 0;

@@ -155,11 +155,23 @@ class Transport {
   virtual bool gate_timed_out() { return false; }
 
   // ---- message chunking (RCCL) ----
-  // Largest single op a message to a peer is posted as (0 = unsplit), and
-  // setting it for every peer (0 = no splitting); both ends must use the same
-  // value, so callers set it collectively.  false / 0 where nothing is split.
-  virtual bool set_max_chunk(size_t /*bytes*/) { return false; }
+  // Largest single op a message to a peer is posted as (0 = unsplit): the
+  // limit the transport derived for that peer, capped by set_chunk_cap(cap)
+  // (0 lifts the cap).  Both ends of a message must split it alike, so callers
+  // set the cap collectively.  false / 0 where nothing is split.
+  virtual bool set_chunk_cap(size_t /*bytes*/) { return false; }
   virtual size_t max_chunk(int /*peer*/) const { return 0; }
+
+  // What the data plane set up towards each peer, as a JSON object (RCCL: the
+  // p2p channels its INFO log reports per communicator, the transport each
+  // peer connection uses, the op limit derived from them); "" where there is
+  // nothing to report.  Local (not collective); call it after the runs, once
+  // the lazy connections exist.
+  virtual std::string link_report() { return ""; }
+  // Per peer, the class of transport the data plane reaches it through
+  // ("P2P", "SHM", "NET", "self"; "" unknown or not connected); empty where
+  // the transport has no such notion.
+  virtual std::vector<std::string> peer_transports() { return {}; }
 
   // ---- health ----
   // Non-empty when the transport saw an asynchronous error (e.g. a peer died).

@@ -46,10 +46,16 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <strings.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
+#include <fstream>
+#include <sstream>
 #include <thread>
 #include <vector>
 
@@ -58,6 +64,7 @@
 #include "hip_check.hpp"
 #include "kernels.hpp"
 #include "provenance.hpp"
+#include "rccl_log.hpp"
 #include "report.hpp"
 #include "stream_gate.hpp"
 #include "topology.hpp"
@@ -66,6 +73,81 @@
 
 namespace p2p {
 namespace {
+
+// RCCL's INFO log, which this process reads to learn the p2p channels and
+// transports RCCL set up (rccl_log.hpp).  Unless the user asked for RCCL's
+// log themselves (NCCL_DEBUG / NCCL_DEBUG_FILE) or P2P_RCCL_LOG=0, the
+// first transport of the process points it at a private file before RCCL's
+// first initialisation reads the variables; the file is removed at exit
+// (P2P_RCCL_LOG=keep keeps it).  Empty path: no log to read.
+struct RcclLog {
+  std::string path;
+  bool ours = false;
+};
+RcclLog& rccl_log() {
+  static RcclLog log = [] {
+    RcclLog l;
+    const char* mode = std::getenv("P2P_RCCL_LOG");
+    if (mode && std::strcmp(mode, "0") == 0) return l;
+    if (const char* f = std::getenv("NCCL_DEBUG_FILE")) {
+      // The user's file: readable only if it names no per-process pattern.
+      if (!std::strchr(f, '%')) l.path = f;
+      return l;
+    }
+    // NCCL_DEBUG=VERSION (set in the image's environment) asks only for the
+    // version banner; any other level is the user asking for RCCL's log on
+    // stderr, which is then left alone.
+    if (const char* lvl = std::getenv("NCCL_DEBUG"); lvl && *lvl && strcasecmp(lvl, "VERSION") != 0) return l;
+    const char* tmp = std::getenv("TMPDIR");
+    l.path = strfmt("%s/p2p_rccl_info_%d.log", tmp && *tmp ? tmp : "/tmp", static_cast<int>(getpid()));
+    l.ours = true;
+    setenv("NCCL_DEBUG", "INFO", 1);
+    if (!std::getenv("NCCL_DEBUG_SUBSYS")) setenv("NCCL_DEBUG_SUBSYS", "INIT,ENV,P2P,NET,SHM", 1);
+    setenv("NCCL_DEBUG_FILE", l.path.c_str(), 1);
+    if (!(mode && std::strcmp(mode, "keep") == 0))
+      std::atexit([] { std::remove(rccl_log().path.c_str()); });
+    return l;
+  }();
+  return log;
+}
+
+size_t log_size() {
+  const std::string& p = rccl_log().path;
+  if (p.empty()) return 0;
+  std::ifstream in(p, std::ios::binary | std::ios::ate);
+  return in ? static_cast<size_t>(in.tellg()) : 0;
+}
+
+std::string log_since(size_t offset) {
+  const std::string& p = rccl_log().path;
+  if (p.empty()) return "";
+  std::ifstream in(p, std::ios::binary);
+  if (!in) return "";
+  in.seekg(static_cast<std::streamoff>(offset));
+  std::stringstream ss;
+  ss << in.rdbuf();
+  return ss.str();
+}
+
+// The last few WARN lines of the log since `offset` (RCCL's own account of an
+// error, which the private log would otherwise hide).
+std::string log_warnings(size_t offset) {
+  std::istringstream in(log_since(offset));
+  std::vector<std::string> warn;
+  for (std::string line; std::getline(in, line);)
+    if (line.find("NCCL WARN") != std::string::npos) warn.push_back(line);
+  std::string out;
+  for (size_t i = warn.size() > 4 ? warn.size() - 4 : 0; i < warn.size(); ++i) out += "\n  rccl: " + warn[i];
+  return out;
+}
+
+// The host RCCL places a rank on: NCCL_HOSTID when set, else the hostname.
+std::string rccl_host_id() {
+  if (const char* h = std::getenv("NCCL_HOSTID")) return h;
+  char name[256] = {0};
+  if (gethostname(name, sizeof(name) - 1) != 0) return "?";
+  return name;
+}
 
 class RcclTransport final : public Transport {
  public:
@@ -224,19 +306,13 @@ class RcclTransport final : public Transport {
       used_.resize(cstreams_.size(), false);
     }
   }
-  // Messages above the peer's chunk are posted as several back-to-back ops of
-  // at most that many bytes inside the same group (matched in order on both
-  // sides).  RCCL 2.26 on MI355X delivers exactly half of a send/recv whose
-  // share of one p2p channel exceeds 16 MiB: with its 64 p2p channels that
-  // is any message above 1 GiB (scripts/rccl_size_probe.py), with
-  // NCCL_MAX_P2P_NCHANNELS=1 / 2 / 4 / 8 anything above 16 / 32 / 64 / 128
-  // MiB (profiles/r2_rccl_channels/p2p_threshold/).  Chunks therefore stay
-  // at 16 MiB x channels: 64 channels (or fewer, as the NCCL_* channel knobs
-  // set) to this rank itself; to other ranks, whose per-peer channel count
-  // RCCL derives from the topology and does not report, 2 channels' worth
-  // (32 MiB, the bench's message size; bench.py halves it further should
-  // its warmup not verify).  P2P_RCCL_MAX_CHUNK=<bytes> sets every peer's,
-  // 0 disables splitting.
+  // Messages above the peer's op limit are posted as several back-to-back
+  // ops of at most that many bytes inside the same group (matched in order
+  // on both sides): RCCL 2.26 / 2.27 on MI355X deliver only the first half of
+  // an op whose share of one p2p channel exceeds 16 MiB
+  // (scripts/rccl_half_repro.cpp, profiles/r3_rccl_half_repro/), so the
+  // limit is 16 MiB x the channels RCCL splits an op to that peer over
+  // (derive_op_limits).
   void send(const void* p, size_t bytes, int peer) override {
     const int j = pick(&send_seq_, peer, bytes);
     const char* c = static_cast<const char*>(p);
@@ -399,10 +475,15 @@ class RcclTransport final : public Transport {
   }
 
   int concurrency() const override { return static_cast<int>(comms_.size()); }
-  // Small messages (latency) run on communicator 0, on the main stream.
-  bool set_max_chunk(size_t bytes) override {
-    self_chunk_ = peer_chunk_ = bytes;
+  bool set_chunk_cap(size_t bytes) override {
+    cap_ = bytes;
     return true;
+  }
+  std::string link_report() override { return peers_json(); }
+  std::vector<std::string> peer_transports() override {
+    std::vector<std::string> out;
+    for (const auto& l : rccl_peer_links(parse_rccl_connections(log_since(log_start_)), rank_, n_)) out.push_back(l.transport);
+    return out;
   }
   size_t max_chunk(int peer) const override { return chunk_for(peer); }
 
@@ -492,18 +573,17 @@ class RcclTransport final : public Transport {
       for (auto& id : ids) nccl_ok(ncclGetUniqueId(&id), "ncclGetUniqueId");
     boot.bcast(ids.data(), sizeof(ncclUniqueId) * ids.size(), 0);
 
-    self_chunk_ = kChunkPerChannel * static_cast<size_t>(p2p_channel_limit(64));
-    peer_chunk_ = kChunkPerChannel * static_cast<size_t>(p2p_channel_limit(2));
-    if (const char* mc = std::getenv("P2P_RCCL_MAX_CHUNK"))
-      self_chunk_ = peer_chunk_ = std::strcmp(mc, "0") ? parse_size(mc) : 0;
     if (const char* sm = std::getenv("P2P_RCCL_SPLIT_MIN")) split_min_ = parse_size(sm);
     if (const char* rg = std::getenv("P2P_RCCL_REGISTER")) register_ = std::atoi(rg);
     const char* blk = std::getenv("P2P_RCCL_BLOCKING");
     nonblocking_ = opt.nonblocking_init && !(blk && std::atoi(blk));
     comms_.assign(static_cast<size_t>(ncomms), nullptr);
     hook_ = push_abort_hook([this](int) { abort_all(); });
+    rccl_log();  // before RCCL's first init in this process reads NCCL_DEBUG*
+    log_start_ = log_size();
     // One communicator after the other, in the same order on every rank.
     for (int j = 0; j < ncomms; ++j) {
+      const size_t before = log_size();
       if (nonblocking_) {
         ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
         cfg.blocking = 0;
@@ -512,7 +592,86 @@ class RcclTransport final : public Transport {
       } else {
         nccl_ok(ncclCommInitRank(&comms_[static_cast<size_t>(j)], n_, ids[static_cast<size_t>(j)], rank_), "ncclCommInitRank");
       }
+      comm_info_.push_back(parse_rccl_init(log_since(before)));
     }
+    derive_op_limits(boot);
+  }
+
+  // Largest op per peer: RCCL delivers only the first half of an op whose
+  // share of one p2p channel exceeds 16 MiB (scripts/rccl_half_repro.cpp,
+  // both RCCLs of the image), so ops stay at 16 MiB x the channels an op to
+  // that peer is split over -- min(p2p channels, p2p channels per peer) of
+  // every communicator from RCCL's INFO log, and at most
+  // NCCL_NCHANNELS_PER_NET_PEER (2) for a peer on another host.  Both ends
+  // must split a message alike, so the ranks agree on min(a's view of b,
+  // b's view of a).  Without the log (the user set NCCL_DEBUG, or RCCL was
+  // initialised before), the conservative guess of round 2 stands: 64
+  // channels to itself, 2 to others, fewer under the NCCL channel knobs.
+  // P2P_RCCL_MAX_CHUNK=<bytes> sets every peer's limit, 0 disables splitting.
+  void derive_op_limits(Bootstrap& boot) {
+    char host[128] = {0};
+    std::snprintf(host, sizeof(host), "%s", rccl_host_id().c_str());
+    std::vector<char> hosts(static_cast<size_t>(n_) * sizeof(host));
+    boot.allgather(host, hosts.data(), sizeof(host));
+    net_peer_.assign(static_cast<size_t>(n_), 0);
+    for (int p = 0; p < n_; ++p)
+      net_peer_[static_cast<size_t>(p)] = std::strcmp(&hosts[static_cast<size_t>(p) * sizeof(host)], host) != 0;
+    int net_per_peer = 2;
+    if (const char* v = std::getenv("NCCL_NCHANNELS_PER_NET_PEER"))
+      if (std::atoi(v) > 0) net_per_peer = std::atoi(v);
+    bool logged = !comm_info_.empty();
+    for (const auto& ci : comm_info_) logged = logged && ci.found();
+    std::vector<int> mine(static_cast<size_t>(n_), 0);
+    for (int p = 0; p < n_; ++p) {
+      int c = 0;
+      if (logged) {
+        for (const auto& ci : comm_info_) {
+          const int x = rccl_op_channels(ci, net_peer_[static_cast<size_t>(p)] != 0, net_per_peer);
+          c = c == 0 ? x : std::min(c, x);
+        }
+      } else {
+        c = p2p_channel_limit(p == rank_ ? 64 : 2);
+      }
+      mine[static_cast<size_t>(p)] = c;
+    }
+    const std::vector<int> all = boot.allgather_vector(mine);
+    op_channels_.assign(static_cast<size_t>(n_), 0);
+    peer_limit_.assign(static_cast<size_t>(n_), 0);
+    for (int p = 0; p < n_; ++p) {
+      const int c = std::min(all[static_cast<size_t>(rank_) * n_ + p], all[static_cast<size_t>(p) * n_ + rank_]);
+      op_channels_[static_cast<size_t>(p)] = c;
+      peer_limit_[static_cast<size_t>(p)] = kRcclBytesPerChannel * static_cast<size_t>(std::max(c, 1));
+    }
+    limit_source_ = logged ? "rccl INFO log: 16M x min(p2p channels, per peer[, net per peer])"
+                           : "default (no RCCL INFO log): 16M x 64 self / 2 peers";
+    if (const char* mc = std::getenv("P2P_RCCL_MAX_CHUNK")) {
+      const size_t v = std::strcmp(mc, "0") ? parse_size(mc) : 0;
+      std::fill(peer_limit_.begin(), peer_limit_.end(), v);
+      limit_source_ = strfmt("P2P_RCCL_MAX_CHUNK=%s", mc);
+    }
+  }
+
+  // link_report(): the communicators' channel counts, and per peer the
+  // transport and channels RCCL's connection lines show, next to the op
+  // limit in use.
+  std::string peers_json() const {
+    const std::string text = log_since(log_start_);
+    const auto links = rccl_peer_links(parse_rccl_connections(text), rank_, n_);
+    std::string o = strfmt("{\"rank\":%d,\"log\":%s,\"op_limit_source\":\"%s\",\"comms\":[", rank_,
+                           rccl_log().path.empty() ? "null" : "true", json_escape(limit_source_).c_str());
+    for (size_t j = 0; j < comm_info_.size(); ++j)
+      o += strfmt("%s{\"p2p_channels\":%d,\"p2p_channels_per_peer\":%d,\"nnodes\":%d}", j ? "," : "",
+                  comm_info_[j].p2p_channels, comm_info_[j].p2p_per_peer, comm_info_[j].nnodes);
+    o += "],\"peers\":[";
+    for (int p = 0; p < n_; ++p) {
+      const auto& l = links[static_cast<size_t>(p)];
+      o += strfmt("%s{\"peer\":%d,\"transport\":\"%s\",\"via\":\"%s\",\"channels_connected\":%d,\"op_channels\":%d,"
+                  "\"op_limit\":%zu,\"net\":%s}",
+                  p ? "," : "", p, json_escape(l.transport).c_str(), json_escape(l.via).c_str(), l.channels_connected,
+                  op_channels_.empty() ? 0 : op_channels_[static_cast<size_t>(p)], chunk_for(p),
+                  !net_peer_.empty() && net_peer_[static_cast<size_t>(p)] ? "true" : "false");
+    }
+    return o + "]}";
   }
 
   void describe(int ncomms, int cu_mask_mode) {
@@ -622,7 +781,8 @@ class RcclTransport final : public Transport {
       return;
     }
     ncclComm_t c = comms_.empty() ? nullptr : comms_[0];
-    std::string msg = strfmt("rank %d: %s failed: %s (%s)", rank_, what, ncclGetErrorString(r), c ? ncclGetLastError(c) : "");
+    std::string msg = strfmt("rank %d: %s failed: %s (%s)", rank_, what, ncclGetErrorString(r), c ? ncclGetLastError(c) : "") +
+                      log_warnings(log_start_);
     abort_all();  // a communicator that returned an error is not used again
     P2P_FATAL(msg);
   }
@@ -653,7 +813,7 @@ class RcclTransport final : public Transport {
     }
     if (r != ncclSuccess) {
       abort_all();
-      P2P_FATAL(strfmt("rank %d: %s failed: %s", rank_, what, ncclGetErrorString(r)));
+      P2P_FATAL(strfmt("rank %d: %s failed: %s", rank_, what, ncclGetErrorString(r)) + log_warnings(log_start_));
     }
   }
 
@@ -665,10 +825,15 @@ class RcclTransport final : public Transport {
   hipStream_t recv_stream_ = nullptr;  // two-stream (reference) layout only
   hipEvent_t join_ = nullptr;
   bool recv_on_side_ = false;
-  // Message chunking (see send()): 16 MiB per RCCL p2p channel.
-  static constexpr size_t kChunkPerChannel = size_t{16} << 20;
-  size_t self_chunk_ = kChunkPerChannel * 64;
-  size_t peer_chunk_ = kChunkPerChannel * 2;
+  // Message chunking (see send()): at most kRcclBytesPerChannel per p2p
+  // channel of the peer (derive_op_limits), capped by set_chunk_cap().
+  std::vector<size_t> peer_limit_;       // per peer; 0 = unsplit
+  std::vector<int> op_channels_;         // per peer: channels an op is split over (0 unknown)
+  std::vector<char> net_peer_;           // per peer: RCCL reaches it through its network transport
+  std::vector<RcclInitInfo> comm_info_;  // per communicator, from RCCL's INFO log
+  std::string limit_source_;             // how peer_limit_ was set
+  size_t cap_ = 0;                       // set_chunk_cap (0: none)
+  size_t log_start_ = 0;                 // this transport's part of the RCCL log
   // `fallback` channels, or fewer where NCCL_MAX_P2P_NCHANNELS /
   // NCCL_NCHANNELS_PER_PEER ask RCCL for fewer.
   static int p2p_channel_limit(int fallback) {
@@ -678,7 +843,11 @@ class RcclTransport final : public Transport {
         if (const int x = std::atoi(v); x > 0) c = std::min(c, x);
     return c;
   }
-  size_t chunk_for(int peer) const { return peer == rank_ ? self_chunk_ : peer_chunk_; }
+  size_t chunk_for(int peer) const {
+    const size_t lim = peer_limit_.empty() ? 0 : peer_limit_[static_cast<size_t>(peer)];
+    if (cap_ == 0) return lim;
+    return lim == 0 ? cap_ : std::min(lim, cap_);
+  }
   size_t chunk_of(size_t bytes, int peer) const {
     const size_t c = chunk_for(peer);
     return (c && bytes > c) ? c : bytes;

@@ -152,6 +152,10 @@ class ShmTransport final : public Transport {
   void group_end() override {
     P2P_CHECK(in_group_, "group_end without group_begin");
     in_group_ = false;
+    std::vector<size_t> sent(static_cast<size_t>(n_), 0);
+    for (const auto& op : ops_)
+      if (op.is_send) sent[static_cast<size_t>(op.peer)] += op.bytes;
+    emulate_link_delay(sent, rank_);
     run_ops();
   }
 

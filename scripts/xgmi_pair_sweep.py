@@ -12,15 +12,20 @@ build/p2p_matrix under every setting that can move a single xGMI link:
               communicator / allocated by ncclMemAlloc: RCCL may then move
               data straight between the user buffers instead of through its
               staging FIFO, csrc/transport_rccl.cpp),
-              P2P_RCCL_MAX_CHUNK=1G (1 GiB ops instead of 32 MiB ones: RCCL
-              loses half of an op above 16 MiB per p2p channel, so this row
-              tells whether the link gets >= 64 channels)
+              P2P_RCCL_MAX_CHUNK=1G (1 GiB ops instead of 16 MiB x the p2p
+              channels RCCL's INFO log reports for the peer: RCCL loses the
+              second half of an op above 16 MiB per p2p channel,
+              scripts/rccl_half_repro.cpp, so this row is corrupt unless the
+              link gets >= 64 channels)
   ipc rows    --ipc-engine kernel (one-sided pull by the gfx950 copy kernel),
               sdma, push, relay (stripes through idle third GPUs, N >= 3)
 
-Every row runs with --verify.  A row whose data does not verify (rc 2: a
-setting under which RCCL delivers wrong bytes) is recorded as corrupt, never
-wins, and the sweep goes on; any other failure (crash, hang, timeout) ends the
+Every row runs with --verify and with the verified-warmup fallback off
+(P2P_RECHUNK=0), so a setting under which RCCL delivers wrong bytes shows as
+such instead of being re-posted in smaller ops under the same label.  A row
+whose data does not verify (rc 2) is recorded as corrupt, never wins, and the
+sweep goes on; every row also records the transport and p2p channels RCCL set
+up for the pair (the p2p_matrix {"type":"links"} record); any other failure (crash, hang, timeout) ends the
 sweep, so the GPU is never driven again after a fault.  Every row's cell GB/s,
 p50 per message and the environment it ran under are written to
 <out>/rows.jsonl.
@@ -169,6 +174,21 @@ def cell_result(js_path, dirs):
     return out
 
 
+def link_result(js_path):
+    """Rank 0's view of peer 1 from the run's {"type":"links"} record: the
+    transport class RCCL connected it through, the p2p channels, the op limit."""
+    with open(js_path) as fh:
+        for line in fh:
+            rec = json.loads(line)
+            if rec.get("type") == "links" and rec.get("ranks") and rec["ranks"][0]:
+                r0 = rec["ranks"][0]
+                peer = r0["peers"][1] if len(r0.get("peers", [])) > 1 else {}
+                return {"transport": peer.get("transport"), "via": peer.get("via"),
+                        "channels_connected": peer.get("channels_connected"), "op_channels": peer.get("op_channels"),
+                        "op_limit": peer.get("op_limit"), "source": r0.get("op_limit_source")}
+    return None
+
+
 def run_row(args, row, np_, exe, tag, t_end=None):
     """One row as its own mpirun job, in a session of its own: on a timeout
     the whole job (launcher, proxies, ranks) is killed, so no rank is left
@@ -185,7 +205,7 @@ def run_row(args, row, np_, exe, tag, t_end=None):
     cmd += row["args"]
     if args.emulate in ("ipc", "rccl"):
         cmd += ["--device", "0"]
-    env = dict(os.environ, **row["env"])
+    env = dict(os.environ, P2P_RECHUNK="0", **row["env"])
     if args.emulate == "rccl":
         env.update(EMULATE_RCCL_ENV)
     t0 = time.time()
@@ -206,6 +226,7 @@ def run_row(args, row, np_, exe, tag, t_end=None):
     if rc == 0:
         res = cell_result(js, set(args.dirs.split(",")))
         rec["cells"] = {"%s/%d" % k: v for k, v in sorted(res.items())}
+        rec["link_0_1"] = link_result(js)
         bad = sum(v["mismatches"] for v in res.values())
         if bad or not res:
             rec["rc"] = 2

@@ -1,0 +1,274 @@
+"""Shared pieces of bench.py: logging, the deadline and its watchdog, the
+result reporter, and the pure functions behind the headline numbers (unit
+tested in tests/test_bench_unit.py through bench.py's re-exports)."""
+
+from __future__ import annotations
+
+import json
+import math
+import os
+import socket
+import statistics
+import sys
+import threading
+import time
+
+import torch
+
+from test_nccl_p2p_amd.utils.proc import kill_children
+
+METRIC = "pairwise P2P GB/s matrix (min/mean) + p50 latency at 1/2/4/8 MI355X"
+BASELINE_VALUE = None  # the reference publishes no numbers
+RESERVE_S = 15.0  # kept free at the end of the deadline for the JSON line and teardown
+T0 = [time.monotonic()]  # the deadline counts from here; bench.py sets it at process start
+
+
+def set_start(t0: float):
+    T0[0] = t0
+
+
+def log(*a):
+    print("[%7.1fs]" % (time.monotonic() - T0[0]), *a, file=sys.stderr, flush=True)
+
+
+def claim_stdout() -> int:
+    """Points fd 1 at stderr for the whole run and returns a private duplicate
+    of the real stdout.  RCCL (version banner) and gloo ("Rank i is connected
+    to ...") print on stdout from every rank; the driver contract wants exactly
+    one JSON line there, written by rank 0 through the returned fd."""
+    sys.stdout.flush()
+    real = os.dup(1)
+    os.dup2(2, 1)
+    return real
+
+
+def free_port() -> int:
+    """A free port below Linux's ephemeral range (32768-60999), so that no
+    outgoing connection takes it before the child process binds it."""
+    import random
+
+    rng = random.Random()
+    for _ in range(256):
+        port = rng.randrange(20000, 32000)
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", port))
+            return port
+        except OSError:
+            continue
+        finally:
+            s.close()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def first_comms(transport: str, comms: int) -> int:
+    """Communicators of the session bench.py opens first (the headline one)."""
+    return comms if transport == "rccl" and comms > 0 else 1
+
+
+def posting_candidates(transport: str, comms: int, batch: int, n: int = 1):
+    """(communicators, batch) pairs the tuning laps time against each other.
+
+    comms: > 0 fixed, -1 = RCCL picks: between 1 and 4 on one GPU (measured:
+    2, 3, 6 and 8 are slower there, profiles/r2_step_shape/), between 1, 2, 4
+    and 8 across GPUs, where no measurement has fixed the count for an xGMI
+    link yet (other transports: 1).  batch: 1 one group per step, 0 one group
+    per message, -1 = both (K = 1 only: with several communicators
+    per-message groups cannot overlap)."""
+    auto = [1, 4] if n == 1 else [1, 2, 4, 8]
+    comms_choices = ([comms] if comms > 0 else auto) if transport == "rccl" else [1]
+    batch_choices = [batch] if batch >= 0 else [0, 1]
+    return [(c, b) for c in comms_choices for b in batch_choices if c == 1 or b == 1 or len(batch_choices) == 1]
+
+
+def tuning_steps(phases: int, min_steps: int = 4) -> int:
+    """Steps per candidate: whole laps of the schedule (every cell once per
+    lap), at least min_steps so a one-round schedule is not timed on one step."""
+    return phases * max(1, math.ceil(min_steps / phases))
+
+
+def headline_stats(job_bytes: float, flows_total: int, steps: int, elapsed: float):
+    """(value, aggregate): the mean per-flow, per-direction rate and the sum
+    over all flows, both from the barrier-bracketed wall clock, in GB/s."""
+    aggregate = job_bytes / elapsed / 1e9
+    mean_flows = flows_total / steps
+    return aggregate / mean_flows, aggregate
+
+
+def cell_matrix(n: int, steps, flows_of, all_ms, bytes_per_flow: float):
+    """Per-cell GB/s medians and sample counts.  A flow's time in a step is
+    the LONGER of its two endpoints' step durations (the conservative choice,
+    the same as p2p_matrix's per-flow time, csrc/runner.cpp run_phase): the
+    endpoint that started first also waited for its partner."""
+    cells = {}
+    for i, k in enumerate(steps):
+        for (src, dst) in flows_of(k):
+            ms = max(all_ms[src][i], all_ms[dst][i])
+            if ms > 0:
+                cells.setdefault((src, dst), []).append(bytes_per_flow / (ms * 1e-3) / 1e9)
+    matrix = [[0.0] * n for _ in range(n)]
+    samples = [[0] * n for _ in range(n)]
+    for (s, d), v in cells.items():
+        matrix[s][d] = statistics.median(v)
+        samples[s][d] = len(v)
+    return matrix, samples, cells
+
+
+def pick_depth(steps: int, phases: int) -> int:
+    """Receive generations so that no timed step overwrites another's slots."""
+    return max(1, math.ceil(steps / phases))
+
+
+class Deadline:
+    """One deadline for the whole run, counted from process start."""
+
+    def __init__(self, seconds: float):
+        self.end = T0[0] + seconds
+
+    def left(self) -> float:
+        return self.end - time.monotonic()
+
+
+class Reporter:
+    """Holds the result and prints it exactly once (rank 0): at the normal end
+    of the run, or from the watchdog when the deadline passes first."""
+
+    def __init__(self, rank: int, real_stdout: int, json_out):
+        self.rank = rank
+        self.fd = real_stdout
+        self.json_out = json_out
+        self.lock = threading.Lock()
+        self.result = None  # set once the timed region is measured
+        self.done = False
+
+    def update(self, **kv):
+        with self.lock:
+            if self.result is not None:
+                self.result.update(kv)
+
+    def emit(self, **extra) -> bool:
+        with self.lock:
+            if self.done:
+                return False
+            self.done = True
+            if self.rank != 0:
+                return True
+            res = dict(self.result) if self.result is not None else {
+                "metric": METRIC, "value": None, "unit": "GB/s", "error": "the timed steps did not finish"}
+            res.update(extra)
+            line = json.dumps(res)
+            os.write(self.fd, (line + "\n").encode())
+            if self.json_out:
+                with open(self.json_out, "w") as f:
+                    f.write(line + "\n")
+            return True
+
+
+def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> threading.Event:
+    """At the deadline: print the JSON line with what is finished (the section
+    still running is named), abort every RCCL communicator so its kernels exit,
+    and end the process.  Exit 0 when the headline was measured."""
+    stop = threading.Event()
+
+    def run():
+        while not stop.wait(max(0.05, min(1.0, deadline.left()))):
+            if deadline.left() <= 0:
+                break
+        if stop.is_set():
+            return
+        log("bench: deadline reached during %s; printing what is done" % state.get("section"))
+        errors = dict(state.get("errors") or {})
+        if state.get("section"):
+            errors[state["section"]] = "deadline reached while running"
+        reporter.emit(deadline_hit=True, untimed_skipped=state.get("skipped") or None, section_errors=errors or None)
+        kill_children(state)
+        try:
+            nat.run_abort_hooks()
+        except Exception:  # noqa: BLE001 -- the process ends either way
+            pass
+        sys.stderr.flush()
+        os._exit(0 if reporter.result is not None else 4)
+
+    threading.Thread(target=run, name="bench-watchdog", daemon=True).start()
+    return stop
+
+
+# Untimed sections in the order bench.py runs them, with the seconds each one
+# keeps reserved: the BASELINE configs come first -- 3 the
+# N x N matrices by the reference's method and by ours, 4 all-pairs, 5 ring
+# and the ring hop, 2 the single-pair sweep -- and while one runs, the slices
+# of those after it stay free, so a slow section cannot crowd a later config
+# out.  The IPC comparisons and the xGMI pair sweep come after them and get
+# whatever is left.
+SECTION_SLICES = (("latency", 5.0), ("latency_preposted", 5.0), ("reference_semantics", 12.0),
+                  ("pair_serial_events", 12.0), ("allpairs_1g", 8.0), ("ring_256m", 5.0), ("ring_hop", 3.0),
+                  ("pair_sweep_0_1", 10.0))
+
+
+def reserved_after(name: str, active) -> float:
+    """Seconds the sections after `name` (those of SECTION_SLICES in
+    `active`) keep reserved while `name` runs; 0 for sections not planned."""
+    names = [s for s, _ in SECTION_SLICES]
+    if name not in names:
+        return 0.0
+    return sum(sec for (s, sec) in SECTION_SLICES[names.index(name) + 1:] if s in active)
+
+
+def pair_matrix_summary(run: dict, n: int) -> dict:
+    """A pair-mode run (report.cpp run JSON) valued like the reference's
+    printed cells: each phase (one ordered pair, or the self cell) moves the
+    bytes of all its flows per iteration (compat_gbps: a bi cell is both
+    directions summed, p2p_matrix.cc:258), here in GB/s (= Gbps / 8).  Row =
+    sender."""
+    m = [[0.0] * n for _ in range(n)]
+    cells = []
+    for ph in run["phases"]:
+        v = ph["compat_gbps"] / 8.0
+        r, c = (ph["row"], ph["col"]) if ph["row"] >= 0 else (0, 0)
+        m[r][c] = round(v, 3)
+        cells.append(v)
+    return {"gbs_min": round(min(cells), 3) if cells else None,
+            "gbs_mean": round(statistics.mean(cells), 3) if cells else None, "cells": len(cells),
+            "mismatches": sum(ph["mismatches"] for ph in run["phases"]), "matrix_gbs": m}
+
+
+def method_ratios(ours: dict, ref: dict, value: float, n: int) -> dict:
+    """method_ratio[dir]: our methodology over the reference's on the same
+    serial pair schedule (mean cells; warmup + hipEvents + pipelined
+    iterations vs host clock + a sync per message), per direction mode.
+    concurrency_ratio: the headline's tournament cell (per link and direction,
+    every disjoint pair at once) over our serial bi cell per direction (both
+    directions summed / 2) -- the schedule's gain alone; None at n == 1,
+    where there are no pairs."""
+    def mean(d, k):
+        return (d or {}).get(k, {}) and (d or {}).get(k, {}).get("gbs_mean")
+
+    out = {"method_ratio": {}, "concurrency_ratio": None}
+    for k in ("uni", "bi"):
+        a, b = mean(ours, k), mean(ref, k)
+        out["method_ratio"][k] = round(a / b, 3) if a and b else None
+    bi = mean(ours, "bi")
+    if n > 1 and bi and value:
+        out["concurrency_ratio"] = round(value / (bi / 2.0), 3)
+    return out
+
+
+def default_device(local_rank: int) -> int:
+    """LOCAL_RANK, modulo the visible GPUs: a launcher that gives each rank
+    one visible GPU (HIP_VISIBLE_DEVICES per process) leaves every rank on
+    its device 0.  torch.cuda.device_count() does not initialise the GPU."""
+    count = torch.cuda.device_count()
+    return local_rank % count if count > 0 else local_rank
+
+
+def hang_requested(section: str, rank: int) -> bool:
+    """Test hook: P2P_BENCH_HANG="<section>@<rank>" makes that rank stop
+    responding inside that untimed section."""
+    spec = os.environ.get("P2P_BENCH_HANG", "")
+    return bool(spec) and spec == "%s@%d" % (section, rank)
+
+

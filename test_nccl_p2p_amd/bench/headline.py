@@ -1,0 +1,362 @@
+"""The headline of bench.py: posting selection, the W warmup and K timed
+steps through RCCL (the verified warmup and its rechunking fallback, the link
+report), the JSON line's timed part, and the IPC fallback should RCCL fail."""
+
+from __future__ import annotations
+
+import json
+import os
+import statistics
+import time
+import types
+
+import torch
+import torch.distributed as dist
+
+from test_nccl_p2p_amd.bench.core import (BASELINE_VALUE, METRIC, cell_matrix, first_comms, headline_stats, log,
+                                          pick_depth, posting_candidates, tuning_steps)
+
+
+class HeadlineMixin:
+    """BenchRun's headline methods (collective, like every BenchRun method)."""
+
+    # ---- the headline -------------------------------------------------------
+    def measure(self, transport):
+        """Posting selection, then the W warmup and K timed steps of the headline
+        through `transport`; returns what the report needs."""
+        args, nat, n, mode, size = self.args, self.nat, self.n, self.mode, self.size
+        headline = transport + (":%d" % args.comms if transport == "rccl" and args.comms > 1 else "")
+        sess = self.create_session(headline, device=self.device, timeout_s=args.timeout)
+        self.log0("bench: %d rank(s), %s, %s" % (n, sess.transport, sess.device_desc))
+        # Test hook: P2P_BENCH_FAIL_HEADLINE=<transport> fails the headline
+        # through that transport on every rank, as a communicator that cannot
+        # be set up does.
+        if os.environ.get("P2P_BENCH_FAIL_HEADLINE") == transport:
+            raise RuntimeError("injected headline failure")
+        provenance = json.loads(sess.provenance(self.device if self.use_gpu else -1))
+        provenance.pop("type", None)
+
+        # Receive-slot budget: every message of every timed step gets its own
+        # slot, up to this much memory per rank (ranks sharing a GPU split it).
+        budget = 0 if args.recv_budget.strip() in ("", "0") else nat.parse_size(args.recv_budget)
+        if budget == 0 and self.use_gpu:
+            free_b, _ = torch.cuda.mem_get_info(self.device)
+            same_gpu = sum(1 for d in provenance.get("rank_devices", []) if d["device"] == self.device) or 1
+            budget = int(0.4 * free_b / same_gpu)
+        elif budget == 0:
+            budget = 256 << 20
+
+        # ---- posting selection: whole untimed laps of the schedule per
+        # candidate (one group per step vs one per message; RCCL: one
+        # communicator vs several whose send/recv kernels run side by side,
+        # posting_candidates), timed by the slowest rank, before the W warmup
+        # steps of the chosen one.
+        self.state["section"] = "tuning"
+        choices = posting_candidates(transport, args.comms, args.batch, n)
+        c0 = first_comms(transport, args.comms)
+        sessions = {c0: sess}
+
+        def session_for(c):
+            if c not in sessions:
+                # A candidate that stalls is aborted and dropped after --timeout.
+                sessions[c] = self.create_session("rccl:%d" % c if c > 1 else "rccl", device=self.device,
+                                                  timeout_s=args.timeout)
+            return sessions[c]
+
+        tuning, failed = {}, {}
+        phases = len(nat.schedule(mode, "bi", n))
+        tune_k = tuning_steps(phases) * args.tune_laps
+        if args.tune_laps > 0 and len(choices) > 1:
+            for i, (c, b) in enumerate(choices):
+                key = "comms%d_%s" % (c, "batch" if b else "per_message")
+                # The headline session's first candidate must work; anything else
+                # (another communicator count, another posting) may be dropped.
+                droppable = i > 0 or c != c0
+                d, err = None, None
+                try:
+                    d = nat.StepDriver(session_for(c), mode, "bi", size, args.msgs, False, bool(b), bool(args.graph))
+                    d.connect()
+                    # Test hook: P2P_BENCH_FAIL_CANDIDATE="<comms>,<batch>" fails
+                    # that candidate on the last rank only.
+                    if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d" % (c, b) and self.env.rank == n - 1:
+                        raise RuntimeError("injected candidate failure")
+                except Exception as e:  # noqa: BLE001 -- reported, and the candidate is skipped everywhere
+                    err = str(e)[:200]
+                if self.agree(err is None):
+                    self.barrier()
+                    w0 = time.perf_counter()
+                    try:
+                        d.run_steps(0, tune_k)
+                        d.sync()
+                        if (os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d,tuning" % (c, b)
+                                and self.env.rank == n - 1):
+                            raise RuntimeError("injected tuning failure")
+                    except Exception as e:  # noqa: BLE001 -- same agreement as above
+                        err = str(e)[:200]
+                    w = time.perf_counter() - w0
+                    if self.agree(err is None):
+                        tuning[(c, b)] = sess.allreduce_max(w) / tune_k
+                        del d
+                        # Only the best communicator count so far, the headline
+                        # session and the single communicator (kept for the
+                        # reference-method comparison) stay open.
+                        best_c = min(tuning, key=tuning.get)[0]
+                        for cc in [cc for cc in sessions if cc not in (c0, 1, best_c)]:
+                            if not any(cc == c2 for (c2, _) in choices[i + 1:]):
+                                del sessions[cc]
+                        continue
+                if not droppable:
+                    raise RuntimeError(err or "the first posting candidate failed on another rank")
+                failed[key] = err or "failed on another rank"
+                log("bench: posting candidate %s dropped: %s" % ((c, b), failed[key]))
+                del d
+                if c != c0 and not any(cc == c for (cc, _) in tuning):
+                    sessions.pop(c, None)
+            comms, batch = min(tuning, key=tuning.get)
+            reason = "fastest of %d candidate(s) over %d untimed step(s) each (%s lap(s) of %d round(s)), slowest " \
+                     "rank's clock" % (len(tuning), tune_k, args.tune_laps, phases)
+        else:
+            comms, batch = choices[0]
+            reason = "single candidate" if len(choices) == 1 else "no tuning laps (--tune-laps 0): first candidate"
+        sess = session_for(comms)
+        # A single-communicator session stays for the reference-method comparison
+        # (the reference uses one communicator); other candidates are closed.
+        ref_sess = sessions.get(1)
+        for c in list(sessions):
+            if c not in (comms, 1):
+                del sessions[c]
+
+        # ---- the headline driver: W warmup steps, poison, K timed steps -------
+        self.state["section"] = "headline"
+        drv = nat.StepDriver(sess, mode, "bi", size, args.msgs, not args.no_verify, bool(batch), bool(args.graph),
+                             depth=pick_depth(args.steps, phases), recv_budget=budget, salt=1)
+        drv.connect()
+        rccl_peers, matrix_transport = (self.link_report(sess) if transport == "rccl" else (None, None))
+        drv.run_steps(0, args.warmup)
+        drv.sync()
+        chunking = None
+        if transport == "rccl" and not args.no_verify and args.warmup > 0:
+            chunking = self.verify_warmup(drv, [x for x in (sess, ref_sess) if x is not None])
+        drv.poison()  # untimed: every receive slot zeroed; a slot passes verification only if a timed step wrote it
+        self.gpu_sync()
+        drv.reset()
+
+        self.barrier()
+        self.gpu_sync()
+        self.barrier()
+        t0 = time.perf_counter()
+        drv.run_steps(args.warmup, args.steps)
+        drv.sync()
+        self.gpu_sync()
+        self.barrier()
+        t1 = time.perf_counter()
+        elapsed = sess.allreduce_max(t1 - t0)
+
+        steps = list(range(args.warmup, args.warmup + args.steps))
+        job_bytes = sum(drv.job_bytes_per_step(k) for k in steps)
+        flows_total = sum(drv.flows_per_step(k) for k in steps)
+        value, aggregate = headline_stats(job_bytes, flows_total, args.steps, elapsed)
+
+        # Per-step GPU durations of every rank -> per-cell bandwidth.
+        my_ms = drv.step_ms()
+        all_ms = [None] * n
+        if n > 1:
+            dist.all_gather_object(all_ms, my_ms)
+        else:
+            all_ms = [my_ms]
+        matrix, samples, cells = cell_matrix(n, steps, drv.phase_flows, all_ms, size * args.msgs)
+        offdiag = [matrix[s][d] for (s, d) in cells if s != d or n == 1]
+
+        vr = drv.verify_steps(args.warmup, args.steps) if not args.no_verify else None
+        depth, recv_bytes = drv.depth, drv.recv_bytes
+        # Everything after this is untimed; release the timed driver's buffers
+        # first so the comparisons run on the same memory footprint as the
+        # timed steps did.
+        del drv
+        return types.SimpleNamespace(
+            sess=sess, ref_sess=ref_sess, sessions=sessions, provenance=provenance, comms=comms, batch=batch,
+            failed=failed, reason=reason, tuning=tuning, elapsed=elapsed, flows_total=flows_total, value=value,
+            aggregate=aggregate, my_ms=my_ms, matrix=matrix, samples=samples, cells=cells, offdiag=offdiag,
+            expected=n * (n - 1) if n > 1 else 1, vr=vr, mismatches=vr["mismatches"] if vr else -1, depth=depth,
+            recv_bytes=recv_bytes, chunking=chunking, rccl_peers=rccl_peers, matrix_transport=matrix_transport)
+
+    def verify_warmup(self, drv, sessions):
+        """RCCL 2.26 / 2.27 deliver only the first half of an op whose share
+        of one p2p channel exceeds 16 MiB, silently (scripts/rccl_half_repro.cpp);
+        the transport posts messages in ops of 16 MiB x the channels RCCL's
+        INFO log reports for each peer (transport_rccl.cpp derive_op_limits).
+        As a second line of defence the warmup's deliveries are verified
+        (collectively); should any word be wrong, every session caps its ops
+        at 16, 4, then 1 MiB, graphs are recorded again, every slot is zeroed
+        once every rank has drained, and the warmup runs again, until it
+        verifies.  P2P_RECHUNK=0 turns the fallback off (the timed check then
+        reports the loss).  Returns what was seen and done (posting.chunking)."""
+        args, sess = self.args, sessions[0]
+        peer = (self.env.rank + 1) % self.n
+        bad = drv.verify_steps(0, args.warmup)["mismatches"]
+        out = {"op_limit_bytes": sess.max_chunk(peer), "warmup_mismatches": bad, "fallback": None, "cap_bytes": None,
+               "recaptured_graphs": 0}
+        if bad and os.environ.get("P2P_RECHUNK") == "0":
+            out["fallback"] = "off (P2P_RECHUNK=0)"
+            return out
+        tried = []
+        for c in (16 << 20, 4 << 20, 1 << 20):
+            if bad == 0:
+                break
+            # Agreed on every rank: all post the same steps, so all take the same branch.
+            current = int(sess.allreduce_max(float(sess.max_chunk(peer) or self.size)))
+            if c >= current:
+                continue
+            self.log0("bench: %d wrong words in the warmup: messages now posted as ops of <= %d MiB" % (bad, c >> 20))
+            for s in sessions:
+                s.set_chunk_cap(c)
+            drv.recapture()
+            drv.clear()
+            drv.run_steps(0, args.warmup)
+            drv.sync()
+            bad = drv.verify_steps(0, args.warmup)["mismatches"]
+            tried.append({"cap_bytes": c, "warmup_mismatches": bad})
+            out["cap_bytes"] = c
+        if tried:
+            out.update(fallback=tried, op_limit_bytes=sess.max_chunk(peer), recaptured_graphs=drv.recaptures)
+        return out
+
+    def link_report(self, sess):
+        """What RCCL set up (transport_rccl.cpp link_report): per rank, the p2p
+        channels of each communicator and, per peer, the transport its INFO log
+        shows (P2P = xGMI through IPC, SHM, NET), the channels connected and the
+        op limit in use; plus matrix_transport, the N x N transport classes
+        (row = rank, col = peer).  Collective."""
+        try:
+            reports = json.loads(sess.link_reports())
+        except Exception as e:  # noqa: BLE001 -- recorded, never fatal
+            return {"error": str(e)[:200]}, None
+        if not any(reports):
+            return None, None
+        matrix = [[(r["peers"][p]["transport"] or "?") if r else "?" for p in range(self.n)] for r in reports]
+        return reports, matrix
+
+    def headline(self):
+        """Measures the headline; should RCCL itself fail on this node
+        (communicator setup, a peer connection, a stalled transfer: every wait
+        is bounded by --timeout and aborts the communicators), the same steps
+        run through the hand-written IPC data plane instead and the line says
+        so (headline_fallback).  With --fallback 0, or if that fails too, the
+        line carries the error and value null; returns that exit status."""
+        args = self.args
+        err = None
+        try:
+            self.h = self.measure(args.transport)
+        except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+            err = str(e)[:300]
+        # Outside the except block the failed attempt's frames are released, and
+        # with them its sessions (aborted communicators, their streams, buffers).
+        if err is None:
+            return None
+        log("bench: headline through %s failed: %s" % (args.transport, err))
+        # The failure is collective (a communicator that cannot be set up or a
+        # stalled transfer times out on every rank): all ranks meet here first.
+        self.agree(False)
+        to = args.fallback_to
+        if not (args.fallback and args.transport in ("rccl", "host") and to != args.transport
+                and (self.use_gpu or to in ("host", "shm"))):
+            self.reporter.emit(error="headline failed: " + err, transport=args.transport)
+            return 5
+        self.fallback = {"from": args.transport, "to": to, "error": err}
+        self.transport_used = to
+        self.state["section"] = "fallback"
+        err2 = None
+        try:
+            self.h = self.measure(to)
+        except Exception as e2:  # noqa: BLE001
+            err2 = str(e2)[:300]
+        if err2 is None:
+            return None
+        log("bench: fallback headline failed: %s" % err2)
+        self.reporter.emit(error="headline failed: %s; fallback through %s failed: %s" % (err, to, err2),
+                           transport=args.transport, headline_fallback=self.fallback)
+        return 5
+
+    def base_result(self) -> dict:
+        """The JSON line as far as the timed steps go; the untimed sections
+        fill in the rest (Reporter.update)."""
+        args, h, n, nat = self.args, self.h, self.n, self.nat
+        headline_transport = h.sess.transport
+        vr = h.vr
+        # A headline that ran on the fallback data plane is not the metric's
+        # (RCCL send/recv): value is null, the fallback's number stays beside it.
+        value = None if self.fallback else round(h.value, 3)
+        fallback = dict(self.fallback, value_gbs=round(h.value, 3)) if self.fallback else None
+        return {
+            "metric": METRIC,
+            "value": value,
+            "unit": "GB/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(h.elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE and value else None),
+            "dtype": "uint8",
+            "data": "synthetic (device PRNG-filled payloads, one stream per message; every timed delivery verified "
+                    "on the device after timing)",
+            "config": {
+                "model": "p2p_matrix: %s %s, %s x %d msgs/step"
+                         % ("RCCL ncclSend/ncclRecv" if headline_transport == "rccl"
+                            else headline_transport + " transport",
+                            "self send/recv (uni)" if self.mode == "self" else self.mode + " bidirectional",
+                            nat.format_size(self.size), args.msgs),
+                "global_batch": args.msgs * n,
+                "seq_len": self.size,
+                "parallelism": "p2p%d" % n,
+            },
+            "value_definition": "mean cell of the GB/s matrix: all flows' bytes / slowest rank's barrier-bracketed "
+                                "wall time / mean flows per step (per direction, 1 GB = 1e9 B)",
+            "aggregate_gbs": round(h.aggregate, 3),
+            "flows_per_step": round(h.flows_total / args.steps, 3),
+            "matrix_gbs_min": round(min(h.offdiag), 3) if h.offdiag else None,
+            "matrix_gbs_mean": round(statistics.mean(h.offdiag), 3) if h.offdiag else None,
+            "matrix_cells": "%d/%d" % (len(h.cells), h.expected),
+            # BASELINE config 3: the full N x N pairwise matrices (row = sender;
+            # GB/s per direction, median over steps, a cell's time = the longer
+            # of its endpoints'; p50 one-way latency, us).
+            "matrix_gbs": [[round(v, 2) for v in row] for row in h.matrix],
+            "matrix_samples": h.samples,
+            "latency_p50_us_matrix": [[0.0] * n for _ in range(n)],
+            "p50_latency_us": None,
+            "p50_latency_preposted_us": None,
+            "latency_preposted_p50_us_matrix": None,
+            "latency_bytes": nat.parse_size(args.latency_size),
+            "per_gpu_gbs": round(h.aggregate / n, 3),
+            "rank0_step_ms_p50": round(statistics.median(h.my_ms) if h.my_ms else 0.0, 4),
+            "verify_mismatches": h.mismatches,
+            "verify_coverage": (round(vr["verified_msgs"] / vr["timed_msgs"], 4) if vr and vr["timed_msgs"] else None),
+            "verify_detail": vr,
+            "recv_slot_generations": h.depth,
+            "recv_slot_bytes_per_rank": h.recv_bytes,
+            "transport": headline_transport,
+            "posting": {"batch": bool(h.batch), "graph": bool(args.graph), "rccl_comms": h.comms, "chunking": h.chunking,
+                        "dropped": h.failed or None, "selection": h.reason,
+                        "tuning_ms_per_step": {"comms%d_%s" % (c, "batch" if b else "per_message"): round(v * 1e3, 4)
+                                               for (c, b), v in h.tuning.items()} or None},
+            "provenance": dict(h.provenance, rccl_peers=h.rccl_peers),
+            "matrix_transport": h.matrix_transport,
+            "reference_semantics": None,
+            "pair_serial_events": None,
+            "method_ratio": None,
+            "concurrency_ratio": None,
+            "extras": None,
+            "ipc_transport": None,
+            "xgmi_pair_sweep": None,
+            "untimed_skipped": None,
+            "headline_fallback": fallback,
+            "note": ("n_gpus=1 has no inter-GPU link: value is RCCL's on-GPU self send/recv copy (HBM-bound), the "
+                     "diagonal the reference prints as 0.00. From n_gpus=2 every step is one tournament round of "
+                     "disjoint pairs, each pair on its own xGMI link; value is the mean per-link, per-direction cell "
+                     "rate and aggregate_gbs the whole fabric")
+                    if n == 1 else
+                    ("each step is one tournament round: %d disjoint pairs exchange in both directions, one xGMI link "
+                     "per pair; value = mean cell (per link and direction), aggregate_gbs = all pairs together"
+                     % (n // 2)),
+        }

@@ -1,0 +1,465 @@
+"""The untimed sections of bench.py, after the timed steps and under one
+deadline: latency, the reference's methodology, the other BASELINE configs
+(all-pairs, ring, ring hop, single-pair sweep), the IPC comparisons and the
+xGMI pair sweep."""
+
+from __future__ import annotations
+
+import json
+import os
+import shutil
+import statistics
+import subprocess
+import sys
+import tempfile
+import time
+
+import torch.distributed as dist
+
+from test_nccl_p2p_amd.bench.compare import steps_through
+from test_nccl_p2p_amd.bench.core import (RESERVE_S, SECTION_SLICES, free_port, hang_requested, log, method_ratios,
+                                          pair_matrix_summary, reserved_after)
+from test_nccl_p2p_amd.utils.proc import run_child
+
+HERE = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # the repository root
+
+
+class SectionsMixin:
+    """BenchRun's untimed sections (collective)."""
+
+    # ---- untimed sections: one deadline, waits shortened to the time left --
+    def budget_left(self) -> float:
+        return min(self.args.untimed_budget - (time.monotonic() - self.untimed_t0), self.deadline.left() - RESERVE_S)
+
+    def section(self, name, fn, min_s=2.0, budgeted=True, sessions=True):
+        """Runs one untimed section if every rank has time for it; an error is
+        logged and returned in its place ({"error": ...}).  budgeted=False:
+        only the deadline counts, not --untimed-budget (the headline's own
+        latency).  The slices of the BASELINE sections after this one
+        (SECTION_SLICES) stay reserved: self.slice_left is what this one may
+        plan with.  Every wait of the live sessions is bounded by all the time
+        left (not the slice: a wait that expires aborts the session); the
+        watchdog prints the line at the deadline whatever runs.  A section
+        that failed may leave the live sessions in disagreement across ranks,
+        so later sections that use them (sessions=True) are skipped."""
+        left = self.budget_left() if budgeted else self.deadline.left() - RESERVE_S
+        wait_left = left
+        # When the time left cannot hold every remaining slice, each keeps its
+        # proportional share (the first ones are not starved).
+        later = reserved_after(name, self.active_sections)
+        mine = dict(SECTION_SLICES).get(name, 0.0)
+        if 0 < left < later + mine:
+            later *= left / (later + mine)
+        left -= later
+        # One collective per section: a failure may be local to some ranks
+        # (a hung rank leaves the others here until the watchdog fires).
+        broken = sessions and self.broken
+        if not self.agree(left > min_s and not broken):
+            self.state["skipped"].append(name)
+            self.log0("bench: skipping %s: %s" % (name, "the sessions failed in %s" % self.broken if broken
+                                                  else "no time left (or another rank's sessions failed)"))
+            return None
+        self.slice_left = left
+        self.slice_t0 = time.monotonic()
+        for s in self.live:
+            s.set_timeout(max(1.0, min(self.args.timeout, wait_left)))
+        self.state["section"] = name
+        if hang_requested(name, self.env.rank):
+            log("bench: injected hang in %s on rank %d" % (name, self.env.rank))
+            while True:
+                time.sleep(1)
+        try:
+            return fn()
+        except Exception as e:  # noqa: BLE001 -- reported in the JSON
+            log("bench: %s failed: %s" % (name, e))
+            self.state["errors"][name] = str(e)[:300]
+            if sessions:
+                self.broken = name
+            return {"error": str(e)[:300]}
+        finally:
+            self.state["section"] = None
+
+    def agreed_min(self, v: float) -> float:
+        """The smallest of every rank's `v` (collective)."""
+        return -self.h.sess.allreduce_max(-float(v)) if self.n > 1 else float(v)
+
+    def slice_remaining(self) -> float:
+        """Seconds the running section has left of its slice."""
+        return self.slice_left - (time.monotonic() - self.slice_t0)
+
+    def plan_sections(self):
+        """The SECTION_SLICES sections this run will attempt (their slices are
+        reserved while the ones before them run)."""
+        args, n = self.args, self.n
+        active = {"latency"}
+        if args.latency_preposted > 0:
+            active.add("latency_preposted")
+        if args.ref_iters > 0:
+            active |= {"reference_semantics", "pair_serial_events"}
+        if n > 1 and args.extras:
+            active |= {"allpairs_1g", "ring_256m", "ring_hop"}
+        if n > 1 and args.sweep:
+            active.add("pair_sweep_0_1")
+        self.active_sections = active
+        self.slice_left, self.slice_t0 = 0.0, time.monotonic()
+        self.broken = None
+
+    def latency_sections(self):
+        """Host-posted ping-pong through the headline session, then the same
+        pre-posted: batches of exchanges wait behind a stream gate on every
+        rank and run back to back once all are posted, so those samples are
+        the operation's GPU-timeline latency without the host's posting rate."""
+        args, n, sess = self.args, self.n, self.h.sess
+        nbytes = self.nat.parse_size(args.latency_size)
+
+        def ping(preposted):
+            m = [[0.0] * n for _ in range(n)]
+            lat = json.loads(sess.latency(nbytes, args.latency_iters, min(50, args.latency_iters), preposted))
+            for p in lat["pairs"]:  # a < b; the ping-pong's one-way time holds for both directions
+                m[p["a"]][p["b"]] = m[p["b"]][p["a"]] = round(p["one_way_us"]["p50"], 3)
+            p50s = [p["one_way_us"]["p50"] for p in lat["pairs"]]
+            return {"p50": float(statistics.median(p50s)) if p50s else None, "matrix": m, "method": lat["method"]}
+
+        r = self.section("latency", lambda: ping(0), budgeted=False)
+        if isinstance(r, dict) and r.get("p50") is not None:
+            self.reporter.update(p50_latency_us=round(r["p50"], 3), latency_p50_us_matrix=r["matrix"])
+        if args.latency_preposted > 0:
+            r = self.section("latency_preposted", lambda: ping(args.latency_preposted), budgeted=False)
+            if isinstance(r, dict) and r.get("p50") is not None and r.get("method") == "preposted":
+                self.reporter.update(p50_latency_preposted_us=round(r["p50"], 3),
+                                     latency_preposted_p50_us_matrix=r["matrix"])
+
+    def reference_section(self):
+        """BASELINE config 3 by two methods on the reference's own schedule
+        (serial ordered pairs, one at a time, p2p_matrix.cc:141-267), both
+        directions modes (uni, and bi with both directions summed, :258):
+          * reference_semantics: the reference's methodology on one
+            communicator -- host clock, a stream sync per message, no warmup;
+          * pair_serial_events: ours on the same schedule -- warmup, hipEvent
+            timing, pipelined iterations, the headline's posting, every
+            delivery verified.
+        method_ratio (ours / the reference's, same schedule) and
+        concurrency_ratio (tournament headline / serial pairs, same method)
+        separate the two changes the headline makes.  With one GPU the
+        reference prints only the diagonal; both methods then run on the self
+        cell (uni only) so the method ratio still compares them.  The
+        iterations shrink, and say so, when a time model (the headline's
+        measured rate, then each direction mode's own) says the full count
+        would not fit the section's slice."""
+        args, n, h = self.args, self.n, self.h
+        if args.ref_iters <= 0:
+            return
+        dirs = ("uni", "bi") if n > 1 else ("uni",)
+        cells = n * (n - 1) if n > 1 else 1
+        # GB/s per cell; the reference's method ran ~3.5x below our cell rate
+        # on the self path, so its estimate assumes a quarter.
+        rate = max(h.value or 1.0, 1e-3) * 1e9
+
+        def matrices(session, timing, warmup, verify, slowdown):
+            # Iterations per direction mode from the time the slice leaves it:
+            # the first at the headline's rate (slowed by `slowdown`) plus a
+            # fixed 10 ms per cell (barriers, fill, verify), later ones at the
+            # previous mode's measured time per cell and iteration.  Agreed on
+            # every rank.
+            out, per_iter = {}, self.size * slowdown / rate + 50e-6
+            for d in dirs:
+                left = self.slice_remaining() / (len(dirs) - len(out))
+                fit = int((left / cells - 0.01) / per_iter) - warmup
+                iters = int(self.agreed_min(min(args.ref_iters, max(min(8, args.ref_iters), fit))))
+                t0 = time.monotonic()
+                r = json.loads(session.run(mode="pair" if n > 1 else "self", dir=d, bytes=self.size, iters=iters,
+                                           warmup=warmup, timing=timing, verify=verify, warm=warmup > 0))
+                # Everything the mode took, charged to its iterations (conservative).
+                per_iter = max(1e-6, self.agreed_min(time.monotonic() - t0) / cells / (warmup + iters))
+                out[d] = dict(pair_matrix_summary(r, n), iters=iters)
+                if iters != args.ref_iters:
+                    out[d]["iters_scaled_from"] = args.ref_iters
+            return out
+
+        def reference_semantics():
+            out = matrices(h.ref_sess or h.sess, "wallclock", 0, False, 4.0)
+            uni = out["uni"]["gbs_mean"]
+            return dict(out, size=self.size, comms=1,
+                        method="reference semantics: serial ordered pairs, wall clock, stream sync per message, no "
+                               "warmup" + ("" if n > 1 else " (applied to the self cell)"),
+                        # Kept from round 2: the headline cell over the
+                        # reference's uni cell (schedule and method together).
+                        value_ratio=round(h.value / uni, 3) if uni else None)
+
+        def pair_serial_events():
+            out = matrices(h.sess, "events", 8, not args.no_verify, 1.5)
+            return dict(out, size=self.size, comms=h.comms,
+                        method="ours on the reference's schedule: serial ordered pairs, 8 warmup iterations, hipEvent "
+                               "timing, iterations posted back to back, the headline's posting, every delivery verified")
+
+        self.log0("bench: reference-method matrices")
+        ref = self.section("reference_semantics", reference_semantics, 5.0)
+        self.reporter.update(reference_semantics=ref)
+        ours = self.section("pair_serial_events", pair_serial_events, 5.0)
+        ratios = method_ratios(ours if isinstance(ours, dict) else None, ref if isinstance(ref, dict) else None,
+                               h.value, n)
+        self.reporter.update(pair_serial_events=ours, **ratios)
+
+    def extras_sections(self):
+        """The other BASELINE.json configs, measured after the timed region so
+        one driver run records them too: all-pairs concurrent exchange at 1 GiB
+        (bisection: every GPU drives all N-1 xGMI links at once), the ring
+        neighbour exchange at 256 MiB, the pipeline-parallel hop latency as a
+        dependent token chain 0 -> 1 -> ... -> N-1 -> 0, and the single-pair
+        (0 -> 1) bandwidth sweep 4 KiB -> 4 GiB (config 2; only cell (0, 1) is
+        scheduled, the other ranks just join the barriers)."""
+        args, n, nat, h = self.args, self.n, self.nat, self.h
+        if n == 1:
+            return
+
+        def concurrent_config(mode_x, dir_x, nbytes, iters):
+            r = json.loads(h.sess.run(mode=mode_x, dir=dir_x, bytes=nbytes, iters=iters, warmup=1, timing="events",
+                                      verify=not args.no_verify, warm=True))
+            ph = r["phases"][0]
+            flows = [f["gbs"] for f in ph["flows"]]
+            p50s = [f["iter_us"]["p50"] for f in ph["flows"]]
+            return {"aggregate_gbs": round(ph["agg_gbs"], 2), "per_gpu_egress_gbs": round(ph["agg_gbs"] / n, 2),
+                    "flow_gbs_min": round(min(flows), 2), "flow_gbs_mean": round(statistics.mean(flows), 2),
+                    "iter_us_p50": round(statistics.median(p50s), 1), "bytes": nbytes, "iters": iters,
+                    "mismatches": ph["mismatches"]}
+
+        def ring_hop():
+            r = json.loads(h.sess.ring_latency(nat.parse_size(args.latency_size), 100, 10, False))
+            return {"hop_us_p50": round(r["hop_us"]["p50"], 3), "hop_us_p99": round(r["hop_us"]["p99"], 3),
+                    "lap_us_p50": round(r["lap_us"]["p50"], 3), "laps": r["laps"], "bytes": r["bytes"],
+                    "method": "dependent token chain 0 -> 1 -> ... -> N-1 -> 0, each hop forwards after its "
+                              "receive completed (grouped send/recv on the stream); hop = lap / N, rank 0's hipEvents"}
+
+        def pair_cell(session, nbytes, iters):
+            r = json.loads(session.run(mode="pair", dir="uni", bytes=nbytes, iters=iters, warmup=2, timing="events",
+                                       verify=not args.no_verify, warm=False, cells=[(0, 1)]))
+            fl = [f for ph in r["phases"] for f in ph["flows"]]
+            return fl[0] if fl else None
+
+        def pair_sweep():
+            # Sizes while the slice lasts (the same decision on every rank);
+            # a size's cost is estimated at the rate the previous one ran.
+            sweep, rate = [], max(h.value or 1.0, 1e-3)
+            for nbytes in [b for b in (4096 << (2 * k) for k in range(11)) if b <= nat.parse_size(args.sweep_max)]:
+                iters = max(4, min(200, (2 << 30) // nbytes))
+                est = (iters + 2) * (nbytes / (rate * 1e9) + 50e-6)
+                if not self.agree(self.slice_remaining() > est + 1.0):
+                    sweep.append({"bytes": nbytes, "skipped": "no time left in the section's slice"})
+                    break
+                self.log0("bench: pair sweep %d B" % nbytes)
+                f = pair_cell(h.sess, nbytes, iters)
+                if f:
+                    rate = max(f["gbs"], 1e-3)
+                    sweep.append({"bytes": nbytes, "iters": iters, "gbs": round(f["gbs"], 2),
+                                  "iter_us_p50": round(f["iter_us"]["p50"], 2), "mismatches": f.get("mismatches", -1)})
+            return sweep
+
+        def pair_one_comm():
+            # The same single pair on one communicator (what the sweep ran with
+            # K of them), at the bench's message size and 256 MiB.
+            return [{"bytes": nb, "gbs": round(f["gbs"], 2)}
+                    for nb in (self.size, 256 << 20) for f in [pair_cell(h.ref_sess, nb, 16)] if f]
+
+        extras = None
+        if args.extras:
+            self.log0("bench: all-pairs / ring extras")
+            extras = {}
+            # Keyed by the BASELINE config names; the sizes can be lowered for
+            # CPU rehearsals (all-pairs holds N - 1 receive slots per rank).
+            for name, mode_x, dir_x, nbytes, iters in (
+                    ("allpairs_1g", "allpairs", "bi", nat.parse_size(args.allpairs_size), 4),
+                    ("ring_256m", "ring", "uni", nat.parse_size(args.ring_size), 8)):
+                v = self.section(name, lambda: concurrent_config(mode_x, dir_x, nbytes, iters), 5.0)
+                if v is not None:
+                    extras[name] = v
+            v = self.section("ring_hop", ring_hop)
+            if v is not None:
+                extras["ring_hop"] = v
+            self.reporter.update(extras=extras)
+        if args.sweep:
+            sw = self.section("pair_sweep_0_1", pair_sweep, 10.0)
+            if sw is not None:
+                extras = dict(extras or {}, pair_sweep_0_1=sw, pair_sweep_rccl_comms=h.comms)
+                if h.ref_sess is not None and h.ref_sess is not h.sess:
+                    oc = self.section("pair_0_1_one_comm", pair_one_comm)
+                    if oc is not None:
+                        extras["pair_0_1_one_comm"] = oc
+            self.reporter.update(extras=extras)
+
+    def isolated(self, transport):
+        """steps_through() for `transport` in a child process per rank.  The
+        comparisons drive the hand-written data plane (hipIpc mappings, signal
+        kernels, relays) across GPUs; if one of them faults or hangs on some
+        node, only the child dies, and the headline line still gets printed
+        with the error in its place."""
+        args, n, rank = self.args, self.n, self.env.rank
+        box = [free_port() if rank == 0 else None]
+        if n > 1:
+            dist.broadcast_object_list(box, src=0)
+        out_path = os.path.join(tempfile.gettempdir(), "p2p_bench_child_%d_%d.json" % (box[0], rank))
+        limit = min(args.child_timeout, max(5.0, self.budget_left()))
+        cmd = [sys.executable, os.path.join(HERE, "bench.py"), "--gpus", str(n), "--steps", str(args.steps),
+               "--warmup", str(args.warmup), "--size", args.size, "--msgs", str(args.msgs), "--mode", self.mode,
+               "--latency-iters", str(args.latency_iters), "--latency-size", args.latency_size,
+               "--child", transport, "--child-port", str(box[0]), "--child-out", out_path,
+               "--child-batch", str(int(self.h.batch)), "--timeout", str(max(5.0, min(args.timeout, limit)))]
+        if args.no_verify:
+            cmd.append("--no-verify")
+        if args.device is not None:
+            cmd += ["--device", str(args.device)]
+        rc = run_child(self.state, cmd, limit)
+        self.barrier()
+        res = None
+        if rank == 0:
+            try:
+                with open(out_path) as f:
+                    res = json.load(f)
+            except (OSError, ValueError):
+                res = {"error": "comparison process failed (exit status %s)" % rc, "transport": transport}
+        try:
+            os.unlink(out_path)
+        except OSError:
+            pass
+        return res
+
+    def comparisons(self):
+        """The same tournament steps through the hand-written data plane on
+        the same links, untimed by the contract: the gfx950 multi-copy kernel
+        pulling from hipIpc-mapped peer buffers ("pull", one-sided), the
+        rendezvous engine that writes into the receiver's slot ("push"), the
+        SDMA copy engines pulling instead of CUs ("sdma"), and multi-path push
+        with two-hop relays through GPUs whose links are idle ("relay").  With
+        one GPU the same engines run the self step (the GPU copies to itself
+        through its own mapping), next to RCCL's self copy.  (With --transport
+        host the same code path runs on the CPU transport, for tests.)"""
+        args, n = self.args, self.n
+        extra_transport = {"rccl": "ipc", "ipc": "ipc", "ipc:push": "ipc", "ipc:relay": "ipc", "host": "host",
+                           "shm": "host"}.get(self.transport_used)
+        if not (args.ipc_extra and extra_transport):
+            return
+        runs = [(extra_transport, None)]
+        if extra_transport == "ipc":
+            runs += [("ipc:push", "push"), ("ipc:sdma", "sdma")] + ([("ipc:relay", "relay")] if n > 2 else [])
+            wanted = [e.strip() for e in args.ipc_engines.split(",") if e.strip()]
+            runs = [(t, k) for (t, k) in runs if (k or "pull") in wanted]
+        engines = {"ipc": "gfx950 multi-copy kernel, one-sided pull over hipIpc mappings",
+                   "ipc:push": "ready/done flags + gfx950 multi-copy kernel writing into the peer's slot",
+                   "ipc:sdma": "one-sided pull by the SDMA copy engines (hipMemcpyAsync per receive)",
+                   "ipc:relay": "push over the direct link + two-hop stripes relayed through GPUs whose links are "
+                                "idle (routing.hpp)"}
+        value, batch = self.h.value, self.h.batch
+
+        def compare(transport):
+            if args.isolate:
+                return self.isolated(transport)
+            isess = self.create_session(transport, device=self.device,
+                                        timeout_s=min(90.0, max(5.0, self.budget_left())))
+            try:
+                return steps_through(self.nat, isess, args, self.mode, self.size, batch, transport)
+            finally:
+                del isess
+
+        ipc = None
+        for transport, key in runs:
+            self.log0("bench: %s comparison" % transport)
+            r = self.section(transport, lambda: compare(transport), 20.0, sessions=False)
+            if r is None or self.env.rank != 0:
+                continue
+            if transport in engines:
+                r["engine"] = engines[transport]
+            if isinstance(r.get("value_gbs"), (int, float)) and value > 0:
+                r["ratio_to_headline"] = round(r["value_gbs"] / value, 3)
+            if key is None:
+                ipc = dict(r, **(ipc or {}))
+            else:
+                ipc = dict(ipc or {}, **{key: r})
+            self.reporter.update(ipc_transport=ipc)
+
+    def xgmi_sweep_section(self):
+        """The xGMI pair-cell tuning sweep in whatever time
+        the deadline leaves: RCCL at 1, 2, 4 and 8 communicators, the IPC
+        engines, then RCCL's channel / chunk / protocol / batch / read knobs,
+        on cell 0 -> 1 (uni) and 0 <-> 1 (bi), every row verified; rows that do
+        not fit are listed as skipped.  Rank 0 runs it as a child job while the
+        other ranks wait at a barrier (their sessions are closed by then)."""
+        args, n = self.args, self.n
+        pcis = [d.get("pci") for d in (self.h.provenance or {}).get("rank_devices", [])]
+        distinct = len(pcis) == n and all(pcis) and len(set(pcis)) == n
+        on = args.xgmi_sweep if args.xgmi_sweep >= 0 else int(n == 2 and distinct and self.use_gpu)
+        if n < 2 or not on:
+            return
+        if not self.use_gpu:
+            emulate = "host"
+        elif distinct:
+            emulate = ""
+        else:
+            emulate = "rccl" if os.environ.get("P2P_RCCL_DISTINCT_HOSTS") == "1" else "ipc"
+
+        def sweep():
+            res = None
+            if self.env.rank == 0:
+                try:
+                    res = self.run_pair_sweep(emulate)
+                except Exception as e:  # noqa: BLE001 -- the other ranks wait at the barrier below
+                    res = {"error": str(e)[:300]}
+            self.barrier()
+            return res
+
+        r = self.section("xgmi_pair_sweep", sweep, 30.0, sessions=False)
+        if r is not None and self.env.rank == 0:
+            self.reporter.update(xgmi_pair_sweep=r)
+
+    def run_pair_sweep(self, emulate):
+        """scripts/xgmi_pair_sweep.py within the time left; returns its rows
+        (cell GB/s and p50 per direction and size; bi = both directions
+        summed, like the reference's bi matrix) and the winner per cell."""
+        args, n = self.args, self.n
+        budget = self.budget_left() - 15.0
+        out = tempfile.mkdtemp(prefix="p2p_xgmi_sweep_")
+        cmd = [sys.executable, os.path.join(HERE, "scripts", "xgmi_pair_sweep.py"), "--np", str(n), "--out", out,
+               "--sizes", args.xgmi_sweep_sizes, "--rows", "rccl,ipc,knobs", "--budget", "%.0f" % budget,
+               "--row-timeout", "%.0f" % min(float(os.environ.get("P2P_XGMI_SWEEP_ROW_TIMEOUT", 90)), budget)]
+        if emulate:
+            cmd += ["--emulate", emulate]
+        log("bench: xGMI pair sweep (%.0f s%s)" % (budget, ", emulated: " + emulate if emulate else ""))
+        t0 = time.monotonic()
+        try:
+            with open(os.path.join(out, "sweep.log"), "w") as lf:
+                rc = run_child(self.state, cmd, budget + 15.0, stdout=lf, stderr=subprocess.STDOUT)
+            res = {"rc": rc, "seconds": round(time.monotonic() - t0, 1), "budget_s": round(budget, 1),
+                   "emulated": emulate or None, "sizes": args.xgmi_sweep_sizes, "cell": "0 -> 1 (uni), 0 <-> 1 (bi)",
+                   "rows": {}}
+            rows_path = os.path.join(out, "rows.jsonl")
+            if os.path.exists(rows_path):
+                with open(rows_path) as f:
+                    for line in f:
+                        r = json.loads(line)
+                        res["rows"][r["name"]] = dict(
+                            {"rc": r["rc"], "seconds": r.get("seconds")},
+                            **{k: {"cell_gbs": round(c["cell_gbs"], 2), "p50_us": round(c["p50_us"], 2)}
+                               for k, c in (r.get("cells") or {}).items()})
+            # The best RCCL row per cell too: the setting the headline itself
+            # could use on this link (the IPC engines are a different data plane).
+            base = res["rows"].get("rccl-comms1", {})
+            best_rccl = {}
+            for name, row in res["rows"].items():
+                for cell, c in row.items():
+                    if name.startswith("rccl-") and row["rc"] == 0 and isinstance(c, dict) and (
+                            cell not in best_rccl or c["cell_gbs"] > best_rccl[cell]["cell_gbs"]):
+                        b0 = (base.get(cell) or {}).get("cell_gbs")
+                        best_rccl[cell] = {"row": name, "cell_gbs": c["cell_gbs"],
+                                           "gain": round(c["cell_gbs"] / b0, 4) if b0 else None}
+            res["best_rccl"] = best_rccl or None
+            try:
+                with open(os.path.join(out, "summary.json")) as f:
+                    summary = json.load(f)
+                res["best"] = {k: {"row": b["row"], "cell_gbs": round(b["cell_gbs"], 2), "gain": b.get("gain")}
+                               for k, b in summary["best"].items()}
+                res.update(skipped=summary["rows_skipped"] or None, corrupt=summary["corrupt_rows"] or None,
+                           failed_row=summary["failed_row"])
+            except (OSError, ValueError, KeyError):
+                with open(os.path.join(out, "sweep.log")) as f:
+                    res["error"] = f.read()[-600:] or "the sweep wrote no summary"
+            return res
+        finally:
+            shutil.rmtree(out, ignore_errors=True)

@@ -100,6 +100,22 @@ def _ring_hop(r: dict) -> str:
     return _get(r, "extras", "ring_hop_8b", "iter_us_p50", fmt="%.2f")
 
 
+def _reference_cells(r: dict) -> str:
+    """The reference methodology's mean cell: uni / bi (round 3 on), or the
+    single uni number of round-2 lines."""
+    ref = r.get("reference_semantics") or {}
+    if "uni" in ref:
+        return "%s / %s" % (_get(ref, "uni", "gbs_mean"), _get(ref, "bi", "gbs_mean"))
+    return _get(r, "reference_semantics", "cell_gbs_mean")
+
+
+def _ratios(r: dict) -> str:
+    m = r.get("method_ratio") or {}
+    if not m and r.get("concurrency_ratio") is None:
+        return "-"
+    return "%s / %s / %s" % (m.get("uni", "-") or "-", m.get("bi", "-") or "-", _get(r, "concurrency_ratio"))
+
+
 def scaling_table(results: Iterable[dict]) -> str:
     """Markdown table of bench.py lines (one per GPU count): `value` (the
     mean cell of the matrix, GB/s per direction), aggregate and per-GPU GB/s,
@@ -112,10 +128,11 @@ def scaling_table(results: Iterable[dict]) -> str:
     rows = sorted((r for r in results if r.get("value") is not None), key=lambda r: r["n_gpus"])
     base = next((r for r in rows if r["n_gpus"] == 2), None)
     out = ["| GPUs | value: mean cell GB/s | aggregate GB/s | per-GPU GB/s | cell rate vs 2 GPUs | RCCL comms "
-           "| matrix min / mean GB/s | p50 latency us | reference-method cell GB/s | all-pairs 1 GiB aggregate GB/s "
+           "| matrix min / mean GB/s | p50 latency us | reference-method cell GB/s (uni / bi) "
+           "| method ratio (uni / bi) / concurrency ratio | all-pairs 1 GiB aggregate GB/s "
            "| ring hop 8 B us | IPC pull / push / SDMA / relay GB/s | relay pair 0->1 GB/s | device ping-pong us "
            "| headline fallback |",
-           "|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
+           "|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
     for r in rows:
         eff = ""
         if base and r["n_gpus"] >= 2 and base["value"]:
@@ -124,10 +141,11 @@ def scaling_table(results: Iterable[dict]) -> str:
         relay_pair = (relay.get("pair_0_1") or [{}])[0]
         agg = _aggregate(r)
         fb = r.get("headline_fallback")
-        out.append("| %d | %.1f | %.1f | %.1f | %s | %s | %s / %s | %s | %s | %s | %s | %s / %s / %s / %s | %s | %s | %s |" % (
+        out.append("| %d | %.1f | %.1f | %.1f | %s | %s | %s / %s | %s | %s | %s | %s | %s | %s / %s / %s / %s | %s | %s "
+                   "| %s |" % (
             r["n_gpus"], r["value"], agg, agg / r["n_gpus"], eff, _get(r, "posting", "rccl_comms", fmt="%d"),
             _get(r, "matrix_gbs_min", fmt="%.2f"), _get(r, "matrix_gbs_mean", fmt="%.2f"),
-            _get(r, "p50_latency_us", fmt="%.2f"), _get(r, "reference_semantics", "cell_gbs_mean"),
+            _get(r, "p50_latency_us", fmt="%.2f"), _reference_cells(r), _ratios(r),
             _get(r, "extras", "allpairs_1g", "aggregate_gbs"), _ring_hop(r),
             _get(r, "ipc_transport", "value_gbs"),
             _get(r, "ipc_transport", "push", "value_gbs"), _get(r, "ipc_transport", "sdma", "value_gbs"),

@@ -2,6 +2,7 @@ import os
 import shutil
 import subprocess
 import sys
+import time
 
 import pytest
 
@@ -12,9 +13,26 @@ if ROOT not in sys.path:
 MPIRUN = os.environ.get("P2P_MPIRUN", "/opt/conda/bin/mpirun")
 
 
+# The multi-GPU tier (tests/test_multi_gpu.py) shares the driver's 900 s
+# `pytest -m gpu` step with the single-GPU tests (~260 s): once it has used
+# this much, its remaining tests are skipped with a reason.
+MULTI_GPU_TIER_S = 550.0
+_MULTI_GPU_T0 = []
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an AMD MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "mpi: needs the MPICH mpirun launcher")
+    config.addinivalue_line("markers", "multigpu: needs >= 2 GPUs; shares the MULTI_GPU_TIER_S budget")
+
+
+def pytest_runtest_setup(item):
+    if item.get_closest_marker("multigpu") is None:
+        return
+    if not _MULTI_GPU_T0:
+        _MULTI_GPU_T0.append(time.monotonic())
+    elif time.monotonic() - _MULTI_GPU_T0[0] > MULTI_GPU_TIER_S:
+        pytest.skip("the multi-GPU tier used its %.0f s of the driver's GPU-test step" % MULTI_GPU_TIER_S)
 
 
 def ensure_built(target: str) -> None:

@@ -6,6 +6,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <fstream>
+#include <sstream>
 #include <functional>
 #include <map>
 #include <set>
@@ -17,6 +19,7 @@
 #include "bootstrap.hpp"
 #include "common.hpp"
 #include "prng.hpp"
+#include "rccl_log.hpp"
 #include "report.hpp"
 #include "routing.hpp"
 #include "runner.hpp"
@@ -756,6 +759,72 @@ TEST(test_remote_slots_repeated_peer) {
       std::sort(sorted.begin(), sorted.end());
       EXPECT(std::unique(sorted.begin(), sorted.end()) == sorted.end());
     }
+}
+
+// RCCL INFO-log parsing (csrc/rccl_log.cpp).  The two files are RCCL
+// 2.26.6's own logs of a 1-rank communicator on MI355X, default channels and
+// NCCL_MAX_P2P_NCHANNELS=1 (WARN lines dropped); the 4-rank connection lines
+// follow NCCL's p2p / net / shm formats.
+static std::string read_file(const std::string& path) {
+  std::ifstream in(path);
+  std::stringstream ss;
+  ss << in.rdbuf();
+  return ss.str();
+}
+
+TEST(test_rccl_log_init_block) {
+  const std::string dir = P2P_TEST_DATA;
+  RcclInitInfo a = parse_rccl_init(read_file(dir + "/rccl_info_self_nch64.txt"));
+  EXPECT(a.found() && a.p2p_channels == 64 && a.p2p_per_peer == 128 && a.nranks == 1 && a.nnodes == 1);
+  EXPECT(rccl_op_channels(a, false, 2) == 64);  // 64 x 16 MiB = the 1 GiB limit seen on the self path
+  RcclInitInfo b = parse_rccl_init(read_file(dir + "/rccl_info_self_nch1.txt"));
+  EXPECT(b.found() && b.p2p_channels == 1 && b.p2p_per_peer == 2);
+  EXPECT(rccl_op_channels(b, false, 2) == 1);  // the 16 MiB limit of the repro
+  EXPECT(parse_rccl_connections(read_file(dir + "/rccl_info_self_nch64.txt")).empty());
+  EXPECT(!parse_rccl_init("no such lines\n").found());
+  EXPECT(rccl_op_channels(RcclInitInfo(), false, 2) == 0);
+  RcclInitInfo c;
+  c.p2p_channels = 64;
+  c.p2p_per_peer = 8;
+  EXPECT(rccl_op_channels(c, false, 2) == 8 && rccl_op_channels(c, true, 2) == 2 && rccl_op_channels(c, true, 0) == 8);
+}
+
+TEST(test_rccl_log_connections) {
+  const std::string log =
+      "host:1:2 [0] NCCL INFO Channel 00/0 : 1[1] -> 2[2] via P2P/IPC/read\n"
+      "host:1:2 [0] NCCL INFO Channel 01/0 : 1[1] -> 2[2] via P2P/IPC/read\n"
+      "host:1:2 [0] NCCL INFO Channel 00/0 : 2[2] -> 1[1] via P2P/IPC/read\n"
+      "host:1:2 [0] NCCL INFO Channel 00/0 : 1[0] -> 3[0] [send] via NET/Socket/0\n"
+      "host:1:2 [0] NCCL INFO Channel 00/0 : 0[0] -> 1[0] [receive] via NET/Socket/0\n"
+      "host:1:2 [0] NCCL INFO Channel 02/0 : 0[0] -> 1[0] [receive] via NET/Socket/0\n"
+      "host:1:2 [0] NCCL INFO Channel 05 : 1[1] -> 4[4] via SHM/direct/direct\n"
+      "host:1:2 [0] NCCL INFO Channel 00/128 : 0\n"
+      "garbage Channel x : via\n";
+  auto conns = parse_rccl_connections(log);
+  EXPECT(conns.size() == 7);
+  EXPECT(conns[0].channel == 0 && conns[0].src == 1 && conns[0].dst == 2 && conns[0].via == "P2P/IPC/read");
+  EXPECT(conns[3].via == "NET/Socket/0" && conns[6].channel == 5 && conns[6].via == "SHM/direct/direct");
+  auto links = rccl_peer_links(conns, 1, 5);
+  EXPECT(links.size() == 5);
+  // peer 0: receive-side lines only (channels 0 and 2)
+  EXPECT(links[0].transport == "NET" && links[0].channels_connected == 2);
+  EXPECT(links[4].transport == "SHM" && links[4].channels_connected == 1);
+  EXPECT(links[1].transport == "self");
+  EXPECT(links[2].transport == "P2P" && links[2].channels_connected == 2 && links[2].via == "P2P/IPC/read");
+  EXPECT(links[3].transport == "NET" && links[3].channels_connected == 1);
+  auto none = rccl_peer_links({}, 0, 2);
+  EXPECT(none[1].transport.empty() && none[1].channels_connected == 0);
+}
+
+TEST(test_link_transport_mismatch) {
+  EXPECT(link_transport_mismatch("XGMI/1", "SHM"));
+  EXPECT(link_transport_mismatch("XGMI/1", "NET"));
+  EXPECT(!link_transport_mismatch("XGMI/1", "P2P"));
+  EXPECT(!link_transport_mismatch("XGMI/1", ""));  // not connected / no log: nothing to judge
+  EXPECT(!link_transport_mismatch("XGMI/2", "SHM"));  // no direct link
+  EXPECT(!link_transport_mismatch("PCIE/2", "SHM"));
+  EXPECT(!link_transport_mismatch("same-gpu", "NET"));
+  EXPECT(!link_transport_mismatch("n/a", "NET"));
 }
 
 int main(int argc, char** argv) {

@@ -76,3 +76,45 @@ def test_default_device_wraps_to_the_visible_gpus(monkeypatch):
     assert [bench.default_device(r) for r in (0, 3, 7)] == [0, 0, 0]
     monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 0)  # CPU transports
     assert bench.default_device(5) == 5
+
+
+def test_pair_matrix_summary_bi_is_both_directions():
+    """A pair-mode run valued like the reference's printed cells: the bi
+    phase's compat_gbps counts both directions' bytes (p2p_matrix.cc:258's
+    x2), and GB/s = Gbps / 8; self runs land on the diagonal."""
+    from test_nccl_p2p_amd.bench.core import pair_matrix_summary
+    run = {"phases": [{"row": 0, "col": 1, "compat_gbps": 800.0, "mismatches": 0},
+                      {"row": 1, "col": 0, "compat_gbps": 400.0, "mismatches": 2}]}
+    s = pair_matrix_summary(run, 2)
+    assert s["matrix_gbs"] == [[0.0, 100.0], [50.0, 0.0]]
+    assert s["gbs_min"] == 50.0 and s["gbs_mean"] == 75.0 and s["cells"] == 2 and s["mismatches"] == 2
+    # One bi exchange of 1 GB each way in 1 s: flows 2 x 1e9 B -> 16 Gbps -> 2 GB/s, twice one direction.
+    bi = {"phases": [{"row": 0, "col": 1, "compat_gbps": 2 * 1e9 * 8 / 1e9, "mismatches": 0}]}
+    assert pair_matrix_summary(bi, 2)["gbs_mean"] == 2.0
+    self_run = {"phases": [{"row": -1, "col": -1, "compat_gbps": 80.0, "mismatches": 0}]}
+    assert pair_matrix_summary(self_run, 1)["matrix_gbs"] == [[10.0]]
+
+
+def test_method_and_concurrency_ratios():
+    from test_nccl_p2p_amd.bench.core import method_ratios
+    ours = {"uni": {"gbs_mean": 60.0}, "bi": {"gbs_mean": 100.0}}
+    ref = {"uni": {"gbs_mean": 20.0}, "bi": {"gbs_mean": 50.0}}
+    r = method_ratios(ours, ref, 65.0, 8)
+    # same schedule, two methods; then the tournament cell vs the serial bi cell per direction (100 / 2)
+    assert r == {"method_ratio": {"uni": 3.0, "bi": 2.0}, "concurrency_ratio": 1.3}
+    assert method_ratios(ours, None, 65.0, 8)["method_ratio"] == {"uni": None, "bi": None}
+    one = method_ratios({"uni": {"gbs_mean": 2400.0}}, {"uni": {"gbs_mean": 700.0}}, 2300.0, 1)
+    assert one["method_ratio"]["uni"] == 3.429 and one["method_ratio"]["bi"] is None and one["concurrency_ratio"] is None
+
+
+def test_section_slices():
+    """While a BASELINE section runs, the slices of the planned ones after it
+    stay reserved (the BASELINE configs run first)."""
+    from test_nccl_p2p_amd.bench.core import SECTION_SLICES, reserved_after
+    names = [n for n, _ in SECTION_SLICES]
+    assert names.index("reference_semantics") < names.index("allpairs_1g") < names.index("pair_sweep_0_1")
+    active = set(names)
+    assert reserved_after("pair_sweep_0_1", active) == 0.0
+    assert reserved_after("allpairs_1g", active) == sum(s for n, s in SECTION_SLICES[names.index("allpairs_1g") + 1:])
+    assert reserved_after("latency", {"latency", "ring_hop"}) == dict(SECTION_SLICES)["ring_hop"]
+    assert reserved_after("ipc", active) == 0.0

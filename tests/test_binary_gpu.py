@@ -141,26 +141,38 @@ def test_bench_drops_a_failing_communicator_candidate():
 
 
 def test_bench_chunks_around_rccl_half_delivery():
-    """RCCL 2.26 delivers exactly half of a send/recv whose share of one p2p
-    channel exceeds 16 MiB.  With one p2p channel (NCCL_MAX_P2P_NCHANNELS=1)
-    the transport posts the bench's 32 MiB messages as 16 MiB ops by itself;
-    with that turned off (P2P_RCCL_MAX_CHUNK=0) the bench's verified warmup
-    sees the loss, reposts as 16 MiB ops, and the timed steps verify."""
+    """RCCL delivers only the first half of a send/recv whose share of one p2p
+    channel exceeds 16 MiB (scripts/rccl_half_repro.cpp).  With one p2p
+    channel (NCCL_MAX_P2P_NCHANNELS=1) the transport reads "1 p2p channels"
+    from RCCL's INFO log and posts the bench's 32 MiB messages as 16 MiB ops
+    by itself (provenance.rccl_peers says so); with its splitting turned off
+    (P2P_RCCL_MAX_CHUNK=0) the bench's verified warmup sees the loss, caps the
+    ops at 16 MiB, and the timed steps verify; with the fallback off too
+    (P2P_RECHUNK=0) the loss reaches the timed check: exit 3."""
     base = [sys.executable, "bench.py", "--steps", "4", "--warmup", "2", "--comms", "1", "--ipc-extra", "0",
             "--ref-iters", "0", "--latency-iters", "20"]
     runs = {}
-    for name, extra in (("transport", {}), ("fallback", {"P2P_RCCL_MAX_CHUNK": "0"})):
+    for name, extra, rc in (("transport", {}, 0), ("fallback", {"P2P_RCCL_MAX_CHUNK": "0"}, 0),
+                            ("off", {"P2P_RCCL_MAX_CHUNK": "0", "P2P_RECHUNK": "0"}, 3)):
         out = subprocess.run(base, capture_output=True, text=True, timeout=600, cwd=ROOT,
                              env=dict(os.environ, NCCL_MAX_P2P_NCHANNELS="1", **extra))
-        assert out.returncode == 0, out.stderr[-3000:]
+        assert out.returncode == rc, (name, out.stderr[-3000:])
         runs[name] = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    for name in ("transport", "fallback"):
         assert runs[name]["verify_mismatches"] == 0 and runs[name]["verify_coverage"] == 1.0, runs[name]
     ch = runs["transport"]["posting"]["chunking"]
-    assert ch == {"max_chunk_bytes": 16 << 20, "warmup_mismatches": 0, "fallback": None}, ch
+    assert ch == {"op_limit_bytes": 16 << 20, "warmup_mismatches": 0, "fallback": None, "cap_bytes": None,
+                  "recaptured_graphs": 0}, ch
+    peers = runs["transport"]["provenance"]["rccl_peers"][0]
+    assert peers["comms"][0]["p2p_channels"] == 1 and peers["op_limit_source"].startswith("rccl INFO log"), peers
+    assert peers["peers"][0]["op_channels"] == 1 and peers["peers"][0]["op_limit"] == 16 << 20, peers
+    assert runs["transport"]["matrix_transport"] == [["self"]]
     ch = runs["fallback"]["posting"]["chunking"]
     assert ch["warmup_mismatches"] > 0, ch
-    assert ch["fallback"] == [{"max_chunk_bytes": 16 << 20, "warmup_mismatches": 0}], ch
-    assert ch["max_chunk_bytes"] == 16 << 20
+    assert ch["fallback"] == [{"cap_bytes": 16 << 20, "warmup_mismatches": 0}], ch
+    assert ch["op_limit_bytes"] == 16 << 20 and ch["cap_bytes"] == 16 << 20
+    ch = runs["off"]["posting"]["chunking"]
+    assert ch["fallback"] == "off (P2P_RECHUNK=0)" and runs["off"]["verify_mismatches"] > 0, ch
 
 
 def test_bench_headline_falls_back_to_ipc():

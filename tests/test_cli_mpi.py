@@ -109,6 +109,34 @@ def test_skipped_transfers_detected(mpirun, host_build):
     assert ok.returncode == 0, ok.stderr[-2000:]
 
 
+def test_every_timed_iteration_is_verified(mpirun, host_build, tmp_path):
+    """P2P_INJECT_FAULT=skip-some@1 drops every other timed delivery on rank 1.
+    A check of the last delivery per slot would pass (the odd iterations
+    delivered); with one receive generation per timed iteration every
+    delivery is checked: exit 2, and the JSON reports full coverage.  Under a
+    budget that holds only 2 generations the coverage says so (2 of 6)."""
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    for transport in ("host", "shm"):
+        js = tmp_path / ("%s.json" % transport)
+        out = run(mpirun, exe, 3, ["--transport", transport, "--mode", "pair,tournament", "--size", "64K", "-n", "6",
+                                   "-w", "2", "--verify", "--no-compat", "--json", str(js)],
+                  env={"P2P_INJECT_FAULT": "skip-some@1"})
+        assert out.returncode == 2, (transport, out.stderr[-2000:])
+        assert "every other timed iteration" in out.stderr and "VERIFICATION FAILED" in out.stderr
+        runs = [json.loads(l) for l in js.read_text().splitlines() if '"type":"run"' in l]
+        assert runs and all(r["verify_coverage"] == 1 and r["timed_msgs"] == r["verified_msgs"] > 0 for r in runs)
+        bad = [ph for r in runs for ph in r["phases"] if ph["mismatches"]]
+        # rank 1 receives in pair cells (0,1), (2,1) and in tournament phases
+        assert bad and all(ph["generations"] == 6 for ph in bad)
+    js = tmp_path / "budget.json"
+    ok = run(mpirun, exe, 2, ["--transport", "host", "--mode", "pair", "--size", "64K", "-n", "6", "-w", "2",
+                              "--verify", "--no-compat", "--json", str(js)], env={"P2P_VERIFY_BUDGET": "300K"})
+    assert ok.returncode == 0, ok.stderr[-2000:]
+    assert "4 of 12 timed deliveries checked" in ok.stdout
+    uni = [json.loads(l) for l in js.read_text().splitlines() if '"type":"run"' in l][0]
+    assert abs(uni["verify_coverage"] - 1 / 3) < 1e-6 and uni["verified_msgs"] == 4
+
+
 def test_json_provenance_and_ring_token(mpirun, host_build, tmp_path):
     """--json starts with the provenance record (knobs, runtime, every rank's
     device and the links between them); --mode ring --latency adds the

@@ -145,15 +145,19 @@ def test_skipped_transfers_detected_on_gpu(exe, engine):
     iterations (pull: its copies are not issued; push: its writes into rank
     0's slots are not issued, the flags still flow, so nothing hangs).  The
     warmup delivered everything, so only the poisoning before timing catches
-    it: exit 2.  The same run without the fault passes."""
+    it: exit 2.  skip-some@1 drops only every other timed iteration; every
+    iteration has a receive generation of its own, so that is caught too.
+    The same run without the fault passes."""
     base = [MPIRUN, "-n", "2", exe, "--transport", "ipc", "--ipc-engine", engine, "--device", "0", "--mode",
-            "pair,tournament", "--size", "1M", "-n", "3", "-w", "2", "--verify", "--no-compat", "--timeout", "60"]
-    out = subprocess.run(base, capture_output=True, text=True, timeout=300,
-                         env=dict(os.environ, P2P_INJECT_FAULT="skip@1"))
-    assert out.returncode == 2, out.stderr[-3000:]
-    assert "VERIFICATION FAILED" in out.stderr
+            "pair,tournament", "--size", "1M", "-n", "4", "-w", "2", "--verify", "--no-compat", "--timeout", "60"]
+    for fault in ("skip@1", "skip-some@1"):
+        out = subprocess.run(base, capture_output=True, text=True, timeout=300,
+                             env=dict(os.environ, P2P_INJECT_FAULT=fault))
+        assert out.returncode == 2, (fault, out.stderr[-3000:])
+        assert "VERIFICATION FAILED" in out.stderr
     ok = subprocess.run(base, capture_output=True, text=True, timeout=300)
     assert ok.returncode == 0, ok.stderr[-3000:]
+    assert "8 of 8 timed deliveries checked" in ok.stdout, ok.stdout[-2000:]
 
 
 def test_ring_token_chain_on_one_gpu(exe, tmp_path):
@@ -236,7 +240,11 @@ def test_bench_emulated_node(nranks):
     m, lat = r["matrix_gbs"], r["latency_p50_us_matrix"]
     assert len(m) == nranks and all(m[a][b] > 0 for a in range(nranks) for b in range(nranks) if a != b)
     assert all(lat[a][b] > 0 for a in range(nranks) for b in range(nranks) if a != b)
-    assert r["reference_semantics"]["cell_gbs_mean"] > 0
+    # BASELINE config 3 by both methods on the reference's serial schedule, uni and bi
+    for key in ("reference_semantics", "pair_serial_events"):
+        assert r[key]["uni"]["gbs_mean"] > 0 and r[key]["bi"]["gbs_mean"] > 0, r[key]
+    assert r["pair_serial_events"]["bi"]["mismatches"] == 0 and r["concurrency_ratio"] > 0
+    assert r["method_ratio"]["uni"] > 0 and r["method_ratio"]["bi"] > 0
     assert r["extras"]["allpairs_1g"]["aggregate_gbs"] > 0 and r["extras"]["ring_256m"]["aggregate_gbs"] > 0
     assert len(r["extras"]["pair_sweep_0_1"]) == 8  # 4 KiB .. 64 MiB in x4 steps
     ipc = r["ipc_transport"]

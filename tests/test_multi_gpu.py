@@ -1,6 +1,15 @@
 """Tier T4: the RCCL data plane across real GPUs.  Runs only
 where >= 2 MI355X are visible (skipped on the 1-GPU test boxes; the 8-GPU
-scaling runs happen through bench.py on a full node)."""
+scaling runs happen through bench.py on a full node).
+
+The driver gives the whole `pytest -m gpu` run one 900 s step, and the
+single-GPU tests take ~260 s of it, so this tier is sized to fit the rest:
+every test's subprocess limits add up to BUDGET_S (checked on the CPU by
+tests/test_scripts_cpu.py::test_multi_gpu_tier_fits_the_driver_step), and
+conftest.py skips whatever is left once the tier has used
+MULTI_GPU_TIER_S.  The tests run in the order of what they prove: the
+reference's matrix over xGMI first, then the concurrent modes, bench.py,
+the hand-written data plane and the fuzzers."""
 import json
 import os
 import subprocess
@@ -21,7 +30,18 @@ def _gpus() -> int:
         return 0
 
 
-pytestmark = [pytest.mark.gpu, pytest.mark.skipif(_gpus() < 2, reason="needs >= 2 GPUs")]
+pytestmark = [pytest.mark.gpu, pytest.mark.multigpu, pytest.mark.skipif(_gpus() < 2, reason="needs >= 2 GPUs")]
+
+# Worst-case seconds of every test (the sum of its subprocess limits).
+BUDGET_S = {
+    "test_reference_matrix_all_gpus": 75,
+    "test_concurrent_modes_all_gpus": 60,
+    "test_bench_all_gpus": 130,
+    "test_ipc_engines_all_gpus": 75,
+    "test_fuzz_all_gpus": 45,
+    "test_cli_fuzz_relay_all_gpus": 45,
+    "test_bench_two_gpus_pair_sweep": 120,
+}
 
 
 @pytest.fixture(scope="module")
@@ -36,10 +56,14 @@ def _n():
 
 @pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
 def test_reference_matrix_all_gpus(exe, tmp_path):
+    """The reference's two matrices (mpirun -n N ./p2p_matrix) over xGMI,
+    every timed delivery verified in a receive generation of its own, and
+    the transport RCCL used for every pair recorded: a pair with a direct
+    xGMI link carried by anything but RCCL's P2P transport fails."""
     n = _n()
     js = tmp_path / "r.json"
-    out = subprocess.run([MPIRUN, "-n", str(n), exe, "--verify", "-n", "16", "--json", str(js)],
-                         capture_output=True, text=True, timeout=900)
+    out = subprocess.run([MPIRUN, "-n", str(n), exe, "--verify", "-n", "16", "--json", str(js), "--timeout", "60",
+                          "--min-gbs", "1"], capture_output=True, text=True, timeout=BUDGET_S["test_reference_matrix_all_gpus"])
     assert out.returncode == 0, out.stderr[-3000:]
     m = parse_compat(out.stdout)
     for key in ("uni", "bi"):
@@ -47,83 +71,80 @@ def test_reference_matrix_all_gpus(exe, tmp_path):
             for j in range(n):
                 assert (m[key][i][j] == 0.0) == (i == j)
     assert "verification: OK" in out.stdout
+    recs = [json.loads(l) for l in js.read_text().splitlines()]
+    assert all(r["verify_coverage"] == 1 for r in recs if r["type"] == "run")
+    # Which RCCL transport carried each pair (RCCL's INFO log); --min-gbs
+    # would have failed a direct xGMI pair carried by SHM or NET.
+    links = [r for r in recs if r["type"] == "links"][0]
+    assert [links["matrix_transport"][a][a] for a in range(n)] == ["self"] * n, links["matrix_transport"]
+    assert "WRONG TRANSPORT" not in out.stderr
 
 
 @pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
 def test_concurrent_modes_all_gpus(exe):
+    """Tournament, ring and all-pairs, verified, with one RCCL communicator
+    and with four (messages >= 1 MiB spread over them, side streams
+    synchronised only around buffer work)."""
     n = _n()
-    out = subprocess.run([MPIRUN, "-n", str(n), exe, "--mode", "tournament,ring,allpairs", "--sizes", "1M,256M",
-                          "-n", "8", "--verify", "--latency", "--no-compat"], capture_output=True, text=True, timeout=900)
-    assert out.returncode == 0, out.stderr[-3000:]
-    assert "verification: OK" in out.stdout and "FAILED" not in out.stdout
+    for comms in ("1", "4"):
+        out = subprocess.run([MPIRUN, "-n", str(n), exe, "--comms", comms, "--mode", "tournament,ring,allpairs",
+                              "--sizes", "1M,64M", "-n", "8", "--verify", "--latency", "--no-compat", "--timeout", "25"],
+                             capture_output=True, text=True, timeout=BUDGET_S["test_concurrent_modes_all_gpus"] / 2)
+        assert out.returncode == 0, out.stderr[-3000:]
+        assert "verification: OK" in out.stdout and "FAILED" not in out.stdout
 
 
 def test_bench_all_gpus():
     n = _n()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
            "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", str(n), "--steps", "14",
-           "--warmup", "7"]
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT)
+           "--warmup", "7", "--deadline", "110", "--sweep-max", "256M", "--timeout", "60"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=BUDGET_S["test_bench_all_gpus"], cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
-    assert r["n_gpus"] == n and r["verify_mismatches"] == 0
+    assert r["n_gpus"] == n and r["verify_mismatches"] == 0 and r["value"] > 0
     assert r["matrix_cells"] == "%d/%d" % (n * (n - 1), n * (n - 1))
+    assert len(r["matrix_transport"]) == n
 
 
 @pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
-@pytest.mark.parametrize("engine", ["kernel", "push", "relay"])
-def test_ipc_engines_all_gpus(exe, engine):
+def test_ipc_engines_all_gpus(exe):
     """The hand-written data plane across real xGMI links: pull (remote reads),
     push (rendezvous + remote writes) and relay (push + two-hop stripes through
     GPUs with idle links; the pair mode's single cells use every GPU),
     verified, plus the device ping-pong matrix."""
     n = _n()
-    modes = "tournament,allpairs,pair" if engine == "relay" else "tournament,allpairs"
-    out = subprocess.run([MPIRUN, "-n", str(n), exe, "--transport", "ipc", "--ipc-engine", engine,
-                          "--mode", modes, "--sizes", "1M,256M", "-n", "8", "--verify",
-                          "--device-latency", "--latency-iters", "200", "--no-compat", "--timeout", "120"],
-                         capture_output=True, text=True, timeout=900)
-    assert out.returncode == 0, out.stderr[-3000:]
-    assert "verification: OK" in out.stdout and "FAILED" not in out.stdout
-    assert "device-initiated ping-pong" in out.stdout
-
-
-@pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
-def test_several_communicators_all_gpus(exe):
-    """--comms 4 across real xGMI links: messages >= 1 MiB spread over four
-    RCCL communicators per rank (side streams synchronised only around buffer
-    work), every mode verified."""
-    n = _n()
-    out = subprocess.run([MPIRUN, "-n", str(n), exe, "--comms", "4", "--mode", "pair,tournament,ring,allpairs",
-                          "--sizes", "64K,1M,256M", "-n", "8", "--verify", "--no-compat", "--timeout", "120"],
-                         capture_output=True, text=True, timeout=900)
-    assert out.returncode == 0, out.stderr[-3000:]
-    assert "verification: OK" in out.stdout and "FAILED" not in out.stdout
+    for engine in ("kernel", "push", "relay"):
+        modes = "tournament,allpairs,pair" if engine == "relay" else "tournament,allpairs"
+        out = subprocess.run([MPIRUN, "-n", str(n), exe, "--transport", "ipc", "--ipc-engine", engine,
+                              "--mode", modes, "--sizes", "1M,64M", "-n", "4", "--verify",
+                              "--device-latency", "--latency-iters", "200", "--no-compat", "--timeout", "20"],
+                             capture_output=True, text=True, timeout=BUDGET_S["test_ipc_engines_all_gpus"] / 3)
+        assert out.returncode == 0, (engine, out.stderr[-3000:])
+        assert "verification: OK" in out.stdout and "FAILED" not in out.stdout
+        assert "device-initiated ping-pong" in out.stdout
 
 
 def test_fuzz_all_gpus():
-    """Random verified message groups across every GPU through RCCL with one
-    and with four communicators per rank."""
+    """Random verified message groups across every GPU through RCCL with four
+    communicators per rank (both ends must route every message alike)."""
     n = _n()
-    for transport in ("rccl", "rccl:4"):
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
-               "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "tests/scripts/fuzz_session.py",
-               transport, "20"]
-        out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT)
-        assert out.returncode == 0, out.stderr[-3000:]
-        assert "FUZZ %s mismatches 0" % transport in out.stdout
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "tests/scripts/fuzz_session.py",
+           "rccl:4", "20"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=BUDGET_S["test_fuzz_all_gpus"], cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "FUZZ rccl:4 mismatches 0" in out.stdout
 
 
 @pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
-@pytest.mark.parametrize("args", [["--comms", "4"], ["--transport", "ipc", "--ipc-engine", "relay"]])
-def test_cli_fuzz_all_gpus(exe, args):
-    """p2p_matrix --fuzz across every GPU: random groups (random pairs incl.
-    self, 1 B .. 64 MiB) over four RCCL communicators, and over the relay
-    engine, whose stripes cross third GPUs."""
+def test_cli_fuzz_relay_all_gpus(exe):
+    """p2p_matrix --fuzz across every GPU over the relay engine, whose stripes
+    cross third GPUs: random groups (random pairs incl. self, 1 B .. 16 MiB)."""
     n = _n()
-    out = subprocess.run([MPIRUN, "-n", str(n), exe] + args + ["--mode", "pair", "--size", "64M", "-n", "2",
-                                                                "--fuzz", "40", "--no-compat", "--timeout", "120"],
-                         capture_output=True, text=True, timeout=900)
+    out = subprocess.run([MPIRUN, "-n", str(n), exe, "--transport", "ipc", "--ipc-engine", "relay", "--mode", "pair",
+                          "--size", "16M", "-n", "2", "--fuzz", "30", "--no-compat", "--timeout", "30"],
+                         capture_output=True, text=True, timeout=BUDGET_S["test_cli_fuzz_relay_all_gpus"])
     assert out.returncode == 0, out.stderr[-3000:]
     assert "all verified" in out.stdout
 
@@ -133,8 +154,11 @@ def test_bench_two_gpus_pair_sweep():
     the time left goes to the xGMI pair sweep (on by default there), whose
     rows cross the real link, every one verified."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2", "--steps", "14", "--warmup", "7"]
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT)
+           "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2", "--steps", "14", "--warmup", "7",
+           "--deadline", "100", "--sweep-max", "256M", "--xgmi-sweep-sizes", "32M", "--ipc-extra", "0",
+           "--timeout", "60"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=BUDGET_S["test_bench_two_gpus_pair_sweep"],
+                         cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     sw = r["xgmi_pair_sweep"]

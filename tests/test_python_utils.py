@@ -81,11 +81,12 @@ def test_gate_probe_unsupported_on_cpu(native):
 
 
 def test_chunking_is_rccl_only(native):
-    """Session.set_max_chunk / max_chunk: only the RCCL transport splits
+    """Session.set_chunk_cap / max_chunk: only the RCCL transport splits
     messages (RCCL's 16 MiB-per-p2p-channel loss); the CPU transports report
-    nothing to split."""
+    nothing to split and no link report."""
     sess = native.Session(0, 1, transport="host")
-    assert sess.set_max_chunk(16 << 20) is False and sess.max_chunk(0) == 0
+    assert sess.set_chunk_cap(16 << 20) is False and sess.max_chunk(0) == 0
+    assert sess.link_reports() == "[null]"
 
 
 def test_child_dies_with_its_parent():

@@ -50,9 +50,14 @@ def test_timings(session, timing):
 
 
 def test_sweep_up_to_1g(session):
+    """Verified self send/recv up to 1 GiB, posted as one op each (the op
+    limit from RCCL's INFO log is 16 MiB x 64 channels): the transport's own
+    chunking must make the verified-warmup fallback unnecessary."""
     for nbytes in [4096, 1 << 20, 64 << 20, 1 << 30]:
         r = json.loads(session.run(mode="self", dir="uni", bytes=nbytes, iters=4, warmup=1, verify=True))
-        assert r["phases"][0]["mismatches"] == 0
+        ph = r["phases"][0]
+        assert ph["mismatches"] == 0 and r["verify_coverage"] == 1, ph
+        assert not r["rechunked"] and ph["warmup_mismatches"] == 0 and ph["op_bytes"] == 0, ph
 
 
 def test_latency(session):
@@ -95,8 +100,9 @@ def test_step_driver_verifies_every_timed_step(native):
 
 def test_skip_fault_is_caught_rccl():
     """P2P_INJECT_FAULT=skip@0 on the RCCL transport: the timed receives land
-    in a sink (the collective still completes); both the run engine and the
-    step driver report every timed delivery as missing."""
+    in a sink (the collective still completes); both the run engine (each of
+    the 4 timed iterations in a receive generation of its own) and the step
+    driver report every timed delivery as missing."""
     code = ("import json\n"
             "from test_nccl_p2p_amd import require_native\n"
             "nat = require_native()\n"
@@ -110,7 +116,37 @@ def test_skip_fault_is_caught_rccl():
                          env=dict(__import__("os").environ, P2P_INJECT_FAULT="skip@0"))
     assert out.returncode == 0, out.stderr[-3000:]
     words = (1 << 20) // 4
-    assert "RUN %d" % words in out.stdout and "STEPS %d" % (3 * 2 * words) in out.stdout, out.stdout
+    assert "RUN %d" % (4 * words) in out.stdout and "STEPS %d" % (3 * 2 * words) in out.stdout, out.stdout
+
+
+def test_skip_some_fault_is_caught_rccl(tmp_path):
+    """P2P_INJECT_FAULT=skip-some@0 on the RCCL self path: every other timed
+    delivery lands in the sink.  The CLI gives every timed iteration its own
+    receive generation, so it exits 2 with full verify_coverage (a check of
+    the last delivery per slot would have passed); the step driver reports
+    exactly the dropped steps' words."""
+    exe = os.path.join(ROOT, "build", "p2p_matrix")
+    js = tmp_path / "r.json"
+    base = [exe, "--mode", "self", "--size", "1M", "-n", "6", "-w", "2", "--verify", "--no-compat", "--timeout", "60",
+            "--json", str(js)]
+    out = subprocess.run(base, capture_output=True, text=True, timeout=120,
+                         env=dict(os.environ, P2P_INJECT_FAULT="skip-some@0"))
+    assert out.returncode == 2, out.stderr[-3000:]
+    run = [json.loads(l) for l in js.read_text().splitlines() if '"type":"run"' in l][0]
+    assert run["verify_coverage"] == 1 and run["timed_msgs"] == 6, run
+    assert run["phases"][0]["mismatches"] == 3 * ((1 << 20) // 4), run["phases"][0]
+    links = [json.loads(l) for l in js.read_text().splitlines() if '"type":"links"' in l][0]
+    assert links["matrix_transport"] == [["self"]] and links["ranks"][0]["comms"][0]["p2p_channels"] > 0, links
+    code = ("from test_nccl_p2p_amd import require_native\n"
+            "nat = require_native()\n"
+            "s = nat.Session(0, 1, device=0, transport='rccl', timeout_s=60)\n"
+            "d = nat.StepDriver(s, 'self', 'bi', 1 << 20, 2, True, True, False, depth=4)\n"
+            "d.connect(); d.run_steps(0, 2); d.sync(); d.poison(); d.run_steps(2, 4); d.sync()\n"
+            "print('STEPS', d.verify_steps(2, 4)['mismatches'])\n")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT,
+                         env=dict(os.environ, P2P_INJECT_FAULT="skip-some@0"))
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "STEPS %d" % (2 * 2 * ((1 << 20) // 4)) in out.stdout, out.stdout
 
 
 def test_ring_latency_and_provenance(native, session):
@@ -131,6 +167,8 @@ def test_message_larger_than_4gib(session):
     r = json.loads(session.run(mode="self", dir="uni", bytes=(5 << 30) + 16, iters=2, warmup=1, verify=True))
     ph = r["phases"][0]
     assert ph["mismatches"] == 0 and ph["flows"][0]["gbs"] > 1.0
+    # posted as 1 GiB ops by the transport itself, not by the warmup fallback
+    assert ph["op_bytes"] == 1 << 30 and ph["warmup_mismatches"] == 0 and not r["rechunked"], ph
 
 
 @pytest.mark.parametrize("comms", [2, 4])
@@ -203,19 +241,26 @@ def test_unmatched_receive_is_reported(transport):
 
 
 def test_chunk_sizes_follow_the_channel_knobs():
-    """RCCL 2.26 loses half of an op above 16 MiB per p2p channel, so the
-    transport's largest op to itself is 16 MiB x RCCL's 64 p2p channels, or
-    fewer under NCCL_MAX_P2P_NCHANNELS (which RCCL caches per process: each
-    setting runs in a process of its own)."""
-    code = ("import test_nccl_p2p_amd as t; n = t.require_native(); "
+    """RCCL loses half of an op above 16 MiB per p2p channel, so the
+    transport's largest op to itself is 16 MiB x the p2p channels RCCL's INFO
+    log reports (64 by default, 4 under NCCL_MAX_P2P_NCHANNELS=4, which RCCL
+    caches per process: each setting runs in a process of its own).  With
+    the user's own NCCL_DEBUG there is no private log and the round-2 guess
+    (64 channels to itself) stands; P2P_RCCL_MAX_CHUNK=0 disables splitting;
+    a cap lowers every limit and 0 lifts it again."""
+    code = ("import json, test_nccl_p2p_amd as t; n = t.require_native(); "
             "s = n.Session(0, 1, device=0, transport='rccl', timeout_s=60); "
-            "a = s.max_chunk(0); ok = s.set_max_chunk(8 << 20); print(a, ok, s.max_chunk(0))")
-    for env, want in (({}, 1 << 30), ({"NCCL_MAX_P2P_NCHANNELS": "4"}, 64 << 20),
-                      ({"P2P_RCCL_MAX_CHUNK": "0"}, 0)):
+            "a = s.max_chunk(0); ok = s.set_chunk_cap(8 << 20); b = s.max_chunk(0); s.set_chunk_cap(0); "
+            "r = json.loads(s.link_reports())[0]; "
+            "print(r['op_limit_source'][:9], r['comms'][0]['p2p_channels'], a, ok, b, s.max_chunk(0))")
+    for env, src, ch, want in (({}, "rccl INFO", 64, 1 << 30), ({"NCCL_MAX_P2P_NCHANNELS": "4"}, "rccl INFO", 4, 64 << 20),
+                               ({"NCCL_DEBUG": "WARN"}, "default (", -1, 1 << 30),
+                               ({"P2P_RCCL_MAX_CHUNK": "0"}, "P2P_RCCL_", 64, 0)):
         out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT,
                              env=dict(os.environ, **env))
         assert out.returncode == 0, out.stderr[-2000:]
-        assert out.stdout.split()[-3:] == [str(want), "True", str(8 << 20)], (env, out.stdout)
+        line = out.stdout.strip().splitlines()[-1]
+        assert line == " ".join([src, str(ch), str(want), "True", str(8 << 20), str(want)]), (env, line)
 
 
 @pytest.mark.parametrize("transport,floor", [("rccl", 800.0), ("rccl:4", 1800.0)])

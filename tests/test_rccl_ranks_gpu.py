@@ -76,7 +76,11 @@ def test_bench_four_rccl_ranks(tmp_path):
     assert all(p["mismatches"] == 0 and p["iter_us_p50"] > 0 for p in ex["pair_sweep_0_1"]), ex["pair_sweep_0_1"]
     lat = r["latency_p50_us_matrix"]
     assert all(lat[a][b] > 0 for a in range(4) for b in range(4) if a != b)
-    assert r["reference_semantics"]["cell_gbs_mean"] > 0
+    # BASELINE config 3 by both methods on the reference's serial schedule, uni and bi
+    for key in ("reference_semantics", "pair_serial_events"):
+        assert r[key]["uni"]["gbs_mean"] > 0 and r[key]["bi"]["gbs_mean"] > 0, r[key]
+    assert r["pair_serial_events"]["bi"]["mismatches"] == 0 and r["concurrency_ratio"] > 0
+    assert r["method_ratio"]["uni"] > 0 and r["method_ratio"]["bi"] > 0
 
 
 @pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")

@@ -56,7 +56,12 @@ def test_scaling_table_comparisons_and_cli(tmp_path, capsys):
             {"metric": "m", "n_gpus": 4, "value": None, "error": "headline failed"}]
     t = scaling_table(rows)
     assert "| 2 | 100.0 | 200.0 | 100.0 | 100.0% | 4 |" in t
-    assert "| 40.0 | 300.0 | 3.25 | 110.0 / 120.0 / - / 150.0 | 250.5 | 1.50 | - |" in t
+    assert "| 40.0 | - | 300.0 | 3.25 | 110.0 / 120.0 / - / 150.0 | 250.5 | 1.50 | - |" in t
+    # Round-3 lines: the reference method in both direction modes, and the ratios.
+    r3 = {"n_gpus": 4, "value": 60.0, "aggregate_gbs": 120.0,
+          "reference_semantics": {"uni": {"gbs_mean": 20.0}, "bi": {"gbs_mean": 38.0}},
+          "method_ratio": {"uni": 2.5, "bi": 2.4}, "concurrency_ratio": 1.3}
+    assert "| 20.0 / 38.0 | 2.5 / 2.4 / 1.3 |" in scaling_table([r3])
     assert "| 8 | 95.0 | 760.0 | 95.0 | 95.0% | - |" in t and "- / - / - / - | - | - | rccl -> ipc |" in t
     assert not any(l.startswith("| 4 |") for l in t.splitlines())  # a line without a value is left out
     files = []

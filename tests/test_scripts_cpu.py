@@ -78,3 +78,27 @@ def test_pair_sweep_resume_keeps_finished_rows(mpirun, host_build, tmp_path):
     rows = [json.loads(l) for l in (tmp_path / "rows.jsonl").read_text().splitlines()]
     assert [r["name"] for r in rows] == ["host"]
     assert json.loads((tmp_path / "summary.json").read_text())["rows_run"] == 1
+
+
+def test_multi_gpu_tier_fits_the_driver_step():
+    """the driver runs `pytest -m gpu` in one 900 s step and
+    the single-GPU tests take ~260 s of it.  Every multi-GPU test has a
+    worst-case budget (the sum of its subprocess limits), they add up to less
+    than 600 s, and conftest's guard stops the tier at MULTI_GPU_TIER_S."""
+    import ast
+
+    import conftest
+
+    src = open(os.path.join(ROOT, "tests", "test_multi_gpu.py")).read()
+    tree = ast.parse(src)
+    tests = [f.name for f in tree.body if isinstance(f, ast.FunctionDef) and f.name.startswith("test_")]
+    budget = next(ast.literal_eval(a.value) for a in tree.body
+                  if isinstance(a, ast.Assign) and getattr(a.targets[0], "id", "") == "BUDGET_S")
+    assert sorted(tests) == sorted(budget), "every multi-GPU test needs a budget"
+    assert sum(budget.values()) < 600 and conftest.MULTI_GPU_TIER_S <= 600
+    # Every subprocess limit in the file is taken from the budget table.
+    for f in tree.body:
+        if isinstance(f, ast.FunctionDef) and f.name.startswith("test_"):
+            for node in ast.walk(f):
+                if isinstance(node, ast.keyword) and node.arg == "timeout" and isinstance(node.value, ast.Constant):
+                    raise AssertionError("%s: a literal subprocess timeout outside BUDGET_S" % f.name)

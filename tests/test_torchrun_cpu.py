@@ -6,6 +6,7 @@ import json
 import os
 import subprocess
 import sys
+import time
 
 import pytest
 
@@ -248,7 +249,11 @@ def test_bench_eight_ranks_with_the_driver_step_counts(native):
     assert ex["allpairs_1g"]["bytes"] == 16 << 20 and ex["allpairs_1g"]["mismatches"] == 0
     assert ex["ring_256m"]["mismatches"] == 0 and ex["ring_hop"]["hop_us_p50"] > 0
     assert len(ex["pair_sweep_0_1"]) == 6
-    assert r["reference_semantics"]["cell_gbs_mean"] > 0
+    # BASELINE config 3 by both methods on the reference's serial schedule, uni and bi
+    for key in ("reference_semantics", "pair_serial_events"):
+        assert r[key]["uni"]["gbs_mean"] > 0 and r[key]["bi"]["gbs_mean"] > 0, r[key]
+    assert r["pair_serial_events"]["bi"]["mismatches"] == 0 and r["concurrency_ratio"] > 0
+    assert r["method_ratio"]["uni"] > 0 and r["method_ratio"]["bi"] > 0
     assert r["ipc_transport"]["verify_mismatches"] == 0
     lat = r["latency_p50_us_matrix"]
     assert all(lat[a][b] > 0 for a in range(8) for b in range(8) if a != b)
@@ -257,19 +262,68 @@ def test_bench_eight_ranks_with_the_driver_step_counts(native):
 def test_bench_headline_fallback(native):
     """A headline transport that cannot be set up (P2P_BENCH_FAIL_HEADLINE,
     as an RCCL communicator that fails on every rank) is replaced by the
-    fallback data plane (host -> shm here; rccl -> ipc on GPUs), and the line
-    says so; with --fallback 0 the line carries the error and value null."""
+    fallback data plane (host -> shm here; rccl -> ipc on GPUs) for the
+    steps, but the line does not pass that off as the metric: value is null
+    and the fallback's number sits in headline_fallback.value_gbs.  With
+    --fallback 0 the line carries the error and value null."""
     args = ["bench.py", "--gpus", "2", "--steps", "3", "--warmup", "2", "--transport", "host", "--size", "256K",
             "--msgs", "2", "--latency-iters", "20", "--sweep", "0", "--extras", "0", "--ref-iters", "0",
             "--ipc-extra", "0", "--fallback-to", "shm"]
     out = torchrun(2, args, env={"P2P_BENCH_FAIL_HEADLINE": "host"})
     assert out.returncode == 0, out.stderr[-3000:]
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
-    assert r["transport"] == "shm" and r["value"] > 0 and r["verify_mismatches"] == 0
-    assert r["headline_fallback"] == {"from": "host", "to": "shm", "error": "injected headline failure"}
+    assert r["transport"] == "shm" and r["value"] is None and r["verify_mismatches"] == 0
+    fb = r["headline_fallback"]
+    assert fb["value_gbs"] > 0 and r["matrix_gbs_mean"] > 0 and r["vs_baseline"] is None
+    assert {k: fb[k] for k in ("from", "to", "error")} == {"from": "host", "to": "shm",
+                                                          "error": "injected headline failure"}
     out = torchrun(2, args + ["--fallback", "0"], env={"P2P_BENCH_FAIL_HEADLINE": "host"})
     assert out.returncode != 0, out.stderr[-3000:]  # torchrun reports the ranks' exit status 5 as 1
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1
     r = json.loads(lines[0])
     assert r["value"] is None and "injected headline failure" in r["error"]
+
+
+def _xgmi_speed_rehearsal(deadline):
+    """bench.py at N = 8 over the shared-memory transport with every size
+    scaled down 1024x (32 MiB -> 32 KiB, the all-pairs 1 GiB -> 1 MiB, the
+    ring 256 MiB -> 256 KiB) and every peer link throttled to 50 GB/s / 1024
+    (P2P_EMULATE_LINK_GBS), so each transfer takes as long as on an xGMI link
+    of ~50 GB/s per direction.  The pair sweep stops at 256 KiB (256 MiB on the
+    node): its iteration count follows absolute sizes."""
+    t0 = time.monotonic()
+    out = torchrun(8, ["bench.py", "--gpus", "8", "--steps", "20", "--warmup", "5", "--transport", "shm",
+                       "--size", "32K", "--allpairs-size", "1M", "--ring-size", "256K", "--sweep-max", "256K",
+                       "--ipc-extra", "0", "--deadline", str(deadline)], timeout=deadline + 60,
+                   env={"P2P_EMULATE_LINK_GBS": "0.0488"})
+    wall = time.monotonic() - t0
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    return r, wall
+
+
+def test_bench_baseline_configs_land_at_xgmi_speed(native):
+    """at N = 8 and xGMI-like transfer times the BASELINE
+    configs run first, each with a reserved slice, and all land in the line
+    within the driver's 300 s deadline: 3 (the matrices by the reference's
+    method and ours, uni and bi, full 128 iterations, latency), 4 (all-pairs),
+    5 (ring and the ring hop), 2 (single-pair sweep).  Under a 60 s deadline
+    the reference-method matrices shrink their iterations to their slices
+    (and say so) and configs 2, 4 and 5 still land."""
+    r, wall = _xgmi_speed_rehearsal(300)
+    assert wall < 300 and r["untimed_skipped"] is None and r.get("section_errors") is None, r
+    for key in ("reference_semantics", "pair_serial_events"):
+        for d in ("uni", "bi"):
+            assert r[key][d]["iters"] == 128 and r[key][d]["cells"] == 56 and r[key][d]["gbs_mean"] > 0, r[key]
+    assert r["pair_serial_events"]["bi"]["mismatches"] == 0 and r["p50_latency_us"] > 0
+    ex = r["extras"]
+    assert {"allpairs_1g", "ring_256m", "ring_hop", "pair_sweep_0_1"} <= set(ex)
+    assert [p["bytes"] for p in ex["pair_sweep_0_1"]] == [4096, 16384, 65536, 262144]
+    r, wall = _xgmi_speed_rehearsal(60)
+    assert wall < 60 and not r.get("deadline_hit") and r.get("section_errors") is None, r
+    ex = r["extras"]
+    assert {"allpairs_1g", "ring_256m", "ring_hop", "pair_sweep_0_1"} <= set(ex), (r["untimed_skipped"], ex)
+    ref = [r[k][d] for k in ("reference_semantics", "pair_serial_events") for d in ("uni", "bi") if r[k]]
+    assert ref and all(x["iters"] <= 128 for x in ref)
+    assert any(x.get("iters_scaled_from") == 128 for x in ref), ref
