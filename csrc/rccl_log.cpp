@@ -82,6 +82,8 @@ std::vector<RcclConnection> parse_rccl_connections(const std::string& text) {
     size_t at = ch + 8;
     c.channel = std::atoi(line.c_str() + at);
     const size_t colon = line.find(" : ", at);
+    const size_t slash = line.find('/', at);
+    if (slash != std::string::npos && slash < colon) c.conn_index = std::atoi(line.c_str() + slash + 1);
     if (colon == std::string::npos || colon > via) continue;
     at = colon + 3;
     if (!rank_dev(line, &at, &c.src)) continue;
@@ -103,6 +105,9 @@ std::vector<RcclConnection> parse_rccl_connections(const std::string& text) {
 std::vector<RcclPeerLink> rccl_peer_links(const std::vector<RcclConnection>& conns, int me, int nranks) {
   std::vector<RcclPeerLink> out(static_cast<size_t>(std::max(nranks, 0)));
   std::map<int, std::set<int>> send_ch, recv_ch;
+  std::set<int> p2p_peers;  // peers with p2p (conn_index > 0) lines: only those count
+  for (const auto& c : conns)
+    if (c.conn_index > 0) p2p_peers.insert(c.src == me ? c.dst : c.src);
   for (int p = 0; p < nranks; ++p) {
     out[static_cast<size_t>(p)].peer = p;
     if (p == me) out[static_cast<size_t>(p)].transport = "self";
@@ -117,7 +122,7 @@ std::vector<RcclPeerLink> rccl_peer_links(const std::vector<RcclConnection>& con
       peer = c.src;
     }
     if (peer < 0 || peer >= nranks) continue;
-    (send ? send_ch : recv_ch)[peer].insert(c.channel);
+    if (c.conn_index > 0 || !p2p_peers.count(peer)) (send ? send_ch : recv_ch)[peer].insert(c.channel);
     auto& l = out[static_cast<size_t>(peer)];
     if (l.via.empty()) {
       l.via = c.via;

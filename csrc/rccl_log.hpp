@@ -25,12 +25,14 @@ struct RcclInitInfo {
   int nnodes = -1;
   int p2p_channels = -1;     // "... %d p2p channels, %d p2p channels per peer"
   int p2p_per_peer = -1;
+  int from_rank = -1;        // set when another rank's log supplied the counts
   bool found() const { return p2p_channels > 0 && p2p_per_peer > 0; }
 };
 
 // One connection line: "Channel 03/0 : 0[2] -> 1[5] [send] via NET/Socket/0".
 struct RcclConnection {
   int channel = -1;
+  int conn_index = 0;  // "Channel 03/1": 1 = the connections p2p ops use (0: collectives' rings / trees)
   int src = -1;  // ranks
   int dst = -1;
   std::string via;  // first token after "via": "P2P/IPC/read", "NET/Socket/0", "SHM/direct/direct", ...
@@ -42,7 +44,8 @@ RcclInitInfo parse_rccl_init(const std::string& text);
 std::vector<RcclConnection> parse_rccl_connections(const std::string& text);
 
 // Per peer of rank `me`: the channels connected towards it (send lines
-// me -> peer; receive-side lines peer -> me where no send line exists) and
+// me -> peer; receive-side lines peer -> me where no send line exists; lines
+// of p2p connections, conn_index > 0, where there are any) and
 // the transport class: "P2P" (xGMI / PCIe peer access through IPC), "SHM",
 // "NET", "self" (peer == me: RCCL copies inside the kernel and logs no
 // connection) or "" (not connected yet).

@@ -554,6 +554,9 @@ class RcclTransport final : public Transport {
 
   // ncclUniqueIds from rank 0 through the bootstrap, then the communicators.
   void open_communicators(Bootstrap& boot, const TransportOptions& opt, int ncomms) {
+    // Before anything of RCCL's runs in this process (ncclGetUniqueId
+    // initialises its logging too): point its INFO log at our file.
+    rccl_log();
     // P2P_RCCL_DISTINCT_HOSTS=1 (tests on one GPU): every rank tells RCCL it
     // is on a host of its own (NCCL_HOSTID, read when RCCL first hashes the
     // host), so several ranks may share one GPU -- RCCL refuses duplicate GPUs
@@ -579,7 +582,6 @@ class RcclTransport final : public Transport {
     nonblocking_ = opt.nonblocking_init && !(blk && std::atoi(blk));
     comms_.assign(static_cast<size_t>(ncomms), nullptr);
     hook_ = push_abort_hook([this](int) { abort_all(); });
-    rccl_log();  // before RCCL's first init in this process reads NCCL_DEBUG*
     log_start_ = log_size();
     // One communicator after the other, in the same order on every rank.
     for (int j = 0; j < ncomms; ++j) {
@@ -619,6 +621,25 @@ class RcclTransport final : public Transport {
     int net_per_peer = 2;
     if (const char* v = std::getenv("NCCL_NCHANNELS_PER_NET_PEER"))
       if (std::atoi(v) > 0) net_per_peer = std::atoi(v);
+    // The channel counts are the communicator's, the same on every rank; a
+    // rank whose log lacks them (no private log, or RCCL printed the line
+    // elsewhere) takes them from the lowest rank that has them.
+    std::vector<int> triples;
+    for (const auto& ci : comm_info_) triples.insert(triples.end(), {ci.p2p_channels, ci.p2p_per_peer, ci.nnodes});
+    const std::vector<int> every = boot.allgather_vector(triples);
+    for (size_t j = 0; j < comm_info_.size(); ++j) {
+      if (comm_info_[j].found()) continue;
+      for (int r = 0; r < n_; ++r) {
+        const int* t = &every[static_cast<size_t>(r) * triples.size() + 3 * j];
+        if (t[0] > 0 && t[1] > 0) {
+          comm_info_[j].p2p_channels = t[0];
+          comm_info_[j].p2p_per_peer = t[1];
+          comm_info_[j].nnodes = t[2];
+          comm_info_[j].from_rank = r;
+          break;
+        }
+      }
+    }
     bool logged = !comm_info_.empty();
     for (const auto& ci : comm_info_) logged = logged && ci.found();
     std::vector<int> mine(static_cast<size_t>(n_), 0);
@@ -660,8 +681,9 @@ class RcclTransport final : public Transport {
     std::string o = strfmt("{\"rank\":%d,\"log\":%s,\"op_limit_source\":\"%s\",\"comms\":[", rank_,
                            rccl_log().path.empty() ? "null" : "true", json_escape(limit_source_).c_str());
     for (size_t j = 0; j < comm_info_.size(); ++j)
-      o += strfmt("%s{\"p2p_channels\":%d,\"p2p_channels_per_peer\":%d,\"nnodes\":%d}", j ? "," : "",
-                  comm_info_[j].p2p_channels, comm_info_[j].p2p_per_peer, comm_info_[j].nnodes);
+      o += strfmt("%s{\"p2p_channels\":%d,\"p2p_channels_per_peer\":%d,\"nnodes\":%d,\"from_rank\":%d}", j ? "," : "",
+                  comm_info_[j].p2p_channels, comm_info_[j].p2p_per_peer, comm_info_[j].nnodes,
+                  comm_info_[j].from_rank < 0 ? rank_ : comm_info_[j].from_rank);
     o += "],\"peers\":[";
     for (int p = 0; p < n_; ++p) {
       const auto& l = links[static_cast<size_t>(p)];

@@ -8,6 +8,7 @@ O=${1:-gpurun_out/session}
 shift
 TESTS=${*:-tests/test_rccl_gpu.py tests/test_binary_gpu.py tests/test_ipc_gpu.py}
 mkdir -p "$O/tmp"
+export P2P_TEST_LOG_DIR="$PWD/$O/testlogs"  # long bench runs inside tests stream their progress here
 : > "$O/status.txt"
 step() {  # step <name> <ok codes regex> <cmd...>
   local name=$1 ok=$2
@@ -20,7 +21,7 @@ step() {  # step <name> <ok codes regex> <cmd...>
     exit "$rc"
   fi
 }
-step pytest "0|1" timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread $TESTS -m gpu \
+step pytest "0|1" timeout -k 10 900 python -u -m pytest --maxfail 5 -v --timeout 300 --timeout-method thread $TESTS -m gpu \
   > "$O/pytest.log" 2>&1
 tail -3 "$O/pytest.log"
 step emu4 "0|2|3" env P2P_RCCL_DISTINCT_HOSTS=1 NCCL_SOCKET_IFNAME=lo NCCL_IB_DISABLE=1 TMPDIR="$PWD/$O/tmp" \

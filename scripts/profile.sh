@@ -1,12 +1,12 @@
 #!/bin/bash
 # rocprofv3 profiles of the flagship paths (run on the MI355X box, from the repo root).
 # Kernel-trace/stats and PMC counters run in SEPARATE invocations (gpurun refuses
-# --pmc together with the trace domains).  Outputs land in gpurun_out/prof/*;
+# --pmc together with the trace domains).  Outputs land in ${1:-gpurun_out/prof}/*;
 # copy the summaries worth keeping into profiles/.
 set -euo pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
+OUT=${1:-gpurun_out/prof}
 mkdir -p "$OUT"
 # 1) kernel trace + stats of the bench (RCCL kernels + fill/verify)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bench" -o bench -- \

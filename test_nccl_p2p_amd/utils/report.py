@@ -153,8 +153,35 @@ def scaling_table(results: Iterable[dict]) -> str:
             _get(r, "ipc_transport", "device_pingpong_p50_us", fmt="%.2f"),
             "%s -> %s" % (fb["from"], fb["to"]) if fb else "-"))
     for r in rows:
-        out += pair_sweep_lines(r)
+        out += transport_lines(r) + pair_sweep_lines(r)
     return "\n".join(out)
+
+
+def transport_lines(r: dict) -> List[str]:
+    """How RCCL carried the pairs of a line (matrix_transport: the transport
+    class per pair from RCCL's INFO log) and the op limits it set up
+    (provenance.rccl_peers): e.g. "P2P 56/56", a fallback to SHM or NET shows
+    up here before it shows up as a slow link."""
+    m = r.get("matrix_transport")
+    if not isinstance(m, list) or r.get("n_gpus", 0) < 2:
+        return []
+    n = len(m)
+    counts = {}
+    for a in range(n):
+        for b in range(n):
+            if a != b:
+                k = m[a][b] or "unknown"
+                counts[k] = counts.get(k, 0) + 1
+    line = "RCCL transports, %d GPUs: %s" % (r["n_gpus"], ", ".join(
+        "%s %d/%d" % (k, v, n * (n - 1)) for k, v in sorted(counts.items())))
+    peers = [p for rk in ((r.get("provenance") or {}).get("rccl_peers") or []) if rk
+             for p in rk.get("peers", []) if p.get("transport") != "self"]
+    if peers:
+        ch = sorted({p.get("op_channels") for p in peers})
+        lim = sorted({p.get("op_limit") for p in peers})
+        line += "; p2p channels per op %s, op limit %s MiB" % ("/".join(map(str, ch)),
+                                                              "/".join(str((x or 0) >> 20) for x in lim))
+    return ["", line]
 
 
 def pair_sweep_lines(r: dict) -> List[str]:

@@ -35,6 +35,28 @@ def pytest_runtest_setup(item):
         pytest.skip("the multi-GPU tier used its %.0f s of the driver's GPU-test step" % MULTI_GPU_TIER_S)
 
 
+def run_logged(cmd, timeout, name="child", **kw):
+    """subprocess.run(cmd, capture_output=True, text=True, timeout=...) whose
+    stderr also lands, as it is written, in $P2P_TEST_LOG_DIR/<name>.log when
+    that is set (the GPU sessions set it under gpurun_out/): a long bench run
+    inside a test shows its progress there instead of looking silent."""
+    log_dir = os.environ.get("P2P_TEST_LOG_DIR")
+    if not log_dir:
+        return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, **kw)
+    os.makedirs(log_dir, exist_ok=True)
+    path = os.path.join(log_dir, "%s.log" % name)
+    with open(path, "w") as err:
+        proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=err, text=True, **kw)
+        try:
+            out, _ = proc.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            proc.kill()
+            proc.communicate()
+            raise
+    with open(path) as f:
+        return subprocess.CompletedProcess(cmd, proc.returncode, out, f.read())
+
+
 def ensure_built(target: str) -> None:
     """Builds a Makefile target in-tree if its artefact is missing."""
     subprocess.run(["make", "-C", ROOT, "-j8", target], check=True, capture_output=True)

@@ -816,6 +816,27 @@ TEST(test_rccl_log_connections) {
   EXPECT(none[1].transport.empty() && none[1].channels_connected == 0);
 }
 
+TEST(test_rccl_log_four_net_ranks) {
+  // Rank 1's own log of a 4-rank RCCL 2.26.6 job on one MI355X, every rank a
+  // host of its own (P2P_RCCL_DISTINCT_HOSTS: RCCL's socket transport).
+  const std::string text = read_file(std::string(P2P_TEST_DATA) + "/rccl_info_4rank_net_rank1.txt");
+  RcclInitInfo info = parse_rccl_init(text);
+  EXPECT(info.nranks == 4 && info.nnodes == 4 && info.p2p_channels == 4 && info.p2p_per_peer == 2);
+  EXPECT(rccl_op_channels(info, true, 2) == 2);
+  auto conns = parse_rccl_connections(text);
+  EXPECT(conns.size() > 12);
+  int p2p = 0;
+  for (const auto& c : conns) p2p += c.conn_index == 1;
+  EXPECT(p2p == 12);
+  auto links = rccl_peer_links(conns, 1, 4);
+  for (int p : {0, 2, 3}) {
+    EXPECT(links[static_cast<size_t>(p)].transport == "NET");
+    EXPECT(links[static_cast<size_t>(p)].via == "NET/Socket/0");
+    EXPECT(links[static_cast<size_t>(p)].channels_connected == 2);  // the p2p connections: 2 per net peer
+  }
+  EXPECT(links[1].transport == "self");
+}
+
 TEST(test_link_transport_mismatch) {
   EXPECT(link_transport_mismatch("XGMI/1", "SHM"));
   EXPECT(link_transport_mismatch("XGMI/1", "NET"));

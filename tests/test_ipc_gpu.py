@@ -10,7 +10,7 @@ import sys
 
 import pytest
 
-from conftest import MPIRUN, ROOT, ensure_built, free_port
+from conftest import MPIRUN, ROOT, ensure_built, free_port, run_logged
 from test_nccl_p2p_amd.utils.report import parse_compat
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")]
@@ -230,8 +230,7 @@ def test_bench_emulated_node(nranks):
            # on the one GPU (8 ranks + 8 children + pytest > the box's 16):
            # isolate them only with 4 ranks.
            "--isolate", "1" if nranks == 4 else "0"]
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT,
-                         env=dict(os.environ, P2P_IPC_POOL="1G"))
+    out = run_logged(cmd, 600, "bench_emulated_node_%d" % nranks, cwd=ROOT, env=dict(os.environ, P2P_IPC_POOL="1G"))
     progress = "\n".join(l for l in out.stderr.splitlines() if "bench:" in l or "fatal" in l)
     assert out.returncode == 0, progress
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])

@@ -17,7 +17,7 @@ import sys
 
 import pytest
 
-from conftest import MPIRUN, ROOT, ensure_built, free_port
+from conftest import MPIRUN, ROOT, ensure_built, free_port, run_logged
 
 pytestmark = [pytest.mark.gpu]
 
@@ -61,7 +61,7 @@ def test_bench_four_rccl_ranks(tmp_path):
            "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "4", "--device", "0", "--size", "4M",
            "--msgs", "8", "--sweep-max", "16M", "--allpairs-size", "16M", "--ring-size", "8M", "--ref-iters", "8",
            "--latency-iters", "30", "--ipc-extra", "0", "--timeout", "60", "--json-out", str(out_json)]
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=ROOT, env=ENV)
+    out = run_logged(cmd, 400, "bench_four_rccl_ranks", cwd=ROOT, env=ENV)
     progress = "\n".join(l for l in out.stderr.splitlines() if "bench:" in l or "fatal" in l or "Error" in l)
     assert out.returncode == 0, progress[-3000:]
     r = json.loads(out_json.read_text())

@@ -94,3 +94,16 @@ def test_scaling_table_pair_sweep():
     assert "- corrupt rows: rccl-nchannels_per_peer=8" in lines and "- skipped rows: rccl-register=2" in lines
     failed = scaling_table([{"n_gpus": 2, "value": 1.0, "xgmi_pair_sweep": {"rc": 1, "error": "no mpirun at x"}}])
     assert "xGMI pair sweep, 2 GPUs: no mpirun at x" in failed
+
+
+def test_scaling_table_transport_lines():
+    """matrix_transport and the RCCL op limits of a multi-GPU line are
+    summarised under the table."""
+    n = 4
+    m = [["self" if a == b else ("P2P" if (a + b) % 3 else "SHM") for b in range(n)] for a in range(n)]
+    peers = [{"peer": 0, "transport": "self", "op_channels": 64, "op_limit": 1 << 30},
+             {"peer": 1, "transport": "P2P", "op_channels": 8, "op_limit": 128 << 20}]
+    r = {"n_gpus": 4, "value": 50.0, "aggregate_gbs": 100.0, "matrix_transport": m,
+         "provenance": {"rccl_peers": [{"peers": peers}, None]}}
+    t = scaling_table([r])
+    assert "RCCL transports, 4 GPUs: P2P 8/12, SHM 4/12; p2p channels per op 8, op limit 128 MiB" in t, t
