@@ -10,14 +10,18 @@ TESTS=${*:-tests/test_rccl_gpu.py tests/test_binary_gpu.py tests/test_ipc_gpu.py
 mkdir -p "$O/tmp"
 export P2P_TEST_LOG_DIR="$PWD/$O/testlogs"  # long bench runs inside tests stream their progress here
 : > "$O/status.txt"
+exec 3>&1
 step() {  # step <name> <ok codes regex> <cmd...>
   local name=$1 ok=$2
   shift 2
   "$@"
   local rc=$?
-  echo "$name rc=$rc" | tee -a "$O/status.txt"
+  # (the step's own redirections cover this function's output: report on fd 3)
+  echo "$name rc=$rc" >> "$O/status.txt"
+  echo "$name rc=$rc" >&3
   if ! [[ $rc =~ ^($ok)$ ]]; then
-    echo "stopping after $name (rc=$rc)" | tee -a "$O/status.txt"
+    echo "stopping after $name (rc=$rc)" >> "$O/status.txt"
+    echo "stopping after $name (rc=$rc)" >&3
     exit "$rc"
   fi
 }

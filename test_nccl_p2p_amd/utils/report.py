@@ -208,6 +208,21 @@ def pair_sweep_lines(r: dict) -> List[str]:
     return out
 
 
+def bench_compat_text(r: dict, key: str = "reference_semantics") -> str:
+    """The reference's two printed matrices for a bench.py line, from its
+    config-3 matrices (`reference_semantics`: the reference's own method, or
+    `pair_serial_events`: ours on its schedule): GB/s x 8 = Gbps, bi = both
+    directions summed, in the exact format p2p_matrix.cc prints -- what
+    `mpirun -n N ./p2p_matrix > result.txt` would have shown on that node."""
+    sec = r.get(key) or {}
+    out = []
+    for d in ("uni", "bi"):
+        m = (sec.get(d) or {}).get("matrix_gbs")
+        if m:
+            out.append(compat_matrix_text([[v * 8.0 for v in row] for row in m], d))
+    return "".join(out)
+
+
 def summarize_compat(text: str) -> str:
     """GB/s min/mean/max (off-diagonal) of each reference-format matrix."""
     from .stats import offdiag_summary
@@ -248,6 +263,12 @@ def main(argv=None) -> int:
         if bench:
             print(scaling_table(bench))
             all_bench.extend(bench)
+            for r in bench:
+                for key in ("reference_semantics", "pair_serial_events"):
+                    txt = bench_compat_text(r, key)
+                    if txt and r.get("n_gpus", 1) > 1:
+                        print("-- %s, %d GPUs, in the reference's format:" % (key, r["n_gpus"]))
+                        print(txt, end="")
         for r in runs:
             print("%-10s %-3s %10d B x %4d: GB/s min %.2f mean %.2f max %.2f"
                   % (r["mode"], r["dir"], r["bytes"], r["iters"], r["gbs_min"], r["gbs_mean"], r["gbs_max"]))

@@ -107,3 +107,17 @@ def test_scaling_table_transport_lines():
          "provenance": {"rccl_peers": [{"peers": peers}, None]}}
     t = scaling_table([r])
     assert "RCCL transports, 4 GPUs: P2P 8/12, SHM 4/12; p2p channels per op 8, op limit 128 MiB" in t, t
+
+
+def test_bench_compat_text_round_trips():
+    """A bench line's config-3 matrices print in the reference's exact format
+    (GB/s x 8 = Gbps; bi = both directions summed), and parse back."""
+    from test_nccl_p2p_amd.utils.report import bench_compat_text, parse_compat
+    r = {"n_gpus": 2, "reference_semantics": {"uni": {"matrix_gbs": [[0.0, 48.5], [47.25, 0.0]]},
+                                              "bi": {"matrix_gbs": [[0.0, 95.0], [95.0, 0.0]]}}}
+    txt = bench_compat_text(r)
+    assert txt.startswith("Evaluating the Uni-Directional NCCL P2P Bandwidth (Gbps)\n   D\\D     0      1 \n")
+    assert "\nEvaluating the Bi-Directional NCCL P2P Bandwidth (Gbps)\n" in txt
+    m = parse_compat(txt)
+    assert m["uni"] == [[0.0, 388.0], [378.0, 0.0]] and m["bi"] == [[0.0, 760.0], [760.0, 0.0]]
+    assert bench_compat_text({"reference_semantics": None}) == ""
