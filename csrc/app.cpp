@@ -99,6 +99,8 @@ output
 environment (recorded in every --json provenance record; docs/OUTPUT.md)
   P2P_RCCL_MAX_CHUNK=B   RCCL: messages above B are posted as B-byte ops in one group, every peer
                          [16M x the p2p channels RCCL set up for the peer; 0 off]
+  P2P_RCCL_UNROLL=U      RCCL kernels' unroll factor (RCCL_UNROLL_FACTOR unless the user set it;
+                         0: RCCL's own choice, 1 on MI355X)                        [4]
   P2P_RCCL_LOG=0|keep    RCCL's INFO log (channels, transports per peer) is captured into a private
                          file unless NCCL_DEBUG asks for it on stderr; 0: off, keep: keep the file
   P2P_RECHUNK=0          --verify: a warmup that does not verify is reported, not retried with

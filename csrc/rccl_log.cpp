@@ -61,6 +61,11 @@ RcclInitInfo parse_rccl_init(const std::string& text) {
       info.nranks = int_after(line, " nRanks ");
       info.nnodes = int_after(line, " nNodes ");
     }
+    const size_t uf = line.find("Unroll Factor");
+    if (uf != std::string::npos) {
+      const size_t colon = line.find(':', uf);
+      if (colon != std::string::npos) info.unroll = std::atoi(line.c_str() + colon + 1);
+    }
     const size_t pp = line.find(" p2p channels per peer");
     if (pp != std::string::npos) {
       info.p2p_per_peer = int_before(line, pp);

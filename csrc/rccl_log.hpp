@@ -26,6 +26,7 @@ struct RcclInitInfo {
   int p2p_channels = -1;     // "... %d p2p channels, %d p2p channels per peer"
   int p2p_per_peer = -1;
   int from_rank = -1;        // set when another rank's log supplied the counts
+  int unroll = -1;           // "RCCL Unroll Factor (pre-set|user-defined): U"
   bool found() const { return p2p_channels > 0 && p2p_per_peer > 0; }
 };
 

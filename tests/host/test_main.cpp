@@ -776,6 +776,8 @@ TEST(test_rccl_log_init_block) {
   const std::string dir = P2P_TEST_DATA;
   RcclInitInfo a = parse_rccl_init(read_file(dir + "/rccl_info_self_nch64.txt"));
   EXPECT(a.found() && a.p2p_channels == 64 && a.p2p_per_peer == 128 && a.nranks == 1 && a.nnodes == 1);
+  EXPECT(a.unroll == 1);  // "RCCL Unroll Factor (pre-set): 1"
+  EXPECT(parse_rccl_init("x NCCL INFO RCCL Unroll Factor (user-defined): 4\n").unroll == 4);
   EXPECT(rccl_op_channels(a, false, 2) == 64);  // 64 x 16 MiB = the 1 GiB limit seen on the self path
   RcclInitInfo b = parse_rccl_init(read_file(dir + "/rccl_info_self_nch1.txt"));
   EXPECT(b.found() && b.p2p_channels == 1 && b.p2p_per_peer == 2);
