@@ -267,11 +267,13 @@ def test_rccl_unroll_factor():
     """The transport asks RCCL for unroll-4 kernels (+7% on the bench step,
     +22% on one communicator's step, profiles/r3_unroll/) and RCCL's own log
     confirms it per communicator; P2P_RCCL_UNROLL=0 leaves RCCL's choice (1)
-    and a user's RCCL_UNROLL_FACTOR wins.  RCCL reads the variable once per
-    process, so each setting runs in a process of its own."""
-    code = ("import json, os, test_nccl_p2p_amd as t; n = t.require_native(); "
+    and a user's RCCL_UNROLL_FACTOR wins; the provenance record holds the
+    value in effect.  RCCL reads the variable once per process, so each
+    setting runs in a process of its own."""
+    code = ("import json, test_nccl_p2p_amd as t; n = t.require_native(); "
             "s = n.Session(0, 1, device=0, transport='rccl', timeout_s=60); "
-            "r = json.loads(s.link_reports())[0]; print(r['comms'][0]['unroll'], os.environ.get('RCCL_UNROLL_FACTOR'))")
+            "r = json.loads(s.link_reports())[0]; p = json.loads(s.provenance(0)); "
+            "print(r['comms'][0]['unroll'], p['env'].get('RCCL_UNROLL_FACTOR'))")
     for env, want in (({}, "4 4"), ({"P2P_RCCL_UNROLL": "0"}, "1 None"), ({"RCCL_UNROLL_FACTOR": "2"}, "2 2")):
         out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT,
                              env=dict(os.environ, **env))
