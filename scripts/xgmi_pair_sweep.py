@@ -85,10 +85,14 @@ RCCL_KNOBS = [
     {"NCCL_P2P_READ_ENABLE": "1"},
     {"P2P_RCCL_REGISTER": "1"},
     {"P2P_RCCL_REGISTER": "2"},
-    # Ops of up to 1 GiB to the peer instead of the transport's 32 MiB: exact
-    # only if RCCL gives the link >= 64 p2p channels (16 MiB each); "corrupt"
-    # otherwise, which measures the channel count it does not report.
+    # Ops of up to 1 GiB to the peer instead of 16 MiB x the channels RCCL's
+    # INFO log reports for it: exact only if the link has >= 64 p2p channels
+    # (16 MiB each), "corrupt" otherwise (the row runs with P2P_RECHUNK=0).
     {"P2P_RCCL_MAX_CHUNK": "1G"},
+    # RCCL's kernel unroll factor: the transport asks for 4 (profiles/r3_unroll/,
+    # +7% / +22% on the self path); RCCL's own pre-set 1 and 2 on the link.
+    {"P2P_RCCL_UNROLL": "0"},
+    {"RCCL_UNROLL_FACTOR": "2"},
 ]
 COMMS = [1, 2, 4, 8]
 IPC_ENGINES = ["kernel", "sdma", "push", "relay"]

@@ -23,7 +23,7 @@ def test_pair_sweep_dry_run_lists_every_knob():
     txt = out.stdout
     for want in ("--comms 8", "NCCL_NCHANNELS_PER_PEER", "NCCL_P2P_NVL_CHUNKSIZE", "NCCL_P2P_NET_CHUNKSIZE",
                  "NCCL_PROTO", "RCCL_P2P_BATCH_ENABLE", "NCCL_P2P_READ_ENABLE", "P2P_RCCL_REGISTER=2",
-                 "--ipc-engine sdma", "--ipc-engine push",
+                 "P2P_RCCL_UNROLL=0", "RCCL_UNROLL_FACTOR=2", "--ipc-engine sdma", "--ipc-engine push",
                  "--ipc-engine relay"):
         assert want in txt, want
 
