@@ -393,11 +393,12 @@ PhaseResult run_phase(Transport& t, Bootstrap& boot, const Phase& phase, size_t 
   // less after a warmup that did not verify (this phase only).
   struct ChunkCap {
     Transport& t;
+    size_t before;  // a cap set by the caller (e.g. bench.py's warmup check) stays after the phase
     bool set = false;
     ~ChunkCap() {
-      if (set) t.set_chunk_cap(0);
+      if (set) t.set_chunk_cap(before);
     }
-  } cap{t};
+  } cap{t, t.chunk_cap()};
 
   if (active) {
     prepare_payload(t, phase, cfg, bufs, gens);

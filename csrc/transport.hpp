@@ -160,6 +160,7 @@ class Transport {
   // (0 lifts the cap).  Both ends of a message must split it alike, so callers
   // set the cap collectively.  false / 0 where nothing is split.
   virtual bool set_chunk_cap(size_t /*bytes*/) { return false; }
+  virtual size_t chunk_cap() const { return 0; }
   virtual size_t max_chunk(int /*peer*/) const { return 0; }
 
   // What the data plane set up towards each peer, as a JSON object (RCCL: the

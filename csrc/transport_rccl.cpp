@@ -499,6 +499,7 @@ class RcclTransport final : public Transport {
     cap_ = bytes;
     return true;
   }
+  size_t chunk_cap() const override { return cap_; }
   std::string link_report() override { return peers_json(); }
   std::vector<std::string> peer_transports() override {
     std::vector<std::string> out;
