@@ -6,7 +6,9 @@
 #      engines across xGMI, fuzz);
 #   2. the reference's own run line, `mpirun -n N ./p2p_matrix` (compat matrices, result.txt);
 #   3. the headline bench at N = 1, 2, 4, 8 and its scaling table (scripts/scaling.sh);
-#   4. the xGMI pair-cell tuning sweep (scripts/xgmi_pair_sweep.py).
+#   4. the xGMI pair-cell tuning sweep (scripts/xgmi_pair_sweep.py);
+#   5. the framework-free RCCL reproducer across two GPUs (scripts/rccl_half_repro.cpp --devices 2: where RCCL's
+#      lost-second-half threshold lies on a real xGMI link, with RCCL's INFO log of the 2-GPU communicator).
 #
 #   bash scripts/node_run.sh [OUT_DIR] [--dry-run]
 set -uo pipefail
@@ -44,9 +46,12 @@ if [ "$DRY" = 0 ]; then
   make -j16 all > "$OUT/build.log" 2>&1 || { echo "node_run: build failed, see $OUT/build.log" >&2; exit 1; }
 fi
 step multi_gpu_tests 1800 python3 -u -m pytest tests/test_multi_gpu.py -m gpu -x -v --timeout 900 --timeout-method thread
-step reference_run 600 "$MPIRUN" -n "$N" ./p2p_matrix
+step reference_run 600 "$MPIRUN" -n "$N" ./p2p_matrix --json "$OUT/reference_run.json"
 [ "$DRY" = 0 ] && cp "$OUT/reference_run.log" "$OUT/result.txt"
 step scaling 3600 bash scripts/scaling.sh "$OUT/scaling.jsonl"
 step pair_sweep 1200 python3 scripts/xgmi_pair_sweep.py --np "$N" --out "$OUT/xgmi_sweep"
+# (exit 3 = some size came back wrong: a finding, not a failure of the step)
+step rccl_repro_2gpu 300 env NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=INIT,P2P NCCL_DEBUG_FILE="$OUT/rccl_repro_2gpu.nccl.txt" \
+  bash -c './build/rccl_half_repro --devices 2 --sizes 16M,32M,64M,128M,256M,512M,1G,1G+16; rc=$?; [ $rc -eq 3 ] && exit 0; exit $rc'
 [ "$DRY" = 0 ] && cat "$OUT/summary.txt"
 exit 0
