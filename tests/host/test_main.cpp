@@ -513,6 +513,38 @@ TEST(test_engine_all_modes_host_transport) {
   for (auto v : mism) EXPECT(v == 0);
 }
 
+TEST(test_engine_receive_generations) {
+  // Every timed iteration in a generation of its own (RunConfig::gens): the
+  // engine checks iters x receivers deliveries, each generation against its
+  // own PRNG stream; the budget caps the generations (256 MiB where the
+  // transport cannot tell free memory: 64 KiB slots -> 2048 generations).
+  const int n = 3;
+  std::vector<int> ok(n, 0);
+  run_ranks(n, [&](Bootstrap& b, Transport& t) {
+    Schedule s = make_schedule(Mode::Tournament, Direction::Bi, n);
+    RunConfig cfg;
+    cfg.bytes = 65536;
+    cfg.iters = 5;
+    cfg.warmup = 2;
+    cfg.verify = true;
+    cfg.gens = verify_generations(t, b, cfg.bytes, s.max_recv_slots(), cfg.iters);
+    EXPECT(cfg.gens == 5);  // min(iters, budget / (64 KiB x (slots + 1)))
+    Buffers bufs(t, cfg.bytes, s.max_recv_slots() * cfg.gens, slot_stride_bytes(cfg.bytes) * static_cast<size_t>(cfg.gens));
+    auto res = run_schedule(t, b, s, cfg, bufs);
+    bool good = true;
+    for (auto& ph : res) {
+      if (ph.idle) continue;
+      good = good && ph.generations == 5 && ph.total_mismatches == 0 && ph.timed_msgs == ph.verified_msgs &&
+             ph.timed_msgs == 5 * ph.flows.size() && ph.op_bytes == 0 && ph.rechunked_to.empty();
+    }
+    // Generations draw from distinct PRNG streams.
+    good = good && generation_seed(1, 4096, 7, 0) != generation_seed(1, 4096, 7, 1) &&
+           generation_seed(1, 4096, 7, 0) == payload_seed(1, 4096, 7);
+    ok[b.rank()] = good ? 1 : 0;
+  });
+  for (int v : ok) EXPECT(v == 1);
+}
+
 TEST(test_engine_all_modes_shm_transport) {
   // Same engine over the shared-memory rings: every mode, odd sizes, and a
   // message larger than the ring (wraps and back-pressure).
