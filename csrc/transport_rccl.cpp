@@ -732,7 +732,7 @@ class RcclTransport final : public Transport {
     if (cu_masked_) desc_ += cu_mask_mode == 1 ? " cu-mask:contig" : " cu-mask:stride";
   }
 
-  static constexpr int kMaxComms = 8;
+  static constexpr int kMaxComms = 16;
 
   // The main stream is about to touch payload buffers: side streams must wait
   // for it before their next transfer.

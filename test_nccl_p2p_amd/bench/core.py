@@ -70,16 +70,17 @@ def first_comms(transport: str, comms: int) -> int:
     return comms if transport == "rccl" and comms > 0 else 1
 
 
-def posting_candidates(transport: str, comms: int, batch: int, n: int = 1):
+def posting_candidates(transport: str, comms: int, batch: int, n: int = 1, hw_queues: int = 4):
     """(communicators, batch) pairs the tuning laps time against each other.
 
-    comms: > 0 fixed, -1 = RCCL picks: between 1 and 4 on one GPU (measured:
-    2, 3, 6 and 8 are slower there, profiles/r2_step_shape/), between 1, 2, 4
-    and 8 across GPUs, where no measurement has fixed the count for an xGMI
-    link yet (other transports: 1).  batch: 1 one group per step, 0 one group
-    per message, -1 = both (K = 1 only: with several communicators
-    per-message groups cannot overlap)."""
-    auto = [1, 4] if n == 1 else [1, 2, 4, 8]
+    comms: > 0 fixed, -1 = RCCL picks: on one GPU between 1 and 4, and 8 when
+    the process has >= 8 hardware queues (measured: 2, 3 and 6 are slower
+    there, and 8 communicators beat 4 only with 8 queues, profiles/r2_step_shape/,
+    profiles/r3_hwq/); between 1, 2, 4 and 8 across GPUs, where no measurement
+    has fixed the count for an xGMI link yet (other transports: 1).  batch: 1
+    one group per step, 0 one group per message, -1 = both (K = 1 only: with
+    several communicators per-message groups cannot overlap)."""
+    auto = ([1, 4] + ([8] if hw_queues >= 8 else [])) if n == 1 else [1, 2, 4, 8]
     comms_choices = ([comms] if comms > 0 else auto) if transport == "rccl" else [1]
     batch_choices = [batch] if batch >= 0 else [0, 1]
     return [(c, b) for c in comms_choices for b in batch_choices if c == 1 or b == 1 or len(batch_choices) == 1]

@@ -17,6 +17,14 @@ from test_nccl_p2p_amd.bench.core import (BASELINE_VALUE, METRIC, cell_matrix, f
                                           pick_depth, posting_candidates, tuning_steps)
 
 
+def hw_queues() -> int:
+    """GPU_MAX_HW_QUEUES in effect for this process (HIP's default: 4)."""
+    try:
+        return int(os.environ.get("GPU_MAX_HW_QUEUES") or 4)
+    except ValueError:
+        return 4
+
+
 class HeadlineMixin:
     """BenchRun's headline methods (collective, like every BenchRun method)."""
 
@@ -52,7 +60,7 @@ class HeadlineMixin:
         # posting_candidates), timed by the slowest rank, before the W warmup
         # steps of the chosen one.
         self.state["section"] = "tuning"
-        choices = posting_candidates(transport, args.comms, args.batch, n)
+        choices = posting_candidates(transport, args.comms, args.batch, n, hw_queues=hw_queues())
         c0 = first_comms(transport, args.comms)
         sessions = {c0: sess}
 
@@ -146,6 +154,7 @@ class HeadlineMixin:
         self.barrier()
         t0 = time.perf_counter()
         drv.run_steps(args.warmup, args.steps)
+        t_posted = time.perf_counter()  # host done posting (diagnostic: a host-bound run posts for ~all of it)
         drv.sync()
         self.gpu_sync()
         self.barrier()
@@ -178,7 +187,8 @@ class HeadlineMixin:
             failed=failed, reason=reason, tuning=tuning, elapsed=elapsed, flows_total=flows_total, value=value,
             aggregate=aggregate, my_ms=my_ms, matrix=matrix, samples=samples, cells=cells, offdiag=offdiag,
             expected=n * (n - 1) if n > 1 else 1, vr=vr, mismatches=vr["mismatches"] if vr else -1, depth=depth,
-            recv_bytes=recv_bytes, chunking=chunking, rccl_peers=rccl_peers, matrix_transport=matrix_transport)
+            recv_bytes=recv_bytes, chunking=chunking, rccl_peers=rccl_peers, matrix_transport=matrix_transport,
+            host_post_ms=(t_posted - t0) * 1e3)
 
     def verify_warmup(self, drv, sessions):
         """RCCL 2.26 / 2.27 deliver only the first half of an op whose share
@@ -295,6 +305,7 @@ class HeadlineMixin:
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(h.elapsed / args.steps * 1e3, 4),
+            "host_post_ms_per_step": round(h.host_post_ms / args.steps, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE and value else None),
@@ -337,6 +348,8 @@ class HeadlineMixin:
             "recv_slot_bytes_per_rank": h.recv_bytes,
             "transport": headline_transport,
             "posting": {"batch": bool(h.batch), "graph": bool(args.graph), "rccl_comms": h.comms, "chunking": h.chunking,
+                        "hw_queues": {"GPU_MAX_HW_QUEUES": hw_queues(),
+                                      "environment_had": os.environ.get("P2P_HW_QUEUES_ENV") or None},
                         "dropped": h.failed or None, "selection": h.reason,
                         "tuning_ms_per_step": {"comms%d_%s" % (c, "batch" if b else "per_message"): round(v * 1e3, 4)
                                                for (c, b), v in h.tuning.items()} or None},

@@ -10,6 +10,8 @@ import bench  # noqa: E402
 def test_posting_candidates_default_rccl():
     # One communicator per-message and batched, four communicators batched.
     assert bench.posting_candidates("rccl", -1, -1) == [(1, 0), (1, 1), (4, 1)]
+    # With 8 hardware queues (bench.py's default) one GPU also tries 8 communicators.
+    assert bench.posting_candidates("rccl", -1, -1, 1, hw_queues=8) == [(1, 0), (1, 1), (4, 1), (8, 1)]
     # Across GPUs the communicator count for one xGMI link is open: 1, 2, 4, 8.
     assert bench.posting_candidates("rccl", -1, -1, 8) == [(1, 0), (1, 1), (2, 1), (4, 1), (8, 1)]
     assert bench.posting_candidates("rccl", 4, -1, 8) == [(4, 1)]
@@ -118,3 +120,17 @@ def test_section_slices():
     assert reserved_after("allpairs_1g", active) == sum(s for n, s in SECTION_SLICES[names.index("allpairs_1g") + 1:])
     assert reserved_after("latency", {"latency", "ring_hop"}) == dict(SECTION_SLICES)["ring_hop"]
     assert reserved_after("ipc", active) == 0.0
+
+
+def test_hw_queues_set_before_hip(monkeypatch):
+    """--hw-queues reaches GPU_MAX_HW_QUEUES before HIP starts; the
+    environment's value is kept for the record; 0 leaves it alone."""
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    bench.set_hw_queues([])
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "8" and os.environ["P2P_HW_QUEUES_ENV"] == "4"
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    bench.set_hw_queues(["--steps", "3", "--hw-queues", "0"])
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "4"
+    bench.set_hw_queues(["--hw-queues=12"])
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "12"
+    assert bench.parse_args(["--hw-queues", "0"]).hw_queues == 0 and bench.parse_args([]).hw_queues == 8
