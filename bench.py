@@ -12,9 +12,9 @@ verify kernels).
 One step = one round of the round-robin "tournament" schedule: the N ranks
 form N/2 disjoint pairs (xGMI is fully connected point-to-point, so pairs never
 share a link) and every pair exchanges --msgs messages of --size bytes in both
-directions (default 32 x 32 MiB = 1 GiB per flow; the reference's cell is
-128 x 32 MiB, p2p_matrix.cc:132), posted back to back inside
-ncclGroupStart/End.  Consecutive steps
+directions (default 128 x 32 MiB = 4 GiB per flow: one step is one of the
+reference's cells, 128 x 32 MiB, p2p_matrix.cc:124,132, for every pair at
+once), posted back to back inside ncclGroupStart/End.  Consecutive steps
 walk through the N-1 rounds, so after N-1 steps every cell of the matrix has
 been measured; per-GPU work per step is constant as N grows (weak scaling).
 With one GPU the step is a self send/recv (uni: the GPU copies to itself; the
@@ -107,10 +107,10 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=28)
     ap.add_argument("--warmup", type=int, default=7)
     ap.add_argument("--size", default="32M", help="message size (reference: 32 MiB, p2p_matrix.cc:124)")
-    ap.add_argument("--msgs", type=int, default=32,
-                    help="messages per direction per step (32 x 32 MiB = 1 GiB per flow: at N = 1 the step takes "
-                         "~0.45 ms, so the barrier + sync bracket costs ~3%% of the timed region instead of ~10%% "
-                         "at 8 messages, profiles/r2_step_shape/)")
+    ap.add_argument("--msgs", type=int, default=128,
+                    help="messages per direction per step (128 x 32 MiB = 4 GiB per flow, the reference's cell "
+                         "(p2p_matrix.cc:132); at N = 1 the step takes ~1.5 ms and the barrier + sync bracket costs "
+                         "~1%% of the timed region, against ~4%% at 32 messages, profiles/r3_hwq/)")
     ap.add_argument("--mode", default="tournament", choices=["tournament", "ring", "allpairs", "pair", "self"])
     ap.add_argument("--transport", default="rccl", choices=["rccl", "ipc", "ipc:sdma", "ipc:push", "ipc:relay", "host", "shm"],
                     help="rccl (headline) | ipc = one-sided gfx950 copy kernel over hipIpc mappings | host = CPU (tests)")
