@@ -10,15 +10,17 @@ import time
 from test_nccl_p2p_amd.bench.core import claim_stdout, default_device, headline_stats, log, pick_depth
 
 
-def steps_through(nat, isess, args, mode, size, batch, transport, deadline=None):
+def steps_through(nat, isess, args, mode, size, batch, transport, recv_budget=0):
     """The timed steps again through another transport session (untimed by
-    the contract); any error is reported instead of failing the run."""
+    the contract); any error is reported (and logged by rank 0) instead of
+    failing the run.  recv_budget: receive-slot bytes this rank may allocate
+    (0: a quarter of the free memory, which ranks sharing a GPU must not use)."""
+    say = (lambda m: log("bench: %s: %s" % (transport, m))) if isess.rank == 0 else (lambda m: None)
     try:
         n = isess.world
         phases = len(nat.schedule(mode, "bi", n))
         idrv = nat.StepDriver(isess, mode, "bi", size, args.msgs, not args.no_verify, bool(batch), False,
-                              depth=pick_depth(args.steps, phases), salt=2)
-        say = (lambda m: log("bench: %s: %s" % (transport, m))) if isess.rank == 0 else (lambda m: None)
+                              depth=pick_depth(args.steps, phases), recv_budget=int(recv_budget), salt=2)
         idrv.connect()
         say("connected (%d receive generations)" % idrv.depth)
         idrv.run_steps(0, args.warmup)
@@ -75,6 +77,7 @@ def steps_through(nat, isess, args, mode, size, batch, transport, deadline=None)
             out["pair_0_1"] = pair
         return out
     except Exception as e:  # report, never fail the headline
+        say("failed: %s" % str(e)[:300])
         return {"error": str(e)[:300], "transport": transport}
 
 
@@ -99,7 +102,8 @@ def child_main(args) -> int:
     try:
         sess = nat.Session(env.rank, env.world, host=env.master_addr, port=args.child_port, device=device,
                            transport=args.child, timeout_s=min(90.0, args.timeout))
-        out = steps_through(nat, sess, args, args.mode, size, args.child_batch, args.child)
+        budget = 0 if args.recv_budget.strip() in ("", "0") else nat.parse_size(args.recv_budget)
+        out = steps_through(nat, sess, args, args.mode, size, args.child_batch, args.child, budget)
         del sess
     except Exception as e:
         out = {"error": str(e)[:300], "transport": args.child}

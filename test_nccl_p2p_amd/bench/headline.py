@@ -28,6 +28,19 @@ def hw_queues() -> int:
 class HeadlineMixin:
     """BenchRun's headline methods (collective, like every BenchRun method)."""
 
+    def recv_budget(self, provenance) -> int:
+        """Bytes of receive slots a driver of this rank may allocate: --recv-budget,
+        else 0.4 of the GPU's free memory now, split between the ranks on the
+        same GPU (they allocate at the same time)."""
+        args = self.args
+        if args.recv_budget.strip() not in ("", "0"):
+            return self.nat.parse_size(args.recv_budget)
+        if not self.use_gpu:
+            return 256 << 20
+        free_b, _ = torch.cuda.mem_get_info(self.device)
+        same_gpu = sum(1 for d in (provenance or {}).get("rank_devices", []) if d["device"] == self.device) or 1
+        return int(0.4 * free_b / same_gpu)
+
     # ---- the headline -------------------------------------------------------
     def measure(self, transport):
         """Posting selection, then the W warmup and K timed steps of the headline
@@ -46,13 +59,7 @@ class HeadlineMixin:
 
         # Receive-slot budget: every message of every timed step gets its own
         # slot, up to this much memory per rank (ranks sharing a GPU split it).
-        budget = 0 if args.recv_budget.strip() in ("", "0") else nat.parse_size(args.recv_budget)
-        if budget == 0 and self.use_gpu:
-            free_b, _ = torch.cuda.mem_get_info(self.device)
-            same_gpu = sum(1 for d in provenance.get("rank_devices", []) if d["device"] == self.device) or 1
-            budget = int(0.4 * free_b / same_gpu)
-        elif budget == 0:
-            budget = 256 << 20
+        budget = self.recv_budget(provenance)
 
         # ---- posting selection: whole untimed laps of the schedule per
         # candidate (one group per step vs one per message; RCCL: one

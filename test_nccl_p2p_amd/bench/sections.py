@@ -286,8 +286,9 @@ class SectionsMixin:
                         extras["pair_0_1_one_comm"] = oc
             self.reporter.update(extras=extras)
 
-    def isolated(self, transport):
-        """steps_through() for `transport` in a child process per rank.  The
+    def isolated(self, transport, recv_budget=0):
+        """steps_through() for `transport` in a child process per rank (with
+        `recv_budget` bytes of receive slots each; 0: the child's default).  The
         comparisons drive the hand-written data plane (hipIpc mappings, signal
         kernels, relays) across GPUs; if one of them faults or hangs on some
         node, only the child dies, and the headline line still gets printed
@@ -302,7 +303,8 @@ class SectionsMixin:
                "--warmup", str(args.warmup), "--size", args.size, "--msgs", str(args.msgs), "--mode", self.mode,
                "--latency-iters", str(args.latency_iters), "--latency-size", args.latency_size,
                "--child", transport, "--child-port", str(box[0]), "--child-out", out_path,
-               "--child-batch", str(int(self.h.batch)), "--timeout", str(max(5.0, min(args.timeout, limit)))]
+               "--child-batch", str(int(self.h.batch)), "--recv-budget", str(int(recv_budget)),
+               "--timeout", str(max(5.0, min(args.timeout, limit)))]
         if args.no_verify:
             cmd.append("--no-verify")
         if args.device is not None:
@@ -350,12 +352,15 @@ class SectionsMixin:
         value, batch = self.h.value, self.h.batch
 
         def compare(transport):
+            # Ranks sharing a GPU split its free memory (the headline's driver
+            # still holds its slots).
+            budget = self.recv_budget(self.h.provenance)
             if args.isolate:
-                return self.isolated(transport)
+                return self.isolated(transport, budget)
             isess = self.create_session(transport, device=self.device,
                                         timeout_s=min(90.0, max(5.0, self.budget_left())))
             try:
-                return steps_through(self.nat, isess, args, self.mode, self.size, batch, transport)
+                return steps_through(self.nat, isess, args, self.mode, self.size, batch, transport, budget)
             finally:
                 del isess
 

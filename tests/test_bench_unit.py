@@ -134,3 +134,22 @@ def test_hw_queues_set_before_hip(monkeypatch):
     bench.set_hw_queues(["--hw-queues=12"])
     assert os.environ["GPU_MAX_HW_QUEUES"] == "12"
     assert bench.parse_args(["--hw-queues", "0"]).hw_queues == 0 and bench.parse_args([]).hw_queues == 8
+
+
+def test_recv_budget_split_between_ranks_on_one_gpu(monkeypatch):
+    import types
+
+    from test_nccl_p2p_amd.bench import headline
+
+    run = types.SimpleNamespace(args=types.SimpleNamespace(recv_budget="0"), use_gpu=True, device=0,
+                                nat=types.SimpleNamespace(parse_size=lambda s: {"2G": 2 << 30}[s]))
+    monkeypatch.setattr(headline.torch.cuda, "mem_get_info", lambda d: (100 << 30, 288 << 30))
+    prov = {"rank_devices": [{"device": 0}] * 4 + [{"device": 1}] * 4}
+    budget = headline.HeadlineMixin.recv_budget
+    # Four ranks on device 0 allocate at once: each plans with 0.4 of a quarter.
+    assert budget(run, prov) == int(0.4 * (100 << 30) / 4)
+    assert budget(run, {}) == int(0.4 * (100 << 30))
+    run.args.recv_budget = "2G"
+    assert budget(run, prov) == 2 << 30
+    run.args.recv_budget, run.use_gpu = "0", False
+    assert budget(run, prov) == 256 << 20

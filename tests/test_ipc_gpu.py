@@ -226,6 +226,9 @@ def test_bench_emulated_node(nranks):
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", str(nranks),
            "--steps", "14", "--warmup", "7", "--transport", "ipc", "--device", "0", "--sweep-max", "64M",
            "--latency-iters", "100", "--deadline", "560",
+           # N ranks share one GPU's memory: 32 messages per step keep every
+           # timed step in its own receive slots (128 would cap the generations).
+           "--msgs", "32",
            # Child processes for the comparisons would double the processes
            # on the one GPU (8 ranks + 8 children + pytest > the box's 16):
            # isolate them only with 4 ranks.
