@@ -348,6 +348,11 @@ class HeadlineMixin:
             "latency_bytes": nat.parse_size(args.latency_size),
             "per_gpu_gbs": round(h.aggregate / n, 3),
             "rank0_step_ms_p50": round(statistics.median(h.my_ms) if h.my_ms else 0.0, 4),
+            # Every timed step's GPU time on rank 0, and what the wall-clock
+            # bracket adds to their sum (launch of the first step, the final
+            # sync and barrier): why `value` sits below `matrix_gbs_mean`.
+            "rank0_step_ms": [round(x, 4) for x in h.my_ms],
+            "bracket_overhead_ms": round(h.elapsed * 1e3 - sum(h.my_ms), 4) if h.my_ms else None,
             "verify_mismatches": h.mismatches,
             "verify_coverage": (round(vr["verified_msgs"] / vr["timed_msgs"], 4) if vr and vr["timed_msgs"] else None),
             "verify_detail": vr,
