@@ -357,16 +357,27 @@ class RcclTransport final : public Transport {
     recv_on_side_ = recv_stream_ != nullptr;
   }
   void group_end() override {
-    if (!deferred_.empty()) {
-      std::stable_sort(deferred_.begin(), deferred_.end(), [](const Op& a, const Op& b) { return a.comm < b.comm; });
-      for (const Op& o : deferred_) post(o);
-      deferred_.clear();
-    }
     in_group_ = false;
-    ncclResult_t r = ncclGroupEnd();
-    // Non-blocking comm: the ops are only enqueued once the comm leaves
-    // ncclInProgress, so wait before any event is recorded behind them.
-    wait_ready(r, "ncclGroupEnd");
+    std::stable_sort(deferred_.begin(), deferred_.end(), [](const Op& a, const Op& b) { return a.comm < b.comm; });
+    if (group_per_comm_ && !deferred_.empty() && deferred_.front().comm != deferred_.back().comm) {
+      // One RCCL group per communicator, in communicator order: the first
+      // communicator's kernel starts once its own ops are posted instead of
+      // after every communicator's (RCCL prepares all of a group's work before
+      // it launches any of it).  The caller's group holds no ops.
+      wait_ready(ncclGroupEnd(), "ncclGroupEnd");
+      for (size_t i = 0; i < deferred_.size();) {
+        const int c = deferred_[i].comm;
+        nccl_ok(ncclGroupStart(), "ncclGroupStart");
+        for (; i < deferred_.size() && deferred_[i].comm == c; ++i) post(deferred_[i]);
+        wait_ready(ncclGroupEnd(), "ncclGroupEnd");
+      }
+    } else {
+      for (const Op& o : deferred_) post(o);
+      // Non-blocking comm: the ops are only enqueued once the comm leaves
+      // ncclInProgress, so wait before any event is recorded behind them.
+      wait_ready(ncclGroupEnd(), "ncclGroupEnd");
+    }
+    deferred_.clear();
     if (recv_on_side_) {
       // Reference two-stream layout (sends on s_0, receives on s_1,
       // p2p_matrix.cc:214-225): join s_1 back so marks and syncs on the main
@@ -600,6 +611,7 @@ class RcclTransport final : public Transport {
     boot.bcast(ids.data(), sizeof(ncclUniqueId) * ids.size(), 0);
 
     if (const char* sm = std::getenv("P2P_RCCL_SPLIT_MIN")) split_min_ = parse_size(sm);
+    if (const char* gp = std::getenv("P2P_RCCL_GROUP_PER_COMM")) group_per_comm_ = std::atoi(gp) != 0;
     if (const char* rg = std::getenv("P2P_RCCL_REGISTER")) register_ = std::atoi(rg);
     const char* blk = std::getenv("P2P_RCCL_BLOCKING");
     nonblocking_ = opt.nonblocking_init && !(blk && std::atoi(blk));
@@ -909,6 +921,7 @@ class RcclTransport final : public Transport {
   std::vector<bool> used_;             // side communicators used by the open group
   bool in_group_ = false;              // between group_begin and group_end
   std::vector<Op> deferred_;           // the open group's ops (several communicators)
+  bool group_per_comm_ = false;        // P2P_RCCL_GROUP_PER_COMM=1: one RCCL group per communicator at group_end
   std::vector<unsigned long long> send_seq_, recv_seq_;  // messages posted to / from each peer
   struct RegSet {
     void* send = nullptr;

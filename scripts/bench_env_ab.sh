@@ -16,7 +16,7 @@ for rep in $(seq 1 "$REPS"); do
     env "${envs[@]}" timeout -k 10 180 python bench.py --steps 20 --warmup 5 --ipc-extra 0 --ref-iters 0 \
       --latency-iters 50 > "$OUT/${tag}_$rep.json" 2> "$OUT/${tag}_$rep.err"
     rc=$?
-    echo "$setting rep=$rep rc=$rc $(python3 -c "import json; r=json.loads([l for l in open('$OUT/${tag}_$rep.json') if l.startswith('{')][0]); print(r['value'], r['matrix_gbs_mean'], r['posting']['rccl_comms'], r['posting']['tuning_ms_per_step'])" 2>/dev/null)" | tee -a "$OUT/summary.txt"
+    echo "$setting rep=$rep rc=$rc $(python3 -c "import json; r=json.loads([l for l in open('$OUT/${tag}_$rep.json') if l.startswith('{')][0]); print(r['value'], r['matrix_gbs_mean'], r['posting']['rccl_comms'], r['posting']['tuning_ms_per_step'], 'first_step_ms', (r.get('rank0_step_ms') or [None])[0], 'bracket_ms', r.get('bracket_overhead_ms'), 'host_post_ms', r.get('host_post_ms_per_step'))" 2>/dev/null)" | tee -a "$OUT/summary.txt"
     if [ $rc -ne 0 ] && [ $rc -ne 3 ]; then exit $rc; fi
   done
 done
