@@ -108,6 +108,8 @@ environment (recorded in every --json provenance record; docs/OUTPUT.md)
   P2P_VERIFY_BUDGET=B    --verify: bytes of receive generations (one per timed iteration)
                          [free HBM / 4, <= 32G]
   P2P_RCCL_SPLIT_MIN=B   --comms: smaller messages stay on communicator 0       [1M]
+  P2P_RCCL_GROUP_PER_COMM=1  --comms: each communicator's ops as an RCCL group of
+                         their own                                                 [0]
   P2P_RCCL_REGISTER=1|2  ncclCommRegister every buffer (2: + ncclMemAlloc)
   P2P_RCCL_BLOCKING=1    blocking ncclCommInitRank instead of the polled non-blocking init
   P2P_RCCL_DISTINCT_HOSTS=1  one NCCL_HOSTID per rank: RCCL ranks may share a GPU (tests,
