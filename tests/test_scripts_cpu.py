@@ -102,3 +102,23 @@ def test_multi_gpu_tier_fits_the_driver_step():
             for node in ast.walk(f):
                 if isinstance(node, ast.keyword) and node.arg == "timeout" and isinstance(node.value, ast.Constant):
                     raise AssertionError("%s: a literal subprocess timeout outside BUDGET_S" % f.name)
+
+
+def test_kernel_overlap_bursts_and_concurrency(tmp_path):
+    """scripts/kernel_overlap.py on a hand-made trace: two bursts split at an
+    idle gap; in the first, two queues overlap for half of each kernel."""
+    rows = [("rcclGenericKernel<4, false>", 1, 0, 100_000), ("rcclGenericKernel<4, false>", 2, 50_000, 150_000),
+            ("fill_grid_kernel", 1, 150_000, 4_000_000),  # not matched: does not bridge the gap
+            ("rcclGenericKernel<4, false>", 1, 5_000_000, 5_100_000)]
+    trace = tmp_path / "t_kernel_trace.csv"
+    with open(trace, "w") as f:
+        f.write('"Kernel_Name","Queue_Id","Start_Timestamp","End_Timestamp"\n')
+        for name, q, s, e in rows:
+            f.write('"%s",%d,%d,%d\n' % (name, q, s, e))
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "kernel_overlap.py"), str(trace),
+                          "--min-kernels", "1", "--json"], capture_output=True, text=True, check=True)
+    first, second = [json.loads(l) for l in out.stdout.splitlines()]
+    assert first["kernels"] == 2 and first["queues"] == 2 and first["peak_concurrency"] == 2
+    assert first["span_ms"] == 0.15 and first["busy_ms"] == 0.15 and first["busy_fraction"] == 1.0
+    assert first["mean_concurrency"] == round(200 / 150, 3)
+    assert second["kernels"] == 1 and second["burst"] == 1
