@@ -1,15 +1,19 @@
 #!/bin/bash
 # Interleaved A/B of environment settings on the driver-shaped 1-GPU bench
 # (untimed sections off).  Each setting is "NAME=VAL[,NAME=VAL...]" or
-# "default"; REPS rounds over all settings.
+# "default"; REPS rounds over all settings, each round starting one setting
+# later than the one before (so no setting always runs first on the box).
 #   bash scripts/bench_env_ab.sh <out_dir> <reps> <setting>...
 set -u
 OUT=$1
 REPS=$2
 shift 2
 mkdir -p "$OUT"
+settings=("$@")
+n=${#settings[@]}
 for rep in $(seq 1 "$REPS"); do
-  for setting in "$@"; do
+  for i in $(seq 0 $((n - 1))); do
+    setting=${settings[$(((i + rep - 1) % n))]}
     envs=(P2P_UNUSED=1)
     [ "$setting" = default ] || IFS=, read -r -a envs <<< "$setting"
     tag=$(echo "$setting" | tr -c 'A-Za-z0-9_=' '_')
