@@ -95,8 +95,8 @@ core.set_start(T0)
 # Re-exported: the pure functions the unit tests pin (tests/test_bench_unit.py).
 from test_nccl_p2p_amd.bench.compare import child_main, steps_through  # noqa: E402,F401
 from test_nccl_p2p_amd.bench.core import (METRIC, Deadline, Reporter, cell_matrix, claim_stdout,  # noqa: E402,F401
-                                          default_device, first_comms, free_port, headline_stats, log, pick_depth,
-                                          posting_candidates, start_watchdog, tuning_steps)
+                                          default_device, first_comms, free_port, headline_stats, link_check, log,
+                                          pick_depth, posting_candidates, start_watchdog, tuning_steps)
 from test_nccl_p2p_amd.bench.headline import HeadlineMixin  # noqa: E402
 from test_nccl_p2p_amd.bench.sections import SectionsMixin  # noqa: E402
 
@@ -116,7 +116,8 @@ def parse_args(argv=None):
                     help="rccl (headline) | ipc = one-sided gfx950 copy kernel over hipIpc mappings | host = CPU (tests)")
     ap.add_argument("--comms", type=int, default=-1,
                     help="rccl: communicators per rank; the messages of a step are spread over them and their "
-                         "send/recv kernels run side by side (-1: the tuning laps pick 1 or 4)")
+                         "send/recv kernels run side by side (-1: the tuning laps pick: 1, 4 or 8 on one GPU, 8 "
+                         "only with >= 8 HW queues; 1, 2, 4 or 8 across GPUs; posting_candidates)")
     ap.add_argument("--device", type=int, default=None, help="GPU index (default LOCAL_RANK)")
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process, set before HIP starts (0: the environment's); more "
@@ -245,6 +246,10 @@ class BenchRun(HeadlineMixin, SectionsMixin):
             return rc
         h = self.h
         self.reporter.result = self.base_result()
+        lc = self.reporter.result.get("link_check")
+        if lc and not lc["ok"]:
+            self.log0("bench: WRONG TRANSPORT: RCCL carried %d of %d direct xGMI pairs over something else than "
+                      "P2P: %s" % (len(lc["not_p2p"]), lc["direct_xgmi_pairs"], ", ".join(lc["not_p2p"][:16])))
         self.log0("bench: value %.2f GB/s per cell (aggregate %.2f GB/s), %.4f ms/step, verify %s" % (
             h.value, h.aggregate, h.elapsed / self.args.steps * 1e3, h.vr))
 

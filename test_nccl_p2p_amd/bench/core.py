@@ -258,6 +258,28 @@ def method_ratios(ours: dict, ref: dict, value: float, n: int) -> dict:
     return out
 
 
+def link_check(rank_links, matrix_transport):
+    """Pairs whose GPUs share a direct xGMI link (provenance.rank_links
+    "XGMI/1", hipExtGetLinkTypeAndHopCount) but which RCCL carried over
+    anything but its P2P transport (matrix_transport, from its INFO log): the
+    same rule as p2p_matrix --min-gbs (rccl_log.cpp link_transport_mismatch).
+    A node where RCCL fell back to SHM or NET would otherwise only look like
+    slow links.  None when either matrix is missing (one GPU, no RCCL log)."""
+    if not rank_links or not matrix_transport:
+        return None
+    n = min(len(rank_links), len(matrix_transport))
+    direct, wrong = 0, []
+    for a in range(n):
+        for b in range(n):
+            if a == b or rank_links[a][b] != "XGMI/1":
+                continue
+            direct += 1
+            t = matrix_transport[a][b]
+            if t and t not in ("?", "P2P", "self"):
+                wrong.append("%d->%d %s" % (a, b, t))
+    return {"direct_xgmi_pairs": direct, "not_p2p": wrong, "ok": not wrong}
+
+
 def default_device(local_rank: int) -> int:
     """LOCAL_RANK, modulo the visible GPUs: a launcher that gives each rank
     one visible GPU (HIP_VISIBLE_DEVICES per process) leaves every rank on

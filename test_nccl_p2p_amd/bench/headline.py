@@ -13,8 +13,8 @@ import types
 import torch
 import torch.distributed as dist
 
-from test_nccl_p2p_amd.bench.core import (BASELINE_VALUE, METRIC, cell_matrix, first_comms, headline_stats, log,
-                                          pick_depth, posting_candidates, tuning_steps)
+from test_nccl_p2p_amd.bench.core import (BASELINE_VALUE, METRIC, cell_matrix, first_comms, headline_stats,
+                                          link_check, log, pick_depth, posting_candidates, tuning_steps)
 
 
 def hw_queues() -> int:
@@ -367,6 +367,7 @@ class HeadlineMixin:
                                                for (c, b), v in h.tuning.items()} or None},
             "provenance": dict(h.provenance, rccl_peers=h.rccl_peers),
             "matrix_transport": h.matrix_transport,
+            "link_check": link_check(h.provenance.get("rank_links"), h.matrix_transport),
             "reference_semantics": None,
             "pair_serial_events": None,
             "method_ratio": None,

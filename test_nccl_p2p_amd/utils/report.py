@@ -181,7 +181,12 @@ def transport_lines(r: dict) -> List[str]:
         lim = sorted({p.get("op_limit") for p in peers})
         line += "; p2p channels per op %s, op limit %s MiB" % ("/".join(map(str, ch)),
                                                               "/".join(str((x or 0) >> 20) for x in lim))
-    return ["", line]
+    out = ["", line]
+    lc = r.get("link_check")
+    if isinstance(lc, dict) and not lc.get("ok", True):
+        out.append("WRONG TRANSPORT on %d of %d direct xGMI pairs: %s" % (
+            len(lc["not_p2p"]), lc["direct_xgmi_pairs"], ", ".join(lc["not_p2p"][:16])))
+    return out
 
 
 def pair_sweep_lines(r: dict) -> List[str]:

@@ -153,3 +153,25 @@ def test_recv_budget_split_between_ranks_on_one_gpu(monkeypatch):
     assert budget(run, prov) == 2 << 30
     run.args.recv_budget, run.use_gpu = "0", False
     assert budget(run, prov) == 256 << 20
+
+
+def test_link_check_flags_direct_xgmi_pairs_not_on_p2p():
+    """bench.py's link_check: a pair whose GPUs share a direct xGMI link but
+    which RCCL carried over SHM or NET is listed (the --min-gbs rule of
+    p2p_matrix); unknown transports, two-hop links and one GPU are not."""
+    links = [["same-gpu", "XGMI/1", "XGMI/1", "XGMI/2"],
+             ["XGMI/1", "same-gpu", "XGMI/1", "XGMI/1"],
+             ["XGMI/1", "XGMI/1", "same-gpu", "XGMI/1"],
+             ["XGMI/2", "XGMI/1", "XGMI/1", "same-gpu"]]
+    t = [["self", "P2P", "SHM", "NET"],
+         ["P2P", "self", "?", "P2P"],
+         ["NET", "P2P", "self", "P2P"],
+         ["SHM", "P2P", "P2P", "self"]]
+    lc = bench.link_check(links, t)
+    assert lc == {"direct_xgmi_pairs": 10, "not_p2p": ["0->2 SHM", "2->0 NET"], "ok": False}
+    ok = bench.link_check(links, [["self" if a == b else "P2P" for b in range(4)] for a in range(4)])
+    assert ok["ok"] and ok["not_p2p"] == [] and ok["direct_xgmi_pairs"] == 10
+    # Ranks sharing one GPU (emulated node, NET by design) have no direct link.
+    emu = bench.link_check([["same-gpu"] * 2] * 2, [["self", "NET"], ["NET", "self"]])
+    assert emu == {"direct_xgmi_pairs": 0, "not_p2p": [], "ok": True}
+    assert bench.link_check(None, t) is None and bench.link_check(links, None) is None

@@ -107,6 +107,9 @@ def test_scaling_table_transport_lines():
          "provenance": {"rccl_peers": [{"peers": peers}, None]}}
     t = scaling_table([r])
     assert "RCCL transports, 4 GPUs: P2P 8/12, SHM 4/12; p2p channels per op 8, op limit 128 MiB" in t, t
+    assert "WRONG TRANSPORT" not in t
+    r["link_check"] = {"direct_xgmi_pairs": 12, "not_p2p": ["0->2 SHM", "2->0 SHM"], "ok": False}
+    assert "WRONG TRANSPORT on 2 of 12 direct xGMI pairs: 0->2 SHM, 2->0 SHM" in scaling_table([r])
 
 
 def test_bench_compat_text_round_trips():
