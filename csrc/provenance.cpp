@@ -80,20 +80,43 @@ RankDev my_rank_dev(int device) {
   return mine;
 }
 // Link between the GPUs of every two ranks, from this host's probe (ranks on
-// other hosts, or ranks without a GPU, read "n/a").
+// other hosts, or ranks without a GPU, read "n/a").  GPUs are matched by PCI
+// bus id, not by device index: a launcher that shows every rank only its own
+// GPU (HIP_VISIBLE_DEVICES per process) leaves every rank on its device 0, and
+// a GPU this process cannot see reads "n/a" rather than "same-gpu".
 std::vector<std::string> link_matrix(const std::vector<RankDev>& all, const RankDev& mine) {
   const int n = static_cast<int>(all.size());
   int ndev = 0;
   auto links = probe_topology(&ndev);
+  std::vector<std::string> visible_pci(static_cast<size_t>(ndev));
+  for (int d = 0; d < ndev; ++d) visible_pci[static_cast<size_t>(d)] = device_pci_id(d);
+  // This process's index of rank r's GPU, -1 if it is not visible here.
+  auto local_index = [&](const RankDev& r) {
+    if (r.device < 0) return -1;
+    if (r.pci[0] == '\0') return r.device < ndev ? r.device : -1;
+    for (int d = 0; d < ndev; ++d)
+      if (visible_pci[static_cast<size_t>(d)] == r.pci) return d;
+    return -1;
+  };
   std::vector<std::string> out(static_cast<size_t>(n) * static_cast<size_t>(n), "n/a");
   for (int a = 0; a < n; ++a)
     for (int b = 0; b < n; ++b) {
-      const int da = all[static_cast<size_t>(a)].device, db = all[static_cast<size_t>(b)].device;
-      const bool local = all[static_cast<size_t>(a)].host == mine.host && all[static_cast<size_t>(b)].host == mine.host;
-      if (local && da >= 0 && db >= 0 && da < ndev && db < ndev) {
-        const LinkInfo& li = links[static_cast<size_t>(da) * ndev + db];
-        out[static_cast<size_t>(a) * n + b] = da == db ? "same-gpu" : strfmt("%s/%d", li.type.c_str(), li.hops);
+      const RankDev& ra = all[static_cast<size_t>(a)];
+      const RankDev& rb = all[static_cast<size_t>(b)];
+      if (ra.host != mine.host || rb.host != mine.host || ra.device < 0 || rb.device < 0) continue;
+      std::string& cell = out[static_cast<size_t>(a) * n + b];
+      if (ra.pci[0] != '\0' && std::strcmp(ra.pci, rb.pci) == 0) {
+        cell = "same-gpu";
+        continue;
       }
+      const int da = local_index(ra), db = local_index(rb);
+      if (da < 0 || db < 0) continue;
+      if (da == db) {
+        cell = "same-gpu";
+        continue;
+      }
+      const LinkInfo& li = links[static_cast<size_t>(da) * ndev + db];
+      cell = strfmt("%s/%d", li.type.c_str(), li.hops);
     }
   return out;
 }

@@ -25,6 +25,17 @@ def hw_queues() -> int:
         return 4
 
 
+def ranks_on_my_gpu(provenance, rank: int, device: int) -> int:
+    """Ranks sharing this rank's GPU (provenance.rank_devices), matched by PCI
+    bus id where known -- under a launcher that shows each rank only its own
+    GPU every rank is on device 0 -- else by device index; at least 1."""
+    devs = (provenance or {}).get("rank_devices") or []
+    mine = next((d for d in devs if d.get("rank") == rank), None)
+    if mine and mine.get("pci"):
+        return sum(1 for d in devs if d.get("pci") == mine["pci"]) or 1
+    return sum(1 for d in devs if d.get("device") == device) or 1
+
+
 class HeadlineMixin:
     """BenchRun's headline methods (collective, like every BenchRun method)."""
 
@@ -38,8 +49,7 @@ class HeadlineMixin:
         if not self.use_gpu:
             return 256 << 20
         free_b, _ = torch.cuda.mem_get_info(self.device)
-        same_gpu = sum(1 for d in (provenance or {}).get("rank_devices", []) if d["device"] == self.device) or 1
-        return int(0.4 * free_b / same_gpu)
+        return int(0.4 * free_b / ranks_on_my_gpu(provenance, self.env.rank, self.device))
 
     # ---- the headline -------------------------------------------------------
     def measure(self, transport):

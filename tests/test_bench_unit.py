@@ -142,6 +142,7 @@ def test_recv_budget_split_between_ranks_on_one_gpu(monkeypatch):
     from test_nccl_p2p_amd.bench import headline
 
     run = types.SimpleNamespace(args=types.SimpleNamespace(recv_budget="0"), use_gpu=True, device=0,
+                                env=types.SimpleNamespace(rank=0),
                                 nat=types.SimpleNamespace(parse_size=lambda s: {"2G": 2 << 30}[s]))
     monkeypatch.setattr(headline.torch.cuda, "mem_get_info", lambda d: (100 << 30, 288 << 30))
     prov = {"rank_devices": [{"device": 0}] * 4 + [{"device": 1}] * 4}
@@ -153,6 +154,20 @@ def test_recv_budget_split_between_ranks_on_one_gpu(monkeypatch):
     assert budget(run, prov) == 2 << 30
     run.args.recv_budget, run.use_gpu = "0", False
     assert budget(run, prov) == 256 << 20
+
+
+def test_ranks_on_my_gpu_match_by_pci():
+    """A launcher that shows each rank only its own GPU puts every rank on
+    device 0: the PCI bus id, not the index, tells whether ranks share a GPU."""
+    from test_nccl_p2p_amd.bench.headline import ranks_on_my_gpu
+
+    own = {"rank_devices": [{"rank": r, "device": 0, "pci": "0000:%02x:00.0" % (0x10 + r)} for r in range(8)]}
+    assert ranks_on_my_gpu(own, 3, 0) == 1
+    shared = {"rank_devices": [{"rank": r, "device": 0, "pci": "0000:8b:00.0"} for r in range(4)]}
+    assert ranks_on_my_gpu(shared, 2, 0) == 4
+    # No PCI ids (CPU transports): the device index decides, as before.
+    assert ranks_on_my_gpu({"rank_devices": [{"rank": r, "device": r % 2, "pci": ""} for r in range(4)]}, 0, 0) == 2
+    assert ranks_on_my_gpu({}, 0, 0) == 1
 
 
 def test_link_check_flags_direct_xgmi_pairs_not_on_p2p():
