@@ -134,6 +134,9 @@ def parse_args(argv=None):
     ap.add_argument("--tune-laps", type=int, default=1,
                     help="untimed laps of the schedule per posting candidate, before the W warmup steps "
                          "(0: no tuning, the first candidate is used)")
+    ap.add_argument("--tune-passes", type=int, default=2,
+                    help="timed passes per posting candidate, back to back; the fastest counts (the first carries "
+                         "first-use costs; tuning_passes_ms_per_step records them all)")
     ap.add_argument("--graph", type=int, default=0, help="1: replay each step as a captured hipGraph")
     ap.add_argument("--recv-budget", default="0",
                     help="receive-slot memory per rank (0: 40%% of free HBM / ranks per GPU); caps the slot "

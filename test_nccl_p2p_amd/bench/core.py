@@ -86,9 +86,14 @@ def posting_candidates(transport: str, comms: int, batch: int, n: int = 1, hw_qu
     return [(c, b) for c in comms_choices for b in batch_choices if c == 1 or b == 1 or len(batch_choices) == 1]
 
 
-def tuning_steps(phases: int, min_steps: int = 4) -> int:
-    """Steps per candidate: whole laps of the schedule (every cell once per
-    lap), at least min_steps so a one-round schedule is not timed on one step."""
+def tuning_steps(phases: int, min_steps: int = 8, lap_enough: int = 4) -> int:
+    """Steps per tuning pass: whole laps of the schedule (every cell once per
+    lap).  A schedule of fewer than lap_enough rounds (one GPU, N = 2, 3) runs
+    laps up to min_steps steps, so a one-round schedule is not timed on a few
+    ~1.5 ms steps; one lap of a longer schedule (N = 8: 7 rounds of 4 GiB per
+    flow over xGMI) is long enough as it is."""
+    if phases >= lap_enough:
+        return phases
     return phases * max(1, math.ceil(min_steps / phases))
 
 

@@ -88,7 +88,7 @@ class HeadlineMixin:
                                                   timeout_s=args.timeout)
             return sessions[c]
 
-        tuning, failed = {}, {}
+        tuning, tuning_passes, failed = {}, {}, {}
         phases = len(nat.schedule(mode, "bi", n))
         tune_k = tuning_steps(phases) * args.tune_laps
         if args.tune_laps > 0 and len(choices) > 1:
@@ -108,19 +108,32 @@ class HeadlineMixin:
                 except Exception as e:  # noqa: BLE001 -- reported, and the candidate is skipped everywhere
                     err = str(e)[:200]
                 if self.agree(err is None):
-                    self.barrier()
-                    w0 = time.perf_counter()
-                    try:
-                        d.run_steps(0, tune_k)
-                        d.sync()
-                        if (os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d,tuning" % (c, b)
-                                and self.env.rank == n - 1):
-                            raise RuntimeError("injected tuning failure")
-                    except Exception as e:  # noqa: BLE001 -- same agreement as above
-                        err = str(e)[:200]
-                    w = time.perf_counter() - w0
-                    if self.agree(err is None):
-                        tuning[(c, b)] = sess.allreduce_max(w) / tune_k
+                    # --tune-passes timed passes back to back; the fastest counts.
+                    # The first pass carries the candidate's first-use costs, and
+                    # one short pass is noisy: with a single 4-step pass, 2 of 16
+                    # one-GPU runs picked 4 communicators over 8 and lost 15%
+                    # (profiles/r3b_nt_ab/).
+                    passes = []
+                    for _ in range(max(1, args.tune_passes)):
+                        self.barrier()
+                        w0 = time.perf_counter()
+                        try:
+                            d.run_steps(0, tune_k)
+                            d.sync()
+                            if (os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d,tuning" % (c, b)
+                                    and self.env.rank == n - 1):
+                                raise RuntimeError("injected tuning failure")
+                        except Exception as e:  # noqa: BLE001 -- same agreement as above
+                            err = str(e)[:200]
+                        w = time.perf_counter() - w0
+                        if not self.agree(err is None):
+                            # Failed on some rank: dropped on every rank alike.
+                            err = err or "failed on another rank"
+                            break
+                        passes.append(sess.allreduce_max(w) / tune_k)
+                    if err is None:
+                        tuning[(c, b)] = min(passes)
+                        tuning_passes[(c, b)] = passes
                         del d
                         # Only the best communicator count so far, the headline
                         # session and the single communicator (kept for the
@@ -138,8 +151,9 @@ class HeadlineMixin:
                 if c != c0 and not any(cc == c for (cc, _) in tuning):
                     sessions.pop(c, None)
             comms, batch = min(tuning, key=tuning.get)
-            reason = "fastest of %d candidate(s) over %d untimed step(s) each (%s lap(s) of %d round(s)), slowest " \
-                     "rank's clock" % (len(tuning), tune_k, args.tune_laps, phases)
+            reason = "fastest of %d candidate(s): best of %d pass(es) of %d untimed step(s) each (%s lap(s) of %d " \
+                     "round(s)), slowest rank's clock" % (len(tuning), max(1, args.tune_passes), tune_k, args.tune_laps,
+                                                         phases)
         else:
             comms, batch = choices[0]
             reason = "single candidate" if len(choices) == 1 else "no tuning laps (--tune-laps 0): first candidate"
@@ -201,7 +215,7 @@ class HeadlineMixin:
         del drv
         return types.SimpleNamespace(
             sess=sess, ref_sess=ref_sess, sessions=sessions, provenance=provenance, comms=comms, batch=batch,
-            failed=failed, reason=reason, tuning=tuning, elapsed=elapsed, flows_total=flows_total, value=value,
+            failed=failed, reason=reason, tuning=tuning, tuning_passes=tuning_passes, elapsed=elapsed, flows_total=flows_total, value=value,
             aggregate=aggregate, my_ms=my_ms, matrix=matrix, samples=samples, cells=cells, offdiag=offdiag,
             expected=n * (n - 1) if n > 1 else 1, vr=vr, mismatches=vr["mismatches"] if vr else -1, depth=depth,
             recv_bytes=recv_bytes, chunking=chunking, rccl_peers=rccl_peers, matrix_transport=matrix_transport,
@@ -374,7 +388,10 @@ class HeadlineMixin:
                                       "environment_had": os.environ.get("P2P_HW_QUEUES_ENV") or None},
                         "dropped": h.failed or None, "selection": h.reason,
                         "tuning_ms_per_step": {"comms%d_%s" % (c, "batch" if b else "per_message"): round(v * 1e3, 4)
-                                               for (c, b), v in h.tuning.items()} or None},
+                                               for (c, b), v in h.tuning.items()} or None,
+                        "tuning_passes_ms_per_step": {"comms%d_%s" % (c, "batch" if b else "per_message"):
+                                                      [round(v * 1e3, 4) for v in vs]
+                                                      for (c, b), vs in h.tuning_passes.items()} or None},
             "provenance": dict(h.provenance, rccl_peers=h.rccl_peers),
             "matrix_transport": h.matrix_transport,
             "link_check": link_check(h.provenance.get("rank_links"), h.matrix_transport),

@@ -26,10 +26,12 @@ def test_posting_candidates_fixed_and_other_transports():
 
 
 def test_tuning_steps_are_whole_laps():
-    # N = 8: 7 rounds, one lap covers every cell; N = 1 / 2: one round, 4 steps.
+    # N = 8: 7 rounds, one lap covers every cell; N = 1 / 2: one round, 8 steps.
     assert bench.tuning_steps(7) == 7
-    assert bench.tuning_steps(3) == 6
-    assert bench.tuning_steps(1) == 4
+    assert bench.tuning_steps(4) == 4
+    assert bench.tuning_steps(3) == 9
+    assert bench.tuning_steps(1) == 8
+    assert bench.tuning_steps(1, min_steps=4) == 4
 
 
 def test_first_comms():
