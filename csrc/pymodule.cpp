@@ -346,6 +346,8 @@ PYBIND11_MODULE(_p2pcore, m) {
            "Enqueue steps [first, first+count); consecutive steps share their boundary timestamp.")
       .def("sync", [](PyStepDriver& s) { s.d().sync(); }, py::call_guard<py::gil_scoped_release>())
       .def("step_ms", [](PyStepDriver& s) { return s.d().step_ms(); })
+      .def("post_ms", [](PyStepDriver& s) { return s.d().post_ms(); },
+           "Host time each recorded step took to post (ms).")
       .def("reset", [](PyStepDriver& s) { s.d().reset(); })
       .def("verify_last", [](PyStepDriver& s) { return s.d().verify_last(); }, py::call_guard<py::gil_scoped_release>())
       .def("bytes_sent_per_step", [](PyStepDriver& s, long k) { return s.d().bytes_sent_per_step(k); })

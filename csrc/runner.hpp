@@ -273,6 +273,9 @@ class StepDriver {
   void run_steps(long first, long count);
   void sync();                  // wait for everything posted
   std::vector<double> step_ms();       // this rank's per-step durations since the last reset
+  // Host time each of those steps took to post (ms, steady clock): a step the
+  // GPU waits for is one whose posting is slower than the step before it ran.
+  const std::vector<double>& post_ms() const { return post_ms_; }
   void reset();                 // forget recorded steps
   // Collective, blocking, untimed: zero every receive slot of every rank once
   // every rank has drained.
@@ -319,6 +322,7 @@ class StepDriver {
   int depth_;                                 // receive generations (the same on every rank)
   Buffers bufs_;
   std::vector<std::pair<int, int>> marks_;
+  std::vector<double> post_ms_;  // host posting time per recorded step
   std::vector<int> graphs_;  // per (generation, phase), when opt_.graph
   long last_step_ = -1;
   bool skip_armed_ = false;

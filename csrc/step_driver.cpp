@@ -2,6 +2,7 @@
 // phase of the schedule per step, posted with no host sync between steps;
 // payload layout and verification as described in runner.hpp.
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <map>
 #include <string>
@@ -183,6 +184,7 @@ void StepDriver::run_steps(long first, long count) {
 }
 
 void StepDriver::step_impl(long k, bool chain) {
+  const auto posted_from = std::chrono::steady_clock::now();
   const int pi = static_cast<int>(k % phases());
   const int g = gen_of(k);
   const Phase& p = sched_.phases[static_cast<size_t>(pi)];
@@ -211,6 +213,7 @@ void StepDriver::step_impl(long k, bool chain) {
     chain_mark_ = b;
   }
   last_step_ = k;
+  post_ms_.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - posted_from).count());
 }
 
 void StepDriver::sync() {
@@ -228,6 +231,7 @@ std::vector<double> StepDriver::step_ms() {
 
 void StepDriver::reset() {
   marks_.clear();
+  post_ms_.clear();
   t_.clear_marks();
 }
 

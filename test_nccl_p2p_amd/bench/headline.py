@@ -199,6 +199,7 @@ class HeadlineMixin:
 
         # Per-step GPU durations of every rank -> per-cell bandwidth.
         my_ms = drv.step_ms()
+        post_ms = list(drv.post_ms())
         all_ms = [None] * n
         if n > 1:
             dist.all_gather_object(all_ms, my_ms)
@@ -219,7 +220,7 @@ class HeadlineMixin:
             aggregate=aggregate, my_ms=my_ms, matrix=matrix, samples=samples, cells=cells, offdiag=offdiag,
             expected=n * (n - 1) if n > 1 else 1, vr=vr, mismatches=vr["mismatches"] if vr else -1, depth=depth,
             recv_bytes=recv_bytes, chunking=chunking, rccl_peers=rccl_peers, matrix_transport=matrix_transport,
-            host_post_ms=(t_posted - t0) * 1e3)
+            host_post_ms=(t_posted - t0) * 1e3, post_ms=post_ms)
 
     def verify_warmup(self, drv, sessions):
         """RCCL 2.26 / 2.27 deliver only the first half of an op whose share
@@ -377,6 +378,9 @@ class HeadlineMixin:
             # sync and barrier): why `value` sits below `matrix_gbs_mean`.
             "rank0_step_ms": [round(x, 4) for x in h.my_ms],
             "bracket_overhead_ms": round(h.elapsed * 1e3 - sum(h.my_ms), 4) if h.my_ms else None,
+            # Host time rank 0 took to post each timed step (the GPU runs ahead of
+            # nothing but the first: later steps are posted while earlier ones run).
+            "rank0_post_ms": [round(x, 4) for x in h.post_ms],
             "verify_mismatches": h.mismatches,
             "verify_coverage": (round(vr["verified_msgs"] / vr["timed_msgs"], 4) if vr and vr["timed_msgs"] else None),
             "verify_detail": vr,
