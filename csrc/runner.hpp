@@ -251,6 +251,13 @@ struct StepOptions {
   bool graph = false;  // capture each (phase, generation) step into a hipGraph (transports that support it)
   int depth = 1;       // receive generations requested (capped by recv_budget)
   size_t recv_budget = 0;  // bytes of receive slots this rank may hold (0: a quarter of free memory)
+  // batch: messages per group (0: the whole step).  group_msgs applies to every
+  // step, first_group_msgs to the first step of a run_steps call only (the one
+  // the GPU waits for while the host posts it).  Every group holds whole
+  // messages, and every rank splits alike.  Env P2P_STEP_GROUP_MSGS /
+  // P2P_STEP_FIRST_GROUP_MSGS set them where the caller did not.
+  int group_msgs = 0;
+  int first_group_msgs = 0;
 };
 
 struct StepVerifyReport {
@@ -329,8 +336,10 @@ class StepDriver {
   bool skip_some_armed_ = false;
   int recaptures_ = 0;
   int chain_mark_ = -1;  // run_steps: the previous step's end mark, the next one's start
+  int per_group_ = 0;    // post_step_ops: messages per group of the step being posted (0: all)
 
   void step_impl(long k, bool chain);
+  void post_step_groups(const Phase& p, int pi, int gen, int per_group);
   void capture_graphs();
 
   void post_step_ops(const Phase& p, int pi, int gen);

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <string>
 #include <utility>
@@ -69,6 +70,9 @@ StepDriver::StepDriver(Transport& t, Bootstrap& boot, Schedule sched, size_t byt
       bufs_(t, bytes, std::max(1, depth_ * gen_slots_[static_cast<size_t>(t.rank())]),
             slot_stride(bytes) * static_cast<size_t>(msgs)) {
   if (opt_.graph && !t_.supports_graphs()) opt_.graph = false;
+  if (const char* g = std::getenv("P2P_STEP_GROUP_MSGS"); g && opt_.group_msgs == 0) opt_.group_msgs = std::atoi(g);
+  if (const char* g = std::getenv("P2P_STEP_FIRST_GROUP_MSGS"); g && opt_.first_group_msgs == 0)
+    opt_.first_group_msgs = std::atoi(g);
   std::string bad = validate(sched_);
   P2P_CHECK(bad.empty(), "invalid schedule: " + bad);
   P2P_CHECK(!sched_.phases.empty(), "empty schedule");
@@ -164,10 +168,14 @@ void StepDriver::post_step_ops(const Phase& p, int pi, int gen) {
       t_.recv_from(bufs_.recv_buf(slot_index(me, gen, pi, m, static_cast<int>(i))), bytes_, ops.recv_from[i], off);
   };
   if (opt_.batch) {
-    // One group: every message of the step, fused into one launch by RCCL.
-    t_.group_begin();
-    for (int m = 0; m < msgs_; ++m) one_message(m);
-    t_.group_end();
+    // One group: every message of the step, fused into one launch by RCCL
+    // (or groups of per_group_ whole messages, post_step_groups).
+    const int per = per_group_ > 0 && per_group_ < msgs_ ? per_group_ : msgs_;
+    for (int m0 = 0; m0 < msgs_; m0 += per) {
+      t_.group_begin();
+      for (int m = m0; m < std::min(msgs_, m0 + per); ++m) one_message(m);
+      t_.group_end();
+    }
   } else {
     for (int m = 0; m < msgs_; ++m) {
       t_.group_begin();
@@ -175,6 +183,18 @@ void StepDriver::post_step_ops(const Phase& p, int pi, int gen) {
       t_.group_end();
     }
   }
+}
+
+// A step posted in groups of `per_group` whole messages (0: one group).  A
+// transport launches nothing of a group before its end (RCCL prepares all of
+// a group's work first), so smaller groups let the GPU start on a step while
+// the host is still posting it; with 8 communicators and messages routed
+// round-robin over them, 16 messages per group give every communicator its
+// usual two-message kernel (profiles/r3b_post/).
+void StepDriver::post_step_groups(const Phase& p, int pi, int gen, int per_group) {
+  per_group_ = per_group;
+  post_step_ops(p, pi, gen);
+  per_group_ = 0;
 }
 
 void StepDriver::step(long k) { step_impl(k, false); }
@@ -193,8 +213,9 @@ void StepDriver::step_impl(long k, bool chain) {
   // honour the discard, so such steps are posted eagerly).
   if (skip_some_armed_) t_.set_discard(k % 2 == 0);
   const bool replay = opt_.graph && !skip_armed_ && !skip_some_armed_;
+  const int per_group = !chain && opt_.first_group_msgs > 0 ? opt_.first_group_msgs : opt_.group_msgs;
   if (!p.participates(t_.rank())) {
-    if (posts_phase(t_, p, t_.rank())) post_step_ops(p, pi, g);  // relay only: no flow of its own to time
+    if (posts_phase(t_, p, t_.rank())) post_step_groups(p, pi, g, per_group);  // relay only: no flow of its own
     marks_.emplace_back(-1, -1);
     chain_mark_ = -1;
   } else {
@@ -207,7 +228,7 @@ void StepDriver::step_impl(long k, bool chain) {
     if (replay && gi < graphs_.size() && graphs_[gi] >= 0)
       t_.graph_launch(graphs_[gi]);
     else
-      post_step_ops(p, pi, g);
+      post_step_groups(p, pi, g, per_group);
     const int b = t_.mark();
     marks_.emplace_back(a, b);
     chain_mark_ = b;
