@@ -780,6 +780,28 @@ TEST(test_step_driver_verifies_timed_steps) {
     }, shm);
 }
 
+// A step posted in groups of whole messages (the first step of a run, or
+// every step) moves and verifies exactly what one group per step does.
+TEST(test_step_driver_split_groups) {
+  for (int mode = 0; mode < 2; ++mode)
+    run_ranks(4, [&](Bootstrap& b, Transport& t) {
+      StepOptions so;
+      so.batch = true;
+      so.depth = 3;
+      (mode == 0 ? so.first_group_msgs : so.group_msgs) = 2;
+      StepDriver d(t, b, make_tournament_schedule(4, Direction::Bi), 4100, 5, true, 13, so);
+      d.connect();
+      d.poison();
+      d.run_steps(0, 9);
+      d.sync();
+      StepVerifyReport r = d.verify_steps(0, 9);
+      EXPECT(r.mismatches == 0);
+      EXPECT(r.timed_msgs == 9u * 4 * 5 && r.verified_msgs == r.timed_msgs);
+      EXPECT(d.post_ms().size() == 9u);
+      b.barrier();
+    }, mode == 1);
+}
+
 // remote_slots: the k-th send to a peer meets the k-th receive from it.
 TEST(test_remote_slots_repeated_peer) {
   Schedule s = make_ring_schedule(2, Direction::Bi);
