@@ -72,7 +72,7 @@ def set_hw_queues(argv) -> None:
     4, 8 queues and 8 communicators move the 1-GPU step 7% faster than 4 and
     4 (profiles/r3_hwq/); the tuning laps still pick the communicator count.
     The value in effect and the environment's are recorded (posting.hw_queues)."""
-    q = "8"
+    q = os.environ.get("P2P_BENCH_HW_QUEUES") or "8"  # (experiments: the default without --hw-queues)
     for i, a in enumerate(argv):
         if a == "--hw-queues" and i + 1 < len(argv):
             q = argv[i + 1]

@@ -542,7 +542,7 @@ class RcclTransport final : public Transport {
  private:
   // Main stream (fill / verify), the optional reference receive stream, and
   // one stream + join event per communicator.  Returns the CU-mask mode
-  // (0 off, 1 contig, 2 stride).
+  // (0 off, 1 contig, 2 stride, 3 full).
   int open_streams(const TransportOptions& opt, int ncomms) {
     HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     if (opt.two_streams) {
@@ -555,9 +555,17 @@ class RcclTransport final : public Transport {
     // bit), so the K concurrent send/recv kernels do not compete for CUs; the
     // main stream (fill / verify) stays unmasked, so communicator 0 moves to
     // a stream of its own as with P2P_RCCL_MAIN_IDLE.
+    // P2P_RCCL_CU_MASK=full: every CU in every communicator's mask.  HIP
+    // gives a stream with a CU mask a hardware queue of its own instead of
+    // sharing one of its GPU_MAX_HW_QUEUES, so no communicator's stream
+    // shares an in-order queue with another's or with RCCL's internal
+    // streams (whose event waits would then hold it up).
     int cu_mask_mode = 0;
     if (const char* cm = std::getenv("P2P_RCCL_CU_MASK"))
-      cu_mask_mode = std::strcmp(cm, "contig") == 0 ? 1 : std::strcmp(cm, "stride") == 0 ? 2 : 0;
+      cu_mask_mode = std::strcmp(cm, "contig") == 0 ? 1
+                     : std::strcmp(cm, "stride") == 0 ? 2
+                     : std::strcmp(cm, "full") == 0   ? 3
+                                                      : 0;
     if (ncomms == 1) cu_mask_mode = 0;
     if (cu_mask_mode) main_idle_ = true;
     int ncus = 0;
@@ -567,7 +575,7 @@ class RcclTransport final : public Transport {
       if (cu_mask_mode) {
         std::vector<uint32_t> mask(static_cast<size_t>((ncus + 31) / 32), 0u);
         for (int c = 0; c < ncus; ++c) {
-          const int owner = cu_mask_mode == 1 ? c * ncomms / ncus : c % ncomms;
+          const int owner = cu_mask_mode == 1 ? c * ncomms / ncus : cu_mask_mode == 2 ? c % ncomms : j;
           if (owner == j) mask[static_cast<size_t>(c / 32)] |= 1u << (c % 32);
         }
         HIPCHECK(hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(mask.size()), mask.data()));
@@ -741,7 +749,7 @@ class RcclTransport final : public Transport {
     desc_ = strfmt("hip:%d %s (%s, %d CUs, %.0f GiB, pci %s) rccl %d", device_, prop.name, prop.gcnArchName,
                    prop.multiProcessorCount, static_cast<double>(prop.totalGlobalMem) / (1ull << 30), pci, ver);
     if (ncomms > 1) desc_ += strfmt(" x%d comms", ncomms);
-    if (cu_masked_) desc_ += cu_mask_mode == 1 ? " cu-mask:contig" : " cu-mask:stride";
+    if (cu_masked_) desc_ += cu_mask_mode == 1 ? " cu-mask:contig" : cu_mask_mode == 2 ? " cu-mask:stride" : " cu-mask:full";
   }
 
   static constexpr int kMaxComms = 16;
