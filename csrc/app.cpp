@@ -110,6 +110,8 @@ environment (recorded in every --json provenance record; docs/OUTPUT.md)
   P2P_RCCL_SPLIT_MIN=B   --comms: smaller messages stay on communicator 0       [1M]
   P2P_RCCL_GROUP_PER_COMM=1  --comms: each communicator's ops as an RCCL group of
                          their own                                                 [0]
+  P2P_RCCL_CU_MASK=contig|stride|full  --comms: each communicator's stream on its own CU
+                         mask (1/K of the CUs, or every CU: a hardware queue of its own); experiment
   P2P_RCCL_REGISTER=1|2  ncclCommRegister every buffer (2: + ncclMemAlloc)
   P2P_RCCL_BLOCKING=1    blocking ncclCommInitRank instead of the polled non-blocking init
   P2P_RCCL_DISTINCT_HOSTS=1  one NCCL_HOSTID per rank: RCCL ranks may share a GPU (tests,
