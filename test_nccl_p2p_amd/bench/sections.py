@@ -5,6 +5,7 @@ xGMI pair sweep."""
 
 from __future__ import annotations
 
+import gc
 import json
 import os
 import shutil
@@ -352,8 +353,15 @@ class SectionsMixin:
         value, batch = self.h.value, self.h.batch
 
         def compare(transport):
-            # Ranks sharing a GPU split its free memory (the headline's driver
-            # still holds its slots).
+            # Ranks sharing a GPU split its free memory.  Every rank first
+            # releases what the sections before it held (sessions, drivers and
+            # their buffers), and only then does any rank read the free memory:
+            # read while a peer on the same GPU was still freeing, it came out
+            # short and halved the comparison's receive generations (8 ranks
+            # on one GPU: verify_coverage 0.5).
+            gc.collect()
+            self.gpu_sync()
+            self.barrier()
             budget = self.recv_budget(self.h.provenance)
             if args.isolate:
                 return self.isolated(transport, budget)
