@@ -79,8 +79,12 @@ def set_hw_queues(argv) -> None:
         elif a.startswith("--hw-queues="):
             q = a.split("=", 1)[1]
     os.environ["P2P_HW_QUEUES_ENV"] = os.environ.get("GPU_MAX_HW_QUEUES", "")
-    if int(q) > 0:
-        os.environ["GPU_MAX_HW_QUEUES"] = str(int(q))
+    try:
+        qn = int(q)
+    except ValueError:  # argparse reports a bad --hw-queues; a bad P2P_BENCH_HW_QUEUES falls back
+        qn = 8
+    if qn > 0:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(qn)
 
 
 if __name__ == "__main__":  # (not when tests import this module)
