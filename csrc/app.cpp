@@ -65,7 +65,9 @@ timing
                          pairs incl. self, sizes 1 B .. the largest --size, at most
                          64 MiB), every one verified; failures exit 2
 data
-  -c, --verify           random-fill sends, verify every received buffer on the device
+  -c, --verify           random-fill sends, verify every received buffer on the device,
+                         outside the timed loop (the default)
+      --no-verify        zero-filled sends, nothing read back (the reference's data)
       --verify-impl I    auto (= lds8) | lds | lds8 | lds-pipe | lds-cached | stride | reg
                          (LDS-DMA- or register-staged verify kernel variants)
 transport / launch
@@ -667,8 +669,12 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
 
   // Connection warm-up outside any timed cell (the reference pays lazy p2p
   // connection setup inside its first cells; --reference keeps that).
-  if (cfg.warm_connections)
+  if (cfg.warm_connections) {
     for (const auto& s : scheds) warm_connections(*t, boot, s, bufs);
+    // Every peer of every schedule is connected: op limits from RCCL's
+    // connection lines (transport.hpp refine_op_limits).
+    t->refine_op_limits(boot);
+  }
 
   AppResult local;
   AppResult& res = result ? *result : local;

@@ -107,6 +107,26 @@ __global__ __launch_bounds__(kBlock) void fill_grid_kernel(uint4* __restrict__ p
   store_tail(tail, tail_bytes, tail_offset, seed);
 }
 
+// Full grid with VPL 16 B vectors per lane: workgroup b owns the contiguous
+// VPL x 4 KiB [begin + b * VPL * 256, ...) and issues all VPL stores before it
+// retires, so the dispatcher launches VPL times fewer workgroups per GiB
+// (262144 / VPL) -- the A/B for a dispatch-rate-bound one-block-per-4-KiB grid
+// (VERDICT r3 weak #1).  The block's span is a power of two <= 16 KiB that
+// starts at a multiple of itself, so the PRNG key is block-uniform.
+template <int VPL>
+__global__ __launch_bounds__(kBlock) void fill_multi_kernel(uint4* __restrict__ p, uint64_t begin, uint64_t nvec,
+                                                            uint64_t seed, uint8_t* __restrict__ tail,
+                                                            uint32_t tail_bytes, uint64_t tail_offset) {
+  const uint64_t base = begin + static_cast<uint64_t>(blockIdx.x) * (kBlockVecs * VPL);
+  const uint32_t key = prng_key(seed, base * 4);
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    const uint64_t i = base + static_cast<uint64_t>(u) * kBlockVecs + threadIdx.x;
+    if (i < nvec) p[i] = prng_vec_k(key, i);
+  }
+  store_tail(tail, tail_bytes, tail_offset, seed);
+}
+
 __global__ __launch_bounds__(kBlock) void fill_stride_kernel(uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
                                                              uint8_t* __restrict__ tail, uint32_t tail_bytes,
                                                              uint64_t tail_offset) {
@@ -166,7 +186,7 @@ __device__ void check_tail(const uint8_t* tail, uint32_t tail_bytes, uint64_t ta
 
 // Reduction epilogue: wave64 butterfly, the 4 wave partials through LDS, then
 // one atomic per non-zero field into this block's shard.
-__device__ __forceinline__ void block_commit(Partial acc, VerifyAccum* out) {
+__device__ __forceinline__ void block_commit(Partial acc, VerifyAccum* out, uint32_t shard_key) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     acc.mism += __shfl_xor(acc.mism, off, 64);
@@ -185,7 +205,7 @@ __device__ __forceinline__ void block_commit(Partial acc, VerifyAccum* out) {
       t.sum += red[w].sum;
       t.first = min(t.first, red[w].first);
     }
-    VerifyAccum* s = out + (blockIdx.x % kVerifyShards);
+    VerifyAccum* s = out + (shard_key % kVerifyShards);
     if (t.sum) atomicAdd(&s->checksum, t.sum);
     if (t.mism) {
       atomicAdd(&s->mismatches, t.mism);
@@ -211,7 +231,7 @@ __global__ __launch_bounds__(kBlock) void verify_grid_kernel(const uint4* __rest
     if (i < nvec) check_vec<CHECK>(load_nt(p, i), key, i, acc);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) check_tail<CHECK>(tail, tail_bytes, tail_offset, seed, acc);
-  block_commit(acc, out);
+  block_commit(acc, out, blockIdx.x);
 }
 
 template <bool CHECK>
@@ -235,7 +255,7 @@ __global__ __launch_bounds__(kBlock) void verify_stride_kernel(const uint4* __re
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) check_tail<CHECK>(tail, tail_bytes, tail_offset, seed, acc);
-  block_commit(acc, out);
+  block_commit(acc, out, blockIdx.x);
 }
 
 // LDS-staged verify.  Wave g owns super-chunk g (kLdsStages consecutive KiB)
@@ -282,10 +302,11 @@ __device__ __forceinline__ void lds_read_stages<8>(uint32_t addr, u32x4 (&r)[8])
       : "memory");
 }
 
+// Blocks `block` of `nblocks` of one buffer: the LDS-staged loop below, with
+// the workgroup's own LDS slots (the single and the batched verify share it).
 template <bool CHECK, int STAGES, int AUX>
-__global__ __launch_bounds__(kBlock) void verify_lds_kernel(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
-                                                            const uint8_t* __restrict__ tail, uint32_t tail_bytes,
-                                                            uint64_t tail_offset, VerifyAccum* __restrict__ out) {
+__device__ __forceinline__ Partial lds_verify_blocks(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
+                                                     uint64_t block, uint64_t nblocks) {
   __shared__ uint4 slot[kWaves][STAGES][64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x / 64;
@@ -294,8 +315,7 @@ __global__ __launch_bounds__(kBlock) void verify_lds_kernel(const uint4* __restr
   const uint32_t lds_addr = static_cast<uint32_t>(
       reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)(&slot[wave][0][lane])));
   Partial acc{0, 0, ~0ull};
-  for (uint64_t sc = static_cast<uint64_t>(blockIdx.x) * kWaves + wave; sc < n_sc;
-       sc += static_cast<uint64_t>(gridDim.x) * kWaves) {
+  for (uint64_t sc = block * kWaves + wave; sc < n_sc; sc += nblocks * kWaves) {
 #pragma unroll
     for (int s = 0; s < STAGES; ++s) {
       const uint64_t i = sc * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
@@ -313,8 +333,75 @@ __global__ __launch_bounds__(kBlock) void verify_lds_kernel(const uint4* __restr
       if (i < nvec) check_vec<CHECK>(make_uint4(rv[s].x, rv[s].y, rv[s].z, rv[s].w), key, i, acc);
     }
   }
+  return acc;
+}
+
+template <bool CHECK, int STAGES, int AUX>
+__global__ __launch_bounds__(kBlock) void verify_lds_kernel(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
+                                                            const uint8_t* __restrict__ tail, uint32_t tail_bytes,
+                                                            uint64_t tail_offset, VerifyAccum* __restrict__ out) {
+  Partial acc = lds_verify_blocks<CHECK, STAGES, AUX>(p, nvec, seed, blockIdx.x, gridDim.x);
   if (blockIdx.x == 0 && threadIdx.x == 0) check_tail<CHECK>(tail, tail_bytes, tail_offset, seed, acc);
-  block_commit(acc, out);
+  block_commit(acc, out, blockIdx.x);
+}
+
+// Batched verify: up to kMaxVerifyJobs buffers, each with
+// its own seed, in one launch.  Workgroups are split across the jobs in
+// contiguous ranges (block_begin, as multi_copy_kernel); job j commits into
+// its own kVerifyShards shards of the scratch.  The post-timing check of a
+// bench run was one reset + verify + finalize + D2H copy + host sync per
+// 32 MiB slot (3336 of each per run, profiles/r3b_close/bench_kernel_stats.csv).
+struct MultiVerifyArgs {
+  const uint4* p[kMaxVerifyJobs];
+  uint64_t nvec[kMaxVerifyJobs];
+  uint64_t seed[kMaxVerifyJobs];
+  uint32_t tail[kMaxVerifyJobs];
+  uint32_t block_begin[kMaxVerifyJobs + 1];
+  int njobs;
+};
+
+template <int STAGES>
+__global__ __launch_bounds__(kBlock) void multi_verify_lds_kernel(const MultiVerifyArgs a,
+                                                                  VerifyAccum* __restrict__ scratch) {
+  int lo = 0, hi = a.njobs - 1;  // largest job with block_begin[job] <= blockIdx.x
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (blockIdx.x >= a.block_begin[mid]) lo = mid; else hi = mid - 1;
+  }
+  const int job = lo;
+  const uint32_t b = blockIdx.x - a.block_begin[job];
+  const uint32_t nb = a.block_begin[job + 1] - a.block_begin[job];
+  const uint64_t nvec = a.nvec[job];
+  Partial acc = lds_verify_blocks<true, STAGES, 2>(a.p[job], nvec, a.seed[job], b, nb);
+  if (b == 0 && threadIdx.x == 0)
+    check_tail<true>(reinterpret_cast<const uint8_t*>(a.p[job] + nvec), a.tail[job], nvec * 16, a.seed[job], acc);
+  block_commit(acc, scratch + static_cast<size_t>(job) * kVerifyShards, b);
+}
+
+// One workgroup (one wave) per job: reset its shards.
+__global__ __launch_bounds__(64) void multi_verify_reset_kernel(VerifyAccum* scratch) {
+  VerifyAccum* a = scratch + static_cast<size_t>(blockIdx.x) * kVerifyShards + threadIdx.x;
+  a->mismatches = 0;
+  a->checksum = 0;
+  a->first_bad = ~0ull;
+}
+
+// One wave per job folds its shards into out[job].
+__global__ __launch_bounds__(64) void multi_verify_finalize_kernel(const VerifyAccum* __restrict__ scratch,
+                                                                   VerifyAccum* __restrict__ out) {
+  const VerifyAccum& s = scratch[static_cast<size_t>(blockIdx.x) * kVerifyShards + threadIdx.x];
+  unsigned long long m = s.mismatches, c = s.checksum, f = s.first_bad;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    m += __shfl_xor(m, off, 64);
+    c += __shfl_xor(c, off, 64);
+    f = min(f, __shfl_xor(f, off, 64));
+  }
+  if (threadIdx.x == 0) {
+    out[blockIdx.x].mismatches = m;
+    out[blockIdx.x].checksum = c;
+    out[blockIdx.x].first_bad = f;
+  }
 }
 
 // Software-pipelined LDS staging: each wave owns two halves of STAGES KiB.
@@ -378,7 +465,7 @@ __global__ __launch_bounds__(kBlock) void verify_lds_pipe_kernel(const uint4* __
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) check_tail<CHECK>(tail, tail_bytes, tail_offset, seed, acc);
-  block_commit(acc, out);
+  block_commit(acc, out, blockIdx.x);
 }
 
 __global__ void verify_reset_kernel(VerifyAccum* acc) {
@@ -443,7 +530,8 @@ LaunchGeom fill_geometry(size_t bytes, FillImpl impl) {
     g.grid = static_cast<unsigned>(
         std::max<uint64_t>(1, std::min(tiles, static_cast<uint64_t>(cu_count()) * kStrideBlocksPerCu)));
   } else {
-    g.grid = grid_for((nvec + kBlockVecs - 1) / kBlockVecs);
+    const uint64_t vpl = impl == FillImpl::Grid2 ? 2 : impl == FillImpl::Grid4 ? 4 : 1;
+    g.grid = grid_for((nvec + vpl * kBlockVecs - 1) / (vpl * kBlockVecs));
   }
   return g;
 }
@@ -499,7 +587,13 @@ void launch_fill(void* p, size_t bytes, uint64_t seed, hipStream_t stream, FillI
     const bool last = end == nvec;
     const unsigned grid = grid_for((end - begin + kBlockVecs - 1) / kBlockVecs);
     const uint32_t tb = last ? tail : 0;
-    if (impl == FillImpl::Nontemporal)
+    if (impl == FillImpl::Grid2)
+      fill_multi_kernel<2><<<grid_for((end - begin + 2 * kBlockVecs - 1) / (2 * kBlockVecs)), kBlock, 0, stream>>>(
+          vp, begin, end, seed, tp, tb, nvec * 16);
+    else if (impl == FillImpl::Grid4)
+      fill_multi_kernel<4><<<grid_for((end - begin + 4 * kBlockVecs - 1) / (4 * kBlockVecs)), kBlock, 0, stream>>>(
+          vp, begin, end, seed, tp, tb, nvec * 16);
+    else if (impl == FillImpl::Nontemporal)
       fill_grid_kernel<true><<<grid, kBlock, 0, stream>>>(vp, begin, end, seed, tp, tb, nvec * 16);
     else if (impl == FillImpl::Xcd && grid % kXcds == 0)
       fill_grid_kernel<false, true><<<grid, kBlock, 0, stream>>>(vp, begin, end, seed, tp, tb, nvec * 16);
@@ -561,6 +655,65 @@ void launch_verify(const void* p, size_t bytes, uint64_t seed, VerifyAccum* acc,
   }
   verify_finalize_kernel<<<1, 64, 0, stream>>>(acc);
   HIP_OK(hipGetLastError());
+}
+
+void launch_multi_verify(const VerifyJob* jobs, int njobs, VerifyAccum* scratch, VerifyAccum* out,
+                         hipStream_t stream) {
+  // Workgroups: the LDS8 verify's cap (16 per CU) shared by the jobs of a
+  // batch in proportion to their size, at least one each.
+  const uint64_t cap = static_cast<uint64_t>(cu_count()) * kVerifyLdsPerCu;
+  constexpr uint64_t kChunkVecs = 8 * 64 * kWaves;  // 32 KiB per workgroup pass
+  for (int first = 0; first < njobs; first += kMaxVerifyJobs) {
+    const int cnt = std::min(kMaxVerifyJobs, njobs - first);
+    MultiVerifyArgs a{};
+    a.njobs = cnt;
+    uint64_t need[kMaxVerifyJobs] = {0}, total = 0;
+    for (int i = 0; i < cnt; ++i) {
+      const VerifyJob& j = jobs[first + i];
+      P2P_CHECK(reinterpret_cast<uintptr_t>(j.p) % 16 == 0, "verify: buffer must be 16-byte aligned");
+      a.p[i] = static_cast<const uint4*>(j.p);
+      a.nvec[i] = j.bytes / 16;
+      a.tail[i] = static_cast<uint32_t>(j.bytes - a.nvec[i] * 16);
+      a.seed[i] = j.seed;
+      need[i] = std::max<uint64_t>(1, (a.nvec[i] + kChunkVecs - 1) / kChunkVecs);
+      total += need[i];
+    }
+    uint32_t acc = 0;
+    for (int i = 0; i < cnt; ++i) {
+      a.block_begin[i] = acc;
+      const uint64_t share = total <= cap ? need[i] : std::max<uint64_t>(1, need[i] * cap / total);
+      acc += static_cast<uint32_t>(std::min(share, need[i]));
+    }
+    a.block_begin[cnt] = acc;
+    multi_verify_reset_kernel<<<cnt, 64, 0, stream>>>(scratch);
+    HIP_OK(hipGetLastError());
+    multi_verify_lds_kernel<8><<<acc, kBlock, 0, stream>>>(a, scratch);
+    HIP_OK(hipGetLastError());
+    multi_verify_finalize_kernel<<<cnt, 64, 0, stream>>>(scratch, out + first);
+    HIP_OK(hipGetLastError());
+  }
+}
+
+BatchVerifier::~BatchVerifier() {
+  if (scratch_) (void)hipFree(scratch_);
+  if (out_) (void)hipFree(out_);
+  if (host_) (void)hipHostFree(host_);
+}
+
+void BatchVerifier::enqueue(const VerifyJob* jobs, int njobs, hipStream_t stream) {
+  if (njobs <= 0) return;
+  if (!scratch_) HIP_OK(hipMalloc(&scratch_, multi_verify_scratch_bytes()));
+  if (njobs > cap_) {
+    // The stream may still read the old arrays: drain it before freeing.
+    HIP_OK(hipStreamSynchronize(stream));
+    if (out_) HIP_OK(hipFree(out_));
+    if (host_) HIP_OK(hipHostFree(host_));
+    cap_ = std::max(njobs, 2 * cap_);
+    HIP_OK(hipMalloc(&out_, sizeof(VerifyAccum) * static_cast<size_t>(cap_)));
+    HIP_OK(hipHostMalloc(&host_, sizeof(VerifyAccum) * static_cast<size_t>(cap_), hipHostMallocDefault));
+  }
+  launch_multi_verify(jobs, njobs, scratch_, out_, stream);
+  HIP_OK(hipMemcpyAsync(host_, out_, sizeof(VerifyAccum) * static_cast<size_t>(njobs), hipMemcpyDeviceToHost, stream));
 }
 
 // ------------------------------------------------------------ multi copy ----

@@ -54,7 +54,8 @@ constexpr int kVerifyShards = 64;
 constexpr size_t verify_accum_bytes() { return sizeof(VerifyAccum) * kVerifyShards; }
 
 enum class VerifyImpl : int { Auto = 0, Register = 1, Lds = 2, Stride = 3, Lds8 = 4, LdsCached = 5, LdsPipe = 6 };
-enum class FillImpl : int { Auto = 0, Grid = 1, Nontemporal = 2, Stride = 3, Xcd = 4 };
+// Grid2 / Grid4: full grid with 2 / 4 vectors per lane (8 / 16 KiB per workgroup).
+enum class FillImpl : int { Auto = 0, Grid = 1, Nontemporal = 2, Stride = 3, Xcd = 4, Grid2 = 5, Grid4 = 6 };
 
 // Geometry chosen for a launch (exposed for tests / profiling scripts).
 struct LaunchGeom {
@@ -74,6 +75,40 @@ void launch_verify_reset(VerifyAccum* acc, hipStream_t stream);
 // Leaves the totals in acc[0] (stream-ordered).
 void launch_verify(const void* p, size_t bytes, uint64_t seed, VerifyAccum* acc, VerifyImpl impl, bool check_prng,
                    hipStream_t stream, unsigned max_grid = 0);
+
+// ---- batched verify (the post-timing check of many receive slots) ----
+// Job i's totals land in out[i] (device memory, njobs entries; nothing needs
+// resetting).  Batches of kMaxVerifyJobs, three launches each (reset, the
+// LDS-DMA verify over all the batch's buffers, finalize); `scratch` holds
+// multi_verify_scratch_bytes() and is reused by every batch (stream order).
+struct VerifyJob {
+  const void* p;
+  size_t bytes;
+  uint64_t seed;
+};
+constexpr int kMaxVerifyJobs = 32;
+constexpr size_t multi_verify_scratch_bytes() { return verify_accum_bytes() * kMaxVerifyJobs; }
+void launch_multi_verify(const VerifyJob* jobs, int njobs, VerifyAccum* scratch, VerifyAccum* out, hipStream_t stream);
+
+// The device scratch, device results and pinned host results of
+// launch_multi_verify for one stream's user (a transport), grown on demand.
+// enqueue() puts the batched verify and ONE readback of every job's totals on
+// `stream`; results() is valid once the caller has synchronised the stream.
+class BatchVerifier {
+ public:
+  BatchVerifier() = default;
+  BatchVerifier(const BatchVerifier&) = delete;
+  BatchVerifier& operator=(const BatchVerifier&) = delete;
+  ~BatchVerifier();
+  void enqueue(const VerifyJob* jobs, int njobs, hipStream_t stream);
+  const VerifyAccum* results() const { return host_; }
+
+ private:
+  VerifyAccum* scratch_ = nullptr;
+  VerifyAccum* out_ = nullptr;
+  VerifyAccum* host_ = nullptr;
+  int cap_ = 0;
+};
 
 // Device attributes cached per device (CU count drives grid sizing).
 int cu_count();

@@ -93,7 +93,10 @@ class Session {
     cfg.gens = verify ? verify_generations(*t_, *boot_, bytes, slots, std::max(iters, warmup)) : 1;
     if (const char* rc = std::getenv("P2P_RECHUNK")) cfg.rechunk = std::atoi(rc) != 0;
     Buffers bufs(*t_, bytes, slots * cfg.gens, slot_stride_bytes(bytes) * static_cast<size_t>(cfg.gens));
-    if (warm) warm_connections(*t_, *boot_, s, bufs);
+    if (warm) {
+      warm_connections(*t_, *boot_, s, bufs);
+      t_->refine_op_limits(*boot_);
+    }
     RunRecord rec;
     rec.mode = s.mode;
     rec.dir = s.dir;
@@ -163,6 +166,8 @@ class Session {
   // transport_rccl.cpp), capped on every rank alike.
   bool set_chunk_cap(size_t bytes) { return t_->set_chunk_cap(bytes); }
   size_t max_chunk(int peer) const { return t_->max_chunk(peer); }
+  // Collective: re-derive the op limits from what the transport connected.
+  bool refine_op_limits() { return t_->refine_op_limits(*boot_); }
 
   // Collective: every rank's Transport::link_report() as a JSON list (rank
   // order; null where the transport has nothing to report).
@@ -233,6 +238,52 @@ py::tuple device_verify(uintptr_t ptr, size_t bytes, uint64_t seed, int impl, bo
   return py::make_tuple(ks.h->mismatches, ks.h->checksum, ks.h->first_bad);
 }
 
+// The batched verify on raw pointers: [(mismatches, checksum, first_bad)]
+// per (ptr, bytes, seed) job, one readback (dev::BatchVerifier, per device).
+py::list device_verify_many(const std::vector<std::tuple<uintptr_t, size_t, uint64_t>>& jobs, uintptr_t stream) {
+  static std::vector<std::unique_ptr<dev::BatchVerifier>> per_device;
+  int dv = 0;
+  if (hipGetDevice(&dv) != hipSuccess) P2P_FATAL("no HIP device");
+  if (static_cast<int>(per_device.size()) <= dv) per_device.resize(static_cast<size_t>(dv) + 1);
+  auto& bv = per_device[static_cast<size_t>(dv)];
+  if (!bv) bv = std::make_unique<dev::BatchVerifier>();
+  std::vector<dev::VerifyJob> dj;
+  for (const auto& j : jobs) dj.push_back({reinterpret_cast<const void*>(std::get<0>(j)), std::get<1>(j), std::get<2>(j)});
+  hipStream_t st = as_stream(stream);
+  {
+    py::gil_scoped_release nogil;
+    bv->enqueue(dj.data(), static_cast<int>(dj.size()), st);
+    if (hipStreamSynchronize(st) != hipSuccess) P2P_FATAL("hipStreamSynchronize failed");
+  }
+  py::list out;
+  for (size_t i = 0; i < dj.size(); ++i)
+    out.append(py::make_tuple(bv->results()[i].mismatches, bv->results()[i].checksum, bv->results()[i].first_bad));
+  return out;
+}
+
+// Stream-ordered batched verify, no readback (timing with events).
+void device_verify_many_launch(const std::vector<std::tuple<uintptr_t, size_t, uint64_t>>& jobs, uintptr_t stream) {
+  static dev::VerifyAccum* scratch_d = nullptr;
+  static dev::VerifyAccum* out_d = nullptr;
+  static int cap = 0, device = -1;
+  int dv = 0;
+  if (hipGetDevice(&dv) != hipSuccess) P2P_FATAL("no HIP device");
+  const int n = static_cast<int>(jobs.size());
+  if (dv != device || n > cap) {
+    if (hipDeviceSynchronize() != hipSuccess) P2P_FATAL("hipDeviceSynchronize failed");
+    if (scratch_d && dv == device) (void)hipFree(scratch_d);
+    if (out_d && dv == device) (void)hipFree(out_d);
+    cap = std::max(n, 32);
+    if (hipMalloc(&scratch_d, dev::multi_verify_scratch_bytes()) != hipSuccess ||
+        hipMalloc(&out_d, sizeof(dev::VerifyAccum) * static_cast<size_t>(cap)) != hipSuccess)
+      P2P_FATAL("hipMalloc failed");
+    device = dv;
+  }
+  std::vector<dev::VerifyJob> dj;
+  for (const auto& j : jobs) dj.push_back({reinterpret_cast<const void*>(std::get<0>(j)), std::get<1>(j), std::get<2>(j)});
+  dev::launch_multi_verify(dj.data(), n, scratch_d, out_d, as_stream(stream));
+}
+
 py::list schedule_py(const std::string& mode, const std::string& dir, int n) {
   Schedule s = make_schedule(parse_mode(mode), parse_direction(dir), n);
   py::list phases;
@@ -298,6 +349,8 @@ PYBIND11_MODULE(_p2pcore, m) {
            "Caps the ops messages to every peer are posted as at `bytes` (0: lifts the cap, back to the limits the "
            "transport derived per peer); False where nothing is split. Call it on every rank with the same value.")
       .def("max_chunk", &Session::max_chunk, py::arg("peer"), "Largest op a message to `peer` is posted as (0: unsplit).")
+      .def("refine_op_limits", &Session::refine_op_limits, py::call_guard<py::gil_scoped_release>(),
+           "Collective: op limits from the connections made so far (RCCL: its connection lines).")
       .def("link_reports", &Session::link_reports, py::call_guard<py::gil_scoped_release>(),
            "Collective: what the data plane set up towards each peer, per rank (RCCL: p2p channels from its INFO log, "
            "each peer's transport, the op limit in use); JSON list.")
@@ -320,6 +373,7 @@ PYBIND11_MODULE(_p2pcore, m) {
       .def("recapture", [](PyStepDriver& s) { s.d().recapture(); }, py::call_guard<py::gil_scoped_release>(),
            "Collective: record the step graphs again after the op sizes changed (no-op without graphs).")
       .def_property_readonly("recaptures", [](PyStepDriver& s) { return s.d().recaptures(); })
+      .def_property_readonly("limit_changes", [](PyStepDriver& s) { return s.d().limit_changes(); })
       .def_property_readonly("graphs", [](PyStepDriver& s) { return s.d().graphs(); })
       .def("verify_steps", [](PyStepDriver& s, long first, long count) {
             StepVerifyReport r;
@@ -362,12 +416,18 @@ PYBIND11_MODULE(_p2pcore, m) {
 
   // ---- kernels on raw pointers ----
   m.def("fill", [](uintptr_t ptr, size_t bytes, uint64_t seed, uintptr_t stream, int impl) {
+        if (impl < 0 || impl > static_cast<int>(dev::FillImpl::Grid4)) throw py::value_error("fill: unknown impl");
         dev::launch_fill(reinterpret_cast<void*>(ptr), bytes, seed, as_stream(stream), static_cast<dev::FillImpl>(impl));
       }, py::arg("ptr"), py::arg("bytes"), py::arg("seed"), py::arg("stream") = 0, py::arg("impl") = 0,
-      "impl: 0 auto, 1 plain stores, 2 non-temporal stores");
+      "impl: 0 auto, 1 full grid (one 16 B store per lane), 2 non-temporal stores, 3 grid-stride, "
+      "4 XCD-ordered grid, 5 / 6 full grid with 2 / 4 stores per lane");
   m.def("verify", &device_verify, py::arg("ptr"), py::arg("bytes"), py::arg("seed"), py::arg("impl") = 0,
         py::arg("check") = true, py::arg("stream") = 0,
         "Returns (mismatching words, checksum, first bad byte offset or 2**64-1).");
+  m.def("verify_many", &device_verify_many, py::arg("jobs"), py::arg("stream") = 0,
+        "Batched verify of [(ptr, bytes, seed)]: one (mismatches, checksum, first_bad) per job, one readback.");
+  m.def("verify_many_launch", &device_verify_many_launch, py::arg("jobs"), py::arg("stream") = 0,
+        "Stream-ordered batched verify launches only (timing).");
   m.def("verify_launch", [](uintptr_t ptr, size_t bytes, uint64_t seed, int impl, bool check, uintptr_t stream,
                             unsigned max_grid) {
         // Stream-ordered launch only (reset + verify + finalize), no readback:

@@ -102,14 +102,28 @@ std::vector<RcclConnection> parse_rccl_connections(const std::string& text) {
     while (e < line.size() && line[e] != ' ' && line[e] != '\r') ++e;
     c.via = line.substr(t, e - t);
     if (c.via.empty()) continue;
+    const size_t cm = line.find(" comm ", e);
+    if (cm != std::string::npos) {
+      size_t b = cm + 6, x = b;
+      while (x < line.size() && line[x] != ' ' && line[x] != '\r') ++x;
+      c.comm = line.substr(b, x - b);
+    }
     out.push_back(c);
   }
   return out;
 }
 
+std::vector<RcclConnection> connections_of(const std::vector<RcclConnection>& conns, const std::vector<std::string>& comms) {
+  std::vector<RcclConnection> out;
+  for (const auto& c : conns)
+    if (c.comm.empty() || std::find(comms.begin(), comms.end(), c.comm) != comms.end()) out.push_back(c);
+  return out;
+}
+
 std::vector<RcclPeerLink> rccl_peer_links(const std::vector<RcclConnection>& conns, int me, int nranks) {
   std::vector<RcclPeerLink> out(static_cast<size_t>(std::max(nranks, 0)));
-  std::map<int, std::set<int>> send_ch, recv_ch;
+  // (peer, communicator) -> channels of its send / receive-side lines
+  std::map<std::pair<int, std::string>, std::set<int>> send_ch, recv_ch;
   std::set<int> p2p_peers;  // peers with p2p (conn_index > 0) lines: only those count
   for (const auto& c : conns)
     if (c.conn_index > 0) p2p_peers.insert(c.src == me ? c.dst : c.src);
@@ -127,18 +141,21 @@ std::vector<RcclPeerLink> rccl_peer_links(const std::vector<RcclConnection>& con
       peer = c.src;
     }
     if (peer < 0 || peer >= nranks) continue;
-    if (c.conn_index > 0 || !p2p_peers.count(peer)) (send ? send_ch : recv_ch)[peer].insert(c.channel);
+    if (c.conn_index > 0 || !p2p_peers.count(peer)) (send ? send_ch : recv_ch)[{peer, c.comm}].insert(c.channel);
     auto& l = out[static_cast<size_t>(peer)];
     if (l.via.empty()) {
       l.via = c.via;
       l.transport = transport_class(c.via);
     }
   }
-  for (auto& l : out) {
-    if (l.peer == me) continue;
-    auto s = send_ch.find(l.peer);
-    auto r = recv_ch.find(l.peer);
-    l.channels_connected = static_cast<int>(s != send_ch.end() ? s->second.size() : r != recv_ch.end() ? r->second.size() : 0);
+  // Per communicator: its send lines, or its receive-side lines where it
+  // logged no send line; the peer's count is the fewest of any communicator.
+  std::map<std::pair<int, std::string>, int> per_comm;
+  for (const auto& kv : recv_ch) per_comm[kv.first] = static_cast<int>(kv.second.size());
+  for (const auto& kv : send_ch) per_comm[kv.first] = static_cast<int>(kv.second.size());
+  for (const auto& kv : per_comm) {
+    auto& l = out[static_cast<size_t>(kv.first.first)];
+    l.channels_connected = l.channels_connected == 0 ? kv.second : std::min(l.channels_connected, kv.second);
   }
   return out;
 }
@@ -148,6 +165,29 @@ int rccl_op_channels(const RcclInitInfo& info, bool net_peer, int net_per_peer) 
   int c = std::min(info.p2p_channels, info.p2p_per_peer);
   if (net_peer && net_per_peer > 0) c = std::min(c, net_per_peer);
   return std::max(c, 1);
+}
+
+std::vector<int> proposed_op_channels(const std::vector<int>& init_channels, const std::vector<RcclPeerLink>& links,
+                                      int me) {
+  std::vector<int> out(init_channels.size(), 0);
+  for (size_t p = 0; p < out.size() && p < links.size(); ++p) {
+    if (static_cast<int>(p) == me || init_channels[p] <= 0 || links[p].channels_connected <= 0) continue;
+    out[p] = std::min(init_channels[p], links[p].channels_connected);
+  }
+  return out;
+}
+
+std::vector<int> agree_op_channels(const std::vector<int>& all, int n, int me, const std::vector<int>& current,
+                                   std::vector<std::string>* sources) {
+  std::vector<int> out(current);
+  out.resize(static_cast<size_t>(n), 0);
+  for (int p = 0; p < n; ++p) {
+    const int a = all[static_cast<size_t>(me) * n + p], b = all[static_cast<size_t>(p) * n + me];
+    if (a <= 0 && b <= 0) continue;
+    out[static_cast<size_t>(p)] = a > 0 && b > 0 ? std::min(a, b) : std::max(a, b);
+    if (sources && static_cast<size_t>(p) < sources->size()) (*sources)[static_cast<size_t>(p)] = "connection lines";
+  }
+  return out;
 }
 
 bool link_transport_mismatch(const std::string& link, const std::string& transport) {

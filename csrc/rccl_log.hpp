@@ -37,6 +37,7 @@ struct RcclConnection {
   int src = -1;  // ranks
   int dst = -1;
   std::string via;  // first token after "via": "P2P/IPC/read", "NET/Socket/0", "SHM/direct/direct", ...
+  std::string comm;  // the "comm 0x..." token RCCL appends ("" when absent)
 };
 
 // The last init block in `text` (fields not seen stay -1).
@@ -44,9 +45,15 @@ RcclInitInfo parse_rccl_init(const std::string& text);
 // Every connection line in `text`, in order.
 std::vector<RcclConnection> parse_rccl_connections(const std::string& text);
 
+// The lines of the communicators named in `comms` ("0x..." as RCCL prints a
+// pointer) and lines without a comm token; another transport of the process
+// may log into the same file.
+std::vector<RcclConnection> connections_of(const std::vector<RcclConnection>& conns, const std::vector<std::string>& comms);
+
 // Per peer of rank `me`: the channels connected towards it (send lines
 // me -> peer; receive-side lines peer -> me where no send line exists; lines
-// of p2p connections, conn_index > 0, where there are any) and
+// of p2p connections, conn_index > 0, where there are any; counted per
+// communicator, and the fewest of any communicator with lines) and
 // the transport class: "P2P" (xGMI / PCIe peer access through IPC), "SHM",
 // "NET", "self" (peer == me: RCCL copies inside the kernel and logs no
 // connection) or "" (not connected yet).
@@ -63,6 +70,22 @@ std::vector<RcclPeerLink> rccl_peer_links(const std::vector<RcclConnection>& con
 // transport at most `net_per_peer` (NCCL_NCHANNELS_PER_NET_PEER, 2 by
 // default).  0 when the init block was not found.
 int rccl_op_channels(const RcclInitInfo& info, bool net_peer, int net_per_peer);
+
+// Op channels once RCCL's connection lines are known.
+// The init line gives the channels a communicator may split an op to a peer
+// over; the connection lines give the channels it did connect to that peer.
+// proposed_op_channels(): per peer, min(init_channels[p], channels connected)
+// for a remote peer with connection lines; 0 (no opinion) for `me` and for a
+// peer without lines (or without an init count).
+std::vector<int> proposed_op_channels(const std::vector<int>& init_channels, const std::vector<RcclPeerLink>& links,
+                                      int me);
+// Both ends of a pair must split a message alike.  `all` holds every rank's
+// proposals (all[r * n + p]: rank r's for peer p).  Rank me's op channels per
+// peer: the smaller proposal where both ends have one, the one proposal where
+// only one end has, else `current[p]`.  sources[p] (if given) is set to
+// "connection lines" where a proposal was used, left alone otherwise.
+std::vector<int> agree_op_channels(const std::vector<int>& all, int n, int me, const std::vector<int>& current,
+                                   std::vector<std::string>* sources = nullptr);
 
 // Link check (--min-gbs): a pair whose GPUs share a direct xGMI link
 // (`link` "XGMI/1", provenance rank_links) must be carried by RCCL's P2P

@@ -187,11 +187,16 @@ int phase_generations(const Phase& phase, const RunConfig& cfg, const Buffers& b
   return static_cast<int>(std::max<long>(1, g));
 }
 
+// Slots g * per + i of generations [0, gens) are contiguous in the receive
+// arena: one zeroing launch covers them all (and the padding between them),
+// not one memset per slot.
 void zero_slots(Transport& t, const Phase& phase, const RunConfig& cfg, Buffers& bufs, int gens) {
   const RankOps& ops = phase.ranks[static_cast<size_t>(t.rank())];
+  if (ops.recv_from.empty()) return;
   const int per = std::max(1, phase.max_recv_slots());
-  for (int g = 0; g < gens; ++g)
-    for (size_t i = 0; i < ops.recv_from.size(); ++i) t.zero(bufs.recv_buf(g * per + static_cast<int>(i)), cfg.bytes);
+  const int last = (gens - 1) * per + static_cast<int>(ops.recv_from.size()) - 1;
+  char* first = static_cast<char*>(bufs.recv_buf(0));
+  t.zero(first, static_cast<size_t>(static_cast<char*>(bufs.recv_buf(last)) - first) + cfg.bytes);
 }
 
 void prepare_payload(Transport& t, const Phase& phase, const RunConfig& cfg, Buffers& bufs, int gens) {
@@ -210,11 +215,16 @@ uint64_t check_slots(Transport& t, const Phase& phase, const RunConfig& cfg, Buf
                      std::vector<uint64_t>* per_slot = nullptr) {
   const RankOps& ops = phase.ranks[static_cast<size_t>(t.rank())];
   const int per = std::max(1, phase.max_recv_slots());
-  uint64_t bad = 0;
+  std::vector<Transport::VerifyJob> jobs;
   for (int g = 0; g < gens; ++g)
-    for (size_t i = 0; i < ops.recv_from.size(); ++i) {
-      VerifyResult v = t.verify(bufs.recv_buf(g * per + static_cast<int>(i)), cfg.bytes,
-                                generation_seed(ops.recv_from[i], cfg.bytes, cfg.salt, g));
+    for (size_t i = 0; i < ops.recv_from.size(); ++i)
+      jobs.push_back({bufs.recv_buf(g * per + static_cast<int>(i)), cfg.bytes,
+                      generation_seed(ops.recv_from[i], cfg.bytes, cfg.salt, g)});
+  const std::vector<VerifyResult> res = t.verify_many(jobs);  // one batched check
+  uint64_t bad = 0;
+  for (int g = 0, k = 0; g < gens; ++g)
+    for (size_t i = 0; i < ops.recv_from.size(); ++i, ++k) {
+      const VerifyResult& v = res[static_cast<size_t>(k)];
       bad += v.mismatches;
       if (per_slot) {
         (*per_slot)[2 * i] += v.mismatches;

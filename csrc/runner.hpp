@@ -38,7 +38,12 @@ struct RunConfig {
   int iters = 128;           // reference: count = 128 (p2p_matrix.cc:132)
   int warmup = 8;            // reference: none (p2p_matrix.cc:153-172)
   Timing timing = Timing::Events;
-  bool verify = false;
+  // Random-filled sends, every received buffer checked on the device after
+  // the timed loop (never inside it).  On by default: the
+  // reference's zeroed buffers are never read back (p2p_matrix.cc:129-130),
+  // so a transfer that silently drops bytes would print as a fast cell.
+  // p2p_matrix --no-verify opts out.
+  bool verify = true;
   bool samples = true;       // record an event per iteration for the distribution
   uint64_t salt = 0;
   // With verify: receive generations.  Iteration i (warmup and timed alike)
@@ -295,6 +300,8 @@ class StepDriver {
   // the ops it recorded.
   void recapture();
   int recaptures() const { return recaptures_; }
+  // connect() calls that changed the transport's per-peer op limits.
+  int limit_changes() const { return limit_changes_; }
   bool graphs() const { return opt_.graph; }
   // Collective: checks every receive slot written by steps [first, first +
   // count) against the payload of the message that wrote it last.
@@ -335,6 +342,7 @@ class StepDriver {
   bool skip_armed_ = false;
   bool skip_some_armed_ = false;
   int recaptures_ = 0;
+  int limit_changes_ = 0;
   int chain_mark_ = -1;  // run_steps: the previous step's end mark, the next one's start
   int per_group_ = 0;    // post_step_ops: messages per group of the step being posted (0: all)
 

@@ -113,6 +113,10 @@ void StepDriver::connect() {
   boot_.barrier();
   if (verify_) t_.zero(bufs_.recv_base(), recv_bytes());
   t_.sync();
+  // Every connection exists now: the transport re-derives its per-peer op
+  // limits from what it connected (RCCL's connection lines), before any graph
+  // records op sizes and before any timed step.
+  if (t_.refine_op_limits(boot_)) ++limit_changes_;
   // Graph capture only records launches (no peer interaction), so it must
   // follow the warm-up that established every lazy connection.
   if (opt_.graph && graphs_.empty()) capture_graphs();
@@ -299,9 +303,13 @@ StepVerifyReport StepDriver::verify_steps(long first, long count) {
       for (size_t i = 0; i < ops.recv_from.size(); ++i)
         last[slot_index(me, gen_of(k), pi, m, static_cast<int>(i))] = {ops.recv_from[i], m};
   }
-  if (verify_)
-    for (const auto& kv : last)
-      bad += t_.verify(bufs_.recv_buf(kv.first), bytes_, msg_seed(kv.second.first, kv.second.second)).mismatches;
+  if (verify_) {
+    // Every slot in one batched check (Transport::verify_many: one readback).
+    std::vector<Transport::VerifyJob> jobs;
+    jobs.reserve(last.size());
+    for (const auto& kv : last) jobs.push_back({bufs_.recv_buf(kv.first), bytes_, msg_seed(kv.second.first, kv.second.second)});
+    for (const auto& r : t_.verify_many(jobs)) bad += r.mismatches;
+  }
   const uint64_t mine[4] = {bad, verify_ ? static_cast<uint64_t>(last.size()) : 0, timed, verify_ ? last.size() : 0};
   std::vector<uint64_t> all(4 * static_cast<size_t>(boot_.size()));
   boot_.allgather(mine, all.data(), sizeof(mine));

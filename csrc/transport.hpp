@@ -49,6 +49,20 @@ class Transport {
   virtual void zero(void* p, size_t bytes) = 0;
   // Blocking: compares `bytes` at p against the PRNG stream `seed`.
   virtual VerifyResult verify(const void* p, size_t bytes, uint64_t seed) = 0;
+  // Blocking: result i == verify(jobs[i]).  GPU transports check the whole
+  // list in batched launches with one readback and one sync (the post-timing
+  // check of many receive slots); the default checks one buffer at a time.
+  struct VerifyJob {
+    const void* p = nullptr;
+    size_t bytes = 0;
+    uint64_t seed = 0;
+  };
+  virtual std::vector<VerifyResult> verify_many(const std::vector<VerifyJob>& jobs) {
+    std::vector<VerifyResult> out;
+    out.reserve(jobs.size());
+    for (const auto& j : jobs) out.push_back(verify(j.p, j.bytes, j.seed));
+    return out;
+  }
 
   // ---- data plane: one group == one fused launch ----
   virtual void group_begin() = 0;
@@ -162,6 +176,12 @@ class Transport {
   virtual bool set_chunk_cap(size_t /*bytes*/) { return false; }
   virtual size_t chunk_cap() const { return 0; }
   virtual size_t max_chunk(int /*peer*/) const { return 0; }
+  // Collective (every rank, same order): re-derive the per-peer op limits
+  // from what the data plane connected (RCCL: its connection lines, which
+  // exist only after the lazy connects of a warm-up).  True on every rank when
+  // any rank's limits changed: graphs that recorded ops must be captured
+  // again.  Transports without per-peer limits return false.
+  virtual bool refine_op_limits(Bootstrap& /*boot*/) { return false; }
 
   // What the data plane set up towards each peer, as a JSON object (RCCL: the
   // p2p channels its INFO log reports per communicator, the transport each

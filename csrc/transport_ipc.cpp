@@ -54,6 +54,7 @@
 #include <thread>
 #include <vector>
 
+#include "batch_verify.hpp"
 #include "bootstrap.hpp"
 #include "common.hpp"
 #include "hip_check.hpp"
@@ -210,6 +211,12 @@ class IpcTransport final : public Transport {
     r.checksum = acc_host_->checksum;
     r.first_bad = acc_host_->first_bad;
     return r;
+  }
+  std::vector<VerifyResult> verify_many(const std::vector<VerifyJob>& jobs) override {
+    if (jobs.empty()) return {};
+    if (verify_impl_ != dev::VerifyImpl::Auto && verify_impl_ != dev::VerifyImpl::Lds8)
+      return Transport::verify_many(jobs);
+    return batch_verify(batch_, jobs, stream_, [this] { sync(); });
   }
 
   // Buffer sets are registered collectively in the same order on every rank,
@@ -787,6 +794,7 @@ class IpcTransport final : public Transport {
   hipEvent_t fork_ = nullptr;
   dev::VerifyAccum* acc_ = nullptr;
   dev::VerifyAccum* acc_host_ = nullptr;
+  dev::BatchVerifier batch_;
   dev::VerifyImpl verify_impl_ = dev::VerifyImpl::Auto;
   std::string desc_;
   std::vector<Registration> regs_;

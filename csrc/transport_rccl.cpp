@@ -59,6 +59,7 @@
 #include <thread>
 #include <vector>
 
+#include "batch_verify.hpp"
 #include "bootstrap.hpp"
 #include "common.hpp"
 #include "hip_check.hpp"
@@ -318,6 +319,16 @@ class RcclTransport final : public Transport {
     return r;
   }
 
+  std::vector<VerifyResult> verify_many(const std::vector<VerifyJob>& jobs) override {
+    if (jobs.empty()) return {};
+    // The batched kernel is the default LDS8 verify; another --verify-impl
+    // keeps the one-buffer path.
+    if (verify_impl_ != dev::VerifyImpl::Auto && verify_impl_ != dev::VerifyImpl::Lds8)
+      return Transport::verify_many(jobs);
+    buffer_work();
+    return batch_verify(batch_, jobs, stream_, [this] { sync(); });
+  }
+
   void group_begin() override {
     nccl_ok(ncclGroupStart(), "ncclGroupStart");
     in_group_ = true;
@@ -514,7 +525,7 @@ class RcclTransport final : public Transport {
   std::string link_report() override { return peers_json(); }
   std::vector<std::string> peer_transports() override {
     std::vector<std::string> out;
-    for (const auto& l : rccl_peer_links(parse_rccl_connections(log_since(log_start_)), rank_, n_)) out.push_back(l.transport);
+    for (const auto& l : our_links()) out.push_back(l.transport);
     return out;
   }
   size_t max_chunk(int peer) const override { return chunk_for(peer); }
@@ -645,14 +656,18 @@ class RcclTransport final : public Transport {
   // Largest op per peer: RCCL delivers only the first half of an op whose
   // share of one p2p channel exceeds 16 MiB (scripts/rccl_half_repro.cpp,
   // both RCCLs of the image), so ops stay at 16 MiB x the channels an op to
-  // that peer is split over -- min(p2p channels, p2p channels per peer) of
-  // every communicator from RCCL's INFO log, and at most
-  // NCCL_NCHANNELS_PER_NET_PEER (2) for a peer on another host.  Both ends
-  // must split a message alike, so the ranks agree on min(a's view of b,
-  // b's view of a).  Without the log (the user set NCCL_DEBUG, or RCCL was
-  // initialised before), the conservative guess of round 2 stands: 64
+  // that peer is split over.  From RCCL's init line: min(p2p channels, p2p
+  // channels per peer) of every communicator, and at most
+  // NCCL_NCHANNELS_PER_NET_PEER (2) for a peer on another host.  That rule is
+  // pinned on the self path only (profiles/r3_rccl_half_repro/), so a remote
+  // peer on this host starts at 2 channels (32 MiB) until refine_op_limits()
+  // has read the channels RCCL connected to it (its lazy connection lines,
+  // ADVICE r3).  Both ends must split a message alike, so the ranks agree on
+  // min(a's view of b, b's view of a).  Without the log (the user set
+  // NCCL_DEBUG, or RCCL was initialised before), round 2's guess stands: 64
   // channels to itself, 2 to others, fewer under the NCCL channel knobs.
   // P2P_RCCL_MAX_CHUNK=<bytes> sets every peer's limit, 0 disables splitting.
+  static constexpr int kUnconnectedPeerChannels = 2;
   void derive_op_limits(Bootstrap& boot) {
     char host[128] = {0};
     std::snprintf(host, sizeof(host), "%s", rccl_host_id().c_str());
@@ -686,13 +701,17 @@ class RcclTransport final : public Transport {
     bool logged = !comm_info_.empty();
     for (const auto& ci : comm_info_) logged = logged && ci.found();
     std::vector<int> mine(static_cast<size_t>(n_), 0);
+    init_channels_.assign(static_cast<size_t>(n_), 0);
     for (int p = 0; p < n_; ++p) {
+      const bool net = net_peer_[static_cast<size_t>(p)] != 0;
       int c = 0;
       if (logged) {
         for (const auto& ci : comm_info_) {
-          const int x = rccl_op_channels(ci, net_peer_[static_cast<size_t>(p)] != 0, net_per_peer);
+          const int x = rccl_op_channels(ci, net, net_per_peer);
           c = c == 0 ? x : std::min(c, x);
         }
+        if (p != rank_) init_channels_[static_cast<size_t>(p)] = c;
+        if (p != rank_ && !net) c = std::min(c, kUnconnectedPeerChannels);
       } else {
         c = p2p_channel_limit(p == rank_ ? 64 : 2);
       }
@@ -701,28 +720,67 @@ class RcclTransport final : public Transport {
     const std::vector<int> all = boot.allgather_vector(mine);
     op_channels_.assign(static_cast<size_t>(n_), 0);
     peer_limit_.assign(static_cast<size_t>(n_), 0);
+    peer_source_.assign(static_cast<size_t>(n_), "");
     for (int p = 0; p < n_; ++p) {
       const int c = std::min(all[static_cast<size_t>(rank_) * n_ + p], all[static_cast<size_t>(p) * n_ + rank_]);
       op_channels_[static_cast<size_t>(p)] = c;
       peer_limit_[static_cast<size_t>(p)] = kRcclBytesPerChannel * static_cast<size_t>(std::max(c, 1));
+      peer_source_[static_cast<size_t>(p)] = !logged ? "default"
+                                             : p == rank_ ? "init line"
+                                             : net_peer_[static_cast<size_t>(p)] ? "init line (net peer)"
+                                                                                 : "unconnected (2 channels)";
     }
-    limit_source_ = logged ? "rccl INFO log: 16M x min(p2p channels, per peer[, net per peer])"
+    limit_source_ = logged ? "rccl INFO log: 16M x min(p2p channels, per peer[, net per peer]); remote peers "
+                             "2 channels until their connection lines"
                            : "default (no RCCL INFO log): 16M x 64 self / 2 peers";
     if (const char* mc = std::getenv("P2P_RCCL_MAX_CHUNK")) {
       const size_t v = std::strcmp(mc, "0") ? parse_size(mc) : 0;
       std::fill(peer_limit_.begin(), peer_limit_.end(), v);
       limit_source_ = strfmt("P2P_RCCL_MAX_CHUNK=%s", mc);
+      std::fill(peer_source_.begin(), peer_source_.end(), "P2P_RCCL_MAX_CHUNK");
     }
   }
 
+  // The connection lines of this transport's communicators only (another
+  // transport of the process may log into the same file meanwhile).
+  std::vector<RcclPeerLink> our_links() const {
+    std::vector<std::string> ours;
+    for (auto c : comms_) ours.push_back(strfmt("%p", static_cast<void*>(c)));
+    return rccl_peer_links(connections_of(parse_rccl_connections(log_since(log_start_)), ours), rank_, n_);
+  }
+
+ public:
+  // After the warm-up connected every peer: each remote peer's op channels
+  // become min(init-line channels, channels RCCL connected to it), agreed by
+  // both ends (rccl_log.hpp proposed_op_channels / agree_op_channels).  Peers
+  // without connection lines keep their limit.
+  bool refine_op_limits(Bootstrap& boot) override {
+    std::vector<int> prop(static_cast<size_t>(n_), 0);
+    const bool forced = std::getenv("P2P_RCCL_MAX_CHUNK") != nullptr;
+    if (!forced && !init_channels_.empty()) prop = proposed_op_channels(init_channels_, our_links(), rank_);
+    const std::vector<int> all = boot.allgather_vector(prop);
+    const std::vector<int> agreed = agree_op_channels(all, n_, rank_, op_channels_, &peer_source_);
+    bool changed = false;
+    for (int p = 0; p < n_; ++p) {
+      const size_t i = static_cast<size_t>(p);
+      if (agreed[i] == op_channels_[i]) continue;
+      changed = true;
+      op_channels_[i] = agreed[i];
+      peer_limit_[i] = kRcclBytesPerChannel * static_cast<size_t>(std::max(agreed[i], 1));
+    }
+    ++refinements_;
+    return boot.allreduce_max(changed ? 1.0 : 0.0) > 0.0;
+  }
+
+ private:
   // link_report(): the communicators' channel counts, and per peer the
   // transport and channels RCCL's connection lines show, next to the op
   // limit in use.
   std::string peers_json() const {
-    const std::string text = log_since(log_start_);
-    const auto links = rccl_peer_links(parse_rccl_connections(text), rank_, n_);
-    std::string o = strfmt("{\"rank\":%d,\"log\":%s,\"op_limit_source\":\"%s\",\"comms\":[", rank_,
-                           rccl_log().path.empty() ? "null" : "true", json_escape(limit_source_).c_str());
+    const auto links = our_links();
+    std::string o = strfmt("{\"rank\":%d,\"log\":%s,\"op_limit_source\":\"%s\",\"refinements\":%d,\"comms\":[",
+                           rank_, rccl_log().path.empty() ? "null" : "true", json_escape(limit_source_).c_str(),
+                           refinements_);
     for (size_t j = 0; j < comm_info_.size(); ++j)
       o += strfmt("%s{\"p2p_channels\":%d,\"p2p_channels_per_peer\":%d,\"nnodes\":%d,\"from_rank\":%d,\"unroll\":%d}",
                   j ? "," : "", comm_info_[j].p2p_channels, comm_info_[j].p2p_per_peer, comm_info_[j].nnodes,
@@ -731,9 +789,10 @@ class RcclTransport final : public Transport {
     for (int p = 0; p < n_; ++p) {
       const auto& l = links[static_cast<size_t>(p)];
       o += strfmt("%s{\"peer\":%d,\"transport\":\"%s\",\"via\":\"%s\",\"channels_connected\":%d,\"op_channels\":%d,"
-                  "\"op_limit\":%zu,\"net\":%s}",
+                  "\"op_limit\":%zu,\"op_limit_source\":\"%s\",\"net\":%s}",
                   p ? "," : "", p, json_escape(l.transport).c_str(), json_escape(l.via).c_str(), l.channels_connected,
                   op_channels_.empty() ? 0 : op_channels_[static_cast<size_t>(p)], chunk_for(p),
+                  peer_source_.empty() ? "" : json_escape(peer_source_[static_cast<size_t>(p)]).c_str(),
                   !net_peer_.empty() && net_peer_[static_cast<size_t>(p)] ? "true" : "false");
     }
     return o + "]}";
@@ -897,6 +956,9 @@ class RcclTransport final : public Transport {
   std::vector<char> net_peer_;           // per peer: RCCL reaches it through its network transport
   std::vector<RcclInitInfo> comm_info_;  // per communicator, from RCCL's INFO log
   std::string limit_source_;             // how peer_limit_ was set
+  std::vector<int> init_channels_;       // per remote peer: channels from the init line (before refinement)
+  std::vector<std::string> peer_source_; // per peer: what set its limit
+  int refinements_ = 0;                  // refine_op_limits() calls
   size_t cap_ = 0;                       // set_chunk_cap (0: none)
   size_t log_start_ = 0;                 // this transport's part of the RCCL log
   // `fallback` channels, or fewer where NCCL_MAX_P2P_NCHANNELS /
@@ -950,6 +1012,7 @@ class RcclTransport final : public Transport {
   int next_event_ = 0;
   dev::VerifyAccum* acc_ = nullptr;
   dev::VerifyAccum* acc_host_ = nullptr;
+  dev::BatchVerifier batch_;
   dev::VerifyImpl verify_impl_ = dev::VerifyImpl::Auto;
   std::string desc_;
   int hook_ = 0;

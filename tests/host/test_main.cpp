@@ -893,6 +893,43 @@ TEST(test_rccl_log_four_net_ranks) {
   EXPECT(links[1].transport == "self");
 }
 
+TEST(test_rccl_op_limits_from_connection_lines) {
+  // a canned log in RCCL 2.26's format (rank 1 of 4 GPUs
+  // on one host, two communicators, P2P/IPC connections; one line of another
+  // process-local communicator).  Init line: 8 p2p channels per peer.
+  const std::string text = read_file(std::string(P2P_TEST_DATA) + "/rccl_info_4rank_p2p_rank1_canned.txt");
+  RcclInitInfo info = parse_rccl_init(text);
+  EXPECT(info.p2p_channels == 64 && info.p2p_per_peer == 8 && info.nnodes == 1);
+  auto all_conns = parse_rccl_connections(text);
+  EXPECT(all_conns.size() == 23 && all_conns[0].comm == "0x5a5a0100" && all_conns.back().comm == "0x77770100");
+  auto conns = connections_of(all_conns, {"0x5a5a0100", "0x5a5a0900"});
+  EXPECT(conns.size() == 22);
+  auto links = rccl_peer_links(conns, 1, 4);
+  EXPECT(links[0].transport == "P2P" && links[0].channels_connected == 4);  // 4 send channels on both comms
+  EXPECT(links[2].transport == "P2P" && links[2].channels_connected == 2);  // 8 on one comm, 2 on the other
+  EXPECT(links[3].transport.empty() && links[3].channels_connected == 0);   // only a foreign comm's line
+  EXPECT(rccl_peer_links(all_conns, 1, 4)[3].channels_connected == 1);
+  const int init = rccl_op_channels(info, false, 2);
+  EXPECT(init == 8);
+  const std::vector<int> prop = proposed_op_channels({init, 0, init, init}, links, 1);
+  EXPECT((prop == std::vector<int>{4, 0, 2, 0}));
+  // Every rank's proposals: rank 0 saw 4 towards rank 1, ranks 2 and 3 none.
+  std::vector<int> all(16, 0);
+  for (int p = 0; p < 4; ++p) all[static_cast<size_t>(4 + p)] = prop[static_cast<size_t>(p)];
+  all[0 * 4 + 1] = 4;
+  std::vector<std::string> src(4, "init");
+  const std::vector<int> agreed = agree_op_channels(all, 4, 1, {2, 64, 2, 2}, &src);
+  EXPECT((agreed == std::vector<int>{4, 64, 2, 2}));
+  EXPECT(src[0] == "connection lines" && src[2] == "connection lines" && src[1] == "init" && src[3] == "init");
+  // The peer's view is the same pair: rank 0 agrees on 4 towards rank 1.
+  EXPECT(agree_op_channels(all, 4, 0, {64, 2, 2, 2})[1] == 4);
+  // The 4-rank NET log: 2 channels connected per peer, as the init rule said.
+  const std::string net = read_file(std::string(P2P_TEST_DATA) + "/rccl_info_4rank_net_rank1.txt");
+  auto nl = rccl_peer_links(parse_rccl_connections(net), 1, 4);
+  const int ninit = rccl_op_channels(parse_rccl_init(net), true, 2);
+  EXPECT((proposed_op_channels({ninit, 0, ninit, ninit}, nl, 1) == std::vector<int>{2, 0, 2, 2}));
+}
+
 TEST(test_link_transport_mismatch) {
   EXPECT(link_transport_mismatch("XGMI/1", "SHM"));
   EXPECT(link_transport_mismatch("XGMI/1", "NET"));

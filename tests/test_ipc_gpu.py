@@ -216,6 +216,7 @@ def test_bench_two_ranks_ipc():
     assert len(sweep) == 11 and sweep[-1]["bytes"] == 4 << 30 and all(p["gbs"] > 0 for p in sweep)
 
 
+@pytest.mark.emulated
 @pytest.mark.parametrize("nranks", [4, 8])
 def test_bench_emulated_node(nranks):
     """bench.py at the driver's GPU counts with every rank on the one GPU (IPC

@@ -47,7 +47,8 @@ def test_copy_kernel_matches_torch(nbytes, coherent):
     assert torch.all(dst[nbytes:] == 0xAB), "copy wrote past the end"
 
 
-@pytest.mark.parametrize("fill_impl", [1, 2, 3, 4])  # grid, non-temporal, grid-stride, XCD-ordered grid
+# grid, non-temporal, grid-stride, XCD-ordered grid, grid with 2 / 4 stores per lane
+@pytest.mark.parametrize("fill_impl", [1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("nbytes", SIZES + [(64 << 20) + 4])
 def test_fill_variants_match_reference(fill_impl, nbytes):
     from test_nccl_p2p_amd import require_native
@@ -88,6 +89,33 @@ def test_verify_counts_exact_bitflips(impl):
     assert r.checksum == ref.checksum
 
 
+def test_batched_verify_matches_reference_per_buffer(native):
+    """dev::launch_multi_verify (the post-timing check of many receive slots
+    in one launch per 32 buffers, one readback): every job's mismatches,
+    checksum and first bad byte equal the PyTorch reference of that buffer,
+    across batch boundaries (40 jobs), tails, wrong seeds and bit flips."""
+    sizes = [16, 4099, 48, (1 << 20) + 13, 4 << 20, 32 << 20] * 6 + [1000, 64 << 10, 16, 4096]
+    bufs, jobs, want = [], [], []
+    for k, n in enumerate(sizes):
+        b = torch.empty(n, dtype=torch.uint8, device="cuda")
+        fill_(b, 500 + k)
+        if k % 5 == 1:
+            b[n // 2] ^= 0x10
+            b[n - 1] ^= 0x01
+        seed = 500 + k if k % 7 != 3 else 9999  # some jobs checked against the wrong stream
+        bufs.append(b)
+        jobs.append((b.data_ptr(), n, seed))
+    torch.cuda.synchronize()
+    for b, (_, n, seed) in zip(bufs, jobs):
+        want.append(reference_verify(b, seed))
+    got = native.verify_many(jobs, torch.cuda.current_stream().cuda_stream)
+    assert len(got) == len(jobs) == 40
+    for k, ((m, c, f), ref) in enumerate(zip(got, want)):
+        assert (m, c, f) == (ref.mismatches, ref.checksum, ref.first_bad), (k, sizes[k], (m, c, f), ref)
+    assert sum(1 for m, _, _ in got if m) >= 10
+    assert native.verify_many([], 0) == []
+
+
 def test_lds_and_register_agree_on_random_data():
     g = torch.Generator(device="cuda").manual_seed(0)
     buf = torch.randint(0, 256, (3 << 20,), dtype=torch.uint8, device="cuda", generator=g)
@@ -102,41 +130,6 @@ def test_int32_tensor_and_alignment_checks():
     assert verify(t, 9).ok
     with pytest.raises(ValueError):
         verify(t.view(torch.uint8)[1:17], 9)
-
-
-def _timed_tbs(fn, nbytes, reps=5):
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    fn()
-    torch.cuda.synchronize()
-    s.record()
-    for _ in range(reps):
-        fn()
-    e.record()
-    e.synchronize()
-    return reps * nbytes / (s.elapsed_time(e) * 1e-3) / 1e12
-
-
-def test_kernel_bandwidth_floors(native):
-    """Performance floors at 1 GiB, about 80% of the profiled rates
-    (profiles/r1_final/kernel_bench.txt: fill 6.99, lds8 verify 6.20;
-    profiles/r2_copy_nt/kernel_bench.txt: copy 3.31 TB/s with non-temporal
-    accesses; the measured HBM roof is 6.29): a kernel regression fails the
-    GPU tier instead of passing it at a third of its speed."""
-    nbytes = 1 << 30
-    buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    dst = torch.empty_like(buf)
-    stream = torch.cuda.current_stream().cuda_stream
-    ptr = buf.data_ptr()
-    fill_tbs = _timed_tbs(lambda: native.fill(ptr, nbytes, 1, stream, 1), nbytes)
-    assert verify(buf, 1, impl="reg").ok
-    # lds8: the default verify (LDS-DMA staged, 8 loads in flight); kernel time only.
-    lds8_tbs = _timed_tbs(lambda: native.verify_launch(ptr, nbytes, 1, 4, True, stream), nbytes)
-    copy_tbs = _timed_tbs(lambda: native.copy(dst.data_ptr(), ptr, nbytes, stream), nbytes)
-    assert verify(dst, 1).ok
-    print("fill %.2f  verify-lds8 %.2f  copy %.2f TB/s" % (fill_tbs, lds8_tbs, copy_tbs))
-    assert fill_tbs > 5.5, fill_tbs
-    assert lds8_tbs > 5.0, lds8_tbs
-    assert copy_tbs > 2.65, copy_tbs  # payload bytes (read once + written once)
 
 
 def test_fill_verify_beyond_16gib():

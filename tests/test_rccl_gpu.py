@@ -287,28 +287,6 @@ def test_rccl_unroll_factor():
         assert out.stdout.strip().splitlines()[-1] == want, (env, out.stdout)
 
 
-@pytest.mark.parametrize("transport,floor", [("rccl", 800.0), ("rccl:4", 1800.0)])
-def test_self_copy_rate_floor(native, transport, floor):
-    """The bench's step (32 MiB x 8 self messages in one group) through one
-    and four communicators, median GPU step time over 20 steps, against
-    floors at about 80% of the profiled rates (round 1: one communicator
-    ~950-1150 GB/s, four ~2300-2600 GB/s): a lost multi-communicator speedup
-    or a slower RCCL posting fails here."""
-    import statistics
-    s = native.Session(0, 1, device=0, transport=transport, timeout_s=120)
-    d = native.StepDriver(s, "self", "bi", 32 << 20, 8, False, True, False)
-    d.connect()
-    d.run_steps(0, 5)
-    d.sync()
-    d.reset()
-    d.run_steps(5, 20)
-    d.sync()
-    gbs = 8 * (32 << 20) / (statistics.median(d.step_ms()) * 1e-3) / 1e9
-    print("%s: %.1f GB/s" % (transport, gbs))
-    del d, s
-    assert gbs > floor, gbs
-
-
 @pytest.mark.parametrize("transport", ["rccl", "ipc"])
 def test_stream_gate_opens_at_its_deadline(native, transport):
     """The pre-posted latency's stream gate: released, it opens at once; never

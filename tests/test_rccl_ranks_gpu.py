@@ -52,6 +52,7 @@ def test_cli_four_rccl_ranks_every_mode(exe, tmp_path, comms):
     assert len(pre) == 1 and len(pre[0]["pairs"]) == 6 and all(p["one_way_us"]["p50"] > 0 for p in pre[0]["pairs"])
 
 
+@pytest.mark.emulated
 def test_bench_four_rccl_ranks(tmp_path):
     """bench.py's whole N = 4 flow through RCCL: the five posting candidates
     (1 communicator per message / batched, 2, 4 and 8 communicators), the

@@ -1,0 +1,148 @@
+"""Performance floors of the GPU tier.  They still fail the tier, but this
+file sorts after every correctness test (and conftest.py orders the `perf`
+marker last), so a missed floor under `pytest -x` can no longer hide the RCCL
+correctness tests (VERDICT r3 "do this" #1: the driver's GPU tier stopped at
+a 3.42 TB/s fill reading and never ran test_rccl_gpu.py).
+
+Method (not a 5-launch window after an idle GPU):
+  * a sustained warm-up of >= 100 ms of 1 GiB fills first;
+  * every launch timed on its own event pair, 20 launches, median;
+  * torch's zero_() and copy_() timed the same way in the same window as the
+    in-process roofs, so the floor is relative as well as absolute;
+  * a "cold" series after 2 s of idling records whether the first launches
+    after idle are slow (clock ramp) -- recorded, never asserted;
+  * every series is printed, and written to $P2P_TEST_LOG_DIR/perf_floors.json
+    when that is set (the GPU sessions point it under gpurun_out/).
+The fill replaces the reference's cudaMemset (p2p_matrix.cc:129-130)."""
+import json
+import os
+import statistics
+import time
+
+import pytest
+import torch
+
+from test_nccl_p2p_amd.ops import verify
+
+pytestmark = [pytest.mark.gpu, pytest.mark.perf]
+
+GIB = 1 << 30
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(native):
+    assert torch.cuda.is_available(), "GPU tier needs a GPU"
+    torch.cuda.set_device(0)
+
+
+def per_launch_ms(fn, reps=20):
+    """Kernel time of each of `reps` back-to-back launches (one event pair
+    around each, all recorded before the single synchronize)."""
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for s, e in ev:
+        s.record()
+        fn()
+        e.record()
+    torch.cuda.synchronize()
+    return [s.elapsed_time(e) for s, e in ev]
+
+
+def tbs(ms_list, nbytes):
+    return nbytes / (statistics.median(ms_list) * 1e-3) / 1e12
+
+
+def warm(fn, seconds=0.1):
+    """Launch fn back to back until `seconds` of GPU work have completed."""
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < seconds or n < 16:
+        for _ in range(16):
+            fn()
+        torch.cuda.synchronize()
+        n += 16
+    return n
+
+
+def _record(name, rec):
+    d = os.environ.get("P2P_TEST_LOG_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        path = os.path.join(d, "perf_floors.json")
+        old = {}
+        if os.path.exists(path):
+            with open(path) as f:
+                old = json.load(f)
+        old[name] = rec
+        with open(path, "w") as f:
+            json.dump(old, f, indent=1)
+
+
+def test_kernel_bandwidth_floors(native):
+    """1 GiB fill / LDS-DMA verify / copy against absolute floors at ~80% of
+    the profiled rates (fill 7.09, lds8 verify 6.27, copy 3.20 read + 3.12
+    written TB/s: profiles/r3b_close/pmc_summary.txt) and the fill against
+    0.8 x torch's zero_() measured in the same window."""
+    buf = torch.empty(GIB, dtype=torch.uint8, device="cuda")
+    dst = torch.empty_like(buf)
+    stream = torch.cuda.current_stream().cuda_stream
+    ptr, dptr = buf.data_ptr(), dst.data_ptr()
+
+    def fill(impl):
+        return lambda: native.fill(ptr, GIB, 1, stream, impl)
+
+    # Cold series first: 2 s idle, then launches with no warm-up.
+    torch.cuda.synchronize()
+    time.sleep(2.0)
+    cold = per_launch_ms(fill(0))
+    warm_launches = warm(fill(0))
+    series = {
+        "fill": per_launch_ms(fill(0)),            # the default (FillImpl::Auto)
+        "zero_": per_launch_ms(lambda: buf.zero_()),
+        "fill_vpl2": per_launch_ms(fill(5)),
+        "fill_vpl4": per_launch_ms(fill(6)),
+        "fill_nt": per_launch_ms(fill(2)),
+    }
+    native.fill(ptr, GIB, 1, stream, 0)
+    assert verify(buf, 1, impl="reg").ok
+    series["verify_lds8"] = per_launch_ms(lambda: native.verify_launch(ptr, GIB, 1, 4, True, stream))
+    series["copy"] = per_launch_ms(lambda: native.copy(dptr, ptr, GIB, stream))
+    series["copy_"] = per_launch_ms(lambda: dst.copy_(buf))
+    series["fill_again"] = per_launch_ms(fill(0))  # same window, after the others
+    native.copy(dptr, ptr, GIB, stream)
+    assert verify(dst, 1).ok
+    rates = {k: round(tbs(v, GIB), 3) for k, v in series.items()}
+    rates["fill_cold"] = round(tbs(cold, GIB), 3)
+    rec = {"tbs_median": rates, "warm_launches": warm_launches,
+           "per_launch_ms": dict(series, fill_cold=cold)}
+    _record("kernel_bandwidth_floors", rec)
+    print(json.dumps(rates))
+    for k, v in rec["per_launch_ms"].items():
+        print("%-12s %s" % (k, " ".join("%.3f" % x for x in v)))
+    msg = json.dumps(rec)
+    assert rates["fill"] > 5.5, msg
+    assert rates["fill"] >= 0.8 * rates["zero_"], msg
+    assert rates["verify_lds8"] > 5.0, msg
+    assert rates["copy"] > 2.65, msg  # payload bytes (read once + written once)
+
+
+@pytest.mark.parametrize("transport,floor", [("rccl", 800.0), ("rccl:4", 1800.0)])
+def test_self_copy_rate_floor(native, transport, floor):
+    """The bench's step (32 MiB x 8 self messages in one group) through one
+    and four communicators, median GPU step time over 20 steps, against
+    floors at about 80% of the profiled rates (round 1: one communicator
+    ~950-1150 GB/s, four ~2300-2600 GB/s): a lost multi-communicator speedup
+    or a slower RCCL posting fails here."""
+    s = native.Session(0, 1, device=0, transport=transport, timeout_s=120)
+    d = native.StepDriver(s, "self", "bi", 32 << 20, 8, False, True, False)
+    d.connect()
+    d.run_steps(0, 5)
+    d.sync()
+    d.reset()
+    d.run_steps(5, 20)
+    d.sync()
+    ms = d.step_ms()
+    gbs = 8 * (32 << 20) / (statistics.median(ms) * 1e-3) / 1e9
+    _record("self_copy_rate_floor[%s]" % transport, {"gbs_median": gbs, "step_ms": ms})
+    print("%s: %.1f GB/s" % (transport, gbs))
+    del d, s
+    assert gbs > floor, (gbs, ms)
