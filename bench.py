@@ -79,12 +79,27 @@ def set_hw_queues(argv) -> None:
         elif a.startswith("--hw-queues="):
             q = a.split("=", 1)[1]
     os.environ["P2P_HW_QUEUES_ENV"] = os.environ.get("GPU_MAX_HW_QUEUES", "")
+    stash_stock_env()
     try:
         qn = int(q)
     except ValueError:  # argparse reports a bad --hw-queues; a bad P2P_BENCH_HW_QUEUES falls back
         qn = 8
     if qn > 0:
         os.environ["GPU_MAX_HW_QUEUES"] = str(qn)
+
+
+# What this process changes about RCCL / HIP before they start (the queue
+# count here, RCCL's unroll factor and INFO log in the native transport).  The
+# environment as it was is kept, so reference_semantics_stock can run the
+# reference's methodology in a child with the stock settings.
+STOCK_ENV_KEYS = ("GPU_MAX_HW_QUEUES", "RCCL_UNROLL_FACTOR", "NCCL_DEBUG", "NCCL_DEBUG_FILE", "NCCL_DEBUG_SUBSYS")
+
+
+def stash_stock_env() -> None:
+    import json
+
+    if "P2P_STOCK_ENV" not in os.environ:  # a child keeps its parent's record
+        os.environ["P2P_STOCK_ENV"] = json.dumps({k: os.environ.get(k) for k in STOCK_ENV_KEYS})
 
 
 if __name__ == "__main__":  # (not when tests import this module)
@@ -188,6 +203,10 @@ def parse_args(argv=None):
     ap.add_argument("--child-port", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--child-out", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--child-batch", type=int, default=1, help=argparse.SUPPRESS)
+    ap.add_argument("--child-ref-iters", default="{}", help=argparse.SUPPRESS)  # ref-stock: {"uni": I, "bi": I}
+    ap.add_argument("--ref-stock", type=int, default=1,
+                    help="1: also run the reference's methodology in a child with the stock RCCL / HIP settings "
+                         "(RCCL's own unroll, the environment's HW queues, no INFO log): reference_semantics_stock")
     return ap.parse_args(argv)
 
 

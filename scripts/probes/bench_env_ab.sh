@@ -3,7 +3,7 @@
 # (untimed sections off).  Each setting is "NAME=VAL[,NAME=VAL...]" or
 # "default"; REPS rounds over all settings, each round starting one setting
 # later than the one before (so no setting always runs first on the box).
-#   bash scripts/bench_env_ab.sh <out_dir> <reps> <setting>...
+#   bash scripts/probes/bench_env_ab.sh <out_dir> <reps> <setting>...
 set -u
 OUT=$1
 REPS=$2

@@ -4,7 +4,7 @@
 # op (P2P_RCCL_MAX_CHUNK=1G, under the 16 MiB x 64 channel limit) against
 # 32 MiB ops, at 1 and 4 communicators, every delivery verified.  Prints one
 # summary line per row; the JSON files stay in the output directory.
-#   bash scripts/chunk_cost.sh [out_dir]
+#   bash scripts/probes/chunk_cost.sh [out_dir]
 set -u
 OUT=${1:-gpurun_out/chunk_cost}
 mkdir -p "$OUT"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # RCCL communicators per rank (--comms K) on the driver-shaped 1-GPU bench,
 # interleaved, REPS rounds, untimed sections off (one box).
-#   bash scripts/comms_probe_bench.sh [out_dir] [reps] [K...]
+#   bash scripts/probes/comms_probe_bench.sh [out_dir] [reps] [K...]
 set -u
 OUT=${1:-gpurun_out/comms_probe}
 REPS=${2:-2}

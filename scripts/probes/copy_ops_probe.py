@@ -4,8 +4,8 @@ the same total size.  The IPC transport launches a group's receives as one
 multi-copy grid (kernels.hip multi_copy_kernel); a bench step at the default
 shape is 32 receives of 32 MiB = two launches of 16 ops.
 
-    python scripts/copy_ops_probe.py            # current lookup
-    P2P_COPY_LOOKUP=linear python scripts/copy_ops_probe.py   # the old scan
+    python scripts/probes/copy_ops_probe.py            # current lookup
+    P2P_COPY_LOOKUP=linear python scripts/probes/copy_ops_probe.py   # the old scan
 """
 import argparse
 import json

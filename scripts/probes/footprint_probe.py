@@ -4,7 +4,7 @@ gfx950 copy and fill kernels on fresh 32 MiB / 1 GiB buffers after allocating
 (and touching) 0, 16, 64 and 128 GiB of other device memory, with plain
 hipMalloc (torch caching allocator) buffers.
 
-    python scripts/footprint_probe.py
+    python scripts/probes/footprint_probe.py
 """
 import os
 import sys

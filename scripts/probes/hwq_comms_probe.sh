@@ -1,7 +1,7 @@
 #!/bin/bash
 # RCCL communicators per rank x HIP hardware queues (GPU_MAX_HW_QUEUES) on the
 # 1-GPU bench at RCCL unroll 4, interleaved, untimed sections off.
-#   bash scripts/hwq_comms_probe.sh [out_dir] [reps] ["queues comms"...]
+#   bash scripts/probes/hwq_comms_probe.sh [out_dir] [reps] ["queues comms"...]
 set -u
 OUT=${1:-gpurun_out/hwq_comms}
 REPS=${2:-2}

@@ -3,7 +3,7 @@
 one GPU, torchrun): one Session.run per size, printing progress, so a failing
 export/import is pinned to a size and engine.
 
-    torchrun --nproc-per-node 2 scripts/ipc_register_probe.py ipc:push
+    torchrun --nproc-per-node 2 scripts/probes/ipc_register_probe.py ipc:push
 """
 import json
 import os

@@ -5,7 +5,7 @@ One step = one grouped 8-byte self send/recv (the latency ping-pong's shape on
 one GPU).  Reports the median per-step GPU time from the StepDriver marks for
 eager posting and for a captured graph replayed per step.
 
-    python scripts/latency_graph_probe.py [--bytes 8] [--steps 2000]
+    python scripts/probes/latency_graph_probe.py [--bytes 8] [--steps 2000]
 """
 import argparse
 import json

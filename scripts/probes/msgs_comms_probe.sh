@@ -2,7 +2,7 @@
 # Messages per step x RCCL communicators on the 1-GPU bench (8 hardware
 # queues, unroll 4), interleaved; prints value, device-time matrix and the
 # host's posting time per step (host_post_ms_per_step vs ms_per_step).
-#   bash scripts/msgs_comms_probe.sh [out_dir] [reps] ["msgs comms"...]
+#   bash scripts/probes/msgs_comms_probe.sh [out_dir] [reps] ["msgs comms"...]
 set -u
 OUT=${1:-gpurun_out/msgs_comms}
 REPS=${2:-2}

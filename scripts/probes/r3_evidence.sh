@@ -3,9 +3,9 @@
 # crash or time limit ends the script, exit statuses 0-3 are results):
 #   1. bench.py with 4 RCCL ranks on the one GPU (distinct hosts to RCCL, so its
 #      NET transport): provenance.rccl_peers / matrix_transport per pair;
-#   2. scripts/chunk_cost.sh: one op vs 32 MiB ops on the self path;
-#   3. scripts/unroll_probe.sh: RCCL_UNROLL_FACTOR on the 1-GPU bench.
-#   bash scripts/r3_evidence.sh [out_dir]
+#   2. scripts/probes/chunk_cost.sh: one op vs 32 MiB ops on the self path;
+#   3. scripts/probes/unroll_probe.sh: RCCL_UNROLL_FACTOR on the 1-GPU bench.
+#   bash scripts/probes/r3_evidence.sh [out_dir]
 O=${1:-gpurun_out/r3_evidence}
 mkdir -p "$O"
 : > "$O/status.txt"
@@ -30,5 +30,5 @@ step emu4_bench "0|3" env P2P_RCCL_DISTINCT_HOSTS=1 NCCL_SOCKET_IFNAME=lo NCCL_I
   bench.py --gpus 4 --device 0 --size 4M --msgs 8 --sweep-max 64M --allpairs-size 64M --ring-size 16M \
   --ref-iters 16 --latency-iters 30 --ipc-extra 0 --timeout 60 --json-out "$O/emu4_bench.json" \
   > "$O/emu4_bench.out" 2> "$O/emu4_bench.err"
-step chunk_cost "0" bash scripts/chunk_cost.sh "$O/chunk_cost"
-step unroll "0" bash scripts/unroll_probe.sh "$O/unroll"
+step chunk_cost "0" bash scripts/probes/chunk_cost.sh "$O/chunk_cost"
+step unroll "0" bash scripts/probes/unroll_probe.sh "$O/unroll"

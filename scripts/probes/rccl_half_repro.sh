@@ -7,7 +7,7 @@
 # Exit 0 / 3 from the binary means "ran" (3: some delivery was wrong); anything
 # else (fault, abort, time limit) ends the script at once.
 #
-#   make tools && bash scripts/rccl_half_repro.sh [out_dir]
+#   make tools && bash scripts/probes/rccl_half_repro.sh [out_dir]
 set -u
 OUT=${1:-gpurun_out/half_repro}
 mkdir -p "$OUT"

@@ -2,7 +2,7 @@
 """Probes RCCL send/recv correctness at large message sizes (self path, one
 GPU) with device-side verification, varying iterations and the comm mode.
 
-    python scripts/rccl_size_probe.py [iters] [sizes...]
+    python scripts/probes/rccl_size_probe.py [iters] [sizes...]
 """
 import json
 import os

@@ -2,7 +2,7 @@
 # 1-GPU bench at several step shapes (messages of 32 MiB per step x RCCL
 # communicators), each run verified; one JSON line per run in
 # gpurun_out/step_shape/.  Run on a GPU box from the repo root:
-#   scripts/step_shape_sweep.sh "8 32 128" "-1 2 3 4"
+#   scripts/probes/step_shape_sweep.sh "8 32 128" "-1 2 3 4"
 set -o pipefail
 out=gpurun_out/step_shape
 mkdir -p $out

@@ -4,7 +4,7 @@
 # Factor (pre-set): 1" on MI355X by default).  Settings are interleaved, REPS
 # rounds, each the driver-shaped bench with the untimed sections off; RCCL's
 # INFO log of every run is kept to show the factor it used.
-#   bash scripts/unroll_probe.sh [out_dir] [reps] [factors...]
+#   bash scripts/probes/unroll_probe.sh [out_dir] [reps] [factors...]
 set -u
 OUT=${1:-gpurun_out/unroll}
 REPS=${2:-2}

@@ -4,10 +4,48 @@ comparisons of bench.py), in this process or as a child job per rank."""
 from __future__ import annotations
 
 import json
+import os
 import statistics
 import time
 
-from test_nccl_p2p_amd.bench.core import claim_stdout, default_device, headline_stats, log, pick_depth
+from test_nccl_p2p_amd.bench.core import (claim_stdout, default_device, headline_stats, log, pair_matrix_summary,
+                                          pick_depth)
+
+REF_STOCK = "ref-stock"  # --child: the reference's methodology with RCCL's and HIP's stock settings
+
+
+def stock_env(environ=None) -> dict:
+    """The environment for reference_semantics_stock: what bench.py found at
+    start for the queue count, RCCL's unroll factor and its log (P2P_STOCK_ENV),
+    RCCL's own unroll (P2P_RCCL_UNROLL=0) and no private INFO log
+    (P2P_RCCL_LOG=0), so the child runs the kernels, queues and logging the
+    reference's stock NCCL setup would."""
+    env = dict(os.environ if environ is None else environ)
+    orig = json.loads(env.get("P2P_STOCK_ENV") or "{}")
+    for k, v in orig.items():
+        if v is None:
+            env.pop(k, None)
+        else:
+            env[k] = v
+    env.update(P2P_RCCL_UNROLL="0", P2P_RCCL_LOG="0")
+    return env
+
+
+def reference_stock(nat, sess, args, dirs, iters) -> dict:
+    """--child ref-stock: the pair (self at N = 1) matrices by the reference's
+    methodology -- one communicator, host clock, a stream sync per message, no
+    warmup, no connection warm-up (p2p_matrix.cc:141-267) -- per direction
+    mode, `iters[d]` iterations per cell (those of reference_semantics)."""
+    n = sess.world
+    out = {}
+    for d in dirs:
+        r = json.loads(sess.run(mode="pair" if n > 1 else "self", dir=d, bytes=nat.parse_size(args.size),
+                                iters=int(iters[d]), warmup=0, timing="wallclock", verify=False, warm=False))
+        out[d] = dict(pair_matrix_summary(r, n), iters=int(iters[d]))
+    out["env"] = {k: os.environ.get(k) for k in ("GPU_MAX_HW_QUEUES", "RCCL_UNROLL_FACTOR", "NCCL_DEBUG",
+                                                 "P2P_RCCL_UNROLL", "P2P_RCCL_LOG")}
+    out["rccl_unroll"] = [c.get("unroll") for c in (json.loads(sess.link_reports())[0] or {}).get("comms", [])]
+    return out
 
 
 def steps_through(nat, isess, args, mode, size, batch, transport, recv_budget=0):
@@ -100,10 +138,15 @@ def child_main(args) -> int:
     if env.rank == 0:
         log("bench: child %s started" % args.child)
     try:
+        transport = "rccl" if args.child == REF_STOCK else args.child
         sess = nat.Session(env.rank, env.world, host=env.master_addr, port=args.child_port, device=device,
-                           transport=args.child, timeout_s=min(90.0, args.timeout))
-        budget = 0 if args.recv_budget.strip() in ("", "0") else nat.parse_size(args.recv_budget)
-        out = steps_through(nat, sess, args, args.mode, size, args.child_batch, args.child, budget)
+                           transport=transport, timeout_s=min(90.0, args.timeout))
+        if args.child == REF_STOCK:
+            iters = json.loads(args.child_ref_iters)
+            out = reference_stock(nat, sess, args, [d for d in ("uni", "bi") if d in iters], iters)
+        else:
+            budget = 0 if args.recv_budget.strip() in ("", "0") else nat.parse_size(args.recv_budget)
+            out = steps_through(nat, sess, args, args.mode, size, args.child_batch, args.child, budget)
         del sess
     except Exception as e:
         out = {"error": str(e)[:300], "transport": args.child}

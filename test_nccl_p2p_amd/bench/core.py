@@ -211,6 +211,7 @@ def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> thread
 # out.  The IPC comparisons and the xGMI pair sweep come after them and get
 # whatever is left.
 SECTION_SLICES = (("latency", 5.0), ("latency_preposted", 5.0), ("reference_semantics", 12.0),
+                  ("reference_semantics_stock", 12.0),
                   ("pair_serial_events", 12.0), ("allpairs_1g", 8.0), ("ring_256m", 5.0), ("ring_hop", 3.0),
                   ("pair_sweep_0_1", 10.0))
 

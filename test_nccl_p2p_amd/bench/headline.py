@@ -400,8 +400,10 @@ class HeadlineMixin:
             "matrix_transport": h.matrix_transport,
             "link_check": link_check(h.provenance.get("rank_links"), h.matrix_transport),
             "reference_semantics": None,
+            "reference_semantics_stock": None,
             "pair_serial_events": None,
             "method_ratio": None,
+            "method_ratio_stock": None,
             "concurrency_ratio": None,
             "extras": None,
             "ipc_transport": None,

@@ -17,7 +17,7 @@ import time
 
 import torch.distributed as dist
 
-from test_nccl_p2p_amd.bench.compare import steps_through
+from test_nccl_p2p_amd.bench.compare import REF_STOCK, steps_through, stock_env
 from test_nccl_p2p_amd.bench.core import (RESERVE_S, SECTION_SLICES, free_port, hang_requested, log, method_ratios,
                                           pair_matrix_summary, reserved_after)
 from test_nccl_p2p_amd.utils.proc import run_child
@@ -97,6 +97,8 @@ class SectionsMixin:
             active.add("latency_preposted")
         if args.ref_iters > 0:
             active |= {"reference_semantics", "pair_serial_events"}
+            if args.ref_stock and self.use_gpu:
+                active.add("reference_semantics_stock")
         if n > 1 and args.extras:
             active |= {"allpairs_1g", "ring_256m", "ring_hop"}
         if n > 1 and args.sweep:
@@ -193,13 +195,35 @@ class SectionsMixin:
                         method="ours on the reference's schedule: serial ordered pairs, 8 warmup iterations, hipEvent "
                                "timing, iterations posted back to back, the headline's posting, every delivery verified")
 
+        def reference_semantics_stock():
+            # The same matrices and iterations in a child per rank with the
+            # stock RCCL / HIP settings: the headline's process runs RCCL's
+            # kernels at unroll 4, 8 HW queues and RCCL's INFO log, which the
+            # reference's stock setup would not.
+            iters = {d: v["iters"] for d, v in ref.items() if d in dirs and isinstance(v, dict)}
+            r = self.child_job(REF_STOCK, ["--child-ref-iters", json.dumps(iters), "--hw-queues", "0"],
+                               env=stock_env())
+            if r is None or "error" in r:
+                return r
+            uni = (r.get("uni") or {}).get("gbs_mean")
+            return dict(r, size=self.size, comms=1, method=ref["method"] + "; stock RCCL / HIP settings",
+                        value_ratio=round(h.value / uni, 3) if uni else None)
+
         self.log0("bench: reference-method matrices")
         ref = self.section("reference_semantics", reference_semantics, 5.0)
         self.reporter.update(reference_semantics=ref)
+        if args.ref_stock and isinstance(ref, dict) and "error" not in ref and self.use_gpu:
+            self.log0("bench: reference-method matrices, stock settings (child)")
+            stock = self.section("reference_semantics_stock", reference_semantics_stock, 5.0, sessions=False)
+            self.reporter.update(reference_semantics_stock=stock)
+        else:
+            stock = None
         ours = self.section("pair_serial_events", pair_serial_events, 5.0)
         ratios = method_ratios(ours if isinstance(ours, dict) else None, ref if isinstance(ref, dict) else None,
                                h.value, n)
-        self.reporter.update(pair_serial_events=ours, **ratios)
+        stock_ratios = method_ratios(ours if isinstance(ours, dict) else None,
+                                     stock if isinstance(stock, dict) else None, h.value, n)
+        self.reporter.update(pair_serial_events=ours, method_ratio_stock=stock_ratios["method_ratio"], **ratios)
 
     def extras_sections(self):
         """The other BASELINE.json configs, measured after the timed region so
@@ -294,23 +318,31 @@ class SectionsMixin:
         kernels, relays) across GPUs; if one of them faults or hangs on some
         node, only the child dies, and the headline line still gets printed
         with the error in its place."""
+        args = self.args
+        extra = ["--mode", self.mode, "--steps", str(args.steps), "--warmup", str(args.warmup),
+                 "--msgs", str(args.msgs), "--latency-iters", str(args.latency_iters),
+                 "--latency-size", args.latency_size, "--child-batch", str(int(self.h.batch)),
+                 "--recv-budget", str(int(recv_budget))]
+        if args.no_verify:
+            extra.append("--no-verify")
+        return self.child_job(transport, extra)
+
+    def child_job(self, child, extra, env=None):
+        """bench.py --child `child` on every rank (its own TCP bootstrap on a
+        port rank 0 picks), bounded by the time left; rank 0 returns the
+        child's JSON (an error record if it wrote none), the others None."""
         args, n, rank = self.args, self.n, self.env.rank
         box = [free_port() if rank == 0 else None]
         if n > 1:
             dist.broadcast_object_list(box, src=0)
         out_path = os.path.join(tempfile.gettempdir(), "p2p_bench_child_%d_%d.json" % (box[0], rank))
         limit = min(args.child_timeout, max(5.0, self.budget_left()))
-        cmd = [sys.executable, os.path.join(HERE, "bench.py"), "--gpus", str(n), "--steps", str(args.steps),
-               "--warmup", str(args.warmup), "--size", args.size, "--msgs", str(args.msgs), "--mode", self.mode,
-               "--latency-iters", str(args.latency_iters), "--latency-size", args.latency_size,
-               "--child", transport, "--child-port", str(box[0]), "--child-out", out_path,
-               "--child-batch", str(int(self.h.batch)), "--recv-budget", str(int(recv_budget)),
-               "--timeout", str(max(5.0, min(args.timeout, limit)))]
-        if args.no_verify:
-            cmd.append("--no-verify")
+        cmd = [sys.executable, os.path.join(HERE, "bench.py"), "--gpus", str(n), "--size", args.size,
+               "--child", child, "--child-port", str(box[0]), "--child-out", out_path,
+               "--timeout", str(max(5.0, min(args.timeout, limit)))] + list(extra)
         if args.device is not None:
             cmd += ["--device", str(args.device)]
-        rc = run_child(self.state, cmd, limit)
+        rc = run_child(self.state, cmd, limit, env=env)
         self.barrier()
         res = None
         if rank == 0:
@@ -318,7 +350,7 @@ class SectionsMixin:
                 with open(out_path) as f:
                     res = json.load(f)
             except (OSError, ValueError):
-                res = {"error": "comparison process failed (exit status %s)" % rc, "transport": transport}
+                res = {"error": "child process failed (exit status %s)" % rc, "transport": child}
         try:
             os.unlink(out_path)
         except OSError:

@@ -192,3 +192,23 @@ def test_link_check_flags_direct_xgmi_pairs_not_on_p2p():
     emu = bench.link_check([["same-gpu"] * 2] * 2, [["self", "NET"], ["NET", "self"]])
     assert emu == {"direct_xgmi_pairs": 0, "not_p2p": [], "ok": True}
     assert bench.link_check(None, t) is None and bench.link_check(links, None) is None
+
+
+def test_stock_env_restores_what_bench_changed():
+    """reference_semantics_stock's child environment: the queue count, RCCL's
+    unroll factor and log settings as bench.py found them at start, RCCL's own
+    unroll and no private INFO log."""
+    import json
+
+    from test_nccl_p2p_amd.bench.compare import stock_env
+
+    env = {"GPU_MAX_HW_QUEUES": "8", "RCCL_UNROLL_FACTOR": "4", "NCCL_DEBUG": "INFO",
+           "NCCL_DEBUG_FILE": "/tmp/p2p_rccl_info_1.log", "NCCL_DEBUG_SUBSYS": "INIT,P2P", "OTHER": "x",
+           "P2P_STOCK_ENV": json.dumps({"GPU_MAX_HW_QUEUES": "4", "RCCL_UNROLL_FACTOR": None, "NCCL_DEBUG": "VERSION",
+                                        "NCCL_DEBUG_FILE": None, "NCCL_DEBUG_SUBSYS": None})}
+    s = stock_env(env)
+    assert s["GPU_MAX_HW_QUEUES"] == "4" and s["NCCL_DEBUG"] == "VERSION" and s["OTHER"] == "x"
+    for k in ("RCCL_UNROLL_FACTOR", "NCCL_DEBUG_FILE", "NCCL_DEBUG_SUBSYS"):
+        assert k not in s
+    assert s["P2P_RCCL_UNROLL"] == "0" and s["P2P_RCCL_LOG"] == "0"
+    assert env["RCCL_UNROLL_FACTOR"] == "4"  # the caller's mapping is left alone

@@ -157,3 +157,23 @@ def test_kernel_overlap_bursts_and_concurrency(tmp_path):
     assert first["span_ms"] == 0.15 and first["busy_ms"] == 0.15 and first["busy_fraction"] == 1.0
     assert first["mean_concurrency"] == round(200 / 150, 3)
     assert second["kernels"] == 1 and second["burst"] == 1
+
+
+def test_every_top_level_script_is_referenced():
+    """the top level of scripts/ holds only maintained
+    tooling -- each file is referenced by a test, the Makefile, README.md,
+    docs/, the package, bench.py or another maintained script; one-shot
+    probes live in scripts/probes/."""
+    import glob
+
+    sources = []
+    for pat in ("tests/*.py", "Makefile", "README.md", "docs/*.md", "bench.py", "__graft_entry__.py",
+                "test_nccl_p2p_amd/**/*.py", "scripts/*"):
+        sources += [p for p in glob.glob(os.path.join(ROOT, pat), recursive=True) if os.path.isfile(p)]
+    texts = {p: open(p, errors="replace").read() for p in sources}
+    for path in glob.glob(os.path.join(ROOT, "scripts", "*")):
+        if os.path.isdir(path):
+            continue
+        name = os.path.basename(path)
+        refs = [p for p, t in texts.items() if p != path and "scripts/" + name in t]
+        assert refs, "scripts/%s is referenced nowhere: move it to scripts/probes/" % name
