@@ -40,5 +40,7 @@ std::vector<std::string> rank_link_matrix(Bootstrap& boot, int device);
 std::string hip_runtime_json();
 std::string rccl_runtime_json();
 std::string device_pci_id(int device);  // "" when unknown
+// "<hostname>:<PCI bus id>" of a local GPU (Transport::device_key).
+std::string gpu_memory_key(int device);
 
 }  // namespace p2p

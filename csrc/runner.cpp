@@ -161,12 +161,23 @@ uint64_t generation_seed(int src, size_t bytes, uint64_t salt, int gen) {
   return payload_seed(src, bytes, gen == 0 ? salt : salt ^ (static_cast<uint64_t>(gen) << 40));
 }
 
+size_t shared_free_budget(Transport& t, Bootstrap& boot, size_t fallback, size_t cap) {
+  t.sync();
+  boot.barrier();
+  size_t free_b = 0, total_b = 0;
+  size_t budget = t.mem_info(&free_b, &total_b) ? std::min(free_b / 4, cap) : fallback;
+  const std::string key = t.device_key();
+  int sharing = 0;
+  for (const auto& k : boot.allgather_string(key)) sharing += !key.empty() && k == key;
+  budget /= static_cast<size_t>(std::max(1, sharing));
+  boot.barrier();  // every rank has read before any rank allocates
+  return budget;
+}
+
 int verify_generations(Transport& t, Bootstrap& boot, size_t max_bytes, int slots, int iters) {
   // One generation = a send region + `slots` receive slots.
   const size_t per_gen = slot_stride(max_bytes) * static_cast<size_t>(std::max(1, slots) + 1);
-  size_t budget = size_t{256} << 20;
-  size_t free_b = 0, total_b = 0;
-  if (t.mem_info(&free_b, &total_b)) budget = std::min(free_b / 4, size_t{32} << 30);
+  size_t budget = shared_free_budget(t, boot, size_t{256} << 20, size_t{32} << 30);
   if (const char* b = std::getenv("P2P_VERIFY_BUDGET")) budget = parse_size(b);
   long g = std::max(1, iters);
   g = std::min<long>(g, std::max<long>(1, static_cast<long>(budget / per_gen)));

@@ -149,6 +149,12 @@ void post_phase_iteration(Transport& t, const Phase& phase, size_t bytes, Buffer
 // quarter of free device memory, at most 32 GiB; 256 MiB where the transport
 // cannot tell), agreed by every rank (collective).
 int verify_generations(Transport& t, Bootstrap& boot, size_t max_bytes, int slots, int iters);
+// Collective: a quarter of this rank's GPU's free memory (at most `cap`;
+// `fallback` where the transport cannot tell), divided between the ranks that
+// share the GPU (Transport::device_key).  Every rank drains its stream and
+// meets a barrier before any reads the free memory, and another before any
+// allocates (ranks sharing a GPU read it while peers still freed).
+size_t shared_free_budget(Transport& t, Bootstrap& boot, size_t fallback, size_t cap);
 
 // Receive-slot / send-region stride for messages of `bytes` (4 KiB aligned).
 size_t slot_stride_bytes(size_t bytes);

@@ -52,10 +52,7 @@ std::vector<int> generation_sizes(const std::vector<std::vector<int>>& base) {
 int agreed_depth(Transport& t, Bootstrap& boot, const StepOptions& o, size_t per_gen_bytes) {
   long d = std::max(1, o.depth);
   size_t budget = o.recv_budget;
-  if (budget == 0) {
-    size_t free_b = 0, total_b = 0;
-    budget = t.mem_info(&free_b, &total_b) ? free_b / 4 : size_t{256} << 20;
-  }
+  if (budget == 0) budget = shared_free_budget(t, boot, size_t{256} << 20, SIZE_MAX);
   if (per_gen_bytes > 0) d = std::min<long>(d, std::max<long>(1, static_cast<long>(budget / per_gen_bytes)));
   return static_cast<int>(-boot.allreduce_max(-static_cast<double>(d)));
 }
@@ -123,6 +120,10 @@ void StepDriver::connect() {
 }
 
 void StepDriver::capture_graphs() {
+  // A recapture (rechunk fallback) replaces the graphs: the transport frees
+  // the old ones instead of keeping them until it is destroyed.
+  for (int h : graphs_)
+    if (h >= 0) t_.graph_release(h);
   graphs_.clear();
   for (int g = 0; g < depth_; ++g)
     for (size_t pi = 0; pi < sched_.phases.size(); ++pi) {

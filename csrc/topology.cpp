@@ -6,6 +6,7 @@
 // topology probe).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <string>
 #include <vector>
@@ -104,6 +105,13 @@ std::string device_pci_id(int device) {
   char pci[64] = {0};
   if (hipDeviceGetPCIBusId(pci, sizeof(pci), device) != hipSuccess) return "";
   return pci;
+}
+
+std::string gpu_memory_key(int device) {
+  char host[256] = {0};
+  if (gethostname(host, sizeof(host) - 1) != 0) host[0] = 0;
+  const std::string pci = device_pci_id(device);
+  return pci.empty() ? strfmt("%s:hip%d", host, device) : std::string(host) + ":" + pci;
 }
 
 }  // namespace p2p

@@ -37,6 +37,9 @@ class Transport {
   virtual int rank() const = 0;
   virtual int nranks() const = 0;
   virtual std::string device_desc() const { return ""; }
+  // Names the memory this rank allocates from: ranks with the same non-empty
+  // key share one GPU's HBM (host name + PCI bus id); "" for host memory.
+  virtual std::string device_key() const { return ""; }
 
   // ---- memory ----
   // Free / total device memory, when the transport knows it (sizing checks).
@@ -137,6 +140,9 @@ class Transport {
   virtual void capture_begin() {}
   virtual int capture_end() { return -1; }
   virtual void graph_launch(int /*handle*/) {}
+  // Frees a captured graph (its handle must not be launched again); after a
+  // drain of the stream that replays it.
+  virtual void graph_release(int /*handle*/) {}
 
   // ---- device-initiated ping-pong (one-sided transports) ----
   // pingpong_setup() is collective (every rank, same order).  Then both

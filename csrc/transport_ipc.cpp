@@ -59,6 +59,7 @@
 #include "common.hpp"
 #include "hip_check.hpp"
 #include "kernels.hpp"
+#include "provenance.hpp"
 #include "routing.hpp"
 #include "stream_gate.hpp"
 #include "transport.hpp"
@@ -130,7 +131,8 @@ class IpcTransport final : public Transport {
     if (sig_status_) (void)hipHostFree(sig_status_);
     if (ping_host_) (void)hipHostFree(ping_host_);
     drain_pool();
-    for (auto ex : execs_) (void)hipGraphExecDestroy(ex);
+    for (auto ex : execs_)
+      if (ex) (void)hipGraphExecDestroy(ex);
     for (auto s : side_) (void)hipStreamDestroy(s);
     for (auto e : side_done_) (void)hipEventDestroy(e);
     if (fork_) (void)hipEventDestroy(fork_);
@@ -144,6 +146,7 @@ class IpcTransport final : public Transport {
   int rank() const override { return rank_; }
   int nranks() const override { return n_; }
   std::string device_desc() const override { return desc_; }
+  std::string device_key() const override { return gpu_memory_key(device_); }
 
   bool mem_info(size_t* free_b, size_t* total_b) override {
     if (hipMemGetInfo(free_b, total_b) != hipSuccess) return false;
@@ -418,7 +421,16 @@ class IpcTransport final : public Transport {
     execs_.push_back(ex);
     return static_cast<int>(execs_.size()) - 1;
   }
-  void graph_launch(int h) override { HIPCHECK(hipGraphLaunch(execs_.at(static_cast<size_t>(h)), stream_)); }
+  void graph_launch(int h) override {
+    hipGraphExec_t ex = execs_.at(static_cast<size_t>(h));
+    P2P_CHECK(ex != nullptr, "graph_launch: the graph was released");
+    HIPCHECK(hipGraphLaunch(ex, stream_));
+  }
+  void graph_release(int h) override {
+    hipGraphExec_t& ex = execs_.at(static_cast<size_t>(h));
+    if (ex) HIPCHECK(hipGraphExecDestroy(ex));
+    ex = nullptr;
+  }
 
   // Signal pages: every rank owns one page of n + 1 inbox slots (slot r =
   // messages from rank r, slot n = replies of the self path), exported over

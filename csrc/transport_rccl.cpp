@@ -208,8 +208,10 @@ class RcclTransport final : public Transport {
     // Graphs that captured RCCL work hold references to the communicator's
     // persistent resources: release them before the communicator, or
     // ncclCommDestroy waits for them forever.
-    for (auto ex : execs_) (void)hipGraphExecDestroy(ex);
-    for (auto g : graphs_) (void)hipGraphDestroy(g);
+    for (auto ex : execs_)
+      if (ex) (void)hipGraphExecDestroy(ex);
+    for (auto g : graphs_)
+      if (g) (void)hipGraphDestroy(g);
     execs_.clear();
     graphs_.clear();
     for (auto& r : reg_sets_)
@@ -248,6 +250,7 @@ class RcclTransport final : public Transport {
   int rank() const override { return rank_; }
   int nranks() const override { return n_; }
   std::string device_desc() const override { return desc_; }
+  std::string device_key() const override { return gpu_memory_key(device_); }
 
   bool mem_info(size_t* free_b, size_t* total_b) override { return hipMemGetInfo(free_b, total_b) == hipSuccess; }
   void* alloc(size_t bytes) override {
@@ -483,7 +486,21 @@ class RcclTransport final : public Transport {
     execs_.push_back(ex);
     return static_cast<int>(execs_.size()) - 1;
   }
-  void graph_launch(int h) override { HIPCHECK(hipGraphLaunch(execs_.at(static_cast<size_t>(h)), stream_)); }
+  void graph_launch(int h) override {
+    hipGraphExec_t ex = execs_.at(static_cast<size_t>(h));
+    P2P_CHECK(ex != nullptr, "graph_launch: the graph was released");
+    HIPCHECK(hipGraphLaunch(ex, stream_));
+  }
+  // The executable graph and the graph that captured RCCL work (both hold
+  // references to the communicator's resources, see the destructor).
+  void graph_release(int h) override {
+    hipGraphExec_t& ex = execs_.at(static_cast<size_t>(h));
+    hipGraph_t& g = graphs_.at(static_cast<size_t>(h));
+    if (ex) HIPCHECK(hipGraphExecDestroy(ex));
+    if (g) HIPCHECK(hipGraphDestroy(g));
+    ex = nullptr;
+    g = nullptr;
+  }
 
   void sync() override {
     // Bounded poll instead of hipStreamSynchronize: spins for the first 20 ms

@@ -137,6 +137,29 @@ def test_every_timed_iteration_is_verified(mpirun, host_build, tmp_path):
     assert abs(uni["verify_coverage"] - 1 / 3) < 1e-6 and uni["verified_msgs"] == 4
 
 
+def test_default_run_verifies(mpirun, host_build, tmp_path):
+    """`mpirun -n N ./p2p_matrix` with no flags verifies
+    every timed delivery (outside the timed loop): an injected skip-some
+    fault exits 2 without --verify, the JSON carries verify_coverage, the
+    compat-only output is the reference's bytes alone, and --no-verify opts
+    out (nothing checked, exit 0 despite the fault)."""
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    for transport in ("host", "shm"):
+        js = tmp_path / ("%s.json" % transport)
+        out = run(mpirun, exe, 2, ["--transport", transport, "--size", "64K", "-n", "6", "-w", "2", "--json", str(js)],
+                  env={"P2P_INJECT_FAULT": "skip-some@1"})
+        assert out.returncode == 2, (transport, out.stderr[-2000:])
+        assert "VERIFICATION FAILED" in out.stderr and "verification: FAILED" in out.stdout
+        runs = [json.loads(l) for l in js.read_text().splitlines() if '"type":"run"' in l]
+        assert runs and all(r["verify_coverage"] == 1 for r in runs)
+    ok = run(mpirun, exe, 2, ["--transport", "shm", "--size", "64K", "-n", "4", "--compat-only"])
+    assert ok.returncode == 0 and "verification" not in ok.stdout
+    assert ok.stdout.startswith("Evaluating the Uni-Directional NCCL P2P Bandwidth (Gbps)\n")
+    off = run(mpirun, exe, 2, ["--transport", "shm", "--size", "64K", "-n", "6", "-w", "2", "--no-verify"],
+              env={"P2P_INJECT_FAULT": "skip-some@1"})
+    assert off.returncode == 0 and "verification:" not in off.stdout, off.stderr[-2000:]
+
+
 def test_json_provenance_and_ring_token(mpirun, host_build, tmp_path):
     """--json starts with the provenance record (knobs, runtime, every rank's
     device and the links between them); --mode ring --latency adds the
