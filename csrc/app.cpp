@@ -44,8 +44,9 @@ timing
   -w, --warmup N         untimed iterations per cell                          [8]
       --timing MODE      events    hipEvents, back-to-back messages, 1 sync  [events]
                          wallclock reference semantics: host clock, sync per message
-      --reference        = --timing wallclock --warmup 0 --no-warm --two-streams
-                         (the reference's methodology, p2p_matrix.cc:141-267)
+      --reference        = --timing wallclock --warmup 0 --no-warm --two-streams, and RCCL's
+                         own kernel unroll (P2P_RCCL_UNROLL is not applied): the reference's
+                         methodology on a stock RCCL setup, p2p_matrix.cc:141-267
       --two-streams      RCCL: receives on a second stream, like the reference's s_1
       --comms K          RCCL: K communicators per rank on K streams; the i-th message
                          of >= 1 MiB from a to b uses communicator (i + a + b) mod K on both
@@ -224,6 +225,7 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
       cfg->run.warmup = 0;
       cfg->warm_connections = false;
       cfg->two_streams = true;
+      cfg->rccl_stock = true;
     } else if (a == "--two-streams") {
       cfg->two_streams = true;
     } else if (a == "--comms") {
@@ -379,6 +381,7 @@ std::unique_ptr<Transport> open_transport(const AppConfig& cfg, Bootstrap& boot,
   topt->ipc_engine = cfg.ipc_engine;
   topt->two_streams = cfg.two_streams;
   topt->rccl_comms = cfg.comms;
+  topt->rccl_stock = cfg.rccl_stock;
   return cfg.transport == "host"  ? make_host_transport(boot, *topt)
          : cfg.transport == "shm" ? make_shm_transport(boot, *topt)
          : cfg.transport == "ipc" ? make_ipc_transport(boot, *topt)

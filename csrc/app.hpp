@@ -52,6 +52,7 @@ struct AppConfig {
   bool warm_connections = true;
   double min_gbs = 0;          // link check: any off-diagonal flow below this fails the run (exit 3)
   bool two_streams = false;  // RCCL receives on a second stream (reference layout)
+  bool rccl_stock = false;   // --reference: RCCL's own kernel unroll (no P2P_RCCL_UNROLL)
   int comms = 1;             // RCCL communicators per rank (messages spread round-robin)
   int verbose = 0;
 };

@@ -251,6 +251,7 @@ struct TransportOptions {
   std::string ipc_engine = "kernel";
   bool two_streams = false;        // RCCL: receives on a second stream (reference layout)
   int rccl_comms = 1;              // RCCL: communicators per rank, messages spread over them (P2P_RCCL_COMMS)
+  bool rccl_stock = false;         // RCCL: leave its kernel unroll alone (--reference)
 };
 
 // HIP + RCCL on the local MI355X.  Defined in transport_rccl.cpp (hipcc).

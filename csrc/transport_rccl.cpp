@@ -626,7 +626,7 @@ class RcclTransport final : public Transport {
     // initialises its logging too): point its INFO log at our file, and pick
     // the kernels' unroll factor.
     rccl_log();
-    rccl_unroll_setup();
+    if (!opt.rccl_stock) rccl_unroll_setup();
     // P2P_RCCL_DISTINCT_HOSTS=1 (tests on one GPU): every rank tells RCCL it
     // is on a host of its own (NCCL_HOSTID, read when RCCL first hashes the
     // host), so several ranks may share one GPU -- RCCL refuses duplicate GPUs

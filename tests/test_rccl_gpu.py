@@ -269,6 +269,24 @@ def test_chunk_sizes_follow_the_channel_knobs():
         assert line == " ".join([src, str(ch), str(want), "True", str(8 << 20), str(want)]), (env, line)
 
 
+def test_reference_mode_keeps_rccl_stock_unroll(tmp_path):
+    """p2p_matrix --reference runs the reference's methodology on a stock
+    RCCL setup: RCCL's own unroll (1 on MI355X), not the unroll 4 the
+    default run asks for; RCCL's log says which ran."""
+    from conftest import ensure_built
+    ensure_built("gpu")
+    exe = os.path.join(ROOT, "build", "p2p_matrix")
+    got = {}
+    for flag in ("--reference", None):
+        js = tmp_path / ("r%s.json" % bool(flag))
+        cmd = [exe, "--mode", "self", "--size", "4M", "-n", "4", "--no-compat", "--json", str(js), "--timeout", "60"]
+        out = subprocess.run(cmd + ([flag] if flag else []), capture_output=True, text=True, timeout=120, cwd=ROOT)
+        assert out.returncode == 0, out.stderr[-2000:]
+        links = [json.loads(l) for l in js.read_text().splitlines() if '"type":"links"' in l][0]
+        got[flag] = links["ranks"][0]["comms"][0]["unroll"]
+    assert got == {"--reference": 1, None: 4}, got
+
+
 def test_rccl_unroll_factor():
     """The transport asks RCCL for unroll-4 kernels (+7% on the bench step,
     +22% on one communicator's step, profiles/r3_unroll/) and RCCL's own log
