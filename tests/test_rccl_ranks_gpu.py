@@ -82,6 +82,16 @@ def test_bench_four_rccl_ranks(tmp_path):
         assert r[key]["uni"]["gbs_mean"] > 0 and r[key]["bi"]["gbs_mean"] > 0, r[key]
     assert r["pair_serial_events"]["bi"]["mismatches"] == 0 and r["concurrency_ratio"] > 0
     assert r["method_ratio"]["uni"] > 0 and r["method_ratio"]["bi"] > 0
+    # Op limits per peer from RCCL's connection lines after the warm-up
+    # (VERDICT r3 item 3): NET peers, 2 channels connected, 32 MiB ops.
+    for rep in r["provenance"]["rccl_peers"]:
+        assert rep["refinements"] >= 1, rep
+        for p in rep["peers"]:
+            if p["peer"] == rep["rank"]:
+                assert p["op_limit_source"] == "init line", p
+            else:
+                assert p["op_limit_source"] == "connection lines" and p["channels_connected"] == 2, p
+                assert p["op_limit"] == 32 << 20, p
 
 
 @pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
