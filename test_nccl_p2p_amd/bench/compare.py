@@ -44,7 +44,6 @@ def reference_stock(nat, sess, args, dirs, iters) -> dict:
         out[d] = dict(pair_matrix_summary(r, n), iters=int(iters[d]))
     out["env"] = {k: os.environ.get(k) for k in ("GPU_MAX_HW_QUEUES", "RCCL_UNROLL_FACTOR", "NCCL_DEBUG",
                                                  "P2P_RCCL_UNROLL", "P2P_RCCL_LOG")}
-    out["rccl_unroll"] = [c.get("unroll") for c in (json.loads(sess.link_reports())[0] or {}).get("comms", [])]
     return out
 
 

@@ -77,6 +77,14 @@ def test_bench_contract_single_gpu():
     assert ipc["verify_mismatches"] == 0 and ipc["value_gbs"] > 0, ipc
     assert ipc["push"]["verify_mismatches"] == 0 and ipc["sdma"]["verify_mismatches"] == 0, ipc
     assert 0 < ipc["device_pingpong_p50_us"] < 50, ipc
+    # The reference's methodology twice on the self cell: in this process
+    # (RCCL unroll 4, 8 HW queues, INFO log) and in a child with the stock
+    # settings, same iterations; both method ratios reported.
+    ref, stock = r["reference_semantics"], r["reference_semantics_stock"]
+    assert stock["uni"]["iters"] == ref["uni"]["iters"] and stock["uni"]["gbs_mean"] > 0, stock
+    assert stock["env"]["P2P_RCCL_UNROLL"] == "0" and stock["env"]["RCCL_UNROLL_FACTOR"] is None, stock
+    assert stock["env"]["GPU_MAX_HW_QUEUES"] in (None, "4"), stock
+    assert r["method_ratio_stock"]["uni"] > 0 and r["method_ratio"]["uni"] > 0
 
 
 def test_topology_probe(exe):
@@ -133,7 +141,8 @@ def test_bench_drops_a_failing_communicator_candidate():
     eight with bench.py's 8 hardware queues) instead; with one warmup step it
     falls back the same way."""
     for warmup in ("1", "4"):
-        out = subprocess.run([sys.executable, "bench.py", "--steps", "4", "--warmup", warmup, "--latency-iters", "20"],
+        out = subprocess.run([sys.executable, "bench.py", "--steps", "4", "--warmup", warmup, "--latency-iters", "20",
+                              "--ref-stock", "0"],
                              capture_output=True, text=True, timeout=600, cwd=ROOT,
                              env=dict(os.environ, P2P_BENCH_FAIL_CANDIDATE="4,1"))
         assert out.returncode == 0, out.stderr[-3000:]
