@@ -208,7 +208,12 @@ class HeadlineMixin:
         matrix, samples, cells = cell_matrix(n, steps, drv.phase_flows, all_ms, size * args.msgs)
         offdiag = [matrix[s][d] for (s, d) in cells if s != d or n == 1]
 
+        # The post-timing check of every slot a timed step wrote (batched:
+        # Transport::verify_many), timed for the record (verify_detail.seconds).
+        v0 = time.perf_counter()
         vr = drv.verify_steps(args.warmup, args.steps) if not args.no_verify else None
+        if vr is not None:
+            vr["seconds"] = round(time.perf_counter() - v0, 4)
         depth, recv_bytes = drv.depth, drv.recv_bytes
         # Everything after this is untimed; release the timed driver's buffers
         # first so the comparisons run on the same memory footprint as the
