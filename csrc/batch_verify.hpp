@@ -6,12 +6,24 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "kernels.hpp"
 #include "transport.hpp"
 
 namespace p2p {
+
+// P2P_VERIFY_BATCH=0: the one-buffer-at-a-time check (the A/B of round 3's
+// post-timing verification against the batched one).
+inline bool batch_verify_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("P2P_VERIFY_BATCH");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
+}
 
 // Transport::verify_many through dev::BatchVerifier on `stream`; `sync` waits
 // for the stream the transport's way (bounded, abort-aware).

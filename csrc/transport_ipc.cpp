@@ -217,7 +217,7 @@ class IpcTransport final : public Transport {
   }
   std::vector<VerifyResult> verify_many(const std::vector<VerifyJob>& jobs) override {
     if (jobs.empty()) return {};
-    if (verify_impl_ != dev::VerifyImpl::Auto && verify_impl_ != dev::VerifyImpl::Lds8)
+    if ((verify_impl_ != dev::VerifyImpl::Auto && verify_impl_ != dev::VerifyImpl::Lds8) || !batch_verify_enabled())
       return Transport::verify_many(jobs);
     return batch_verify(batch_, jobs, stream_, [this] { sync(); });
   }

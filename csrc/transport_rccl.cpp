@@ -326,7 +326,7 @@ class RcclTransport final : public Transport {
     if (jobs.empty()) return {};
     // The batched kernel is the default LDS8 verify; another --verify-impl
     // keeps the one-buffer path.
-    if (verify_impl_ != dev::VerifyImpl::Auto && verify_impl_ != dev::VerifyImpl::Lds8)
+    if ((verify_impl_ != dev::VerifyImpl::Auto && verify_impl_ != dev::VerifyImpl::Lds8) || !batch_verify_enabled())
       return Transport::verify_many(jobs);
     buffer_work();
     return batch_verify(batch_, jobs, stream_, [this] { sync(); });

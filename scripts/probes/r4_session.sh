@@ -11,6 +11,9 @@ for i in 1 2; do
   timeout -k 10 300 python bench.py > "$O/bench_default_$i.json" 2> "$O/bench_default_$i.err"; ok $?
   P2P_RCCL_LOG=0 timeout -k 10 300 python bench.py > "$O/bench_log0_$i.json" 2> "$O/bench_log0_$i.err"; ok $?
 done
+# The post-timing verification one buffer at a time (round 3's way), for
+# verify_detail.seconds against the batched default above.
+P2P_VERIFY_BATCH=0 timeout -k 10 300 python bench.py > "$O/bench_verify_unbatched.json" 2> "$O/bench_verify_unbatched.err"; ok $?
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o bench -- \
   python3 bench.py --steps 20 --warmup 5 > "$O/prof_bench.json" 2> "$O/prof_bench.err"; ok $?
