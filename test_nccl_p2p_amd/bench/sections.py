@@ -97,7 +97,7 @@ class SectionsMixin:
             active.add("latency_preposted")
         if args.ref_iters > 0:
             active |= {"reference_semantics", "pair_serial_events"}
-            if args.ref_stock and self.use_gpu:
+            if self.stock_reference_planned():
                 active.add("reference_semantics_stock")
         if n > 1 and args.extras:
             active |= {"allpairs_1g", "ring_256m", "ring_hop"}
@@ -106,6 +106,22 @@ class SectionsMixin:
         self.active_sections = active
         self.slice_left, self.slice_t0 = 0.0, time.monotonic()
         self.broken = None
+
+    # At most this many processes may hold one GPU (the test boxes' limit is
+    # 16, pytest included): a child per rank doubles the ranks on a GPU.
+    MAX_PROCS_PER_GPU = 15
+
+    def stock_reference_planned(self) -> bool:
+        """reference_semantics_stock runs for an RCCL headline (the stock
+        settings are RCCL's and HIP's), when a child per rank still leaves
+        the GPU within MAX_PROCS_PER_GPU processes (same answer on every
+        rank: the provenance is shared)."""
+        if not (self.args.ref_stock and self.args.ref_iters > 0 and self.transport_used == "rccl" and self.use_gpu):
+            return False
+        devs = (self.h.provenance or {}).get("rank_devices") or []
+        keys = [d.get("pci") or "dev%s" % d.get("device") for d in devs]
+        per_gpu = max([keys.count(k) for k in keys] or [self.n])
+        return 2 * per_gpu <= self.MAX_PROCS_PER_GPU
 
     def latency_sections(self):
         """Host-posted ping-pong through the headline session, then the same
@@ -212,7 +228,7 @@ class SectionsMixin:
         self.log0("bench: reference-method matrices")
         ref = self.section("reference_semantics", reference_semantics, 5.0)
         self.reporter.update(reference_semantics=ref)
-        if args.ref_stock and isinstance(ref, dict) and "error" not in ref and self.use_gpu:
+        if self.stock_reference_planned() and isinstance(ref, dict) and "error" not in ref:
             self.log0("bench: reference-method matrices, stock settings (child)")
             stock = self.section("reference_semantics_stock", reference_semantics_stock, 5.0, sessions=False)
             self.reporter.update(reference_semantics_stock=stock)

@@ -212,3 +212,25 @@ def test_stock_env_restores_what_bench_changed():
         assert k not in s
     assert s["P2P_RCCL_UNROLL"] == "0" and s["P2P_RCCL_LOG"] == "0"
     assert env["RCCL_UNROLL_FACTOR"] == "4"  # the caller's mapping is left alone
+
+
+def test_stock_reference_only_for_rccl_within_the_process_limit():
+    """reference_semantics_stock starts a child per rank: planned for an RCCL
+    headline only, and only while two processes per rank sharing a GPU stay
+    within the box's limit (8 ranks on one GPU + 8 children + pytest = 17 was
+    killed by the process guard)."""
+    import types
+
+    from test_nccl_p2p_amd.bench.sections import SectionsMixin
+
+    def run(transport, pcis, ref_stock=1):
+        o = SectionsMixin()
+        o.args = types.SimpleNamespace(ref_stock=ref_stock, ref_iters=128)
+        o.transport_used, o.use_gpu, o.n, o.device = transport, True, len(pcis), 0
+        o.h = types.SimpleNamespace(provenance={"rank_devices": [{"rank": r, "device": 0, "pci": p}
+                                                                 for r, p in enumerate(pcis)]})
+        return o.stock_reference_planned()
+
+    assert run("rccl", ["a"]) and run("rccl", ["a", "b", "c", "d", "e", "f", "g", "h"])
+    assert run("rccl", ["a"] * 4) and not run("rccl", ["a"] * 8)
+    assert not run("ipc", ["a"]) and not run("rccl", ["a"], ref_stock=0)
