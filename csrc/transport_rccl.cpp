@@ -81,12 +81,56 @@ namespace {
 // first transport of the process points it at a private file before RCCL's
 // first initialisation reads the variables; the file is removed at exit
 // (P2P_RCCL_LOG=keep keeps it).  Empty path: no log to read.
+//
+// What this process sets in its environment for RCCL (the private log's
+// NCCL_DEBUG* below and RCCL_UNROLL_FACTOR) is inherited by every child it
+// starts: bench.py's comparison children, a test's p2p_matrix.  Each setting
+// is made by set_owned(), which records the value it replaced
+// (P2P_RCCL_PREV_<name>: "=<value>", or "" for unset) and this pid
+// (P2P_RCCL_ENV_OWNER).  A process that finds another pid's settings puts the
+// replaced values back before it decides anything, so a child never writes
+// RCCL's log into its parent's file or mistakes the parent's unroll for the
+// user's (profiles/r4_session: p2p_matrix --reference under pytest ran at the
+// parent's unroll 4).
+constexpr const char* kOwnedVars[] = {"NCCL_DEBUG", "NCCL_DEBUG_SUBSYS", "NCCL_DEBUG_FILE", "RCCL_UNROLL_FACTOR"};
+
+void undo_inherited_rccl_env() {
+  static const bool done = [] {
+    const char* owner = std::getenv("P2P_RCCL_ENV_OWNER");
+    if (!owner || std::atoi(owner) == static_cast<int>(getpid())) return true;
+    for (const char* k : kOwnedVars) {
+      const std::string saved = strfmt("P2P_RCCL_PREV_%s", k);
+      const char* v = std::getenv(saved.c_str());
+      if (!v) continue;
+      if (*v == '=')
+        setenv(k, v + 1, 1);
+      else
+        unsetenv(k);
+      unsetenv(saved.c_str());
+    }
+    unsetenv("P2P_RCCL_ENV_OWNER");
+    return true;
+  }();
+  (void)done;
+}
+
+void set_owned(const char* name, const char* value) {
+  const std::string saved = strfmt("P2P_RCCL_PREV_%s", name);
+  if (!std::getenv(saved.c_str())) {
+    const char* prev = std::getenv(name);
+    setenv(saved.c_str(), prev ? (std::string("=") + prev).c_str() : "", 1);
+  }
+  setenv(name, value, 1);
+  setenv("P2P_RCCL_ENV_OWNER", std::to_string(static_cast<int>(getpid())).c_str(), 1);
+}
+
 struct RcclLog {
   std::string path;
   bool ours = false;
 };
 RcclLog& rccl_log() {
   static RcclLog log = [] {
+    undo_inherited_rccl_env();
     RcclLog l;
     const char* mode = std::getenv("P2P_RCCL_LOG");
     if (mode && std::strcmp(mode, "0") == 0) return l;
@@ -102,9 +146,9 @@ RcclLog& rccl_log() {
     const char* tmp = std::getenv("TMPDIR");
     l.path = strfmt("%s/p2p_rccl_info_%d.log", tmp && *tmp ? tmp : "/tmp", static_cast<int>(getpid()));
     l.ours = true;
-    setenv("NCCL_DEBUG", "INFO", 1);
-    if (!std::getenv("NCCL_DEBUG_SUBSYS")) setenv("NCCL_DEBUG_SUBSYS", "INIT,ENV,P2P,NET,SHM", 1);
-    setenv("NCCL_DEBUG_FILE", l.path.c_str(), 1);
+    set_owned("NCCL_DEBUG", "INFO");
+    if (!std::getenv("NCCL_DEBUG_SUBSYS")) set_owned("NCCL_DEBUG_SUBSYS", "INIT,ENV,P2P,NET,SHM");
+    set_owned("NCCL_DEBUG_FILE", l.path.c_str());
     if (!(mode && std::strcmp(mode, "keep") == 0))
       std::atexit([] { std::remove(rccl_log().path.c_str()); });
     return l;
@@ -123,10 +167,11 @@ RcclLog& rccl_log() {
 // RCCL's log confirms it per communicator (link_report comms[].unroll).
 void rccl_unroll_setup() {
   static const bool done = [] {
+    undo_inherited_rccl_env();
     if (std::getenv("RCCL_UNROLL_FACTOR")) return true;
     const char* want = std::getenv("P2P_RCCL_UNROLL");
     const std::string v = want ? want : "4";
-    if (v != "0" && !v.empty()) setenv("RCCL_UNROLL_FACTOR", v.c_str(), 0);
+    if (v != "0" && !v.empty()) set_owned("RCCL_UNROLL_FACTOR", v.c_str());
     return true;
   }();
   (void)done;
