@@ -123,6 +123,7 @@ environment (recorded in every --json provenance record; docs/OUTPUT.md)
   P2P_SDMA_STREAMS=K     --ipc-engine sdma: side streams the receives share      [4]
   P2P_BOOTSTRAP_PORT, P2P_BOOTSTRAP_TIMEOUT   TCP bootstrap port / receive deadline
   P2P_HOSTNAME=name      hostname for the placement check (emulated hosts)
+  P2P_DEVICE=N           default of --device
   P2P_INJECT_FAULT=kind@rank[:phase]   corrupt | exit | hang | skip | skip-some (tests)
   P2P_ROCTX=1, P2P_LOG=1 roctx ranges; engine log on stderr
 )";
@@ -154,6 +155,9 @@ std::vector<Mode> parse_modes(const std::string& s) {
 bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out) {
   *exit_code = 0;
   bool size_given = false;
+  // P2P_DEVICE: the default of --device (a multi-GPU rehearsal on one GPU
+  // puts every rank on device 0 without editing the command lines).
+  if (const char* d = std::getenv("P2P_DEVICE"); d && *d) cfg->device = std::atoi(d);
   for (int i = 0; i < argc; ++i) {
     std::string a = argv[i];
     std::string val;

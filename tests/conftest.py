@@ -36,6 +36,12 @@ def _gpu_count() -> int:
 
 def pytest_sessionstart(session):
     _SESSION_T0[0] = time.monotonic()
+    if os.environ.get("P2P_REHEARSE_MULTI_GPU"):
+        # tests/test_multi_gpu.py rehearsed on one GPU: every rank on device 0
+        # (p2p_matrix: P2P_DEVICE; bench.py: LOCAL_RANK mod the visible GPUs;
+        # the fuzz script: P2P_FUZZ_DEVICE), each rank an RCCL host of its own.
+        os.environ.update(P2P_DEVICE="0", P2P_FUZZ_DEVICE="0", P2P_RCCL_DISTINCT_HOSTS="1",
+                          NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
 
 
 def pytest_configure(config):
