@@ -174,7 +174,7 @@ def test_bench_two_gpus_pair_sweep():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2", "--steps", "14", "--warmup", "7",
            "--deadline", "75", "--sweep-max", "256M", "--xgmi-sweep-sizes", "32M", "--ipc-extra", "0",
-           "--timeout", "45"] + BENCH_MSGS
+           "--timeout", "45"] + BENCH_MSGS + (["--xgmi-sweep", "1"] if REHEARSAL else [])
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=BUDGET_S["test_bench_two_gpus_pair_sweep"],
                          cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
