@@ -168,17 +168,21 @@ def test_cli_fuzz_relay_all_gpus(exe):
 
 
 def test_bench_two_gpus_pair_sweep():
-    """The driver's N = 2 bench on two distinct GPUs: after the other sections
-    the time left goes to the xGMI pair sweep (on by default there), whose
-    rows cross the real link, every one verified."""
+    """The driver's N = 2 bench on two distinct GPUs: the time left after the
+    other sections goes to the xGMI pair sweep (on by default there), whose
+    rows cross the real link, every one verified.  The other untimed sections
+    are off here (test_bench_all_gpus runs them), so the sweep has the time:
+    the one-GPU rehearsal with them on skipped it for lack of time."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2", "--steps", "14", "--warmup", "7",
-           "--deadline", "75", "--sweep-max", "256M", "--xgmi-sweep-sizes", "32M", "--ipc-extra", "0",
+           "--deadline", "75", "--xgmi-sweep-sizes", "32M", "--ipc-extra", "0", "--extras", "0", "--sweep", "0",
+           "--ref-iters", "0", "--latency-preposted", "0", "--latency-iters", "50",
            "--timeout", "45"] + BENCH_MSGS + (["--xgmi-sweep", "1"] if REHEARSAL else [])
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=BUDGET_S["test_bench_two_gpus_pair_sweep"],
                          cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     sw = r["xgmi_pair_sweep"]
+    assert sw is not None, (r["untimed_skipped"], out.stderr[-2000:])
     assert sw["emulated"] == ("rccl" if REHEARSAL else None) and sw["rows"]["rccl-comms1"]["rc"] == 0, sw
     assert sw["best"] and sw["best_rccl"], sw
