@@ -82,26 +82,27 @@ def test_pair_sweep_resume_keeps_finished_rows(mpirun, host_build, tmp_path):
 
 def measured_single_gpu_tier_s():
     """Duration of the single-GPU tier as measured on a one-GPU MI355X box:
-    the final line of every profiles/*/pytest_gpu*.log of the current suite
-    size (the logs with the most collected GPU tests), worst case."""
+    the final line of every profiles/r<k>*/pytest_gpu*.log of the latest
+    round k that has one (a whole tier, not a failed run), worst case."""
     import glob
     import re
 
     runs = []
-    for path in glob.glob(os.path.join(ROOT, "profiles", "*", "pytest_gpu*.log")):
+    for path in glob.glob(os.path.join(ROOT, "profiles", "r*", "pytest_gpu*.log")):
+        rnd = re.match(r"r(\d+)", os.path.basename(os.path.dirname(path)))
         with open(path) as f:
             lines = [l for l in f.read().splitlines() if l.strip()]
-        m = re.search(r"(\d+) passed(?:, (\d+) skipped)?.* in ([\d.]+)s", lines[-1] if lines else "")
-        if m and "failed" not in lines[-1]:
-            runs.append((int(m.group(1)) + int(m.group(2) or 0), float(m.group(3)), path))
+        m = re.search(r"(\d+) passed.* in ([\d.]+)s", lines[-1] if lines else "")
+        if rnd and m and "failed" not in lines[-1]:
+            runs.append((int(rnd.group(1)), float(m.group(2)), path))
     assert runs, "no measured GPU-tier log under profiles/"
-    size = max(r[0] for r in runs)
-    return max((r[1], r[2]) for r in runs if r[0] == size)
+    latest = max(r[0] for r in runs)
+    return max((r[1], r[2]) for r in runs if r[0] == latest)
 
 
 def test_multi_gpu_tier_fits_the_driver_step():
     """the driver runs `pytest -m gpu` in one 900 s step.
-    The measured single-GPU duration (worst run of the current suite) + every
+    The measured single-GPU duration (worst run of the latest round) + every
     multi-GPU test's worst-case budget (the sum of its subprocess limits) ends
     by conftest.SESSION_LIMIT_S, which leaves 60 s for the perf floors; the
     guard in conftest.py applies the same rule per test at run time."""

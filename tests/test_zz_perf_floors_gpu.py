@@ -125,13 +125,9 @@ def test_kernel_bandwidth_floors(native):
     assert rates["copy"] > 2.65, msg  # payload bytes (read once + written once)
 
 
-@pytest.mark.parametrize("transport,floor", [("rccl", 800.0), ("rccl:4", 1800.0)])
-def test_self_copy_rate_floor(native, transport, floor):
-    """The bench's step (32 MiB x 8 self messages in one group) through one
-    and four communicators, median GPU step time over 20 steps, against
-    floors at about 80% of the profiled rates (round 1: one communicator
-    ~950-1150 GB/s, four ~2300-2600 GB/s): a lost multi-communicator speedup
-    or a slower RCCL posting fails here."""
+def _self_step_gbs(native, transport):
+    """Median GB/s of the bench's step shape (32 MiB x 8 self messages in one
+    group) over 20 steps after 5 warm ones, and the per-step times."""
     s = native.Session(0, 1, device=0, transport=transport, timeout_s=120)
     d = native.StepDriver(s, "self", "bi", 32 << 20, 8, False, True, False)
     d.connect()
@@ -141,8 +137,23 @@ def test_self_copy_rate_floor(native, transport, floor):
     d.run_steps(5, 20)
     d.sync()
     ms = d.step_ms()
-    gbs = 8 * (32 << 20) / (statistics.median(ms) * 1e-3) / 1e9
-    _record("self_copy_rate_floor[%s]" % transport, {"gbs_median": gbs, "step_ms": ms})
-    print("%s: %.1f GB/s" % (transport, gbs))
     del d, s
-    assert gbs > floor, (gbs, ms)
+    return 8 * (32 << 20) / (statistics.median(ms) * 1e-3) / 1e9, ms
+
+
+def test_self_copy_rate_floors(native):
+    """The RCCL self step through one and four communicators: absolute floors
+    at about 2/3 of the rates this tier measured (one: 1206-1250 GB/s, four:
+    1886-1966 GB/s, profiles/r4_gpu_tier/, profiles/r4_tier2/), and four at
+    least 1.3x one measured in the same process (1.51-1.63x measured): a lost
+    multi-communicator speedup or a slower RCCL posting fails here, a slower
+    box alone does not."""
+    one, ms1 = _self_step_gbs(native, "rccl")
+    four, ms4 = _self_step_gbs(native, "rccl:4")
+    rec = {"rccl": {"gbs_median": one, "step_ms": ms1}, "rccl:4": {"gbs_median": four, "step_ms": ms4},
+           "ratio": four / one}
+    _record("self_copy_rate_floors", rec)
+    print("rccl %.1f  rccl:4 %.1f GB/s  ratio %.2f" % (one, four, four / one))
+    assert one > 800.0, rec
+    assert four > 1300.0, rec
+    assert four >= 1.3 * one, rec
