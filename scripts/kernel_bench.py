@@ -57,6 +57,17 @@ def main():
             t = timed(lambda: nat.verify_launch(ptr, sz, 7, impl, check, stream), a.reps)
             res[name] = t
             assert nat.verify(ptr, sz, 7, impl, True, stream)[0] == 0
+        # The batched post-timing check (dev::launch_multi_verify): the buffer
+        # as 32 MiB slots with a PRNG stream each, like a bench step's
+        # receive slots; reset + verify + finalize per 32 slots, no readback.
+        chunk = 32 << 20
+        if sz % chunk == 0:
+            jobs = [(ptr + i * chunk, chunk, 1000 + i) for i in range(sz // chunk)]
+            for p_, n_, seed_ in jobs:
+                nat.fill(p_, n_, seed_, stream)
+            res["verify_multi32m"] = timed(lambda: nat.verify_many_launch(jobs, stream), a.reps)
+            assert all(m == 0 for m, _, _ in nat.verify_many(jobs, stream))
+            nat.fill(ptr, sz, 7, stream)
         row = {"bytes": sz, "fill_tbs": sz / t_fill / 1e12, "fill_nt_tbs": sz / t_fill_nt / 1e12,
                "fill_stride_tbs": sz / t_fill_stride / 1e12, "fill_xcd_tbs": sz / t_fill_xcd / 1e12}
         # Roofs measured the same way: torch zero_() (write-only) and copy_()
@@ -88,6 +99,8 @@ def main():
                  row["verify_lds_tbs"], row["verify_lds8_tbs"], row["verify_ldspipe_tbs"], row["checksum_reg_tbs"], row["checksum_lds_tbs"], HBM_MEASURED_TBS), flush=True)
         print("        roofs: torch zero_ %.2f  torch copy_ %.2f  ours copy %.2f TB/s (copy counts bytes once)"
               % (row["torch_zero_tbs"], row["torch_copy_tbs"], row["copy_kernel_tbs"]), flush=True)
+        if "verify_multi32m_tbs" in row:
+            print("        batched verify, 32 MiB slots: %.2f TB/s" % row["verify_multi32m_tbs"], flush=True)
         del buf
         torch.cuda.empty_cache()
     if a.json:
