@@ -60,7 +60,7 @@ def test_copy_many_matches_torch(arena, group):
 
 
 @GPU_SETTINGS
-@given(st.integers(1, 3 << 20), st.integers(0, (1 << 64) - 1), st.sampled_from([1, 2, 3, 4]))
+@given(st.integers(1, 3 << 20), st.integers(0, (1 << 64) - 1), st.sampled_from([1, 2, 3, 4, 5, 6]))
 def test_fill_matches_reference_any_size(arena, nbytes, seed, impl):
     native, _ = arena
     buf = torch.full((nbytes + 64,), 0xAB, dtype=torch.uint8, device="cuda")
@@ -86,3 +86,27 @@ def test_verify_matches_reference_on_corruption(arena, nbytes, seed, impl, data)
     assert r == ref
     assert r.mismatches == len({o // 4 for o in flips})
     assert r.first_bad == (4 * (min(flips) // 4) if flips else 2**64 - 1)
+
+
+@GPU_SETTINGS
+@given(st.lists(st.tuples(st.integers(0, 1 << 20), st.integers(0, (1 << 63) - 1), st.booleans()),
+                min_size=1, max_size=40), st.data())
+def test_batched_verify_matches_reference(arena, jobs, data):
+    """dev::launch_multi_verify on any list of buffers (empty ones, tails,
+    more than one batch of 32), some corrupted: every job's result is the
+    PyTorch reference's for that buffer."""
+    native, _ = arena
+    bufs, args = [], []
+    for nbytes, seed, corrupt in jobs:
+        b = torch.empty(max(nbytes, 16), dtype=torch.uint8, device="cuda")[:nbytes]
+        if nbytes:
+            fill_(b, seed)
+            if corrupt:
+                b[data.draw(st.integers(0, nbytes - 1))] ^= 0x21
+        bufs.append(b)
+        args.append((b.data_ptr(), nbytes, seed))
+    torch.cuda.synchronize()
+    got = native.verify_many(args, torch.cuda.current_stream().cuda_stream)
+    for b, (_, nbytes, seed), g in zip(bufs, args, got):
+        ref = reference_verify(b, seed) if nbytes else (0, 0, 2**64 - 1)
+        assert tuple(g) == tuple(ref), (nbytes, seed, g, ref)
