@@ -10,17 +10,36 @@
 #   5. the framework-free RCCL reproducer across two GPUs (scripts/rccl_half_repro.cpp --devices 2: where RCCL's
 #      lost-second-half threshold lies on a real xGMI link, with RCCL's INFO log of the 2-GPU communicator).
 #
-#   bash scripts/node_run.sh [OUT_DIR] [--dry-run]
+#   bash scripts/node_run.sh [OUT_DIR] [--dry-run] [--rehearse]
+#
+# --rehearse runs the same steps on a one-GPU box, with 4 ranks on device 0, each rank its own RCCL host (RCCL's
+# socket transport, not xGMI), benches at 32 messages per step under a 150 s deadline, the pair sweep emulated
+# through RCCL, and no 2-GPU reproducer: it checks this script's steps end to end before a node run.
 set -uo pipefail
 cd "$(dirname "$0")/.."
-OUT=${1:-gpurun_out/node}
+OUT=gpurun_out/node
 DRY=0
-for a in "$@"; do [ "$a" = "--dry-run" ] && DRY=1; done
-[ "$OUT" = "--dry-run" ] && OUT=gpurun_out/node
+REHEARSE=0
+for a in "$@"; do
+  case "$a" in
+    --dry-run) DRY=1 ;;
+    --rehearse) REHEARSE=1 ;;
+    *) OUT=$a ;;
+  esac
+done
 MPIRUN=${P2P_MPIRUN:-/opt/conda/bin/mpirun}
 NGPU=$(python3 -c "import torch; print(torch.cuda.device_count())")
 N=$(( NGPU < 8 ? NGPU : 8 ))
 [ "$DRY" = 1 ] && [ "$N" -lt 2 ] && N=8  # show the node commands anywhere
+SWEEP_EMULATE=()
+BENCH_EXTRA=()
+if [ "$REHEARSE" = 1 ]; then
+  N=4
+  export P2P_REHEARSE_MULTI_GPU=$N P2P_DEVICE=0 P2P_FUZZ_DEVICE=0 P2P_RCCL_DISTINCT_HOSTS=1 NCCL_SOCKET_IFNAME=lo \
+    NCCL_IB_DISABLE=1 P2P_SCALING_GPUS=$N
+  SWEEP_EMULATE=(--emulate rccl --sizes 32M)
+  BENCH_EXTRA=(--msgs 32 --deadline 150)
+fi
 
 step() {  # name, seconds, command...
   local name=$1 secs=$2
@@ -36,9 +55,9 @@ step() {  # name, seconds, command...
   fi
 }
 
-if [ "$N" -lt 2 ] && [ "$DRY" = 0 ]; then
+if [ "$N" -lt 2 ] && [ "$DRY" = 0 ] && [ "$REHEARSE" = 0 ]; then
   echo "node_run: needs >= 2 visible GPUs (found $NGPU); on one GPU use scripts/gpu_check.sh," \
-       "scripts/emulated_node.sh and scripts/rccl_emulated_node.sh" >&2
+       "scripts/emulated_node.sh and scripts/rccl_emulated_node.sh, or --rehearse" >&2
   exit 1
 fi
 mkdir -p "$OUT"
@@ -48,8 +67,12 @@ fi
 step multi_gpu_tests 1800 python3 -u -m pytest tests/test_multi_gpu.py -m gpu -x -v --timeout 900 --timeout-method thread
 step reference_run 600 "$MPIRUN" -n "$N" ./p2p_matrix --json "$OUT/reference_run.json"
 [ "$DRY" = 0 ] && cp "$OUT/reference_run.log" "$OUT/result.txt"
-step scaling 3600 bash scripts/scaling.sh "$OUT/scaling.jsonl"
-step pair_sweep 1200 python3 scripts/xgmi_pair_sweep.py --np "$N" --out "$OUT/xgmi_sweep"
+step scaling 3600 bash scripts/scaling.sh "$OUT/scaling.jsonl" "${BENCH_EXTRA[@]}"
+step pair_sweep 1200 python3 scripts/xgmi_pair_sweep.py --np "$N" --out "$OUT/xgmi_sweep" "${SWEEP_EMULATE[@]}"
+if [ "$REHEARSE" = 1 ]; then
+  [ "$DRY" = 0 ] && cat "$OUT/summary.txt"
+  exit 0
+fi
 # (exit 3 = some size came back wrong: a finding, not a failure of the step)
 step rccl_repro_2gpu 300 env NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=INIT,P2P NCCL_DEBUG_FILE="$OUT/rccl_repro_2gpu.nccl.txt" \
   bash -c './build/rccl_half_repro --devices 2 --sizes 16M,32M,64M,128M,256M,512M,1G,1G+16; rc=$?; [ $rc -eq 3 ] && exit 0; exit $rc'

@@ -8,7 +8,8 @@ set -euo pipefail
 cd "$(dirname "$0")/.."
 OUT=${1:-scaling.jsonl}
 shift || true
-NGPU=$(python3 -c "import torch; print(torch.cuda.device_count())")
+# P2P_SCALING_GPUS: how many ranks to go up to (node_run.sh --rehearse: 4 ranks on one GPU).
+NGPU=${P2P_SCALING_GPUS:-$(python3 -c "import torch; print(torch.cuda.device_count())")}
 : > "$OUT"
 for N in 1 2 4 8; do
   if [ "$N" -gt "$NGPU" ]; then break; fi
