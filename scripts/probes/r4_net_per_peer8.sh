@@ -16,6 +16,15 @@ run() {  # name, env..., -- args
   echo "$name rc=$rc"
   [ $rc -le 3 ] || exit $rc  # a crash or time limit ends the probe
 }
+if [ "${2:-}" = "rule" ]; then
+  # Which knob values lose data: per-peer channels vs the p2p channel count
+  # (4 by default on the socket transport).
+  run pp4_32m NCCL_NCHANNELS_PER_PEER=4 -- --sizes 32M
+  run pp8_min8_32m NCCL_NCHANNELS_PER_PEER=8 NCCL_MIN_P2P_NCHANNELS=8 -- --sizes 32M
+  run pp8_1m NCCL_NCHANNELS_PER_PEER=8 -- --sizes 1M
+  run pp16_min8_32m NCCL_NCHANNELS_PER_PEER=16 NCCL_MIN_P2P_NCHANNELS=8 -- --sizes 32M
+  exit 0
+fi
 run pp8_32m NCCL_NCHANNELS_PER_PEER=8 -- --sizes 32M
 run pp8_16m NCCL_NCHANNELS_PER_PEER=8 -- --sizes 16M
 run pp8_32m_norechunk NCCL_NCHANNELS_PER_PEER=8 P2P_RECHUNK=0 -- --sizes 32M
