@@ -68,7 +68,10 @@ step multi_gpu_tests 1800 python3 -u -m pytest tests/test_multi_gpu.py -m gpu -x
 step reference_run 600 "$MPIRUN" -n "$N" ./p2p_matrix --json "$OUT/reference_run.json"
 [ "$DRY" = 0 ] && cp "$OUT/reference_run.log" "$OUT/result.txt"
 step scaling 3600 bash scripts/scaling.sh "$OUT/scaling.jsonl" "${BENCH_EXTRA[@]}"
-step pair_sweep 1200 python3 scripts/xgmi_pair_sweep.py --np "$N" --out "$OUT/xgmi_sweep" "${SWEEP_EMULATE[@]}"
+# (exit 2 = some row's bytes failed verification: a finding listed in
+# xgmi_sweep/summary.json corrupt_rows, never a winner; the run goes on)
+step pair_sweep 1200 bash -c 'python3 scripts/xgmi_pair_sweep.py "$@"; rc=$?; [ $rc -eq 2 ] && exit 0; exit $rc' _ \
+  --np "$N" --out "$OUT/xgmi_sweep" "${SWEEP_EMULATE[@]}"
 if [ "$REHEARSE" = 1 ]; then
   [ "$DRY" = 0 ] && cat "$OUT/summary.txt"
   exit 0
