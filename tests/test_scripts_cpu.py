@@ -65,6 +65,12 @@ def test_node_run_dry_run_and_refusal():
     assert "-n 8 ./p2p_matrix" in out.stdout
     out = subprocess.run(["bash", script, "/tmp/p2p_node_real"], capture_output=True, text=True, timeout=120)
     assert out.returncode == 1 and "needs >= 2 visible GPUs" in out.stderr
+    # --rehearse: the same steps with 4 ranks on one GPU (profiles/r4_node_rehearsal/)
+    out = subprocess.run(["bash", script, "/tmp/p2p_node_dry", "--dry-run", "--rehearse"], capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "-n 4 ./p2p_matrix" in out.stdout and "--emulate rccl" in out.stdout and "--msgs 32" in out.stdout
+    assert "rccl_repro_2gpu" not in out.stdout
 
 
 @pytest.mark.mpi
