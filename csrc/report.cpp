@@ -213,7 +213,8 @@ std::string run_to_json(const RunRecord& rec, int n) {
       << ",\"compat_gbps\":" << num(compat_cell_gbps(ph)) << ",\"wall_seconds\":" << num(ph.wall_seconds)
       << ",\"mismatches\":" << ph.total_mismatches << ",\"generations\":" << ph.generations
       << ",\"timed_msgs\":" << ph.timed_msgs << ",\"verified_msgs\":" << ph.verified_msgs << ",\"op_bytes\":" << ph.op_bytes
-      << ",\"warmup_mismatches\":" << ph.warmup_mismatches << ",\"rechunked_to\":[";
+      << ",\"warmup_mismatches\":" << ph.warmup_mismatches << ",\"warmup_residual\":" << ph.warmup_residual
+      << ",\"rechunked_to\":[";
     for (size_t i = 0; i < ph.rechunked_to.size(); ++i) o << (i ? "," : "") << ph.rechunked_to[i];
     o << "],\"flows\":[";
     for (size_t i = 0; i < ph.flows.size(); ++i) {

@@ -362,6 +362,13 @@ void rechunk_until_warmup_verifies(Transport& t, Bootstrap& boot, const Phase& p
     }
     bad = boot.allreduce_sum_u64(local_mismatches());
   }
+  res->warmup_residual = bad;
+  if (bad && me == 0 && !res->rechunked_to.empty())
+    std::fprintf(stderr,
+                 "[p2p] %s: still %llu wrong words in the warmup with ops of <= %zu KiB: the loss does not follow "
+                 "the op size (RCCL channel knobs? e.g. NCCL_NCHANNELS_PER_PEER above the p2p channel count lost half "
+                 "of every message over RCCL's socket transport, profiles/r4_node_rehearsal/)\n",
+                 phase.label.c_str(), static_cast<unsigned long long>(bad), res->rechunked_to.back() >> 10);
 }
 
 // Largest op this rank posts for the phase's messages (0: one op each).

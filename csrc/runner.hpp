@@ -97,6 +97,9 @@ struct PhaseResult {
   size_t op_bytes = 0;
   uint64_t warmup_mismatches = 0;
   std::vector<size_t> rechunked_to;
+  // Wrong words the warmup still had after the last re-chunking (0: the
+  // smaller ops fixed it).  Non-zero: the loss does not follow the op size.
+  uint64_t warmup_residual = 0;
 };
 
 // Send buffer + receive slots for one rank.  The slots are carved from one
