@@ -50,6 +50,16 @@ def test_cli_four_rccl_ranks_every_mode(exe, tmp_path, comms):
     # ran through RCCL across ranks: every pair has samples.
     pre = [r for r in recs if r["type"] == "latency" and r["method"] == "preposted"]
     assert len(pre) == 1 and len(pre[0]["pairs"]) == 6 and all(p["one_way_us"]["p50"] > 0 for p in pre[0]["pairs"])
+    # The CLI re-derives each peer's op limit from RCCL's connection lines
+    # after its warm-up; both ends of every pair agree.
+    links = [r for r in recs if r["type"] == "links"][0]
+    for rep in links["ranks"]:
+        assert rep["refinements"] >= 1, rep
+        for p in rep["peers"]:
+            if p["peer"] != rep["rank"]:
+                assert p["op_limit_source"] == "connection lines" and p["op_limit"] == 32 << 20, p
+    limit = {(rep["rank"], p["peer"]): p["op_limit"] for rep in links["ranks"] for p in rep["peers"]}
+    assert all(limit[(a, b)] == limit[(b, a)] for (a, b) in limit), limit
 
 
 @pytest.mark.emulated
