@@ -261,27 +261,30 @@ py::list device_verify_many(const std::vector<std::tuple<uintptr_t, size_t, uint
   return out;
 }
 
-// Stream-ordered batched verify, no readback (timing with events).
+// Stream-ordered batched verify, no readback (timing with events): the
+// scratch and results live per device and grow with the job count.
 void device_verify_many_launch(const std::vector<std::tuple<uintptr_t, size_t, uint64_t>>& jobs, uintptr_t stream) {
-  static dev::VerifyAccum* scratch_d = nullptr;
-  static dev::VerifyAccum* out_d = nullptr;
-  static int cap = 0, device = -1;
+  struct Buffers {
+    dev::VerifyAccum* scratch = nullptr;
+    dev::VerifyAccum* out = nullptr;
+    int cap = 0;
+  };
+  static std::vector<Buffers> per_device;
   int dv = 0;
   if (hipGetDevice(&dv) != hipSuccess) P2P_FATAL("no HIP device");
+  if (static_cast<int>(per_device.size()) <= dv) per_device.resize(static_cast<size_t>(dv) + 1);
+  Buffers& b = per_device[static_cast<size_t>(dv)];
   const int n = static_cast<int>(jobs.size());
-  if (dv != device || n > cap) {
-    if (hipDeviceSynchronize() != hipSuccess) P2P_FATAL("hipDeviceSynchronize failed");
-    if (scratch_d && dv == device) (void)hipFree(scratch_d);
-    if (out_d && dv == device) (void)hipFree(out_d);
-    cap = std::max(n, 32);
-    if (hipMalloc(&scratch_d, dev::multi_verify_scratch_bytes()) != hipSuccess ||
-        hipMalloc(&out_d, sizeof(dev::VerifyAccum) * static_cast<size_t>(cap)) != hipSuccess)
-      P2P_FATAL("hipMalloc failed");
-    device = dv;
+  if (!b.scratch && hipMalloc(&b.scratch, dev::multi_verify_scratch_bytes()) != hipSuccess) P2P_FATAL("hipMalloc failed");
+  if (n > b.cap) {
+    if (hipStreamSynchronize(as_stream(stream)) != hipSuccess) P2P_FATAL("hipStreamSynchronize failed");
+    if (b.out) (void)hipFree(b.out);
+    b.cap = std::max(n, 2 * b.cap);
+    if (hipMalloc(&b.out, sizeof(dev::VerifyAccum) * static_cast<size_t>(b.cap)) != hipSuccess) P2P_FATAL("hipMalloc failed");
   }
   std::vector<dev::VerifyJob> dj;
   for (const auto& j : jobs) dj.push_back({reinterpret_cast<const void*>(std::get<0>(j)), std::get<1>(j), std::get<2>(j)});
-  dev::launch_multi_verify(dj.data(), n, scratch_d, out_d, as_stream(stream));
+  dev::launch_multi_verify(dj.data(), n, b.scratch, b.out, as_stream(stream));
 }
 
 py::list schedule_py(const std::string& mode, const std::string& dir, int n) {
