@@ -71,7 +71,8 @@ gpu: $(BUILD)/p2p_matrix
 	ln -sf $(BUILD)/p2p_matrix p2p_matrix
 host: $(BUILD)/p2p_matrix_host $(BUILD)/p2p_host_tests
 ext: $(EXT)
-tools: $(BUILD)/fill_probe $(BUILD)/copy_probe $(BUILD)/ipc_export_probe $(BUILD)/rccl_half_repro $(BUILD)/rccl_half_repro_rocm
+tools: $(BUILD)/fill_probe $(BUILD)/copy_probe $(BUILD)/ipc_export_probe $(BUILD)/rccl_half_repro $(BUILD)/rccl_half_repro_rocm \
+       $(BUILD)/rccl_net_repro
 
 $(BUILD)/gpu $(BUILD)/host $(BUILD)/asan:
 	mkdir -p $@
@@ -150,6 +151,12 @@ $(BUILD)/rccl_half_repro: scripts/rccl_half_repro.cpp $(RT_STAMP) | $(BUILD)/gpu
 
 $(BUILD)/rccl_half_repro_rocm: scripts/rccl_half_repro.cpp | $(BUILD)/gpu
 	$(HIPCC) --offload-arch=$(ARCH) -O2 $(WARN) $< -o $@ -Wl,-rpath,$(ROCM)/lib -L$(ROCM)/lib -lrccl
+
+# Framework-free two-rank reproducer (scripts/rccl_net_repro.cpp): raw HIP +
+# RCCL + MPI, one send and one receive per message between two ranks.
+$(BUILD)/rccl_net_repro: scripts/rccl_net_repro.cpp $(RT_STAMP) $(MPILIB)/.stamp | $(BUILD)/gpu
+	$(HIPCC) --offload-arch=$(ARCH) -O2 $(WARN) $(MPI_INC) $< -o $@ $(BIN_RPATH) -L$(ROCM)/lib -lrccl \
+	    -L$(MPILIB) -lmpi -Wl,-rpath,'$$ORIGIN/mpilib'
 
 # AddressSanitizer / UBSan on host code only (GPU sanitizers are not available):
 # the unit tests, and the MPI host binary that tests/test_host_unit.py runs as
