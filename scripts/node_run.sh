@@ -7,8 +7,11 @@
 #   2. the reference's own run line, `mpirun -n N ./p2p_matrix` (compat matrices, result.txt);
 #   3. the headline bench at N = 1, 2, 4, 8 and its scaling table (scripts/scaling.sh);
 #   4. the xGMI pair-cell tuning sweep (scripts/xgmi_pair_sweep.py);
-#   5. the framework-free RCCL reproducer across two GPUs (scripts/rccl_half_repro.cpp --devices 2: where RCCL's
-#      lost-second-half threshold lies on a real xGMI link, with RCCL's INFO log of the 2-GPU communicator).
+#   5. the framework-free RCCL reproducers across two GPUs: scripts/rccl_half_repro.cpp --devices 2 (where RCCL's
+#      lost-second-half threshold lies on a real xGMI link, with RCCL's INFO log of the 2-GPU communicator), and
+#      scripts/rccl_net_repro.cpp as two MPI ranks on GPUs 0 and 1 with RCCL's defaults and with
+#      NCCL_NCHANNELS_PER_PEER=8 (which loses half of every message over RCCL's socket transport,
+#      profiles/r4_node_rehearsal/).
 #
 #   bash scripts/node_run.sh [OUT_DIR] [--dry-run] [--rehearse]
 #
@@ -79,5 +82,11 @@ fi
 # (exit 3 = some size came back wrong: a finding, not a failure of the step)
 step rccl_repro_2gpu 300 env NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=INIT,P2P NCCL_DEBUG_FILE="$OUT/rccl_repro_2gpu.nccl.txt" \
   bash -c './build/rccl_half_repro --devices 2 --sizes 16M,32M,64M,128M,256M,512M,1G,1G+16; rc=$?; [ $rc -eq 3 ] && exit 0; exit $rc'
+# (exit 3 = some message came back wrong: a finding, not a failure of the step)
+for pp in default 8; do
+  step "rccl_pair_repro_pp$pp" 300 env $([ "$pp" = default ] || echo NCCL_NCHANNELS_PER_PEER=$pp) NCCL_DEBUG=INFO \
+    NCCL_DEBUG_SUBSYS=INIT,P2P NCCL_DEBUG_FILE="$OUT/rccl_pair_repro_pp$pp.nccl.%p.txt" \
+    bash -c '"$0" -n 2 ./build/rccl_net_repro --sizes 1M,32M,1G --iters 2; rc=$?; [ $rc -eq 3 ] && exit 0; exit $rc' "$MPIRUN"
+done
 [ "$DRY" = 0 ] && cat "$OUT/summary.txt"
 exit 0
