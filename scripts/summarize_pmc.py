@@ -21,9 +21,12 @@ def main(paths):
     for p in paths:
         for r in csv.DictReader(open(p)):
             dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-            agg[(short(r["Kernel_Name"]), r["Counter_Name"])].append(
+            # Keyed by grid too: one kernel launched at several sizes (e.g.
+            # the 1 GiB fill and the 32 MiB slot fills) gets a row per size.
+            agg[(short(r["Kernel_Name"]) + " g" + r["Grid_Size"], r["Counter_Name"])].append(
                 (float(r["Counter_Value"]), dur, r["Grid_Size"], r["LDS_Block_Size"], r["VGPR_Count"]))
-    print("%-24s %-22s %14s %10s %9s %6s %4s %s" % ("kernel", "counter", "value(med)", "dur_ns", "grid", "lds", "vgpr", "derived"))
+    print("%-40s %-22s %14s %10s %9s %6s %4s %s" % ("kernel gGRID", "counter", "value(med)", "dur_ns", "grid", "lds", "vgpr",
+                                                     "derived"))
     for (k, c), v in sorted(agg.items()):
         v.sort(key=lambda x: x[1])
         m = v[len(v) // 2]
@@ -31,7 +34,7 @@ def main(paths):
         if c in ("FETCH_SIZE", "WRITE_SIZE") and m[1] > 0:
             kb = m[0] * (2 if c == "FETCH_SIZE" else 1)
             derived = "%.2f TB/s%s" % (kb * 1024 / m[1] / 1e3, " (x2 corrected)" if c == "FETCH_SIZE" else "")
-        print("%-24s %-22s %14.1f %10d %9s %6s %4s %s" % (k, c, m[0], m[1], m[2], m[3], m[4], derived))
+        print("%-40s %-22s %14.1f %10d %9s %6s %4s %s" % (k, c, m[0], m[1], m[2], m[3], m[4], derived))
 
 
 if __name__ == "__main__":
