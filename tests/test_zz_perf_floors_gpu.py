@@ -78,10 +78,11 @@ def _record(name, rec):
 
 
 def test_kernel_bandwidth_floors(native):
-    """1 GiB fill / LDS-DMA verify / copy against absolute floors at ~80% of
-    the profiled rates (fill 7.09, lds8 verify 6.27, copy 3.20 read + 3.12
-    written TB/s: profiles/r3b_close/pmc_summary.txt) and the fill against
-    0.8 x torch's zero_() measured in the same window."""
+    """1 GiB fill / LDS-DMA verify / copy against absolute floors at ~75-80%
+    of the lowest per-launch medians this test measured in round 4 (fill
+    6.93, verify with its reset + finalize launches 5.80, copy 3.14 TB/s:
+    profiles/r4_gpu_tier/, r4_tier2/, r4_final/) and the fill against 0.8 x
+    torch's zero_() measured in the same window."""
     buf = torch.empty(GIB, dtype=torch.uint8, device="cuda")
     dst = torch.empty_like(buf)
     stream = torch.cuda.current_stream().cuda_stream
@@ -121,8 +122,8 @@ def test_kernel_bandwidth_floors(native):
     msg = json.dumps(rec)
     assert rates["fill"] > 5.5, msg
     assert rates["fill"] >= 0.8 * rates["zero_"], msg
-    assert rates["verify_lds8"] > 5.0, msg
-    assert rates["copy"] > 2.65, msg  # payload bytes (read once + written once)
+    assert rates["verify_lds8"] > 4.6, msg
+    assert rates["copy"] > 2.5, msg  # payload bytes (read once + written once)
 
 
 def _self_step_gbs(native, transport):
