@@ -1,5 +1,7 @@
 #include "common.hpp"
 
+#include <atomic>
+
 #include <dlfcn.h>
 #include <unistd.h>
 
@@ -22,6 +24,8 @@ std::vector<std::pair<int, AbortHook>>& hooks() {
 }
 int g_next_hook = 1;
 bool g_throw = false;
+std::atomic<bool> g_abort_requested{false};
+std::atomic<bool> g_abort_done{false};
 int g_log_level = -1;
 }  // namespace
 
@@ -57,6 +61,11 @@ void run_abort_hooks(int code) {
 }
 
 void set_throw_on_fatal(bool enable) { g_throw = enable; }
+
+void request_abort() { g_abort_requested.store(true, std::memory_order_relaxed); }
+bool abort_requested() { return g_abort_requested.load(std::memory_order_relaxed); }
+void note_abort_done() { g_abort_done.store(true, std::memory_order_release); }
+bool abort_done() { return g_abort_done.load(std::memory_order_acquire); }
 
 void fatal(const char* file, int line, const std::string& what) {
   std::string msg = strfmt("p2p fatal error at %s:%d: %s", file, line, what.c_str());

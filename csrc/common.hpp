@@ -28,6 +28,16 @@ void clear_abort_hooks();
 // a watchdog that must end the process calls it so RCCL communicators are
 // aborted (their kernels exit) before the process goes.
 void run_abort_hooks(int code);
+// Cooperative abort from another thread (bench.py's deadline watchdog): the
+// transports' bounded waits poll abort_requested() and, on the thread that
+// owns the communicators, abort them and fail.  Aborting a communicator from
+// a second thread while its owner is inside RCCL crashed the owner (SIGSEGV,
+// profiles/r4_rehearsal/); this keeps every RCCL call on one thread.
+void request_abort();
+bool abort_requested();
+// Set by a transport once it has aborted its communicators on request.
+void note_abort_done();
+bool abort_done();
 
 [[noreturn]] void fatal(const char* file, int line, const std::string& what);
 

@@ -468,6 +468,11 @@ PYBIND11_MODULE(_p2pcore, m) {
   m.def("rccl_available", &rccl_transport_available);
   m.def("runtime_json", &runtime_json, "HIP runtime / RCCL library versions and paths, visible devices and links.");
   m.def("env_knobs_json", &env_knobs_json, "Every NCCL_/RCCL_/HSA_/HIP_/GPU_... environment knob that is set.");
+  m.def("request_abort", []() { request_abort(); },
+        "Ask every transport wait of this process to abort its communicators on its own thread and fail.");
+  m.def("abort_requested", []() { return abort_requested(); });
+  m.def("abort_done", []() { return abort_done(); },
+        "True once a transport wait has aborted its communicators after request_abort().");
   m.def("run_abort_hooks", []() { run_abort_hooks(1); }, py::call_guard<py::gil_scoped_release>(),
         "Aborts every live RCCL communicator / bootstrap (their kernels exit); for a watchdog about to end the "
         "process.");

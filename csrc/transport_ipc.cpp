@@ -529,6 +529,10 @@ class IpcTransport final : public Transport {
       }
       if (e != hipErrorNotReady) P2P_FATAL(strfmt("stream error: %s", hipGetErrorString(e)));
       if ((it & 255) == 0) {
+        if (abort_requested()) {
+          note_abort_done();
+          P2P_FATAL(strfmt("rank %d: aborted while waiting (the run's deadline passed)", rank_));
+        }
         double now = now_seconds();
         if (now > deadline) P2P_FATAL(strfmt("rank %d: ipc stream did not finish within %.0f s", rank_, timeout_));
         if (now - t0 > 20e-3) std::this_thread::sleep_for(std::chrono::microseconds(20));

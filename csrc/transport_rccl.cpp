@@ -559,6 +559,11 @@ class RcclTransport final : public Transport {
       if (e == hipSuccess) return;
       if (e != hipErrorNotReady) P2P_FATAL(strfmt("stream error: %s", hipGetErrorString(e)));
       if ((it & 255) == 0) {
+        if (abort_requested()) {
+          abort_all();
+          note_abort_done();
+          P2P_FATAL(strfmt("rank %d: aborted while waiting (the run's deadline passed)", rank_));
+        }
         // Either way the communicators are aborted first: RCCL's kernels poll
         // the abort flag and exit, so the streams (and any hardware queue they
         // share with another session's streams) drain instead of staying
@@ -977,6 +982,11 @@ class RcclTransport final : public Transport {
   void wait_ready(ncclResult_t r, const char* what) {
     double deadline = now_seconds() + timeout_;
     while (r == ncclInProgress) {
+      if (abort_requested()) {
+        abort_all();
+        note_abort_done();
+        P2P_FATAL(strfmt("rank %d: %s aborted (the run's deadline passed)", rank_, what));
+      }
       if (now_seconds() > deadline) {
         abort_all();
         P2P_FATAL(strfmt("rank %d: %s did not complete within %.0f s (peer missing?)", rank_, what, timeout_));

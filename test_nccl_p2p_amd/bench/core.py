@@ -174,10 +174,20 @@ class Reporter:
             return True
 
 
+ABORT_GRACE_S = 3.0
+
+
 def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> threading.Event:
     """At the deadline: print the JSON line with what is finished (the section
-    still running is named), abort every RCCL communicator so its kernels exit,
-    and end the process.  Exit 0 when the headline was measured."""
+    still running is named), have the communicators aborted so their kernels
+    exit, and end the process.  Exit 0 when the headline was measured.
+
+    The abort is requested, not performed, here: the main thread may be inside
+    RCCL, and aborting a communicator from this thread meanwhile crashed it
+    (SIGSEGV on 3 of 8 ranks, profiles/r4_rehearsal/).  Every bounded wait of
+    the transports polls the request and aborts on its own thread; after up to
+    ABORT_GRACE_S the process ends either way (process exit tears the GPU
+    queues down)."""
     stop = threading.Event()
 
     def run():
@@ -193,7 +203,10 @@ def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> thread
         reporter.emit(deadline_hit=True, untimed_skipped=state.get("skipped") or None, section_errors=errors or None)
         kill_children(state)
         try:
-            nat.run_abort_hooks()
+            nat.request_abort()
+            t_end = time.monotonic() + ABORT_GRACE_S
+            while not nat.abort_done() and time.monotonic() < t_end:
+                time.sleep(0.02)
         except Exception:  # noqa: BLE001 -- the process ends either way
             pass
         sys.stderr.flush()
