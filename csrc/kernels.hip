@@ -304,7 +304,11 @@ __device__ __forceinline__ void lds_read_stages<8>(uint32_t addr, u32x4 (&r)[8])
 
 // Blocks `block` of `nblocks` of one buffer: the LDS-staged loop below, with
 // the workgroup's own LDS slots (the single and the batched verify share it).
-template <bool CHECK, int STAGES, int AUX>
+// SPAN = true: block b owns the contiguous super-chunks
+// [b * n_sc / nblocks, (b + 1) * n_sc / nblocks) and its waves interleave
+// inside them, instead of the grid-stride walk over the whole buffer (the
+// A/B of VerifyImpl::Lds8Span).
+template <bool CHECK, int STAGES, int AUX, bool SPAN = false>
 __device__ __forceinline__ Partial lds_verify_blocks(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
                                                      uint64_t block, uint64_t nblocks) {
   __shared__ uint4 slot[kWaves][STAGES][64];
@@ -315,7 +319,10 @@ __device__ __forceinline__ Partial lds_verify_blocks(const uint4* __restrict__ p
   const uint32_t lds_addr = static_cast<uint32_t>(
       reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)(&slot[wave][0][lane])));
   Partial acc{0, 0, ~0ull};
-  for (uint64_t sc = block * kWaves + wave; sc < n_sc; sc += nblocks * kWaves) {
+  const uint64_t first = SPAN ? block * n_sc / nblocks + wave : block * kWaves + wave;
+  const uint64_t end = SPAN ? (block + 1) * n_sc / nblocks : n_sc;
+  const uint64_t step = SPAN ? kWaves : nblocks * kWaves;
+  for (uint64_t sc = first; sc < end; sc += step) {
 #pragma unroll
     for (int s = 0; s < STAGES; ++s) {
       const uint64_t i = sc * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
@@ -336,11 +343,11 @@ __device__ __forceinline__ Partial lds_verify_blocks(const uint4* __restrict__ p
   return acc;
 }
 
-template <bool CHECK, int STAGES, int AUX>
+template <bool CHECK, int STAGES, int AUX, bool SPAN = false>
 __global__ __launch_bounds__(kBlock) void verify_lds_kernel(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
                                                             const uint8_t* __restrict__ tail, uint32_t tail_bytes,
                                                             uint64_t tail_offset, VerifyAccum* __restrict__ out) {
-  Partial acc = lds_verify_blocks<CHECK, STAGES, AUX>(p, nvec, seed, blockIdx.x, gridDim.x);
+  Partial acc = lds_verify_blocks<CHECK, STAGES, AUX, SPAN>(p, nvec, seed, blockIdx.x, gridDim.x);
   if (blockIdx.x == 0 && threadIdx.x == 0) check_tail<CHECK>(tail, tail_bytes, tail_offset, seed, acc);
   block_commit(acc, out, blockIdx.x);
 }
@@ -545,12 +552,12 @@ LaunchGeom verify_geometry(size_t bytes, VerifyImpl impl, unsigned max_grid) {
   // epilogue 256K times per GiB; the defaults below cap the grid so each
   // workgroup streams tens of KiB per epilogue (kernel_bench A/B).
   const bool lds = impl == VerifyImpl::Lds || impl == VerifyImpl::Lds8 || impl == VerifyImpl::LdsCached ||
-                   impl == VerifyImpl::LdsPipe;
+                   impl == VerifyImpl::LdsPipe || impl == VerifyImpl::Lds8Span;
   const uint64_t per_cu = lds ? kVerifyLdsPerCu : impl == VerifyImpl::Stride ? kVerifyStridePerCu : kVerifyGridPerCu;
   const uint64_t cap = max_grid ? max_grid : static_cast<uint64_t>(cu_count()) * per_cu;
   if (lds) {
     // KiB per chunk a wave checks, and KiB of LDS a wave owns.
-    const uint64_t stages = impl == VerifyImpl::Lds8 ? 8 : kLdsStages;
+    const uint64_t stages = impl == VerifyImpl::Lds8 || impl == VerifyImpl::Lds8Span ? 8 : kLdsStages;
     const uint64_t lds_stages = impl == VerifyImpl::LdsPipe ? 2 * stages : stages;
     const uint64_t sc_vecs = stages * 64;
     const uint64_t waves = (nvec + sc_vecs - 1) / sc_vecs;
@@ -621,6 +628,9 @@ void launch_verify_t(const uint4* vp, uint64_t nvec, uint64_t seed, const uint8_
       break;
     case VerifyImpl::Lds8:
       verify_lds_kernel<CHECK, 8, 2><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
+      break;
+    case VerifyImpl::Lds8Span:
+      verify_lds_kernel<CHECK, 8, 2, true><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
       break;
     case VerifyImpl::LdsCached:
       verify_lds_kernel<CHECK, kLdsStages, 0><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);

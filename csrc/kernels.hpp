@@ -53,7 +53,9 @@ struct alignas(64) VerifyAccum {
 constexpr int kVerifyShards = 64;
 constexpr size_t verify_accum_bytes() { return sizeof(VerifyAccum) * kVerifyShards; }
 
-enum class VerifyImpl : int { Auto = 0, Register = 1, Lds = 2, Stride = 3, Lds8 = 4, LdsCached = 5, LdsPipe = 6 };
+// Lds8Span: Lds8 with each workgroup on a contiguous span instead of a grid-stride walk (A/B).
+enum class VerifyImpl : int { Auto = 0, Register = 1, Lds = 2, Stride = 3, Lds8 = 4, LdsCached = 5, LdsPipe = 6,
+                              Lds8Span = 7 };
 // Grid2 / Grid4: full grid with 2 / 4 vectors per lane (8 / 16 KiB per workgroup).
 enum class FillImpl : int { Auto = 0, Grid = 1, Nontemporal = 2, Stride = 3, Xcd = 4, Grid2 = 5, Grid4 = 6 };
 

@@ -57,7 +57,7 @@ def main():
         t_fill_stride = timed(lambda: nat.fill(ptr, sz, 7, stream, 3), a.reps)
         t_fill_xcd = timed(lambda: nat.fill(ptr, sz, 7, stream, 4), a.reps)
         res = {}
-        for name, impl, check in [("verify_reg", 1, True), ("verify_stride", 3, True), ("verify_lds", 2, True), ("verify_lds8", 4, True), ("verify_ldspipe", 6, True),
+        for name, impl, check in [("verify_reg", 1, True), ("verify_stride", 3, True), ("verify_lds", 2, True), ("verify_lds8", 4, True), ("verify_ldspipe", 6, True), ("verify_lds8span", 7, True),
                                   ("checksum_reg", 1, False), ("checksum_lds", 2, False)]:
             # Kernel time only: reset + verify + finalize launches, no readback.
             t = timed(lambda: nat.verify_launch(ptr, sz, 7, impl, check, stream), a.reps)
@@ -105,6 +105,7 @@ def main():
                  row["verify_lds_tbs"], row["verify_lds8_tbs"], row["verify_ldspipe_tbs"], row["checksum_reg_tbs"], row["checksum_lds_tbs"], HBM_MEASURED_TBS), flush=True)
         print("        roofs: torch zero_ %.2f  torch copy_ %.2f  ours copy %.2f TB/s (copy counts bytes once)"
               % (row["torch_zero_tbs"], row["torch_copy_tbs"], row["copy_kernel_tbs"]), flush=True)
+        print("        lds8 contiguous spans per workgroup: %.2f TB/s" % row["verify_lds8span_tbs"], flush=True)
         if "verify_multi32m_tbs" in row:
             print("        batched verify, 32 MiB slots: %.2f TB/s" % row["verify_multi32m_tbs"], flush=True)
         del buf

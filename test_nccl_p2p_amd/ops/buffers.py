@@ -19,7 +19,7 @@ import torch
 from .._native import require_native
 
 M32 = 0xFFFFFFFF
-IMPLS = {"auto": 0, "reg": 1, "register": 1, "grid": 1, "lds": 2, "stride": 3, "lds8": 4, "lds-cached": 5, "lds-pipe": 6}
+IMPLS = {"auto": 0, "reg": 1, "register": 1, "grid": 1, "lds": 2, "stride": 3, "lds8": 4, "lds-cached": 5, "lds-pipe": 6, "lds8-span": 7}
 
 
 class VerifyResult(NamedTuple):

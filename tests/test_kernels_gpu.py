@@ -59,7 +59,7 @@ def test_fill_variants_match_reference(fill_impl, nbytes):
     assert torch.all(buf[nbytes:] == 0xAB), "fill wrote past the end"
 
 
-@pytest.mark.parametrize("impl", ["reg", "lds", "stride", "lds8", "lds-cached", "lds-pipe"])
+@pytest.mark.parametrize("impl", ["reg", "lds", "stride", "lds8", "lds-cached", "lds-pipe", "lds8-span"])
 @pytest.mark.parametrize("nbytes", SIZES)
 def test_verify_clean_and_checksum(impl, nbytes):
     buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
@@ -73,7 +73,7 @@ def test_verify_clean_and_checksum(impl, nbytes):
     assert wrong.mismatches == reference_verify(buf, 78).mismatches > 0
 
 
-@pytest.mark.parametrize("impl", ["reg", "lds", "stride", "lds8", "lds-cached", "lds-pipe"])
+@pytest.mark.parametrize("impl", ["reg", "lds", "stride", "lds8", "lds-cached", "lds-pipe", "lds8-span"])
 def test_verify_counts_exact_bitflips(impl):
     nbytes = (8 << 20) + 5
     buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")

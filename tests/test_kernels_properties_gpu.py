@@ -72,7 +72,7 @@ def test_fill_matches_reference_any_size(arena, nbytes, seed, impl):
 
 @GPU_SETTINGS
 @given(st.integers(16, 3 << 20), st.integers(0, (1 << 63) - 1),
-       st.sampled_from(["reg", "lds", "stride", "lds8", "lds-cached", "lds-pipe"]), st.data())
+       st.sampled_from(["reg", "lds", "stride", "lds8", "lds-cached", "lds-pipe", "lds8-span"]), st.data())
 def test_verify_matches_reference_on_corruption(arena, nbytes, seed, impl, data):
     """Any set of corrupted bytes: every verify kernel reports the reference's
     mismatching-word count, first bad offset and checksum."""
