@@ -69,7 +69,7 @@ data
   -c, --verify           random-fill sends, verify every received buffer on the device,
                          outside the timed loop (the default)
       --no-verify        zero-filled sends, nothing read back (the reference's data)
-      --verify-impl I    auto (= lds8) | lds | lds8 | lds-pipe | lds-cached | stride | reg
+      --verify-impl I    auto (= lds8) | lds | lds8 | lds8-span | lds-pipe | lds-cached | stride | reg
                          (LDS-DMA- or register-staged verify kernel variants)
 transport / launch
       --transport T      rccl  MI355X + RCCL ncclSend/ncclRecv over xGMI      [rccl]
@@ -263,6 +263,7 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
                          : v == "lds8"                 ? 4
                          : v == "lds-cached"           ? 5
                          : v == "lds-pipe"             ? 6
+                         : v == "lds8-span"            ? 7
                                                        : 0;
     } else if (a == "--transport") {
       cfg->transport = next();
