@@ -310,7 +310,10 @@ class SectionsMixin:
             for name, mode_x, dir_x, nbytes, iters in (
                     ("allpairs_1g", "allpairs", "bi", nat.parse_size(args.allpairs_size), 4),
                     ("ring_256m", "ring", "uni", nat.parse_size(args.ring_size), 8)):
-                v = self.section(name, lambda: concurrent_config(mode_x, dir_x, nbytes, iters), 5.0)
+                # A fixed handful of iterations (well under a second at 256 MiB -
+                # 1 GiB on xGMI), so half the ring's 5 s slice is enough: under
+                # a tight deadline the proportional shares leave it just under 5.
+                v = self.section(name, lambda: concurrent_config(mode_x, dir_x, nbytes, iters), 2.5)
                 if v is not None:
                     extras[name] = v
             v = self.section("ring_hop", ring_hop)
