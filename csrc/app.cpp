@@ -264,7 +264,13 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
                          : v == "lds-cached"           ? 5
                          : v == "lds-pipe"             ? 6
                          : v == "lds8-span"            ? 7
-                                                       : 0;
+                         : v == "auto"                 ? 0
+                                                       : -1;
+      if (cfg->verify_impl < 0) {
+        std::fprintf(stderr, "p2p_matrix: unknown --verify-impl '%s' (see --help)\n", v.c_str());
+        *exit_code = 1;
+        return false;
+      }
     } else if (a == "--transport") {
       cfg->transport = next();
     } else if (a == "--ipc-engine") {

@@ -452,6 +452,26 @@ TEST(test_cli_defaults_match_reference) {
   EXPECT(auto_iters(4ull << 30, 4ull << 30) == 8);
 }
 
+TEST(test_cli_verify_impl_names) {
+  const std::pair<const char*, int> known[] = {{"auto", 0}, {"reg", 1},        {"lds", 2},      {"stride", 3},
+                                               {"lds8", 4}, {"lds-cached", 5}, {"lds-pipe", 6}, {"lds8-span", 7}};
+  for (const auto& [name, impl] : known) {
+    std::vector<std::string> args{"--verify-impl", name};
+    std::vector<char*> argv;
+    for (auto& a : args) argv.push_back(&a[0]);
+    AppConfig cfg;
+    int code = -1;
+    EXPECT(parse_cli(static_cast<int>(argv.size()), argv.data(), &cfg, &code) && cfg.verify_impl == impl);
+  }
+  // A misspelt name is an error, not a silent fall-back to the default.
+  std::vector<std::string> args{"--verify-impl", "lds8span"};
+  std::vector<char*> argv;
+  for (auto& a : args) argv.push_back(&a[0]);
+  AppConfig cfg;
+  int code = -1;
+  EXPECT(!parse_cli(static_cast<int>(argv.size()), argv.data(), &cfg, &code) && code == 1);
+}
+
 // ------------------------------------------- multi-rank engine (threads) ----
 
 static void run_ranks(int n, const std::function<void(Bootstrap&, Transport&)>& body, bool shm = false) {
