@@ -32,9 +32,16 @@ from test_nccl_p2p_amd.utils.report import parse_compat
 # checks the command lines, the assertions and the budgets before a node run.
 REHEARSAL = int(os.environ.get("P2P_REHEARSE_MULTI_GPU") or 0)
 # Loopback sockets move ~5-8 GB/s per pair, xGMI ~50: the rehearsal's benches
-# send a quarter of the messages per step and its link check a lower floor.
-BENCH_MSGS = ["--msgs", "32"] if REHEARSAL else []
+# send a quarter of the messages per step (8 ranks share the one box's
+# sockets: a sixteenth) and its link check a lower floor; with 8 ranks the
+# concurrent modes stop at 16 MiB instead of 64.
+BENCH_MSGS = (["--msgs", "8"] if REHEARSAL >= 8 else ["--msgs", "32"]) if REHEARSAL else []
 MIN_GBS = "0.05" if REHEARSAL else "1"
+CONCURRENT_SIZES = "1M,16M" if REHEARSAL >= 8 else "1M,64M"
+# 8 ranks over one box's loopback sockets took 77-98 s per communicator
+# setting for the concurrent modes, and the reference's matrices 60 s of
+# their 60 (profiles/r4_reh8/); a node's xGMI takes seconds.
+CONCURRENT_TIMEOUT_S = 150 if REHEARSAL >= 8 else None
 # 8 ranks on one GPU plus a comparison child per rank would pass the test
 # box's 16 processes per GPU; on a node each rank has a GPU of its own.
 ISOLATE = ["--isolate", "0"] if REHEARSAL >= 8 else []
@@ -84,7 +91,8 @@ def test_reference_matrix_all_gpus(exe, tmp_path):
     n = _n()
     js = tmp_path / "r.json"
     out = subprocess.run([MPIRUN, "-n", str(n), exe, "--verify", "-n", "16", "--json", str(js), "--timeout", "45",
-                          "--min-gbs", MIN_GBS], capture_output=True, text=True, timeout=BUDGET_S["test_reference_matrix_all_gpus"])
+                          "--min-gbs", MIN_GBS], capture_output=True, text=True,
+                         timeout=BUDGET_S["test_reference_matrix_all_gpus"] * (2 if REHEARSAL >= 8 else 1))
     assert out.returncode == 0, out.stderr[-3000:]
     m = parse_compat(out.stdout)
     for key in ("uni", "bi"):
@@ -109,8 +117,9 @@ def test_concurrent_modes_all_gpus(exe):
     n = _n()
     for comms in ("1", "4"):
         out = subprocess.run([MPIRUN, "-n", str(n), exe, "--comms", comms, "--mode", "tournament,ring,allpairs",
-                              "--sizes", "1M,64M", "-n", "8", "--verify", "--latency", "--no-compat", "--timeout", "20"],
-                             capture_output=True, text=True, timeout=BUDGET_S["test_concurrent_modes_all_gpus"] / 2)
+                              "--sizes", CONCURRENT_SIZES, "-n", "8", "--verify", "--latency", "--no-compat", "--timeout",
+                              "60" if CONCURRENT_TIMEOUT_S else "20"], capture_output=True, text=True,
+                             timeout=CONCURRENT_TIMEOUT_S or BUDGET_S["test_concurrent_modes_all_gpus"] / 2)
         assert out.returncode == 0, out.stderr[-3000:]
         assert "verification: OK" in out.stdout and "FAILED" not in out.stdout
 
