@@ -113,9 +113,10 @@ from test_nccl_p2p_amd.bench import core  # noqa: E402
 core.set_start(T0)
 # Re-exported: the pure functions the unit tests pin (tests/test_bench_unit.py).
 from test_nccl_p2p_amd.bench.compare import child_main, steps_through  # noqa: E402,F401
-from test_nccl_p2p_amd.bench.core import (METRIC, Deadline, Reporter, cell_matrix, claim_stdout,  # noqa: E402,F401
-                                          default_device, first_comms, free_port, headline_stats, link_check, log,
-                                          pick_depth, posting_candidates, start_watchdog, tuning_steps)
+from test_nccl_p2p_amd.bench.core import (METRIC, Deadline, Reporter, Timeline, candidate_budget,  # noqa: E402,F401
+                                          cell_matrix, claim_stdout, default_device, first_candidate_budget,
+                                          first_comms, free_port, headline_stats, link_check, log, pick_depth,
+                                          posting_candidates, process_age, start_watchdog, tuning_steps)
 from test_nccl_p2p_amd.bench.headline import HeadlineMixin  # noqa: E402
 from test_nccl_p2p_amd.bench.sections import SectionsMixin  # noqa: E402
 
@@ -222,6 +223,8 @@ class BenchRun(HeadlineMixin, SectionsMixin):
         from test_nccl_p2p_amd.parallel.session import create_session, init_control_plane
 
         self.args = args
+        self.timeline = Timeline(T0)
+        self.timeline.begin("init")
         self.nat = require_native()
         self.create_session = create_session
         self.deadline = Deadline(args.deadline)
@@ -233,7 +236,7 @@ class BenchRun(HeadlineMixin, SectionsMixin):
         self.device = default_device(self.env.local_rank) if args.device is None else args.device
         if self.use_gpu:
             torch.cuda.set_device(self.device)
-        self.reporter = Reporter(self.env.rank, real_stdout, args.json_out)
+        self.reporter = Reporter(self.env.rank, real_stdout, args.json_out, self.timeline, self.deadline)
         self.state = {"section": "setup", "skipped": [], "errors": {}}
         start_watchdog(self.deadline, self.reporter, self.nat, self.state)
         self.size = self.nat.parse_size(args.size)
@@ -261,6 +264,16 @@ class BenchRun(HeadlineMixin, SectionsMixin):
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         return bool(t.item())
 
+    def allmax(self, v: float) -> float:
+        """The largest of every rank's `v`, over the gloo control plane (not a
+        native session's bootstrap, which a failed candidate may leave out of
+        step)."""
+        if self.n == 1:
+            return float(v)
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
     def log0(self, msg: str):
         if self.env.rank == 0:
             log(msg)
@@ -280,6 +293,7 @@ class BenchRun(HeadlineMixin, SectionsMixin):
             h.value, h.aggregate, h.elapsed / self.args.steps * 1e3, h.vr))
 
         self.untimed_t0 = time.monotonic()
+        self.timeline.begin("untimed")
         self.plan_sections()
         self.live = list({id(x): x for x in (h.sess, h.ref_sess) if x is not None}.values())
         self.latency_sections()
@@ -292,6 +306,7 @@ class BenchRun(HeadlineMixin, SectionsMixin):
         self.comparisons()
         self.xgmi_sweep_section()
 
+        self.timeline.begin("report")
         self.reporter.update(untimed_skipped=self.state["skipped"] or None,
                              section_errors=self.state["errors"] or None)
         if self.env.rank == 0:
@@ -304,6 +319,9 @@ class BenchRun(HeadlineMixin, SectionsMixin):
         self.barrier()
         if self.n > 1 and dist.is_initialized():
             dist.destroy_process_group()
+        # The timeline ends at the JSON line; this is the whole process (a
+        # test holds the timeline's total against it).
+        self.log0("bench: process wall %.3f s" % process_age())
         return 0 if h.mismatches in (0, -1) else 3
 
 

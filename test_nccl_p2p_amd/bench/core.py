@@ -139,14 +139,91 @@ class Deadline:
         return self.end - time.monotonic()
 
 
+# Posting candidates' waits.  Every wait of a session is
+# bounded by its timeout (the transports' bounded polls abort and fail), so a
+# candidate that hangs costs what its session's timeout says, not --timeout:
+#   * the first candidate (the headline session's; it must work, or the
+#     headline fails over to the fallback data plane) gets FIRST_SHARE of the
+#     time the deadline leaves, at least CANDIDATE_MIN_S, at most --timeout;
+#   * every later (droppable) candidate gets CANDIDATE_COST_FACTOR x what the
+#     first one took to connect and run one tuning pass, at least
+#     CANDIDATE_MIN_S, and never more than CANDIDATE_SHARE of the time left;
+#   * all tuning together stays within TUNING_SHARE of the time left when it
+#     starts: a droppable candidate whose budget would not fit is skipped.
+CANDIDATE_MIN_S = 10.0
+CANDIDATE_COST_FACTOR = 10.0
+CANDIDATE_SHARE = 0.15
+FIRST_SHARE = 0.25
+TUNING_SHARE = 0.4
+
+
+def first_candidate_budget(timeout: float, left: float) -> float:
+    """Seconds any one wait of the first posting candidate may take, `left`
+    being what the deadline leaves (less RESERVE_S)."""
+    return min(timeout, max(CANDIDATE_MIN_S, FIRST_SHARE * left))
+
+
+def candidate_budget(first_cost: float, left: float, timeout: float) -> float:
+    """Seconds any one wait of a droppable candidate may take: scaled from
+    the first candidate's measured connect + one pass (slowest rank), capped
+    by a share of the time left and by --timeout."""
+    return min(timeout, CANDIDATE_SHARE * max(0.0, left),
+               max(CANDIDATE_MIN_S, CANDIDATE_COST_FACTOR * first_cost))
+
+
+def process_age() -> float:
+    """Seconds since this process started, by the kernel's record of its start
+    (/proc/self/stat starttime against /proc/uptime, 10 ms ticks); 0 if
+    unknown."""
+    try:
+        with open("/proc/self/stat") as f:
+            start_ticks = int(f.read().rsplit(")", 1)[1].split()[19])
+        with open("/proc/uptime") as f:
+            up = float(f.read().split()[0])
+        return max(0.0, up - start_ticks / os.sysconf("SC_CLK_TCK"))
+    except (OSError, ValueError, IndexError):
+        return 0.0
+
+
+class Timeline:
+    """Where the run's wall time went, for the JSON line (timeline_s; VERDICT
+    r4 item 2): contiguous phases from process start, each begin() closing the
+    open one, so the entries add up to the time from process start to the
+    snapshot.  The first entry is the interpreter's start up to bench.py's
+    first line (T0); the open entry at a watchdog emit names the phase the
+    deadline caught."""
+
+    def __init__(self, t0: float):
+        self.start = time.monotonic() - process_age()
+        self.start = min(self.start, t0)
+        self.lock = threading.Lock()
+        self.entries = [["startup", t0 - self.start]]
+        self.name, self.t = "imports", t0
+
+    def begin(self, name: str):
+        with self.lock:
+            now = time.monotonic()
+            self.entries.append([self.name, now - self.t])
+            self.name, self.t = name, now
+
+    def snapshot(self, deadline=None) -> dict:
+        with self.lock:
+            now = time.monotonic()
+            entries = [[n, round(s, 4)] for n, s in self.entries] + [[self.name, round(now - self.t, 4)]]
+            return {"entries": entries, "open": self.name, "total_s": round(now - self.start, 4),
+                    "deadline_left_s": round(deadline.left(), 3) if deadline is not None else None}
+
+
 class Reporter:
     """Holds the result and prints it exactly once (rank 0): at the normal end
     of the run, or from the watchdog when the deadline passes first."""
 
-    def __init__(self, rank: int, real_stdout: int, json_out):
+    def __init__(self, rank: int, real_stdout: int, json_out, timeline=None, deadline=None):
         self.rank = rank
         self.fd = real_stdout
         self.json_out = json_out
+        self.timeline = timeline  # its snapshot goes into every line (timeline_s)
+        self.deadline = deadline
         self.lock = threading.Lock()
         self.result = None  # set once the timed region is measured
         self.done = False
@@ -166,6 +243,8 @@ class Reporter:
             res = dict(self.result) if self.result is not None else {
                 "metric": METRIC, "value": None, "unit": "GB/s", "error": "the timed steps did not finish"}
             res.update(extra)
+            if self.timeline is not None:
+                res["timeline_s"] = self.timeline.snapshot(self.deadline)
             line = json.dumps(res)
             os.write(self.fd, (line + "\n").encode())
             if self.json_out:
@@ -312,5 +391,25 @@ def hang_requested(section: str, rank: int) -> bool:
     responding inside that untimed section."""
     spec = os.environ.get("P2P_BENCH_HANG", "")
     return bool(spec) and spec == "%s@%d" % (section, rank)
+
+
+def candidate_hang_requested(transport: str, comms: int, batch: int, phase: str, rank: int) -> bool:
+    """Test hook: P2P_BENCH_HANG="candidate:[<transport>:]<comms>,<batch>[:connect]@<rank>"
+    makes that rank stop making progress in that posting candidate's first
+    tuning pass (or its connect), as a peer whose transfer never completes:
+    it posts nothing, and its own wait ends only at its session's timeout."""
+    spec = os.environ.get("P2P_BENCH_HANG", "")
+    if not spec.startswith("candidate:") or "@" not in spec:
+        return False
+    what, at = spec[len("candidate:"):].rsplit("@", 1)
+    parts = what.split(":")
+    want_phase = "tuning"
+    if parts and parts[-1] in ("connect", "tuning"):
+        want_phase = parts.pop()
+    if len(parts) == 2:
+        if parts[0] != transport:
+            return False
+        parts = parts[1:]
+    return len(parts) == 1 and parts[0] == "%d,%d" % (comms, batch) and phase == want_phase and at == str(rank)
 
 

@@ -13,8 +13,19 @@ import types
 import torch
 import torch.distributed as dist
 
-from test_nccl_p2p_amd.bench.core import (BASELINE_VALUE, METRIC, cell_matrix, first_comms, headline_stats,
-                                          link_check, log, pick_depth, posting_candidates, tuning_steps)
+from test_nccl_p2p_amd.bench.core import (BASELINE_VALUE, METRIC, RESERVE_S, TUNING_SHARE, candidate_budget,
+                                          candidate_hang_requested, cell_matrix, first_candidate_budget, first_comms,
+                                          headline_stats, link_check, log, pick_depth, posting_candidates,
+                                          tuning_steps)
+
+
+def emulate_hang(seconds: float):
+    """The P2P_BENCH_HANG candidate hook: this rank posts nothing and waits
+    as a transport wait that never completes does, until its session's
+    timeout (the candidate's budget), then fails."""
+    log("bench: injected hang for the candidate's budget (%.1f s)" % seconds)
+    time.sleep(seconds)
+    raise RuntimeError("injected hang: no progress within %.1f s" % seconds)
 
 
 def hw_queues() -> int:
@@ -57,13 +68,19 @@ class HeadlineMixin:
         through `transport`; returns what the report needs."""
         args, nat, n, mode, size = self.args, self.nat, self.n, self.mode, self.size
         headline = transport + (":%d" % args.comms if transport == "rccl" and args.comms > 1 else "")
-        sess = self.create_session(headline, device=self.device, timeout_s=args.timeout)
+        tl, pre = self.timeline, ("fallback/" if self.fallback else "")
+        # The first candidate's budget: a share of the time the deadline
+        # leaves, so that should it hang the fallback still fits (core.py).
+        first_budget = first_candidate_budget(args.timeout, self.deadline.left() - RESERVE_S)
+        tl.begin(pre + "session_init")
+        sess = self.create_session(headline, device=self.device, timeout_s=first_budget)
         self.log0("bench: %d rank(s), %s, %s" % (n, sess.transport, sess.device_desc))
         # Test hook: P2P_BENCH_FAIL_HEADLINE=<transport> fails the headline
         # through that transport on every rank, as a communicator that cannot
         # be set up does.
         if os.environ.get("P2P_BENCH_FAIL_HEADLINE") == transport:
             raise RuntimeError("injected headline failure")
+        tl.begin(pre + "provenance")
         provenance = json.loads(sess.provenance(self.device if self.use_gpu else -1))
         provenance.pop("type", None)
 
@@ -75,32 +92,57 @@ class HeadlineMixin:
         # candidate (one group per step vs one per message; RCCL: one
         # communicator vs several whose send/recv kernels run side by side,
         # posting_candidates), timed by the slowest rank, before the W warmup
-        # steps of the chosen one.
+        # steps of the chosen one.  Every wait of a candidate is bounded by its
+        # budget (first_candidate_budget / candidate_budget), so one that hangs
+        # on some rank is dropped on every rank in seconds, not at --timeout.
         self.state["section"] = "tuning"
         choices = posting_candidates(transport, args.comms, args.batch, n, hw_queues=hw_queues())
         c0 = first_comms(transport, args.comms)
         sessions = {c0: sess}
 
-        def session_for(c):
+        def session_for(c, timeout_s):
             if c not in sessions:
-                # A candidate that stalls is aborted and dropped after --timeout.
-                sessions[c] = self.create_session("rccl:%d" % c if c > 1 else "rccl", device=self.device,
-                                                  timeout_s=args.timeout)
+                name = transport + (":%d" % c if transport == "rccl" and c > 1 else "")
+                sessions[c] = self.create_session(name, device=self.device, timeout_s=timeout_s)
+            else:
+                sessions[c].set_timeout(timeout_s)
             return sessions[c]
 
-        tuning, tuning_passes, failed = {}, {}, {}
+        tuning, tuning_passes, failed, skipped, budgets = {}, {}, {}, {}, {}
         phases = len(nat.schedule(mode, "bi", n))
         tune_k = tuning_steps(phases) * args.tune_laps
+        first_cost = None
         if args.tune_laps > 0 and len(choices) > 1:
+            tuning_t0 = time.monotonic()
+            tuning_cap = TUNING_SHARE * max(0.0, self.deadline.left() - RESERVE_S)
             for i, (c, b) in enumerate(choices):
                 key = "comms%d_%s" % (c, "batch" if b else "per_message")
                 # The headline session's first candidate must work; anything else
                 # (another communicator count, another posting) may be dropped.
                 droppable = i > 0 or c != c0
-                d, err = None, None
+                if droppable and first_cost is not None:
+                    wait_s = candidate_budget(first_cost, self.deadline.left() - RESERVE_S, args.timeout)
+                    used = time.monotonic() - tuning_t0
+                    if not self.agree(wait_s >= 1.0 and used + wait_s <= tuning_cap):
+                        skipped[key] = "no time left: budget %.1f s, tuning used %.1f of %.1f s" % (
+                            wait_s, used, tuning_cap)
+                        self.log0("bench: posting candidate %s skipped: %s" % ((c, b), skipped[key]))
+                        continue
+                else:
+                    wait_s = first_budget
+                budgets[key] = round(wait_s, 2)
+                d, err, connect_s = None, None, 0.0
+                t_phase = time.monotonic()
+                tl.begin("%stuning/%s/init" % (pre, key))
                 try:
-                    d = nat.StepDriver(session_for(c), mode, "bi", size, args.msgs, False, bool(b), bool(args.graph))
+                    s_c = session_for(c, wait_s)
+                    tl.begin("%stuning/%s/connect" % (pre, key))
+                    t_conn = time.monotonic()
+                    if candidate_hang_requested(transport, c, b, "connect", self.env.rank):
+                        emulate_hang(wait_s)
+                    d = nat.StepDriver(s_c, mode, "bi", size, args.msgs, False, bool(b), bool(args.graph))
                     d.connect()
+                    connect_s = time.monotonic() - t_conn
                     # Test hook: P2P_BENCH_FAIL_CANDIDATE="<comms>,<batch>" fails
                     # that candidate on the last rank only.
                     if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d" % (c, b) and self.env.rank == n - 1:
@@ -114,10 +156,14 @@ class HeadlineMixin:
                     # one-GPU runs picked 4 communicators over 8 and lost 15%
                     # (profiles/r3b_nt_ab/).
                     passes = []
-                    for _ in range(max(1, args.tune_passes)):
+                    for p in range(max(1, args.tune_passes)):
                         self.barrier()
+                        tl.begin("%stuning/%s/pass%d" % (pre, key, p))
+                        t_phase = time.monotonic()
                         w0 = time.perf_counter()
                         try:
+                            if p == 0 and candidate_hang_requested(transport, c, b, "tuning", self.env.rank):
+                                emulate_hang(wait_s)
                             d.run_steps(0, tune_k)
                             d.sync()
                             if (os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d,tuning" % (c, b)
@@ -130,10 +176,12 @@ class HeadlineMixin:
                             # Failed on some rank: dropped on every rank alike.
                             err = err or "failed on another rank"
                             break
-                        passes.append(sess.allreduce_max(w) / tune_k)
+                        passes.append(self.allmax(w) / tune_k)
                     if err is None:
                         tuning[(c, b)] = min(passes)
                         tuning_passes[(c, b)] = passes
+                        if first_cost is None:
+                            first_cost = self.allmax(connect_s) + min(passes) * tune_k
                         del d
                         # Only the best communicator count so far, the headline
                         # session and the single communicator (kept for the
@@ -143,13 +191,22 @@ class HeadlineMixin:
                             if not any(cc == c2 for (c2, _) in choices[i + 1:]):
                                 del sessions[cc]
                         continue
+                # Failed (on every rank alike).  A wait that ran out its budget
+                # on the slowest rank is reported as a timeout.
+                tl.begin("%stuning/%s/dropped" % (pre, key))
+                timed_out = self.allmax(time.monotonic() - t_phase) >= 0.9 * wait_s
+                err = err or "failed on another rank"
+                if timed_out:
+                    err = "timed out (waits bounded at %.1f s): %s" % (wait_s, err)
                 if not droppable:
-                    raise RuntimeError(err or "the first posting candidate failed on another rank")
-                failed[key] = err or "failed on another rank"
-                log("bench: posting candidate %s dropped: %s" % ((c, b), failed[key]))
+                    raise RuntimeError("first posting candidate %s: %s" % (key, err))
+                failed[key] = err
+                self.log0("bench: posting candidate %s dropped: %s" % ((c, b), failed[key]))
                 del d
-                if c != c0 and not any(cc == c for (cc, _) in tuning):
-                    sessions.pop(c, None)
+                # Its session may be out of step across ranks (an aborted
+                # communicator, a transfer cut off mid-message): closed on every
+                # rank, and opened afresh should the headline need it.
+                sessions.pop(c, None)
             comms, batch = min(tuning, key=tuning.get)
             reason = "fastest of %d candidate(s): best of %d pass(es) of %d untimed step(s) each (%s lap(s) of %d " \
                      "round(s)), slowest rank's clock" % (len(tuning), max(1, args.tune_passes), tune_k, args.tune_laps,
@@ -157,29 +214,36 @@ class HeadlineMixin:
         else:
             comms, batch = choices[0]
             reason = "single candidate" if len(choices) == 1 else "no tuning laps (--tune-laps 0): first candidate"
-        sess = session_for(comms)
+        tl.begin(pre + "headline/session")
+        sess = session_for(comms, args.timeout)
         # A single-communicator session stays for the reference-method comparison
         # (the reference uses one communicator); other candidates are closed.
         ref_sess = sessions.get(1)
+        if ref_sess is not None:
+            ref_sess.set_timeout(args.timeout)
         for c in list(sessions):
             if c not in (comms, 1):
                 del sessions[c]
 
         # ---- the headline driver: W warmup steps, poison, K timed steps -------
         self.state["section"] = "headline"
+        tl.begin(pre + "headline/connect")
         drv = nat.StepDriver(sess, mode, "bi", size, args.msgs, not args.no_verify, bool(batch), bool(args.graph),
                              depth=pick_depth(args.steps, phases), recv_budget=budget, salt=1)
         drv.connect()
         rccl_peers, matrix_transport = (self.link_report(sess) if transport == "rccl" else (None, None))
+        tl.begin(pre + "headline/warmup")
         drv.run_steps(0, args.warmup)
         drv.sync()
         chunking = None
         if transport == "rccl" and not args.no_verify and args.warmup > 0:
             chunking = self.verify_warmup(drv, [x for x in (sess, ref_sess) if x is not None])
+        tl.begin(pre + "headline/poison")
         drv.poison()  # untimed: every receive slot zeroed; a slot passes verification only if a timed step wrote it
         self.gpu_sync()
         drv.reset()
 
+        tl.begin(pre + "headline/timed")
         self.barrier()
         self.gpu_sync()
         self.barrier()
@@ -198,6 +262,7 @@ class HeadlineMixin:
         value, aggregate = headline_stats(job_bytes, flows_total, args.steps, elapsed)
 
         # Per-step GPU durations of every rank -> per-cell bandwidth.
+        tl.begin(pre + "headline/matrix")
         my_ms = drv.step_ms()
         post_ms = list(drv.post_ms())
         all_ms = [None] * n
@@ -210,6 +275,7 @@ class HeadlineMixin:
 
         # The post-timing check of every slot a timed step wrote (batched:
         # Transport::verify_many), timed for the record (verify_detail.seconds).
+        tl.begin(pre + "headline/verify")
         v0 = time.perf_counter()
         vr = drv.verify_steps(args.warmup, args.steps) if not args.no_verify else None
         if vr is not None:
@@ -221,7 +287,7 @@ class HeadlineMixin:
         del drv
         return types.SimpleNamespace(
             sess=sess, ref_sess=ref_sess, sessions=sessions, provenance=provenance, comms=comms, batch=batch,
-            failed=failed, reason=reason, tuning=tuning, tuning_passes=tuning_passes, elapsed=elapsed, flows_total=flows_total, value=value,
+            failed=failed, skipped=skipped, budgets=budgets, first_cost=first_cost, reason=reason, tuning=tuning, tuning_passes=tuning_passes, elapsed=elapsed, flows_total=flows_total, value=value,
             aggregate=aggregate, my_ms=my_ms, matrix=matrix, samples=samples, cells=cells, offdiag=offdiag,
             expected=n * (n - 1) if n > 1 else 1, vr=vr, mismatches=vr["mismatches"] if vr else -1, depth=depth,
             recv_bytes=recv_bytes, chunking=chunking, rccl_peers=rccl_peers, matrix_transport=matrix_transport,
@@ -395,7 +461,9 @@ class HeadlineMixin:
             "posting": {"batch": bool(h.batch), "graph": bool(args.graph), "rccl_comms": h.comms, "chunking": h.chunking,
                         "hw_queues": {"GPU_MAX_HW_QUEUES": hw_queues(),
                                       "environment_had": os.environ.get("P2P_HW_QUEUES_ENV") or None},
-                        "dropped": h.failed or None, "selection": h.reason,
+                        "dropped": h.failed or None, "skipped": h.skipped or None, "selection": h.reason,
+                        "candidate_budget_s": h.budgets or None,
+                        "first_candidate_cost_s": round(h.first_cost, 4) if h.first_cost is not None else None,
                         "tuning_ms_per_step": {"comms%d_%s" % (c, "batch" if b else "per_message"): round(v * 1e3, 4)
                                                for (c, b), v in h.tuning.items()} or None,
                         "tuning_passes_ms_per_step": {"comms%d_%s" % (c, "batch" if b else "per_message"):

@@ -55,7 +55,11 @@ class SectionsMixin:
         # One collective per section: a failure may be local to some ranks
         # (a hung rank leaves the others here until the watchdog fires).
         broken = sessions and self.broken
+        # (Its own timeline entry: a rank whose peer stopped responding waits
+        # here, and the watchdog's line then shows that wait as the open one.)
+        self.timeline.begin("agree:" + name)
         if not self.agree(left > min_s and not broken):
+            self.timeline.begin("untimed")
             self.state["skipped"].append(name)
             self.log0("bench: skipping %s: %s" % (name, "the sessions failed in %s" % self.broken if broken
                                                   else "no time left (or another rank's sessions failed)"))
@@ -65,6 +69,7 @@ class SectionsMixin:
         for s in self.live:
             s.set_timeout(max(1.0, min(self.args.timeout, wait_left)))
         self.state["section"] = name
+        self.timeline.begin("section:" + name)
         if hang_requested(name, self.env.rank):
             log("bench: injected hang in %s on rank %d" % (name, self.env.rank))
             while True:
@@ -79,6 +84,7 @@ class SectionsMixin:
             return {"error": str(e)[:300]}
         finally:
             self.state["section"] = None
+            self.timeline.begin("untimed")
 
     def agreed_min(self, v: float) -> float:
         """The smallest of every rank's `v` (collective)."""

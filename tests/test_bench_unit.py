@@ -234,3 +234,53 @@ def test_stock_reference_only_for_rccl_within_the_process_limit():
     assert run("rccl", ["a"]) and run("rccl", ["a", "b", "c", "d", "e", "f", "g", "h"])
     assert run("rccl", ["a"] * 4) and not run("rccl", ["a"] * 8)
     assert not run("ipc", ["a"]) and not run("rccl", ["a"], ref_stock=0)
+
+
+def test_candidate_budgets():
+    from test_nccl_p2p_amd.bench import core
+
+    # The first candidate: a quarter of the time left, at least 10 s, at most --timeout.
+    assert core.first_candidate_budget(120.0, 280.0) == 70.0
+    assert core.first_candidate_budget(120.0, 20.0) == 10.0
+    assert core.first_candidate_budget(30.0, 280.0) == 30.0
+    # Later candidates: 10 x the first one's connect + pass, at least 10 s,
+    # never more than 15% of the time left (nor --timeout).
+    assert core.candidate_budget(0.05, 280.0, 120.0) == 10.0
+    assert abs(core.candidate_budget(3.0, 280.0, 120.0) - 30.0) < 1e-9
+    assert abs(core.candidate_budget(6.0, 280.0, 120.0) - 42.0) < 1e-9
+    assert abs(core.candidate_budget(0.05, 40.0, 120.0) - 6.0) < 1e-9
+    assert core.candidate_budget(6.0, -5.0, 120.0) == 0.0
+
+
+def test_candidate_hang_hook(monkeypatch):
+    from test_nccl_p2p_amd.bench.core import candidate_hang_requested as hang
+
+    monkeypatch.setenv("P2P_BENCH_HANG", "candidate:4,1@3")
+    assert hang("rccl", 4, 1, "tuning", 3) and hang("host", 4, 1, "tuning", 3)
+    assert not hang("rccl", 4, 1, "tuning", 2) and not hang("rccl", 4, 0, "tuning", 3)
+    assert not hang("rccl", 4, 1, "connect", 3)
+    monkeypatch.setenv("P2P_BENCH_HANG", "candidate:host:1,0:connect@0")
+    assert hang("host", 1, 0, "connect", 0)
+    assert not hang("shm", 1, 0, "connect", 0) and not hang("host", 1, 0, "tuning", 0)
+    monkeypatch.setenv("P2P_BENCH_HANG", "latency@3")
+    assert not hang("rccl", 1, 0, "tuning", 3)
+
+
+def test_timeline_entries_are_contiguous():
+    import time
+
+    from test_nccl_p2p_amd.bench.core import Deadline, Timeline, process_age
+
+    assert process_age() > 0
+    t0 = time.monotonic()
+    tl = Timeline(t0)
+    tl.begin("a")
+    time.sleep(0.02)
+    tl.begin("b")
+    snap = tl.snapshot(Deadline(1000.0))
+    names = [n for n, _ in snap["entries"]]
+    assert names == ["startup", "imports", "a", "b"] and snap["open"] == "b"
+    # Contiguous from process start: the entries add up to the total.
+    assert abs(sum(s for _, s in snap["entries"]) - snap["total_s"]) < 1e-3
+    assert dict(snap["entries"])["a"] >= 0.019
+    assert snap["total_s"] >= process_age() - 0.05 and snap["deadline_left_s"] > 0

@@ -4,6 +4,7 @@ native engine under torchrun (TCP bootstrap + host transport), and bench.py's
 full control flow with the host transport."""
 import json
 import os
+import re
 import subprocess
 import sys
 import time
@@ -152,6 +153,55 @@ def test_bench_drops_a_candidate_failing_in_warmup(native):
     assert r["posting"]["dropped"]["comms1_batch"] in ("injected tuning failure", "failed on another rank")
 
 
+HANG_ARGS = ["bench.py", "--gpus", "4", "--steps", "3", "--warmup", "2", "--transport", "host", "--size", "64K",
+             "--msgs", "2", "--latency-iters", "10", "--sweep", "0", "--extras", "0", "--ref-iters", "0",
+             "--ipc-extra", "0", "--deadline", "120", "--fallback-to", "shm"]
+
+
+def test_bench_drops_a_hung_candidate_within_its_budget(native):
+    """a droppable posting candidate that hangs on one rank
+    (P2P_BENCH_HANG=candidate:...: the rank posts nothing, so its peers'
+    transfers never complete) costs its budget -- 10 x the first candidate's
+    connect + pass, at least 10 s -- not --timeout (120 s): every rank drops
+    it, says it timed out, and the verified headline comes well within the
+    deadline."""
+    t0 = time.monotonic()
+    out = torchrun(4, HANG_ARGS, env={"P2P_BENCH_HANG": "candidate:1,1@3"}, timeout=200)
+    wall = time.monotonic() - t0
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert out.returncode == 0 and len(lines) == 1, out.stderr[-3000:]
+    r = json.loads(lines[0])
+    assert r["value"] is not None and r["value"] > 0 and r["verify_mismatches"] == 0, r
+    post = r["posting"]
+    assert post["batch"] is False and post["candidate_budget_s"]["comms1_batch"] == 10.0, post
+    assert post["dropped"]["comms1_batch"].startswith("timed out (waits bounded at 10.0 s)"), post["dropped"]
+    assert not r.get("deadline_hit") and r["headline_fallback"] is None
+    assert wall < 120, wall
+    # The timeline shows where the 10 s went.
+    spent = dict(r["timeline_s"]["entries"])
+    assert 9.0 < spent["tuning/comms1_batch/pass0"] < 30.0, r["timeline_s"]
+
+
+def test_bench_hung_first_candidate_falls_back_within_the_deadline(native):
+    """The same hang in the first candidate, which the headline's own session
+    must pass: its waits are bounded by a quarter of the time the deadline
+    leaves, the headline fails over to the fallback data plane (host -> shm
+    here, rccl -> ipc on GPUs) and the line -- value null, the fallback's
+    number beside it -- still comes before the deadline."""
+    t0 = time.monotonic()
+    out = torchrun(4, HANG_ARGS, env={"P2P_BENCH_HANG": "candidate:host:1,0@3"}, timeout=200)
+    wall = time.monotonic() - t0
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert out.returncode == 0 and len(lines) == 1, out.stderr[-3000:]
+    r = json.loads(lines[0])
+    fb = r["headline_fallback"]
+    assert r["value"] is None and r["transport"] == "shm" and fb["value_gbs"] > 0, r
+    assert "timed out" in fb["error"] and "comms1_per_message" in fb["error"], fb
+    assert r["verify_mismatches"] == 0 and not r.get("deadline_hit")
+    assert wall < 120, wall
+    names = [n for n, _ in r["timeline_s"]["entries"]]
+    assert "tuning/comms1_per_message/pass0" in names and "fallback/headline/timed" in names, names
+
 
 def test_fuzz_session_over_shm_and_host(native):
     """Random verified message groups, 3 processes, over the shared-memory and
@@ -224,6 +274,12 @@ def test_bench_deadline_with_a_hung_section(native):
     assert r["value"] is not None and r["value"] > 0 and r["deadline_hit"] is True, (r, out.stderr[-2000:])
     assert "latency" in (r["section_errors"] or {}), r["section_errors"]
     assert wall < 80 + 30, wall
+    # The watchdog's line carries the timeline: rank 0's latency section ran
+    # until its waits gave up (their bound is the time left), and the open
+    # entry is its wait for the others to agree on the next section.
+    tl = r["timeline_s"]
+    assert dict(tl["entries"])["section:latency"] > 10 and tl["open"] == "agree:latency_preposted", tl
+    assert tl["entries"][-1][0] == tl["open"] and tl["deadline_left_s"] <= 0.5, tl
 
 
 def test_bench_eight_ranks_with_the_driver_step_counts(native):
@@ -233,9 +289,11 @@ def test_bench_eight_ranks_with_the_driver_step_counts(native):
     every timed delivery is verified, and no section is skipped or fails.
     The extras' sizes are lowered to fit the CPU container (all-pairs holds
     7 receive slots per rank)."""
+    t0 = time.monotonic()
     out = torchrun(8, ["bench.py", "--gpus", "8", "--steps", "20", "--warmup", "5", "--transport", "shm",
                        "--size", "256K", "--msgs", "4", "--sweep-max", "4M", "--ref-iters", "8",
                        "--latency-iters", "50", "--allpairs-size", "16M", "--ring-size", "4M"], timeout=300)
+    wall = time.monotonic() - t0
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1
@@ -257,6 +315,17 @@ def test_bench_eight_ranks_with_the_driver_step_counts(native):
     assert r["ipc_transport"]["verify_mismatches"] == 0
     lat = r["latency_p50_us_matrix"]
     assert all(lat[a][b] > 0 for a in range(8) for b in range(8) if a != b)
+    # the timeline accounts for rank 0's whole process up to
+    # the line (what is left is the teardown after it), per candidate and pass.
+    tl = r["timeline_s"]
+    total = sum(s for _, s in tl["entries"])
+    proc = float(re.search(r"bench: process wall ([0-9.]+) s", out.stderr).group(1))
+    assert abs(total - tl["total_s"]) < 0.01 and abs(total - proc) <= 0.05 * proc, (total, proc, tl)
+    assert total < wall
+    names = [n for n, _ in tl["entries"]]
+    for n in ("tuning/comms1_per_message/connect", "tuning/comms1_batch/pass1", "headline/timed",
+              "section:reference_semantics", "section:allpairs_1g", "section:host"):
+        assert n in names, names
 
 
 def test_bench_headline_fallback(native):
