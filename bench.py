@@ -289,6 +289,10 @@ class BenchRun(HeadlineMixin, SectionsMixin):
         if lc and not lc["ok"]:
             self.log0("bench: WRONG TRANSPORT: RCCL carried %d of %d direct xGMI pairs over something else than "
                       "P2P: %s" % (len(lc["not_p2p"]), lc["direct_xgmi_pairs"], ", ".join(lc["not_p2p"][:16])))
+        up = self.reporter.result.get("unparsed_peers")
+        if up:
+            self.log0("bench: WARN RCCL connection lines not parsed for %s: their ops stay at the 2-channel limit "
+                      "(raw lines: provenance.rccl_peers[].unparsed_peers)" % ", ".join(up[:16]))
         self.log0("bench: value %.2f GB/s per cell (aggregate %.2f GB/s), %.4f ms/step, verify %s" % (
             h.value, h.aggregate, h.elapsed / self.args.steps * 1e3, h.vr))
 

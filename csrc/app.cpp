@@ -18,6 +18,27 @@
 
 namespace p2p {
 
+int parse_verify_impl(const std::string& v, std::string* note) {
+  if (v == "auto") return 0;
+  if (v == "lds8" || v == "lds") return 1;
+  if (v == "stride" || v == "reg" || v == "register") return 2;
+  // Variants that lost their A/B against lds8 / stride and were removed in
+  // round 5 (their measurements stay in profiles/).
+  static const char* const kRemoved[][2] = {
+      {"lds-cached", "profiles/r1_tuned/ (5.7-5.9 TB/s, default-cache LDS-DMA)"},
+      {"lds-pipe", "profiles/r1_tuned/ (pipelined LDS loop, no gain)"},
+      {"lds8-span", "profiles/r4_verify_span/ (per-workgroup spans, no gain)"},
+      {"grid", "profiles/r1_tuned/ (full-grid register loop, 5.6-6.4 TB/s)"},
+  };
+  for (const auto& r : kRemoved)
+    if (v == r[0]) {
+      if (note) *note = strfmt("removed in round 5: it lost its A/B (%s); use lds8 or stride", r[1]);
+      return -2;
+    }
+  if (note) *note = "unknown (auto | lds8 | stride; see --help)";
+  return -1;
+}
+
 std::string usage_text() {
   return R"(p2p_matrix — MI355X inter-GPU point-to-point bandwidth / latency matrix (RCCL over xGMI)
 
@@ -46,7 +67,9 @@ timing
                          wallclock reference semantics: host clock, sync per message
       --reference        = --timing wallclock --warmup 0 --no-warm --two-streams, and RCCL's
                          own kernel unroll (P2P_RCCL_UNROLL is not applied): the reference's
-                         methodology on a stock RCCL setup, p2p_matrix.cc:141-267
+                         methodology on a stock RCCL setup, p2p_matrix.cc:141-267; and its
+                         buffers: one send and one receive region reused by every
+                         iteration (:124-130), so --verify checks the last delivery
       --two-streams      RCCL: receives on a second stream, like the reference's s_1
       --comms K          RCCL: K communicators per rank on K streams; the i-th message
                          of >= 1 MiB from a to b uses communicator (i + a + b) mod K on both
@@ -69,8 +92,8 @@ data
   -c, --verify           random-fill sends, verify every received buffer on the device,
                          outside the timed loop (the default)
       --no-verify        zero-filled sends, nothing read back (the reference's data)
-      --verify-impl I    auto (= lds8) | lds | lds8 | lds8-span | lds-pipe | lds-cached | stride | reg
-                         (LDS-DMA- or register-staged verify kernel variants)
+      --verify-impl I    auto (= lds8) | lds8 (alias lds) | stride (alias reg)
+                         (LDS-DMA- or register-staged verify kernel)
 transport / launch
       --transport T      rccl  MI355X + RCCL ncclSend/ncclRecv over xGMI      [rccl]
                          ipc   one-sided pulls from hipIpc-mapped peer buffers (gfx950 copy
@@ -111,10 +134,6 @@ environment (recorded in every --json provenance record; docs/OUTPUT.md)
   P2P_VERIFY_BUDGET=B    --verify: bytes of receive generations (one per timed iteration)
                          [free HBM / 4, <= 32G]
   P2P_RCCL_SPLIT_MIN=B   --comms: smaller messages stay on communicator 0       [1M]
-  P2P_RCCL_GROUP_PER_COMM=1  --comms: each communicator's ops as an RCCL group of
-                         their own                                                 [0]
-  P2P_RCCL_CU_MASK=contig|stride|full  --comms: each communicator's stream on its own CU
-                         mask (1/K of the CUs, or every CU: a hardware queue of its own); experiment
   P2P_RCCL_REGISTER=1|2  ncclCommRegister every buffer (2: + ncclMemAlloc)
   P2P_RCCL_BLOCKING=1    blocking ncclCommInitRank instead of the polled non-blocking init
   P2P_RCCL_DISTINCT_HOSTS=1  one NCCL_HOSTID per rank: RCCL ranks may share a GPU (tests,
@@ -229,6 +248,7 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
       cfg->run.warmup = 0;
       cfg->warm_connections = false;
       cfg->two_streams = true;
+      cfg->reference_buffers = true;
       cfg->rccl_stock = true;
     } else if (a == "--two-streams") {
       cfg->two_streams = true;
@@ -256,18 +276,11 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
     } else if (a == "--no-verify") {
       cfg->run.verify = false;
     } else if (a == "--verify-impl") {
-      std::string v = next();
-      cfg->verify_impl = v == "reg" || v == "register" ? 1
-                         : v == "lds"                  ? 2
-                         : v == "stride"               ? 3
-                         : v == "lds8"                 ? 4
-                         : v == "lds-cached"           ? 5
-                         : v == "lds-pipe"             ? 6
-                         : v == "lds8-span"            ? 7
-                         : v == "auto"                 ? 0
-                                                       : -1;
+      const std::string v = next();
+      std::string note;
+      cfg->verify_impl = parse_verify_impl(v, &note);
       if (cfg->verify_impl < 0) {
-        std::fprintf(stderr, "p2p_matrix: unknown --verify-impl '%s' (see --help)\n", v.c_str());
+        std::fprintf(stderr, "p2p_matrix: --verify-impl '%s': %s\n", v.c_str(), note.c_str());
         *exit_code = 1;
         return false;
       }
@@ -672,7 +685,10 @@ int run_app(const AppConfig& cfg, Bootstrap& boot, FILE* out, AppResult* result)
   // allows, so the check after timing covers each delivery, not only the last
   // one into a slot (runner.hpp RunConfig::gens; verify_coverage in the output).
   AppConfig run_cfg = cfg;
-  if (cfg.run.verify) {
+  // --reference keeps the reference's footprint (one 32 MiB send and receive
+  // buffer for all 128 iterations, p2p_matrix.cc:124-130, which can stay in
+  // the 256 MB Infinity Cache): one generation, the last delivery verified.
+  if (cfg.run.verify && !cfg.reference_buffers) {
     int most_iters = std::max(cfg.run.iters, cfg.run.warmup);
     if (cfg.iters_auto)
       for (size_t b : cfg.sizes) most_iters = std::max(most_iters, auto_iters(b, cfg.target_bytes));

@@ -46,6 +46,7 @@ struct AppConfig {
   bool compat = true;      // reference matrices for pair mode
   bool extended = true;    // GB/s / latency tables after the compat section
   double timeout_s = 300;
+  bool reference_buffers = false;  // --reference: one send / receive region for every iteration
   int verify_impl = 0;
   bool dry_run = false;    // print the schedules and exit (no transport)
   bool topology_only = false;  // print the GPU link matrix and exit
@@ -61,6 +62,11 @@ struct AppConfig {
 // when the program should exit immediately (--help, --version, bad flag).
 bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out = stdout);
 std::string usage_text();
+// --verify-impl / ops.verify(impl=) names -> dev::VerifyImpl values
+// (kernels.hpp): auto 0, lds8 (alias lds) 1, stride (aliases reg, register)
+// 2.  Returns -2 for a variant removed in round 5 and -1 for an unknown
+// name, with the reason in *note.
+int parse_verify_impl(const std::string& name, std::string* note);
 
 // Iterations for a message size under --iters auto.
 int auto_iters(size_t bytes, size_t target_bytes);

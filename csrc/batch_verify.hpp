@@ -33,6 +33,7 @@ inline std::vector<VerifyResult> batch_verify(dev::BatchVerifier& bv, const std:
   std::vector<dev::VerifyJob> dj;
   dj.reserve(jobs.size());
   for (const auto& j : jobs) dj.push_back({j.p, j.bytes, j.seed});
+  bv.reserve(static_cast<int>(dj.size()), sync);
   bv.enqueue(dj.data(), static_cast<int>(dj.size()), stream);
   sync();
   std::vector<VerifyResult> out(jobs.size());

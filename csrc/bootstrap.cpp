@@ -62,11 +62,14 @@ void set_sockopts(int fd) {
   setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
 }
 
-// Waits until fd is readable/writable or the deadline passes.
+// Waits until fd is readable/writable or the deadline passes.  A requested
+// abort (bench.py's deadline watchdog) ends the wait too, so the thread leaves
+// the engine and the watchdog can abort the communicators (abort_if_idle).
 void wait_fd(int fd, short events, double deadline, const char* what) {
   for (;;) {
     double left = deadline - now_seconds();
     if (left <= 0) P2P_FATAL(strfmt("bootstrap timeout while %s", what));
+    if (abort_requested()) P2P_FATAL(strfmt("bootstrap wait aborted while %s (the run's deadline passed)", what));
     pollfd p{fd, events, 0};
     int ms = static_cast<int>(std::min(left, 1.0) * 1000) + 1;
     int rc = ::poll(&p, 1, ms);

@@ -62,6 +62,37 @@ void run_abort_hooks(int code) {
 
 void set_throw_on_fatal(bool enable) { g_throw = enable; }
 
+namespace {
+std::mutex g_call_mu;
+int g_calls = 0;        // NativeCalls open
+bool g_closed = false;  // abort_if_idle ran: the engine takes no more calls
+}  // namespace
+
+NativeCall::NativeCall() {
+  std::lock_guard<std::mutex> lk(g_call_mu);
+  if (g_closed) P2P_FATAL("the engine was aborted (the run's deadline passed)");
+  ++g_calls;
+}
+
+NativeCall::~NativeCall() {
+  std::lock_guard<std::mutex> lk(g_call_mu);
+  --g_calls;
+}
+
+bool abort_if_idle() {
+  std::lock_guard<std::mutex> lk(g_call_mu);
+  if (g_calls > 0) return false;
+  g_closed = true;
+  run_abort_hooks(1);  // still holding g_call_mu: no call can enter meanwhile
+  note_abort_done();
+  return true;
+}
+
+void abort_wait(const char* who) {
+  note_abort_done();
+  P2P_FATAL(strfmt("%s: wait aborted (the run's deadline passed)", who));
+}
+
 void request_abort() { g_abort_requested.store(true, std::memory_order_relaxed); }
 bool abort_requested() { return g_abort_requested.load(std::memory_order_relaxed); }
 void note_abort_done() { g_abort_done.store(true, std::memory_order_release); }

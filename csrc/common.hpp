@@ -38,6 +38,25 @@ bool abort_requested();
 // Set by a transport once it has aborted its communicators on request.
 void note_abort_done();
 bool abort_done();
+// The other half of the cooperative abort: a thread that is not
+// inside the engine at all -- the main thread in a gloo barrier, a torch sync
+// or plain Python -- never reaches a polling wait.  Every binding that can
+// touch a communicator holds a NativeCall while it runs; abort_if_idle(),
+// called by the watchdog, runs the abort hooks on its own thread only when
+// no NativeCall is open (so no RCCL call can be running), refuses every
+// later NativeCall and notes the abort done.  Returns false (nothing done)
+// while a call is in flight.
+class NativeCall {
+ public:
+  NativeCall();
+  ~NativeCall();
+  NativeCall(const NativeCall&) = delete;
+  NativeCall& operator=(const NativeCall&) = delete;
+};
+bool abort_if_idle();
+// A CPU transport's wait that saw abort_requested(): nothing to abort but the
+// wait itself; notes the abort done and fails.
+[[noreturn]] void abort_wait(const char* who);
 
 [[noreturn]] void fatal(const char* file, int line, const std::string& what);
 

@@ -39,18 +39,16 @@ constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
 constexpr uint64_t kBlockVecs = kBlock;     // 16 B vectors per block iteration (4 KiB)
 constexpr uint64_t kMaxGrid = 1ull << 20;   // 4 GiB per grid pass
-constexpr int kStrideUnroll = 4;            // legacy grid-stride variants
-constexpr int kStrideBlocksPerCu = 8;        // legacy fill stride grid
-constexpr int kLdsStages = 4;               // 1 KiB LDS-DMA pieces per wave (4 KiB per wave)
-// Verify grid caps per variant, from scripts/verify_grid_sweep.py on MI355X
-// (1 GiB / 4 GiB, TB/s, run-to-run noise ~5%): LDS-DMA nt 8 KiB/wave 16/CU
-// 6.44 / 6.64; 4 KiB/wave 5.5-6.3 / 6.4-6.6; register stride 16/CU 6.5 / 6.7;
-// full-grid register 256/CU 5.6-6.4 / 6.7 (uncapped: 2.3 / 2.5, epilogue-bound);
-// LDS-DMA default cache policy 5.7 / 5.9 at any cap.
+constexpr int kStrideUnroll = 4;            // register verify: loads in flight per lane
+constexpr int kLdsStages = 8;               // 1 KiB LDS-DMA pieces per wave (8 KiB per wave)
+// Verify grid caps, from scripts/verify_grid_sweep.py on MI355X (1 GiB /
+// 4 GiB, TB/s, run-to-run noise ~5%): LDS-DMA nt 8 KiB/wave 16/CU 6.44 /
+// 6.64; register stride 16/CU 6.5 / 6.7.  The variants that lost this A/B
+// (4 KiB/wave and default-cache LDS-DMA, the pipelined LDS loop, per-block
+// spans, the full-grid register loop: 5.5-6.4 TB/s) were removed in round 5;
+// their numbers stay in profiles/r1_tuned/, r4_verify_span/.
 constexpr int kVerifyStridePerCu = 16;
-constexpr int kVerifyGridPerCu = 256;
 constexpr int kVerifyLdsPerCu = 16;
-constexpr FillImpl kDefaultFill = FillImpl::Grid;
 // LDS-staged verify is the default: 8 KiB of non-temporal LDS-DMA per wave
 // runs within 1-2% of register staging (profiles/r1_tuned/verify_grid_sweep.txt:
 // 6.44 / 6.64 TB/s at 1 / 4 GiB vs 6.53 / 6.74).
@@ -73,71 +71,21 @@ __device__ __forceinline__ void store_tail(uint8_t* tail, uint32_t tail_bytes, u
 
 // ------------------------------------------------------------------ fill ----
 
-// XCD-aware block order (XCD = true): the dispatcher hands workgroup b to XCD
-// b % 8, so in launch order consecutive 4 KiB blocks land on different XCDs.
-// Remapped, XCD x owns one contiguous eighth of the buffer (logical block
-// (b % 8) * (G / 8) + b / 8); requires G % 8 == 0 (launch_fill checks).
-constexpr unsigned kXcds = 8;
-template <bool XCD>
-__device__ __forceinline__ uint64_t logical_block() {
-  if (!XCD) return blockIdx.x;
-  return static_cast<uint64_t>(blockIdx.x % kXcds) * (gridDim.x / kXcds) + blockIdx.x / kXcds;
-}
-
 // Vectors [begin, nvec) of the buffer at p (launch_fill issues one full grid
 // per 4 GiB chunk); the tail bytes go with the last chunk (tail_bytes > 0).
-template <bool NT, bool XCD = false>
+// The one fill: one 16 B store per lane, one 4 KiB block per workgroup
+// (7.0 TB/s by WRITE_SIZE, profiles/r4_pmc/).  Its A/B losers -- non-temporal
+// stores, an XCD-ordered block map, a grid-stride loop over a capped grid, 2
+// or 4 stores per lane (6.0-6.9 TB/s, profiles/r3b_nt_ab/, r4_gpu_tier/) --
+// were removed in round 5.
 __global__ __launch_bounds__(kBlock) void fill_grid_kernel(uint4* __restrict__ p, uint64_t begin, uint64_t nvec,
                                                            uint64_t seed, uint8_t* __restrict__ tail,
                                                            uint32_t tail_bytes, uint64_t tail_offset) {
-  for (uint64_t base = begin + logical_block<XCD>() * kBlockVecs; base < nvec;
+  for (uint64_t base = begin + static_cast<uint64_t>(blockIdx.x) * kBlockVecs; base < nvec;
        base += static_cast<uint64_t>(gridDim.x) * kBlockVecs) {
     const uint32_t key = prng_key(seed, base * 4);  // block-uniform: scalar ALU
     const uint64_t i = base + threadIdx.x;
-    if (i < nvec) {
-      const uint4 v = prng_vec_k(key, i);
-      if (NT) {
-        u32x4 w = {v.x, v.y, v.z, v.w};
-        __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p) + i);
-      } else {
-        p[i] = v;
-      }
-    }
-  }
-  store_tail(tail, tail_bytes, tail_offset, seed);
-}
-
-// Full grid with VPL 16 B vectors per lane: workgroup b owns the contiguous
-// VPL x 4 KiB [begin + b * VPL * 256, ...) and issues all VPL stores before it
-// retires, so the dispatcher launches VPL times fewer workgroups per GiB
-// (262144 / VPL) -- the A/B for a dispatch-rate-bound one-block-per-4-KiB grid
-// (VERDICT r3 weak #1).  The block's span is a power of two <= 16 KiB that
-// starts at a multiple of itself, so the PRNG key is block-uniform.
-template <int VPL>
-__global__ __launch_bounds__(kBlock) void fill_multi_kernel(uint4* __restrict__ p, uint64_t begin, uint64_t nvec,
-                                                            uint64_t seed, uint8_t* __restrict__ tail,
-                                                            uint32_t tail_bytes, uint64_t tail_offset) {
-  const uint64_t base = begin + static_cast<uint64_t>(blockIdx.x) * (kBlockVecs * VPL);
-  const uint32_t key = prng_key(seed, base * 4);
-#pragma unroll
-  for (int u = 0; u < VPL; ++u) {
-    const uint64_t i = base + static_cast<uint64_t>(u) * kBlockVecs + threadIdx.x;
     if (i < nvec) p[i] = prng_vec_k(key, i);
-  }
-  store_tail(tail, tail_bytes, tail_offset, seed);
-}
-
-__global__ __launch_bounds__(kBlock) void fill_stride_kernel(uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
-                                                             uint8_t* __restrict__ tail, uint32_t tail_bytes,
-                                                             uint64_t tail_offset) {
-  const uint64_t tile = static_cast<uint64_t>(kBlock) * kStrideUnroll;
-  for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * tile; base < nvec; base += static_cast<uint64_t>(gridDim.x) * tile) {
-    const uint32_t key = prng_key(seed, base * 4);
-#pragma unroll
-    for (int u = 0; u < kStrideUnroll; ++u) {
-      const uint64_t i = base + static_cast<uint64_t>(u) * kBlock + threadIdx.x;
-      if (i < nvec) p[i] = prng_vec_k(key, i);
-    }
   }
   store_tail(tail, tail_bytes, tail_offset, seed);
 }
@@ -220,21 +168,6 @@ __device__ __forceinline__ uint4 load_nt(const uint4* p, uint64_t i) {
 }
 
 template <bool CHECK>
-__global__ __launch_bounds__(kBlock) void verify_grid_kernel(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
-                                                             const uint8_t* __restrict__ tail, uint32_t tail_bytes,
-                                                             uint64_t tail_offset, VerifyAccum* __restrict__ out) {
-  Partial acc{0, 0, ~0ull};
-  for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBlockVecs; base < nvec;
-       base += static_cast<uint64_t>(gridDim.x) * kBlockVecs) {
-    const uint64_t i = base + threadIdx.x;
-    const uint32_t key = prng_key(seed, base * 4);
-    if (i < nvec) check_vec<CHECK>(load_nt(p, i), key, i, acc);
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) check_tail<CHECK>(tail, tail_bytes, tail_offset, seed, acc);
-  block_commit(acc, out, blockIdx.x);
-}
-
-template <bool CHECK>
 __global__ __launch_bounds__(kBlock) void verify_stride_kernel(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
                                                                const uint8_t* __restrict__ tail, uint32_t tail_bytes,
                                                                uint64_t tail_offset, VerifyAccum* __restrict__ out) {
@@ -267,26 +200,10 @@ __global__ __launch_bounds__(kBlock) void verify_stride_kernel(const uint4* __re
 // wrote.  The four ds_read_b128 live in one asm statement: hipcc cannot tell
 // which LDS-DMA a ds_read aliases and would put a vmcnt(0) in front of each
 // one; the asm drains its own reads (lgkmcnt(0)).
-// Reads this lane's 16 B of each of STAGES consecutive 1 KiB LDS pieces in
+// Reads this lane's 16 B of each of the 8 consecutive 1 KiB LDS pieces in
 // one asm statement and drains them (lgkmcnt(0)) before returning.
-template <int STAGES>
-__device__ __forceinline__ void lds_read_stages(uint32_t addr, u32x4 (&r)[STAGES]);
-
-template <>
-__device__ __forceinline__ void lds_read_stages<4>(uint32_t addr, u32x4 (&r)[4]) {
-  asm volatile(
-      "ds_read_b128 %0, %4\n\t"
-      "ds_read_b128 %1, %4 offset:1024\n\t"
-      "ds_read_b128 %2, %4 offset:2048\n\t"
-      "ds_read_b128 %3, %4 offset:3072\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3])
-      : "v"(addr)
-      : "memory");
-}
-
-template <>
-__device__ __forceinline__ void lds_read_stages<8>(uint32_t addr, u32x4 (&r)[8]) {
+__device__ __forceinline__ void lds_read_stages(uint32_t addr, u32x4 (&r)[kLdsStages]) {
+  static_assert(kLdsStages == 8, "one ds_read_b128 per stage below");
   asm volatile(
       "ds_read_b128 %0, %8\n\t"
       "ds_read_b128 %1, %8 offset:1024\n\t"
@@ -304,13 +221,12 @@ __device__ __forceinline__ void lds_read_stages<8>(uint32_t addr, u32x4 (&r)[8])
 
 // Blocks `block` of `nblocks` of one buffer: the LDS-staged loop below, with
 // the workgroup's own LDS slots (the single and the batched verify share it).
-// SPAN = true: block b owns the contiguous super-chunks
-// [b * n_sc / nblocks, (b + 1) * n_sc / nblocks) and its waves interleave
-// inside them, instead of the grid-stride walk over the whole buffer (the
-// A/B of VerifyImpl::Lds8Span).
-template <bool CHECK, int STAGES, int AUX, bool SPAN = false>
+// aux = 2 on the LDS-DMA: non-temporal (6.3-6.6 TB/s against 5.7-5.9 with the
+// default cache policy; MI355X_MICROARCH.md ldsdma-fill row agrees).
+template <bool CHECK>
 __device__ __forceinline__ Partial lds_verify_blocks(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
                                                      uint64_t block, uint64_t nblocks) {
+  constexpr int STAGES = kLdsStages;
   __shared__ uint4 slot[kWaves][STAGES][64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x / 64;
@@ -319,20 +235,17 @@ __device__ __forceinline__ Partial lds_verify_blocks(const uint4* __restrict__ p
   const uint32_t lds_addr = static_cast<uint32_t>(
       reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)(&slot[wave][0][lane])));
   Partial acc{0, 0, ~0ull};
-  const uint64_t first = SPAN ? block * n_sc / nblocks + wave : block * kWaves + wave;
-  const uint64_t end = SPAN ? (block + 1) * n_sc / nblocks : n_sc;
-  const uint64_t step = SPAN ? kWaves : nblocks * kWaves;
-  for (uint64_t sc = first; sc < end; sc += step) {
+  for (uint64_t sc = block * kWaves + wave; sc < n_sc; sc += nblocks * kWaves) {
 #pragma unroll
     for (int s = 0; s < STAGES; ++s) {
       const uint64_t i = sc * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
       if (i < nvec)
         __builtin_amdgcn_global_load_lds(static_cast<const void*>(p + i),
-                                         (__attribute__((address_space(3))) void*)(&slot[wave][s][0]), 16, 0, AUX);
+                                         (__attribute__((address_space(3))) void*)(&slot[wave][s][0]), 16, 0, 2);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     u32x4 rv[STAGES];
-    lds_read_stages<STAGES>(lds_addr, rv);
+    lds_read_stages(lds_addr, rv);
     const uint32_t key = prng_key(seed, sc * sc_vecs * 4);  // wave-uniform
 #pragma unroll
     for (int s = 0; s < STAGES; ++s) {
@@ -343,11 +256,11 @@ __device__ __forceinline__ Partial lds_verify_blocks(const uint4* __restrict__ p
   return acc;
 }
 
-template <bool CHECK, int STAGES, int AUX, bool SPAN = false>
+template <bool CHECK>
 __global__ __launch_bounds__(kBlock) void verify_lds_kernel(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
                                                             const uint8_t* __restrict__ tail, uint32_t tail_bytes,
                                                             uint64_t tail_offset, VerifyAccum* __restrict__ out) {
-  Partial acc = lds_verify_blocks<CHECK, STAGES, AUX, SPAN>(p, nvec, seed, blockIdx.x, gridDim.x);
+  Partial acc = lds_verify_blocks<CHECK>(p, nvec, seed, blockIdx.x, gridDim.x);
   if (blockIdx.x == 0 && threadIdx.x == 0) check_tail<CHECK>(tail, tail_bytes, tail_offset, seed, acc);
   block_commit(acc, out, blockIdx.x);
 }
@@ -367,7 +280,6 @@ struct MultiVerifyArgs {
   int njobs;
 };
 
-template <int STAGES>
 __global__ __launch_bounds__(kBlock) void multi_verify_lds_kernel(const MultiVerifyArgs a,
                                                                   VerifyAccum* __restrict__ scratch) {
   int lo = 0, hi = a.njobs - 1;  // largest job with block_begin[job] <= blockIdx.x
@@ -379,7 +291,7 @@ __global__ __launch_bounds__(kBlock) void multi_verify_lds_kernel(const MultiVer
   const uint32_t b = blockIdx.x - a.block_begin[job];
   const uint32_t nb = a.block_begin[job + 1] - a.block_begin[job];
   const uint64_t nvec = a.nvec[job];
-  Partial acc = lds_verify_blocks<true, STAGES, 2>(a.p[job], nvec, a.seed[job], b, nb);
+  Partial acc = lds_verify_blocks<true>(a.p[job], nvec, a.seed[job], b, nb);
   if (b == 0 && threadIdx.x == 0)
     check_tail<true>(reinterpret_cast<const uint8_t*>(a.p[job] + nvec), a.tail[job], nvec * 16, a.seed[job], acc);
   block_commit(acc, scratch + static_cast<size_t>(job) * kVerifyShards, b);
@@ -409,70 +321,6 @@ __global__ __launch_bounds__(64) void multi_verify_finalize_kernel(const VerifyA
     out[blockIdx.x].checksum = c;
     out[blockIdx.x].first_bad = f;
   }
-}
-
-// Software-pipelined LDS staging: each wave owns two halves of STAGES KiB.
-// While it checks half b, the LDS-DMAs of its next chunk are already landing
-// in half b^1: issue next -> s_waitcnt vmcnt(STAGES) (only the next chunk's
-// DMAs may still be in flight, so the current half has landed) -> ds_read
-// half b -> compare.  The wave never idles on its own loads the way the
-// load-all / wait-all loop above does between chunks.  A partial final chunk
-// issues fewer DMAs, so the wait before it is a full vmcnt(0).
-template <int N>
-__device__ __forceinline__ void wait_vmcnt();
-template <>
-__device__ __forceinline__ void wait_vmcnt<0>() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-template <>
-__device__ __forceinline__ void wait_vmcnt<4>() { asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
-
-template <bool CHECK, int STAGES, int AUX>
-__global__ __launch_bounds__(kBlock) void verify_lds_pipe_kernel(const uint4* __restrict__ p, uint64_t nvec,
-                                                                 uint64_t seed, const uint8_t* __restrict__ tail,
-                                                                 uint32_t tail_bytes, uint64_t tail_offset,
-                                                                 VerifyAccum* __restrict__ out) {
-  __shared__ uint4 slot[kWaves][2][STAGES][64];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x / 64;
-  const uint64_t sc_vecs = static_cast<uint64_t>(STAGES) * 64;
-  const uint64_t n_sc = (nvec + sc_vecs - 1) / sc_vecs;
-  const uint64_t step = static_cast<uint64_t>(gridDim.x) * kWaves;
-  auto issue = [&](uint64_t c, int half) {
-#pragma unroll
-    for (int s = 0; s < STAGES; ++s) {
-      const uint64_t i = c * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
-      if (i < nvec)
-        __builtin_amdgcn_global_load_lds(static_cast<const void*>(p + i),
-                                         (__attribute__((address_space(3))) void*)(&slot[wave][half][s][0]), 16, 0, AUX);
-    }
-  };
-  Partial acc{0, 0, ~0ull};
-  uint64_t sc = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
-  int half = 0;
-  if (sc < n_sc) issue(sc, 0);
-  for (; sc < n_sc; sc += step, half ^= 1) {
-    const uint64_t next = sc + step;
-    if (next < n_sc) {
-      issue(next, half ^ 1);
-      if ((next + 1) * sc_vecs <= nvec)
-        wait_vmcnt<STAGES>();
-      else
-        wait_vmcnt<0>();
-    } else {
-      wait_vmcnt<0>();
-    }
-    const uint32_t lds_addr = static_cast<uint32_t>(
-        reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)(&slot[wave][half][0][lane])));
-    u32x4 rv[STAGES];
-    lds_read_stages<STAGES>(lds_addr, rv);
-    const uint32_t key = prng_key(seed, sc * sc_vecs * 4);  // wave-uniform
-#pragma unroll
-    for (int s = 0; s < STAGES; ++s) {
-      const uint64_t i = sc * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
-      if (i < nvec) check_vec<CHECK>(make_uint4(rv[s].x, rv[s].y, rv[s].z, rv[s].w), key, i, acc);
-    }
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) check_tail<CHECK>(tail, tail_bytes, tail_offset, seed, acc);
-  block_commit(acc, out, blockIdx.x);
 }
 
 __global__ void verify_reset_kernel(VerifyAccum* acc) {
@@ -529,17 +377,9 @@ int cu_count() {
   return c.cus[static_cast<size_t>(d)];
 }
 
-LaunchGeom fill_geometry(size_t bytes, FillImpl impl) {
+LaunchGeom fill_geometry(size_t bytes, FillImpl) {
   LaunchGeom g;
-  const uint64_t nvec = bytes / 16;
-  if (impl == FillImpl::Stride) {
-    const uint64_t tiles = (nvec + kBlock * kStrideUnroll - 1) / (kBlock * kStrideUnroll);
-    g.grid = static_cast<unsigned>(
-        std::max<uint64_t>(1, std::min(tiles, static_cast<uint64_t>(cu_count()) * kStrideBlocksPerCu)));
-  } else {
-    const uint64_t vpl = impl == FillImpl::Grid2 ? 2 : impl == FillImpl::Grid4 ? 4 : 1;
-    g.grid = grid_for((nvec + vpl * kBlockVecs - 1) / (vpl * kBlockVecs));
-  }
+  g.grid = grid_for((bytes / 16 + kBlockVecs - 1) / kBlockVecs);
   return g;
 }
 
@@ -549,43 +389,31 @@ LaunchGeom verify_geometry(size_t bytes, VerifyImpl impl, unsigned max_grid) {
   if (impl == VerifyImpl::Auto) impl = kDefaultVerify;
   // Unlike fill/copy, verify ends every workgroup with a reduction and an
   // atomic commit, so a full grid (one 4 KiB block per workgroup) pays that
-  // epilogue 256K times per GiB; the defaults below cap the grid so each
-  // workgroup streams tens of KiB per epilogue (kernel_bench A/B).
-  const bool lds = impl == VerifyImpl::Lds || impl == VerifyImpl::Lds8 || impl == VerifyImpl::LdsCached ||
-                   impl == VerifyImpl::LdsPipe || impl == VerifyImpl::Lds8Span;
-  const uint64_t per_cu = lds ? kVerifyLdsPerCu : impl == VerifyImpl::Stride ? kVerifyStridePerCu : kVerifyGridPerCu;
-  const uint64_t cap = max_grid ? max_grid : static_cast<uint64_t>(cu_count()) * per_cu;
-  if (lds) {
-    // KiB per chunk a wave checks, and KiB of LDS a wave owns.
-    const uint64_t stages = impl == VerifyImpl::Lds8 || impl == VerifyImpl::Lds8Span ? 8 : kLdsStages;
-    const uint64_t lds_stages = impl == VerifyImpl::LdsPipe ? 2 * stages : stages;
-    const uint64_t sc_vecs = stages * 64;
-    const uint64_t waves = (nvec + sc_vecs - 1) / sc_vecs;
-    g.grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min((waves + kWaves - 1) / kWaves, cap)));
-    g.lds_bytes = sizeof(uint4) * kWaves * lds_stages * 64;
-  } else if (impl == VerifyImpl::Stride) {
+  // epilogue 256K times per GiB; the caps below let each workgroup stream
+  // tens of KiB per epilogue (kernel_bench A/B).
+  const uint64_t cap = max_grid ? max_grid
+                                : static_cast<uint64_t>(cu_count()) *
+                                      (impl == VerifyImpl::Stride ? kVerifyStridePerCu : kVerifyLdsPerCu);
+  if (impl == VerifyImpl::Stride) {
     const uint64_t tiles = (nvec + kBlock * kStrideUnroll - 1) / (kBlock * kStrideUnroll);
     g.grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min(tiles, cap)));
   } else {
-    g.grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min((nvec + kBlockVecs - 1) / kBlockVecs, cap)));
+    // Waves of 8 KiB chunks, and the 8 KiB of LDS each wave owns.
+    const uint64_t sc_vecs = static_cast<uint64_t>(kLdsStages) * 64;
+    const uint64_t waves = (nvec + sc_vecs - 1) / sc_vecs;
+    g.grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min((waves + kWaves - 1) / kWaves, cap)));
+    g.lds_bytes = sizeof(uint4) * kWaves * kLdsStages * 64;
   }
   return g;
 }
 
-void launch_fill(void* p, size_t bytes, uint64_t seed, hipStream_t stream, FillImpl impl) {
+void launch_fill(void* p, size_t bytes, uint64_t seed, hipStream_t stream, FillImpl) {
   if (!bytes) return;
   P2P_CHECK(reinterpret_cast<uintptr_t>(p) % 16 == 0, "fill: buffer must be 16-byte aligned");
-  if (impl == FillImpl::Auto) impl = kDefaultFill;
   const uint64_t nvec = bytes / 16;
   const uint32_t tail = static_cast<uint32_t>(bytes - nvec * 16);
   auto* vp = reinterpret_cast<uint4*>(p);
   auto* tp = static_cast<uint8_t*>(p) + nvec * 16;
-  if (impl == FillImpl::Stride) {
-    LaunchGeom g = fill_geometry(bytes, impl);
-    fill_stride_kernel<<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16);
-    HIP_OK(hipGetLastError());
-    return;
-  }
   // Full grids: one launch per 4 GiB chunk (a capped grid striding over a
   // larger buffer streams 16% slower: 5.9 vs 7.0 TB/s at 16 GiB).
   const uint64_t chunk = kMaxGrid * kBlockVecs;
@@ -593,19 +421,7 @@ void launch_fill(void* p, size_t bytes, uint64_t seed, hipStream_t stream, FillI
     const uint64_t end = std::min(nvec, begin + chunk);
     const bool last = end == nvec;
     const unsigned grid = grid_for((end - begin + kBlockVecs - 1) / kBlockVecs);
-    const uint32_t tb = last ? tail : 0;
-    if (impl == FillImpl::Grid2)
-      fill_multi_kernel<2><<<grid_for((end - begin + 2 * kBlockVecs - 1) / (2 * kBlockVecs)), kBlock, 0, stream>>>(
-          vp, begin, end, seed, tp, tb, nvec * 16);
-    else if (impl == FillImpl::Grid4)
-      fill_multi_kernel<4><<<grid_for((end - begin + 4 * kBlockVecs - 1) / (4 * kBlockVecs)), kBlock, 0, stream>>>(
-          vp, begin, end, seed, tp, tb, nvec * 16);
-    else if (impl == FillImpl::Nontemporal)
-      fill_grid_kernel<true><<<grid, kBlock, 0, stream>>>(vp, begin, end, seed, tp, tb, nvec * 16);
-    else if (impl == FillImpl::Xcd && grid % kXcds == 0)
-      fill_grid_kernel<false, true><<<grid, kBlock, 0, stream>>>(vp, begin, end, seed, tp, tb, nvec * 16);
-    else
-      fill_grid_kernel<false><<<grid, kBlock, 0, stream>>>(vp, begin, end, seed, tp, tb, nvec * 16);
+    fill_grid_kernel<<<grid, kBlock, 0, stream>>>(vp, begin, end, seed, tp, last ? tail : 0, nvec * 16);
     HIP_OK(hipGetLastError());
     if (last) break;
   }
@@ -620,30 +436,10 @@ namespace {
 template <bool CHECK>
 void launch_verify_t(const uint4* vp, uint64_t nvec, uint64_t seed, const uint8_t* tp, uint32_t tail, VerifyAccum* acc,
                      VerifyImpl impl, const LaunchGeom& g, hipStream_t stream) {
-  switch (impl) {
-    case VerifyImpl::Lds:
-      // aux = 2: non-temporal LDS-DMA (MI355X_MICROARCH.md ldsdma-fill row: 6.4 TB/s default
-      // policy vs 6.5-6.8 nt); measured here 6.3 / 6.6 TB/s nt vs 5.7 / 5.9 default policy.
-      verify_lds_kernel<CHECK, kLdsStages, 2><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
-      break;
-    case VerifyImpl::Lds8:
-      verify_lds_kernel<CHECK, 8, 2><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
-      break;
-    case VerifyImpl::Lds8Span:
-      verify_lds_kernel<CHECK, 8, 2, true><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
-      break;
-    case VerifyImpl::LdsCached:
-      verify_lds_kernel<CHECK, kLdsStages, 0><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
-      break;
-    case VerifyImpl::LdsPipe:
-      verify_lds_pipe_kernel<CHECK, 4, 2><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
-      break;
-    case VerifyImpl::Stride:
-      verify_stride_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
-      break;
-    default:
-      verify_grid_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
-  }
+  if (impl == VerifyImpl::Stride)
+    verify_stride_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
+  else
+    verify_lds_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
 }
 }  // namespace
 
@@ -672,7 +468,7 @@ void launch_multi_verify(const VerifyJob* jobs, int njobs, VerifyAccum* scratch,
   // Workgroups: the LDS8 verify's cap (16 per CU) shared by the jobs of a
   // batch in proportion to their size, at least one each.
   const uint64_t cap = static_cast<uint64_t>(cu_count()) * kVerifyLdsPerCu;
-  constexpr uint64_t kChunkVecs = 8 * 64 * kWaves;  // 32 KiB per workgroup pass
+  constexpr uint64_t kChunkVecs = kLdsStages * 64 * kWaves;  // 32 KiB per workgroup pass
   for (int first = 0; first < njobs; first += kMaxVerifyJobs) {
     const int cnt = std::min(kMaxVerifyJobs, njobs - first);
     MultiVerifyArgs a{};
@@ -697,7 +493,7 @@ void launch_multi_verify(const VerifyJob* jobs, int njobs, VerifyAccum* scratch,
     a.block_begin[cnt] = acc;
     multi_verify_reset_kernel<<<cnt, 64, 0, stream>>>(scratch);
     HIP_OK(hipGetLastError());
-    multi_verify_lds_kernel<8><<<acc, kBlock, 0, stream>>>(a, scratch);
+    multi_verify_lds_kernel<<<acc, kBlock, 0, stream>>>(a, scratch);
     HIP_OK(hipGetLastError());
     multi_verify_finalize_kernel<<<cnt, 64, 0, stream>>>(scratch, out + first);
     HIP_OK(hipGetLastError());
@@ -710,18 +506,22 @@ BatchVerifier::~BatchVerifier() {
   if (host_) (void)hipHostFree(host_);
 }
 
+void BatchVerifier::reserve(int njobs, const std::function<void()>& drain) {
+  if (!scratch_) HIP_OK(hipMalloc(&scratch_, multi_verify_scratch_bytes()));
+  if (njobs <= cap_) return;
+  // The stream may still read the old arrays: the caller drains it first.
+  if (out_ || host_) drain();
+  if (out_) HIP_OK(hipFree(out_));
+  if (host_) HIP_OK(hipHostFree(host_));
+  out_ = host_ = nullptr;
+  cap_ = std::max(njobs, 2 * cap_);
+  HIP_OK(hipMalloc(&out_, sizeof(VerifyAccum) * static_cast<size_t>(cap_)));
+  HIP_OK(hipHostMalloc(&host_, sizeof(VerifyAccum) * static_cast<size_t>(cap_), hipHostMallocDefault));
+}
+
 void BatchVerifier::enqueue(const VerifyJob* jobs, int njobs, hipStream_t stream) {
   if (njobs <= 0) return;
-  if (!scratch_) HIP_OK(hipMalloc(&scratch_, multi_verify_scratch_bytes()));
-  if (njobs > cap_) {
-    // The stream may still read the old arrays: drain it before freeing.
-    HIP_OK(hipStreamSynchronize(stream));
-    if (out_) HIP_OK(hipFree(out_));
-    if (host_) HIP_OK(hipHostFree(host_));
-    cap_ = std::max(njobs, 2 * cap_);
-    HIP_OK(hipMalloc(&out_, sizeof(VerifyAccum) * static_cast<size_t>(cap_)));
-    HIP_OK(hipHostMalloc(&host_, sizeof(VerifyAccum) * static_cast<size_t>(cap_), hipHostMallocDefault));
-  }
+  P2P_CHECK(scratch_ && njobs <= cap_, "BatchVerifier::enqueue: reserve(njobs) first");
   launch_multi_verify(jobs, njobs, scratch_, out_, stream);
   HIP_OK(hipMemcpyAsync(host_, out_, sizeof(VerifyAccum) * static_cast<size_t>(njobs), hipMemcpyDeviceToHost, stream));
 }

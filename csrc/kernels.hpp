@@ -4,21 +4,19 @@
 // cudaMemset (p2p_matrix.cc:129-130) and never read back.
 // These kernels replace that with verifiable random payloads:
 //   fill    — counter-based PRNG, one 16-byte global_store_dwordx4 per lane
-//   verify  — regenerates the stream and compares; staging variants:
-//               * LDS (default Lds8): non-temporal global_load_lds_dwordx4
+//   verify  — regenerates the stream and compares; two stagings, the A/B
+//             SURVEY.md §7.5 item 6 asks for:
+//               * LDS (Lds8, the default): non-temporal global_load_lds_dwordx4
 //                           (LDS-DMA, 1 KiB per wave instruction) into a
-//                           per-wave LDS slot of 8 KiB (Lds: 4 KiB), then
-//                           ds_read_b128 — the LDS-staged form the north star
-//                           asks for; 6.44 / 6.64 TB/s at 1 / 4 GiB, within
-//                           1-2% of register staging (SURVEY.md §7.5 item 6
-//                           A/B).  LdsCached keeps the default cache policy
-//                           (5.7-5.9 TB/s, the A/B that chose nt)
+//                           per-wave LDS slot of 8 KiB, then ds_read_b128 —
+//                           the LDS-staged form the north star asks for;
+//                           6.44 / 6.64 TB/s at 1 / 4 GiB, within 1-2% of
+//                           register staging
 //               * stride:   register staging, 4 x global_load_dwordx4 in flight
 //                           per lane, grid capped at 16 workgroups per CU so the
 //                           reduction epilogue is amortised over 64 KiB+
-//               * register: one global_load_dwordx4 per lane per iteration
-//                           (the full-grid shape of fill/copy, capped at
-//                           256 workgroups per CU)
+//             (round 5 removed the variants that lost: profiles/r1_tuned/,
+//             r4_verify_span/)
 //   reduce  — fused epilogue of verify: wave64 __shfl_xor tree -> LDS across
 //             the 4 waves -> one atomic per block into one of kVerifyShards
 //             64-byte counters (no single hot address), then a one-wave
@@ -36,6 +34,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 
 #include "prng.hpp"
 
@@ -53,11 +52,10 @@ struct alignas(64) VerifyAccum {
 constexpr int kVerifyShards = 64;
 constexpr size_t verify_accum_bytes() { return sizeof(VerifyAccum) * kVerifyShards; }
 
-// Lds8Span: Lds8 with each workgroup on a contiguous span instead of a grid-stride walk (A/B).
-enum class VerifyImpl : int { Auto = 0, Register = 1, Lds = 2, Stride = 3, Lds8 = 4, LdsCached = 5, LdsPipe = 6,
-                              Lds8Span = 7 };
-// Grid2 / Grid4: full grid with 2 / 4 vectors per lane (8 / 16 KiB per workgroup).
-enum class FillImpl : int { Auto = 0, Grid = 1, Nontemporal = 2, Stride = 3, Xcd = 4, Grid2 = 5, Grid4 = 6 };
+// Verify staging (app.hpp parse_verify_impl maps the CLI / Python names).
+enum class VerifyImpl : int { Auto = 0, Lds8 = 1, Stride = 2 };
+// One fill kernel, the full grid; the enum stays so callers name it.
+enum class FillImpl : int { Auto = 0, Grid = 1 };
 
 // Geometry chosen for a launch (exposed for tests / profiling scripts).
 struct LaunchGeom {
@@ -94,15 +92,20 @@ void launch_multi_verify(const VerifyJob* jobs, int njobs, VerifyAccum* scratch,
 
 // The device scratch, device results and pinned host results of
 // launch_multi_verify for one stream's user (a transport), grown on demand.
-// enqueue() puts the batched verify and ONE readback of every job's totals on
-// `stream`; results() is valid once the caller has synchronised the stream.
+// reserve() makes room for njobs results: should the arrays grow, it calls
+// `drain` first -- the stream may still read the old ones -- which is the
+// caller's own wait for its stream (the transports' is bounded and
+// abort-aware).  enqueue() then puts the batched verify and ONE
+// readback of every job's totals on `stream`; results() is valid once the
+// caller has synchronised the stream.
 class BatchVerifier {
  public:
   BatchVerifier() = default;
   BatchVerifier(const BatchVerifier&) = delete;
   BatchVerifier& operator=(const BatchVerifier&) = delete;
   ~BatchVerifier();
-  void enqueue(const VerifyJob* jobs, int njobs, hipStream_t stream);
+  void reserve(int njobs, const std::function<void()>& drain);
+  void enqueue(const VerifyJob* jobs, int njobs, hipStream_t stream);  // after reserve(njobs)
   const VerifyAccum* results() const { return host_; }
 
  private:

@@ -224,13 +224,21 @@ KernelScratch& scratch() {
   return s;
 }
 
+dev::VerifyImpl verify_impl_arg(int impl) {
+  if (impl < 0 || impl > static_cast<int>(dev::VerifyImpl::Stride))
+    throw py::value_error(strfmt("verify: impl %d is not 0 (auto), 1 (lds8) or 2 (stride); round 5 removed the "
+                                 "other variants (parse_verify_impl names them)", impl));
+  return static_cast<dev::VerifyImpl>(impl);
+}
+
 py::tuple device_verify(uintptr_t ptr, size_t bytes, uint64_t seed, int impl, bool check, uintptr_t stream) {
+  const dev::VerifyImpl vi = verify_impl_arg(impl);
   KernelScratch& ks = scratch();
   hipStream_t st = as_stream(stream);
   {
     py::gil_scoped_release nogil;
     dev::launch_verify_reset(ks.d, st);
-    dev::launch_verify(reinterpret_cast<const void*>(ptr), bytes, seed, ks.d, static_cast<dev::VerifyImpl>(impl), check, st);
+    dev::launch_verify(reinterpret_cast<const void*>(ptr), bytes, seed, ks.d, vi, check, st);
     if (hipMemcpyAsync(ks.h, ks.d, sizeof(dev::VerifyAccum), hipMemcpyDeviceToHost, st) != hipSuccess)
       P2P_FATAL("hipMemcpyAsync failed");
     if (hipStreamSynchronize(st) != hipSuccess) P2P_FATAL("hipStreamSynchronize failed");
@@ -240,18 +248,23 @@ py::tuple device_verify(uintptr_t ptr, size_t bytes, uint64_t seed, int impl, bo
 
 // The batched verify on raw pointers: [(mismatches, checksum, first_bad)]
 // per (ptr, bytes, seed) job, one readback (dev::BatchVerifier, per device).
+// The verifiers are never destroyed (like KernelScratch): a static
+// destructor would free device memory after the HIP runtime shut down.
 py::list device_verify_many(const std::vector<std::tuple<uintptr_t, size_t, uint64_t>>& jobs, uintptr_t stream) {
-  static std::vector<std::unique_ptr<dev::BatchVerifier>> per_device;
+  static auto* per_device = new std::vector<dev::BatchVerifier*>();
   int dv = 0;
   if (hipGetDevice(&dv) != hipSuccess) P2P_FATAL("no HIP device");
-  if (static_cast<int>(per_device.size()) <= dv) per_device.resize(static_cast<size_t>(dv) + 1);
-  auto& bv = per_device[static_cast<size_t>(dv)];
-  if (!bv) bv = std::make_unique<dev::BatchVerifier>();
+  if (static_cast<int>(per_device->size()) <= dv) per_device->resize(static_cast<size_t>(dv) + 1, nullptr);
+  dev::BatchVerifier*& bv = (*per_device)[static_cast<size_t>(dv)];
+  if (!bv) bv = new dev::BatchVerifier();
   std::vector<dev::VerifyJob> dj;
   for (const auto& j : jobs) dj.push_back({reinterpret_cast<const void*>(std::get<0>(j)), std::get<1>(j), std::get<2>(j)});
   hipStream_t st = as_stream(stream);
   {
     py::gil_scoped_release nogil;
+    bv->reserve(static_cast<int>(dj.size()), [st] {
+      if (hipStreamSynchronize(st) != hipSuccess) P2P_FATAL("hipStreamSynchronize failed");
+    });
     bv->enqueue(dj.data(), static_cast<int>(dj.size()), st);
     if (hipStreamSynchronize(st) != hipSuccess) P2P_FATAL("hipStreamSynchronize failed");
   }
@@ -321,30 +334,30 @@ PYBIND11_MODULE(_p2pcore, m) {
       .def(py::init<int, int, const std::string&, int, int, const std::string&, double, TcpListener*>(), py::arg("rank"),
            py::arg("world"), py::arg("host") = "127.0.0.1", py::arg("port") = 0, py::arg("device") = 0,
            py::arg("transport") = "rccl", py::arg("timeout_s") = 300.0, py::arg("listener") = nullptr,
-           py::call_guard<py::gil_scoped_release>())
+           py::call_guard<NativeCall, py::gil_scoped_release>())
       .def_property_readonly("rank", &Session::rank)
       .def_property_readonly("world", &Session::world)
       .def_property_readonly("transport", &Session::transport)
       .def_property_readonly("device_desc", &Session::device_desc)
-      .def("barrier", &Session::barrier, py::call_guard<py::gil_scoped_release>())
-      .def("allreduce_max", &Session::allreduce_max, py::call_guard<py::gil_scoped_release>())
-      .def("allreduce_sum", &Session::allreduce_sum, py::call_guard<py::gil_scoped_release>())
+      .def("barrier", &Session::barrier, py::call_guard<NativeCall, py::gil_scoped_release>())
+      .def("allreduce_max", &Session::allreduce_max, py::call_guard<NativeCall, py::gil_scoped_release>())
+      .def("allreduce_sum", &Session::allreduce_sum, py::call_guard<NativeCall, py::gil_scoped_release>())
       .def("run", &Session::run, py::arg("mode") = "pair", py::arg("dir") = "uni", py::arg("bytes") = 32u << 20,
            py::arg("iters") = 128, py::arg("warmup") = 8, py::arg("timing") = "events", py::arg("verify") = false,
-           py::arg("warm") = true, py::arg("cells") = std::vector<std::pair<int, int>>{}, py::call_guard<py::gil_scoped_release>())
+           py::arg("warm") = true, py::arg("cells") = std::vector<std::pair<int, int>>{}, py::call_guard<NativeCall, py::gil_scoped_release>())
       .def("gate_probe", &Session::gate_probe, py::arg("timeout_s") = 0.2, py::arg("release") = true,
-           py::call_guard<py::gil_scoped_release>())
+           py::call_guard<NativeCall, py::gil_scoped_release>())
       .def("device_latency", &Session::device_latency, py::arg("bytes") = 8, py::arg("iters") = 1000,
-           py::arg("warmup") = 100, py::call_guard<py::gil_scoped_release>())
+           py::arg("warmup") = 100, py::call_guard<NativeCall, py::gil_scoped_release>())
       .def("latency", &Session::latency, py::arg("bytes") = 8, py::arg("iters") = 1000, py::arg("warmup") = 100,
-           py::arg("preposted") = 0, py::call_guard<py::gil_scoped_release>(),
+           py::arg("preposted") = 0, py::call_guard<NativeCall, py::gil_scoped_release>(),
            "Ping-pong matrix (collective).  preposted=B: exchanges posted B at a time behind a stream gate and "
            "released together (GPU-timeline latency; host-posted where the transport has no gate).")
       .def("fuzz", &Session::fuzz, py::arg("rounds") = 20, py::arg("seed") = 1, py::arg("max_bytes") = size_t{4} << 20,
-           py::call_guard<py::gil_scoped_release>(),
+           py::call_guard<NativeCall, py::gil_scoped_release>(),
            "Random groups of verified messages through the transport (collective); returns mismatching words.")
       .def("ring_latency", &Session::ring_latency, py::arg("bytes") = 8, py::arg("laps") = 200, py::arg("warmup") = 20,
-           py::arg("device") = false, py::call_guard<py::gil_scoped_release>(),
+           py::arg("device") = false, py::call_guard<NativeCall, py::gil_scoped_release>(),
            "Dependent ring token chain 0 -> 1 -> ... -> 0 (collective); JSON with per-hop and per-lap times.")
       .def("set_timeout", &Session::set_timeout, py::arg("seconds"),
            "Bounds every later wait of the session (transport sync / rendezvous, bootstrap receives).")
@@ -352,15 +365,15 @@ PYBIND11_MODULE(_p2pcore, m) {
            "Caps the ops messages to every peer are posted as at `bytes` (0: lifts the cap, back to the limits the "
            "transport derived per peer); False where nothing is split. Call it on every rank with the same value.")
       .def("max_chunk", &Session::max_chunk, py::arg("peer"), "Largest op a message to `peer` is posted as (0: unsplit).")
-      .def("refine_op_limits", &Session::refine_op_limits, py::call_guard<py::gil_scoped_release>(),
+      .def("refine_op_limits", &Session::refine_op_limits, py::call_guard<NativeCall, py::gil_scoped_release>(),
            "Collective: op limits from the connections made so far (RCCL: its connection lines).")
-      .def("link_reports", &Session::link_reports, py::call_guard<py::gil_scoped_release>(),
+      .def("link_reports", &Session::link_reports, py::call_guard<NativeCall, py::gil_scoped_release>(),
            "Collective: what the data plane set up towards each peer, per rank (RCCL: p2p channels from its INFO log, "
            "each peer's transport, the op limit in use); JSON list.")
-      .def("provenance", &Session::provenance, py::arg("device") = -1, py::call_guard<py::gil_scoped_release>(),
+      .def("provenance", &Session::provenance, py::arg("device") = -1, py::call_guard<NativeCall, py::gil_scoped_release>(),
            "Collective: runtime, RCCL library, knobs, every rank's GPU and the links between them (JSON).")
       .def("_unmatched_recv", &Session::unmatched_recv, py::arg("bytes") = size_t{1} << 20,
-           py::call_guard<py::gil_scoped_release>(), "Test hook: a receive no send matches; returns the watchdog's error.");
+           py::call_guard<NativeCall, py::gil_scoped_release>(), "Test hook: a receive no send matches; returns the watchdog's error.");
 
   py::class_<PyStepDriver>(m, "StepDriver")
       .def(py::init<std::shared_ptr<Session>, const std::string&, const std::string&, size_t, int, bool, bool, bool, int,
@@ -368,12 +381,12 @@ PYBIND11_MODULE(_p2pcore, m) {
            py::arg("session"), py::arg("mode") = "tournament", py::arg("dir") = "bi", py::arg("bytes") = 32u << 20,
            py::arg("msgs") = 8, py::arg("verify") = false, py::arg("batch") = false, py::arg("graph") = false,
            py::arg("depth") = 1, py::arg("recv_budget") = size_t{0}, py::arg("salt") = uint64_t{0},
-           py::call_guard<py::gil_scoped_release>())
-      .def("poison", [](PyStepDriver& s) { s.d().poison(); }, py::call_guard<py::gil_scoped_release>(),
+           py::call_guard<NativeCall, py::gil_scoped_release>())
+      .def("poison", [](PyStepDriver& s) { s.d().poison(); }, py::call_guard<NativeCall, py::gil_scoped_release>(),
            "Collective: zero every receive slot (after the warmup, before the timed steps) and arm the skip faults.")
-      .def("clear", [](PyStepDriver& s) { s.d().clear(); }, py::call_guard<py::gil_scoped_release>(),
+      .def("clear", [](PyStepDriver& s) { s.d().clear(); }, py::call_guard<NativeCall, py::gil_scoped_release>(),
            "Collective: zero every receive slot once every rank has drained (no fault armed).")
-      .def("recapture", [](PyStepDriver& s) { s.d().recapture(); }, py::call_guard<py::gil_scoped_release>(),
+      .def("recapture", [](PyStepDriver& s) { s.d().recapture(); }, py::call_guard<NativeCall, py::gil_scoped_release>(),
            "Collective: record the step graphs again after the op sizes changed (no-op without graphs).")
       .def_property_readonly("recaptures", [](PyStepDriver& s) { return s.d().recaptures(); })
       .def_property_readonly("limit_changes", [](PyStepDriver& s) { return s.d().limit_changes(); })
@@ -381,6 +394,7 @@ PYBIND11_MODULE(_p2pcore, m) {
       .def("verify_steps", [](PyStepDriver& s, long first, long count) {
             StepVerifyReport r;
             {
+              NativeCall in_engine;
               py::gil_scoped_release nogil;
               r = s.d().verify_steps(first, count);
             }
@@ -396,17 +410,17 @@ PYBIND11_MODULE(_p2pcore, m) {
       .def_property_readonly("depth", [](PyStepDriver& s) { return s.d().depth(); })
       .def_property_readonly("msgs", [](PyStepDriver& s) { return s.d().msgs(); })
       .def_property_readonly("recv_bytes", [](PyStepDriver& s) { return s.d().recv_bytes(); })
-      .def("connect", [](PyStepDriver& s) { s.d().connect(); }, py::call_guard<py::gil_scoped_release>())
-      .def("step", [](PyStepDriver& s, long k) { s.d().step(k); }, py::call_guard<py::gil_scoped_release>())
+      .def("connect", [](PyStepDriver& s) { s.d().connect(); }, py::call_guard<NativeCall, py::gil_scoped_release>())
+      .def("step", [](PyStepDriver& s, long k) { s.d().step(k); }, py::call_guard<NativeCall, py::gil_scoped_release>())
       .def("run_steps", [](PyStepDriver& s, long first, long count) { s.d().run_steps(first, count); },
-           py::call_guard<py::gil_scoped_release>(),
+           py::call_guard<NativeCall, py::gil_scoped_release>(),
            "Enqueue steps [first, first+count); consecutive steps share their boundary timestamp.")
-      .def("sync", [](PyStepDriver& s) { s.d().sync(); }, py::call_guard<py::gil_scoped_release>())
+      .def("sync", [](PyStepDriver& s) { s.d().sync(); }, py::call_guard<NativeCall, py::gil_scoped_release>())
       .def("step_ms", [](PyStepDriver& s) { return s.d().step_ms(); })
       .def("post_ms", [](PyStepDriver& s) { return s.d().post_ms(); },
            "Host time each recorded step took to post (ms).")
       .def("reset", [](PyStepDriver& s) { s.d().reset(); })
-      .def("verify_last", [](PyStepDriver& s) { return s.d().verify_last(); }, py::call_guard<py::gil_scoped_release>())
+      .def("verify_last", [](PyStepDriver& s) { return s.d().verify_last(); }, py::call_guard<NativeCall, py::gil_scoped_release>())
       .def("bytes_sent_per_step", [](PyStepDriver& s, long k) { return s.d().bytes_sent_per_step(k); })
       .def("job_bytes_per_step", [](PyStepDriver& s, long k) { return s.d().job_bytes_per_step(k); })
       .def_property_readonly("phases", [](PyStepDriver& s) { return s.d().phases(); })
@@ -419,14 +433,18 @@ PYBIND11_MODULE(_p2pcore, m) {
 
   // ---- kernels on raw pointers ----
   m.def("fill", [](uintptr_t ptr, size_t bytes, uint64_t seed, uintptr_t stream, int impl) {
-        if (impl < 0 || impl > static_cast<int>(dev::FillImpl::Grid4)) throw py::value_error("fill: unknown impl");
+        if (impl >= 2 && impl <= 6)
+          throw py::value_error(strfmt("fill: impl %d (non-temporal / grid-stride / XCD-ordered / 2 or 4 stores per "
+                                       "lane) was removed in round 5: it lost its A/B against the full grid "
+                                       "(profiles/r3b_nt_ab/, r4_gpu_tier/); use 0 or 1", impl));
+        if (impl < 0 || impl > static_cast<int>(dev::FillImpl::Grid)) throw py::value_error("fill: unknown impl");
         dev::launch_fill(reinterpret_cast<void*>(ptr), bytes, seed, as_stream(stream), static_cast<dev::FillImpl>(impl));
       }, py::arg("ptr"), py::arg("bytes"), py::arg("seed"), py::arg("stream") = 0, py::arg("impl") = 0,
-      "impl: 0 auto, 1 full grid (one 16 B store per lane), 2 non-temporal stores, 3 grid-stride, "
-      "4 XCD-ordered grid, 5 / 6 full grid with 2 / 4 stores per lane");
+      "impl: 0 auto = 1 full grid (one 16 B store per lane, one 4 KiB block per workgroup)");
   m.def("verify", &device_verify, py::arg("ptr"), py::arg("bytes"), py::arg("seed"), py::arg("impl") = 0,
         py::arg("check") = true, py::arg("stream") = 0,
-        "Returns (mismatching words, checksum, first bad byte offset or 2**64-1).");
+        "impl: 0 auto (= 1), 1 LDS-DMA staged (lds8), 2 register staged (stride).  Returns (mismatching words, "
+        "checksum, first bad byte offset or 2**64-1).");
   m.def("verify_many", &device_verify_many, py::arg("jobs"), py::arg("stream") = 0,
         "Batched verify of [(ptr, bytes, seed)]: one (mismatches, checksum, first_bad) per job, one readback.");
   m.def("verify_many_launch", &device_verify_many_launch, py::arg("jobs"), py::arg("stream") = 0,
@@ -435,10 +453,10 @@ PYBIND11_MODULE(_p2pcore, m) {
                             unsigned max_grid) {
         // Stream-ordered launch only (reset + verify + finalize), no readback:
         // for timing the kernel with events.
+        const dev::VerifyImpl vi = verify_impl_arg(impl);
         KernelScratch& ks = scratch();
         dev::launch_verify_reset(ks.d, as_stream(stream));
-        dev::launch_verify(reinterpret_cast<const void*>(ptr), bytes, seed, ks.d, static_cast<dev::VerifyImpl>(impl),
-                           check, as_stream(stream), max_grid);
+        dev::launch_verify(reinterpret_cast<const void*>(ptr), bytes, seed, ks.d, vi, check, as_stream(stream), max_grid);
       }, py::arg("ptr"), py::arg("bytes"), py::arg("seed"), py::arg("impl") = 0, py::arg("check") = true,
       py::arg("stream") = 0, py::arg("max_grid") = 0);
   m.def("copy", [](uintptr_t dst, uintptr_t src, size_t bytes, uintptr_t stream, int max_blocks, bool coherent) {
@@ -462,7 +480,7 @@ PYBIND11_MODULE(_p2pcore, m) {
     return py::make_tuple(g.grid, g.block, g.lds_bytes);
   });
   m.def("verify_geometry", [](size_t bytes, int impl) {
-    auto g = dev::verify_geometry(bytes, static_cast<dev::VerifyImpl>(impl));
+    auto g = dev::verify_geometry(bytes, verify_impl_arg(impl));
     return py::make_tuple(g.grid, g.block, g.lds_bytes);
   });
   m.def("rccl_available", &rccl_transport_available);
@@ -473,6 +491,9 @@ PYBIND11_MODULE(_p2pcore, m) {
   m.def("abort_requested", []() { return abort_requested(); });
   m.def("abort_done", []() { return abort_done(); },
         "True once a transport wait has aborted its communicators after request_abort().");
+  m.def("abort_if_idle", &abort_if_idle,
+        "Watchdog: when no thread is inside the engine, abort every communicator from this thread, take no more "
+        "engine calls and note the abort done; False (nothing done) while a call is in flight.  Holds the GIL.");
   m.def("run_abort_hooks", []() { run_abort_hooks(1); }, py::call_guard<py::gil_scoped_release>(),
         "Aborts every live RCCL communicator / bootstrap (their kernels exit); for a watchdog about to end the "
         "process.");
@@ -528,6 +549,12 @@ PYBIND11_MODULE(_p2pcore, m) {
     return d;
   });
   m.def("usage", &usage_text);
+  m.def("parse_verify_impl", [](const std::string& name) {
+        std::string note;
+        const int v = parse_verify_impl(name, &note);
+        if (v < 0) throw py::value_error("verify impl '" + name + "': " + note);
+        return v;
+      }, py::arg("name"), "Verify kernel name -> impl number (auto 0, lds8 1, stride 2), as p2p_matrix --verify-impl.");
   // The full p2p_matrix application in-process (TCP/env or local bootstrap),
   // e.g. `torchrun --nproc-per-node 8 -m test_nccl_p2p_amd --mode all`.
   m.def("run_cli", [](std::vector<std::string> args) {

@@ -1,13 +1,162 @@
 #include "rccl_log.hpp"
 
+#include <strings.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <cctype>
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <fstream>
 #include <map>
 #include <set>
 #include <sstream>
 
+#include "common.hpp"
+
 namespace p2p {
+namespace {
+
+// RCCL's INFO log, which this process reads to learn the p2p channels and
+// transports RCCL set up (rccl_log.hpp).  Unless the user asked for RCCL's
+// log themselves (NCCL_DEBUG / NCCL_DEBUG_FILE) or P2P_RCCL_LOG=0, the
+// first transport of the process points it at a private file before RCCL's
+// first initialisation reads the variables; the file is removed at exit
+// (P2P_RCCL_LOG=keep keeps it).  Empty path: no log to read.
+//
+// What this process sets in its environment for RCCL (the private log's
+// NCCL_DEBUG* below and RCCL_UNROLL_FACTOR) is inherited by every child it
+// starts: bench.py's comparison children, a test's p2p_matrix.  Each setting
+// is made by set_owned(), which records the value it replaced
+// (P2P_RCCL_PREV_<name>: "=<value>", or "" for unset) and this pid
+// (P2P_RCCL_ENV_OWNER).  A process that finds another pid's settings puts the
+// replaced values back before it decides anything, so a child never writes
+// RCCL's log into its parent's file or mistakes the parent's unroll for the
+// user's (profiles/r4_session: p2p_matrix --reference under pytest ran at the
+// parent's unroll 4).
+constexpr const char* kOwnedVars[] = {"NCCL_DEBUG", "NCCL_DEBUG_SUBSYS", "NCCL_DEBUG_FILE", "RCCL_UNROLL_FACTOR"};
+
+void undo_inherited_rccl_env() {
+  static const bool done = [] {
+    const char* owner = std::getenv("P2P_RCCL_ENV_OWNER");
+    if (!owner || std::atoi(owner) == static_cast<int>(getpid())) return true;
+    for (const char* k : kOwnedVars) {
+      const std::string saved = strfmt("P2P_RCCL_PREV_%s", k);
+      const char* v = std::getenv(saved.c_str());
+      if (!v) continue;
+      if (*v == '=')
+        setenv(k, v + 1, 1);
+      else
+        unsetenv(k);
+      unsetenv(saved.c_str());
+    }
+    unsetenv("P2P_RCCL_ENV_OWNER");
+    return true;
+  }();
+  (void)done;
+}
+
+void set_owned(const char* name, const char* value) {
+  const std::string saved = strfmt("P2P_RCCL_PREV_%s", name);
+  if (!std::getenv(saved.c_str())) {
+    const char* prev = std::getenv(name);
+    setenv(saved.c_str(), prev ? (std::string("=") + prev).c_str() : "", 1);
+  }
+  setenv(name, value, 1);
+  setenv("P2P_RCCL_ENV_OWNER", std::to_string(static_cast<int>(getpid())).c_str(), 1);
+}
+
+}  // namespace
+
+const RcclLogFile& rccl_log_file() {
+  static RcclLogFile log = [] {
+    undo_inherited_rccl_env();
+    RcclLogFile l;
+    const char* mode = std::getenv("P2P_RCCL_LOG");
+    if (mode && std::strcmp(mode, "0") == 0) return l;
+    if (const char* f = std::getenv("NCCL_DEBUG_FILE")) {
+      // The user's file: readable only if it names no per-process pattern.
+      if (!std::strchr(f, '%')) l.path = f;
+      return l;
+    }
+    // NCCL_DEBUG=VERSION (set in the image's environment) asks only for the
+    // version banner; any other level is the user asking for RCCL's log on
+    // stderr, which is then left alone.
+    if (const char* lvl = std::getenv("NCCL_DEBUG"); lvl && *lvl && strcasecmp(lvl, "VERSION") != 0) return l;
+    const char* tmp = std::getenv("TMPDIR");
+    l.path = strfmt("%s/p2p_rccl_info_%d.log", tmp && *tmp ? tmp : "/tmp", static_cast<int>(getpid()));
+    l.ours = true;
+    set_owned("NCCL_DEBUG", "INFO");
+    if (!std::getenv("NCCL_DEBUG_SUBSYS")) set_owned("NCCL_DEBUG_SUBSYS", "INIT,ENV,P2P,NET,SHM");
+    set_owned("NCCL_DEBUG_FILE", l.path.c_str());
+    if (!(mode && std::strcmp(mode, "keep") == 0))
+      std::atexit([] { std::remove(rccl_log_file().path.c_str()); });
+    return l;
+  }();
+  return log;
+}
+
+// RCCL's copy-loop unroll factor for the kernels of every communicator of
+// this process.  RCCL's kernel table holds unroll 1, 2 and 4 and picks 1 on
+// MI355X; with 4, a single communicator's self send/recv step runs in 0.92 ms
+// instead of 1.13 ms and the 4-communicator bench gains 7% (2428 vs 2272 GB/s
+// over 4 interleaved runs, profiles/r3_unroll/), small-message latency
+// unchanged.  Set before RCCL's first init (it reads the variable once), never
+// over the user's own RCCL_UNROLL_FACTOR; P2P_RCCL_UNROLL=<n> picks another,
+// 0 leaves RCCL's choice.  The value is in every provenance record (env) and
+// RCCL's log confirms it per communicator (link_report comms[].unroll).
+void rccl_unroll_setup() {
+  static const bool done = [] {
+    undo_inherited_rccl_env();
+    if (std::getenv("RCCL_UNROLL_FACTOR")) return true;
+    const char* want = std::getenv("P2P_RCCL_UNROLL");
+    const std::string v = want ? want : "4";
+    if (v != "0" && !v.empty()) set_owned("RCCL_UNROLL_FACTOR", v.c_str());
+    return true;
+  }();
+  (void)done;
+}
+
+size_t rccl_log_size() {
+  const std::string& p = rccl_log_file().path;
+  if (p.empty()) return 0;
+  std::ifstream in(p, std::ios::binary | std::ios::ate);
+  return in ? static_cast<size_t>(in.tellg()) : 0;
+}
+
+std::string rccl_log_since(size_t offset) {
+  const std::string& p = rccl_log_file().path;
+  if (p.empty()) return "";
+  std::ifstream in(p, std::ios::binary);
+  if (!in) return "";
+  in.seekg(static_cast<std::streamoff>(offset));
+  std::stringstream ss;
+  ss << in.rdbuf();
+  return ss.str();
+}
+
+// The last few WARN lines of the log since `offset` (RCCL's own account of an
+// error, which the private log would otherwise hide).
+std::string rccl_log_warnings(size_t offset) {
+  std::istringstream in(rccl_log_since(offset));
+  std::vector<std::string> warn;
+  for (std::string line; std::getline(in, line);)
+    if (line.find("NCCL WARN") != std::string::npos) warn.push_back(line);
+  std::string out;
+  for (size_t i = warn.size() > 4 ? warn.size() - 4 : 0; i < warn.size(); ++i) out += "\n  rccl: " + warn[i];
+  return out;
+}
+
+// The host RCCL places a rank on: NCCL_HOSTID when set, else the hostname.
+std::string rccl_host_id() {
+  if (const char* h = std::getenv("NCCL_HOSTID")) return h;
+  char name[256] = {0};
+  if (gethostname(name, sizeof(name) - 1) != 0) return "?";
+  return name;
+}
+
+
 namespace {
 
 // Integer right after `key` (spaces skipped) in `line`; -1 if absent.
@@ -186,6 +335,64 @@ std::vector<int> agree_op_channels(const std::vector<int>& all, int n, int me, c
     if (a <= 0 && b <= 0) continue;
     out[static_cast<size_t>(p)] = a > 0 && b > 0 ? std::min(a, b) : std::max(a, b);
     if (sources && static_cast<size_t>(p) < sources->size()) (*sources)[static_cast<size_t>(p)] = "connection lines";
+  }
+  return out;
+}
+
+namespace {
+// Does `line` name rank `r` as a connection endpoint or a peer?
+bool names_rank(const std::string& line, int r) {
+  const std::string d = std::to_string(r);
+  for (size_t at = line.find(d); at != std::string::npos; at = line.find(d, at + 1)) {
+    const bool digit_before = at > 0 && std::isdigit(static_cast<unsigned char>(line[at - 1]));
+    const size_t end = at + d.size();
+    const bool digit_after = end < line.size() && std::isdigit(static_cast<unsigned char>(line[end]));
+    if (digit_before || digit_after) continue;
+    size_t b = at;
+    while (b > 0 && line[b - 1] == ' ') --b;
+    size_t e = end;
+    while (e < line.size() && line[e] == ' ') ++e;
+    const std::string before = line.substr(b >= 5 ? b - 5 : 0, b >= 5 ? 5 : b);
+    if ((end < line.size() && line[end] == '[') || line.compare(e, 2, "->") == 0 ||
+        (b >= 2 && line.compare(b - 2, 2, "->") == 0) || (b >= 2 && line.compare(b - 2, 2, "=>") == 0) ||
+        line.compare(e, 2, "=>") == 0 || before == " rank" || before == "rank" || before == " peer" ||
+        before == "peer")
+      return true;
+  }
+  return false;
+}
+
+bool connection_like(const std::string& line) {
+  for (const char* k : {"Channel", "channel", " via ", "P2P", "Connect", "connect"})
+    if (line.find(k) != std::string::npos) return true;
+  return false;
+}
+}  // namespace
+
+std::vector<RcclUnparsedPeer> rccl_unparsed_peers(const std::string& text, const std::vector<RcclPeerLink>& links,
+                                                  const std::vector<char>& net_peer, const std::vector<char>& touched,
+                                                  int me, size_t max_lines) {
+  std::vector<RcclUnparsedPeer> out;
+  for (size_t p = 0; p < links.size(); ++p) {
+    const int peer = static_cast<int>(p);
+    if (peer == me || links[p].channels_connected > 0) continue;
+    if (p < net_peer.size() && net_peer[p]) continue;
+    if (p >= touched.size() || !touched[p]) continue;
+    RcclUnparsedPeer u;
+    u.peer = peer;
+    std::vector<std::string> other;
+    std::istringstream in(text);
+    for (std::string line; std::getline(in, line);) {
+      if (!names_rank(line, peer)) continue;
+      if (!line.empty() && line.back() == '\r') line.pop_back();
+      if (connection_like(line)) {
+        if (u.lines.size() < max_lines) u.lines.push_back(line);
+      } else if (other.size() < max_lines) {
+        other.push_back(line);
+      }
+    }
+    for (size_t i = 0; i < other.size() && u.lines.size() < max_lines; ++i) u.lines.push_back(other[i]);
+    out.push_back(std::move(u));
   }
   return out;
 }

@@ -93,6 +93,45 @@ std::vector<int> agree_op_channels(const std::vector<int>& all, int n, int me, c
 // fallback that would read as a slow link.
 bool link_transport_mismatch(const std::string& link, const std::string& transport);
 
+// Peers whose connections the parser did not see: a
+// remote peer on this host (not `me`, net_peer[p] == 0) that this rank has
+// exchanged messages with (touched[p] != 0) but for which rccl_peer_links
+// found no channel -- RCCL connected it, so a line in a layout
+// parse_rccl_connections does not know was missed, and the peer's op limit
+// stayed at the unconnected default.  For each, up to `max_lines` lines of
+// `text` that name the peer's rank as an endpoint ("<p>[", "-> <p>",
+// "<p> ->", "rank <p>", "peer <p>"), preferring connection-like lines, so the
+// record shows the format that was missed.
+struct RcclUnparsedPeer {
+  int peer = -1;
+  std::vector<std::string> lines;
+};
+std::vector<RcclUnparsedPeer> rccl_unparsed_peers(const std::string& text, const std::vector<RcclPeerLink>& links,
+                                                  const std::vector<char>& net_peer, const std::vector<char>& touched,
+                                                  int me, size_t max_lines = 20);
+
+// ---- this process's RCCL environment and INFO log file -----------------
+// RCCL's INFO log, which this process reads to learn the p2p channels and
+// transports RCCL set up.  Unless the user asked for RCCL's log themselves
+// (NCCL_DEBUG / NCCL_DEBUG_FILE) or P2P_RCCL_LOG=0, the first call points it
+// at a private file before RCCL's first initialisation reads the variables;
+// the file is removed at exit (P2P_RCCL_LOG=keep keeps it).  Empty path: no
+// log to read.  What this sets in the environment (NCCL_DEBUG*,
+// RCCL_UNROLL_FACTOR) is recorded with the values it replaced, so a child
+// process puts them back before deciding anything (rccl_log.cpp set_owned).
+struct RcclLogFile {
+  std::string path;
+  bool ours = false;
+};
+const RcclLogFile& rccl_log_file();
+// RCCL's copy-loop unroll factor for this process (4 unless the user set
+// RCCL_UNROLL_FACTOR; P2P_RCCL_UNROLL=<n>, 0 = RCCL's choice).
+void rccl_unroll_setup();
+size_t rccl_log_size();                            // bytes in the log so far
+std::string rccl_log_since(size_t offset);         // the log from `offset` on
+std::string rccl_log_warnings(size_t offset);      // its last 4 WARN lines, one "\n  rccl: " each
+std::string rccl_host_id();                        // NCCL_HOSTID, else the hostname
+
 // RCCL's half-delivery threshold: bytes of one op per p2p channel.
 constexpr size_t kRcclBytesPerChannel = size_t{16} << 20;
 

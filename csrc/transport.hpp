@@ -244,7 +244,7 @@ struct TransportOptions {
   int device = -1;                 // -1: local rank from placement
   double timeout_s = 300.0;        // watchdog for init / sync
   bool nonblocking_init = true;    // RCCL: ncclCommInitRankConfig(blocking=0) + polling
-  int verify_impl = 0;             // 0 = auto, 1 = register-staged, 2 = LDS-staged (global_load_lds)
+  int verify_impl = 0;             // dev::VerifyImpl: 0 auto (= 1), 1 LDS-DMA staged (lds8), 2 register staged (stride)
   // IPC transport: kernel (gfx950 pull kernel) | sdma | push (rendezvous +
   // remote writes) | relay (push over the direct link plus two-hop relays
   // through the other GPUs, routing.hpp)

@@ -260,6 +260,7 @@ class HostTransport final : public Transport {
       P2P_CHECK(rc >= 0, "poll failed");
       if (rc == 0) {
         if (now_seconds() > deadline) P2P_FATAL("host transport: group timed out (peer hung or dead)");
+        if (abort_requested()) abort_wait("host transport");
         continue;
       }
       for (auto& pf : pfds) {

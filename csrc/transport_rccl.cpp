@@ -75,146 +75,6 @@
 namespace p2p {
 namespace {
 
-// RCCL's INFO log, which this process reads to learn the p2p channels and
-// transports RCCL set up (rccl_log.hpp).  Unless the user asked for RCCL's
-// log themselves (NCCL_DEBUG / NCCL_DEBUG_FILE) or P2P_RCCL_LOG=0, the
-// first transport of the process points it at a private file before RCCL's
-// first initialisation reads the variables; the file is removed at exit
-// (P2P_RCCL_LOG=keep keeps it).  Empty path: no log to read.
-//
-// What this process sets in its environment for RCCL (the private log's
-// NCCL_DEBUG* below and RCCL_UNROLL_FACTOR) is inherited by every child it
-// starts: bench.py's comparison children, a test's p2p_matrix.  Each setting
-// is made by set_owned(), which records the value it replaced
-// (P2P_RCCL_PREV_<name>: "=<value>", or "" for unset) and this pid
-// (P2P_RCCL_ENV_OWNER).  A process that finds another pid's settings puts the
-// replaced values back before it decides anything, so a child never writes
-// RCCL's log into its parent's file or mistakes the parent's unroll for the
-// user's (profiles/r4_session: p2p_matrix --reference under pytest ran at the
-// parent's unroll 4).
-constexpr const char* kOwnedVars[] = {"NCCL_DEBUG", "NCCL_DEBUG_SUBSYS", "NCCL_DEBUG_FILE", "RCCL_UNROLL_FACTOR"};
-
-void undo_inherited_rccl_env() {
-  static const bool done = [] {
-    const char* owner = std::getenv("P2P_RCCL_ENV_OWNER");
-    if (!owner || std::atoi(owner) == static_cast<int>(getpid())) return true;
-    for (const char* k : kOwnedVars) {
-      const std::string saved = strfmt("P2P_RCCL_PREV_%s", k);
-      const char* v = std::getenv(saved.c_str());
-      if (!v) continue;
-      if (*v == '=')
-        setenv(k, v + 1, 1);
-      else
-        unsetenv(k);
-      unsetenv(saved.c_str());
-    }
-    unsetenv("P2P_RCCL_ENV_OWNER");
-    return true;
-  }();
-  (void)done;
-}
-
-void set_owned(const char* name, const char* value) {
-  const std::string saved = strfmt("P2P_RCCL_PREV_%s", name);
-  if (!std::getenv(saved.c_str())) {
-    const char* prev = std::getenv(name);
-    setenv(saved.c_str(), prev ? (std::string("=") + prev).c_str() : "", 1);
-  }
-  setenv(name, value, 1);
-  setenv("P2P_RCCL_ENV_OWNER", std::to_string(static_cast<int>(getpid())).c_str(), 1);
-}
-
-struct RcclLog {
-  std::string path;
-  bool ours = false;
-};
-RcclLog& rccl_log() {
-  static RcclLog log = [] {
-    undo_inherited_rccl_env();
-    RcclLog l;
-    const char* mode = std::getenv("P2P_RCCL_LOG");
-    if (mode && std::strcmp(mode, "0") == 0) return l;
-    if (const char* f = std::getenv("NCCL_DEBUG_FILE")) {
-      // The user's file: readable only if it names no per-process pattern.
-      if (!std::strchr(f, '%')) l.path = f;
-      return l;
-    }
-    // NCCL_DEBUG=VERSION (set in the image's environment) asks only for the
-    // version banner; any other level is the user asking for RCCL's log on
-    // stderr, which is then left alone.
-    if (const char* lvl = std::getenv("NCCL_DEBUG"); lvl && *lvl && strcasecmp(lvl, "VERSION") != 0) return l;
-    const char* tmp = std::getenv("TMPDIR");
-    l.path = strfmt("%s/p2p_rccl_info_%d.log", tmp && *tmp ? tmp : "/tmp", static_cast<int>(getpid()));
-    l.ours = true;
-    set_owned("NCCL_DEBUG", "INFO");
-    if (!std::getenv("NCCL_DEBUG_SUBSYS")) set_owned("NCCL_DEBUG_SUBSYS", "INIT,ENV,P2P,NET,SHM");
-    set_owned("NCCL_DEBUG_FILE", l.path.c_str());
-    if (!(mode && std::strcmp(mode, "keep") == 0))
-      std::atexit([] { std::remove(rccl_log().path.c_str()); });
-    return l;
-  }();
-  return log;
-}
-
-// RCCL's copy-loop unroll factor for the kernels of every communicator of
-// this process.  RCCL's kernel table holds unroll 1, 2 and 4 and picks 1 on
-// MI355X; with 4, a single communicator's self send/recv step runs in 0.92 ms
-// instead of 1.13 ms and the 4-communicator bench gains 7% (2428 vs 2272 GB/s
-// over 4 interleaved runs, profiles/r3_unroll/), small-message latency
-// unchanged.  Set before RCCL's first init (it reads the variable once), never
-// over the user's own RCCL_UNROLL_FACTOR; P2P_RCCL_UNROLL=<n> picks another,
-// 0 leaves RCCL's choice.  The value is in every provenance record (env) and
-// RCCL's log confirms it per communicator (link_report comms[].unroll).
-void rccl_unroll_setup() {
-  static const bool done = [] {
-    undo_inherited_rccl_env();
-    if (std::getenv("RCCL_UNROLL_FACTOR")) return true;
-    const char* want = std::getenv("P2P_RCCL_UNROLL");
-    const std::string v = want ? want : "4";
-    if (v != "0" && !v.empty()) set_owned("RCCL_UNROLL_FACTOR", v.c_str());
-    return true;
-  }();
-  (void)done;
-}
-
-size_t log_size() {
-  const std::string& p = rccl_log().path;
-  if (p.empty()) return 0;
-  std::ifstream in(p, std::ios::binary | std::ios::ate);
-  return in ? static_cast<size_t>(in.tellg()) : 0;
-}
-
-std::string log_since(size_t offset) {
-  const std::string& p = rccl_log().path;
-  if (p.empty()) return "";
-  std::ifstream in(p, std::ios::binary);
-  if (!in) return "";
-  in.seekg(static_cast<std::streamoff>(offset));
-  std::stringstream ss;
-  ss << in.rdbuf();
-  return ss.str();
-}
-
-// The last few WARN lines of the log since `offset` (RCCL's own account of an
-// error, which the private log would otherwise hide).
-std::string log_warnings(size_t offset) {
-  std::istringstream in(log_since(offset));
-  std::vector<std::string> warn;
-  for (std::string line; std::getline(in, line);)
-    if (line.find("NCCL WARN") != std::string::npos) warn.push_back(line);
-  std::string out;
-  for (size_t i = warn.size() > 4 ? warn.size() - 4 : 0; i < warn.size(); ++i) out += "\n  rccl: " + warn[i];
-  return out;
-}
-
-// The host RCCL places a rank on: NCCL_HOSTID when set, else the hostname.
-std::string rccl_host_id() {
-  if (const char* h = std::getenv("NCCL_HOSTID")) return h;
-  char name[256] = {0};
-  if (gethostname(name, sizeof(name) - 1) != 0) return "?";
-  return name;
-}
-
 class RcclTransport final : public Transport {
  public:
   RcclTransport(Bootstrap& boot, const TransportOptions& opt)
@@ -233,16 +93,17 @@ class RcclTransport final : public Transport {
     P2P_CHECK(ncomms >= 1 && ncomms <= kMaxComms, strfmt("rccl communicators per rank: 1..%d", kMaxComms));
     P2P_CHECK(ncomms == 1 || !opt.two_streams, "--two-streams (the reference layout) uses one communicator");
     HIPCHECK(hipSetDevice(device_));
-    const int cu_mask_mode = open_streams(opt, ncomms);
+    open_streams(opt, ncomms);
     stale_.assign(static_cast<size_t>(ncomms), true);
     pending_.assign(static_cast<size_t>(ncomms), false);
     unjoined_.assign(static_cast<size_t>(ncomms), false);
     send_seq_.assign(static_cast<size_t>(n_), 0);
     recv_seq_.assign(static_cast<size_t>(n_), 0);
+    touched_.assign(static_cast<size_t>(n_), 0);
     HIPCHECK(hipMalloc(&acc_, dev::verify_accum_bytes()));
     HIPCHECK(hipHostMalloc(&acc_host_, sizeof(dev::VerifyAccum), hipHostMallocDefault));
     open_communicators(boot, opt, ncomms);
-    describe(ncomms, cu_mask_mode);
+    describe(ncomms);
   }
 
   ~RcclTransport() override {
@@ -394,6 +255,7 @@ class RcclTransport final : public Transport {
   // (derive_op_limits).
   void send(const void* p, size_t bytes, int peer) override {
     const int j = pick(&send_seq_, peer, bytes);
+    touched_[static_cast<size_t>(peer)] = 1;
     const char* c = static_cast<const char*>(p);
     do {
       size_t n = chunk_of(bytes, peer);
@@ -404,6 +266,7 @@ class RcclTransport final : public Transport {
   }
   void recv(void* p, size_t bytes, int peer) override {
     const int j = pick(&recv_seq_, peer, bytes);
+    touched_[static_cast<size_t>(peer)] = 1;
     hipStream_t s = j == 0 && recv_stream_ ? recv_stream_ : cstreams_[static_cast<size_t>(j)];
     // Injected skip fault: the receive completes into a private sink.
     char* c = static_cast<char*>(discarding() ? discard_sink(bytes) : p);
@@ -418,24 +281,10 @@ class RcclTransport final : public Transport {
   void group_end() override {
     in_group_ = false;
     std::stable_sort(deferred_.begin(), deferred_.end(), [](const Op& a, const Op& b) { return a.comm < b.comm; });
-    if (group_per_comm_ && !deferred_.empty() && deferred_.front().comm != deferred_.back().comm) {
-      // One RCCL group per communicator, in communicator order: the first
-      // communicator's kernel starts once its own ops are posted instead of
-      // after every communicator's (RCCL prepares all of a group's work before
-      // it launches any of it).  The caller's group holds no ops.
-      wait_ready(ncclGroupEnd(), "ncclGroupEnd");
-      for (size_t i = 0; i < deferred_.size();) {
-        const int c = deferred_[i].comm;
-        nccl_ok(ncclGroupStart(), "ncclGroupStart");
-        for (; i < deferred_.size() && deferred_[i].comm == c; ++i) post(deferred_[i]);
-        wait_ready(ncclGroupEnd(), "ncclGroupEnd");
-      }
-    } else {
-      for (const Op& o : deferred_) post(o);
-      // Non-blocking comm: the ops are only enqueued once the comm leaves
-      // ncclInProgress, so wait before any event is recorded behind them.
-      wait_ready(ncclGroupEnd(), "ncclGroupEnd");
-    }
+    for (const Op& o : deferred_) post(o);
+    // Non-blocking comm: the ops are only enqueued once the comm leaves
+    // ncclInProgress, so wait before any event is recorded behind them.
+    wait_ready(ncclGroupEnd(), "ncclGroupEnd");
     deferred_.clear();
     if (recv_on_side_) {
       // Reference two-stream layout (sends on s_0, receives on s_1,
@@ -598,7 +447,6 @@ class RcclTransport final : public Transport {
   size_t max_chunk(int peer) const override { return chunk_for(peer); }
 
   bool gate_arm(double timeout_s) override {
-    if (main_idle_) return false;
     gate_.arm(stream_, timeout_s);
     return true;
   }
@@ -618,56 +466,26 @@ class RcclTransport final : public Transport {
   }
 
  private:
-  // Main stream (fill / verify), the optional reference receive stream, and
-  // one stream + join event per communicator.  Returns the CU-mask mode
-  // (0 off, 1 contig, 2 stride, 3 full).
-  int open_streams(const TransportOptions& opt, int ncomms) {
+  // Main stream (fill / verify; communicator 0's too), the optional
+  // reference receive stream, and one stream + join event per further
+  // communicator.  (Round 5 removed the experiments that gave communicator 0
+  // a stream of its own or each communicator a CU mask, P2P_RCCL_MAIN_IDLE /
+  // P2P_RCCL_CU_MASK: neutral or slower, profiles/r2_cu_mask/.)
+  void open_streams(const TransportOptions& opt, int ncomms) {
     HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     if (opt.two_streams) {
       HIPCHECK(hipStreamCreateWithFlags(&recv_stream_, hipStreamNonBlocking));
       HIPCHECK(hipEventCreateWithFlags(&join_, hipEventDisableTiming));
     }
-    if (const char* mi = std::getenv("P2P_RCCL_MAIN_IDLE")) main_idle_ = ncomms > 1 && std::atoi(mi) != 0;
-    // P2P_RCCL_CU_MASK=contig|stride (experiment): every communicator's
-    // stream gets its own 1/K of the CUs (contiguous mask bits, or every K-th
-    // bit), so the K concurrent send/recv kernels do not compete for CUs; the
-    // main stream (fill / verify) stays unmasked, so communicator 0 moves to
-    // a stream of its own as with P2P_RCCL_MAIN_IDLE.
-    // P2P_RCCL_CU_MASK=full: every CU in every communicator's mask.  HIP
-    // gives a stream with a CU mask a hardware queue of its own instead of
-    // sharing one of its GPU_MAX_HW_QUEUES, so no communicator's stream
-    // shares an in-order queue with another's or with RCCL's internal
-    // streams (whose event waits would then hold it up).
-    int cu_mask_mode = 0;
-    if (const char* cm = std::getenv("P2P_RCCL_CU_MASK"))
-      cu_mask_mode = std::strcmp(cm, "contig") == 0 ? 1
-                     : std::strcmp(cm, "stride") == 0 ? 2
-                     : std::strcmp(cm, "full") == 0   ? 3
-                                                      : 0;
-    if (ncomms == 1) cu_mask_mode = 0;
-    if (cu_mask_mode) main_idle_ = true;
-    int ncus = 0;
-    HIPCHECK(hipDeviceGetAttribute(&ncus, hipDeviceAttributeMultiprocessorCount, device_));
     for (int j = 0; j < ncomms; ++j) {
       hipStream_t s = stream_;
-      if (cu_mask_mode) {
-        std::vector<uint32_t> mask(static_cast<size_t>((ncus + 31) / 32), 0u);
-        for (int c = 0; c < ncus; ++c) {
-          const int owner = cu_mask_mode == 1 ? c * ncomms / ncus : cu_mask_mode == 2 ? c % ncomms : j;
-          if (owner == j) mask[static_cast<size_t>(c / 32)] |= 1u << (c % 32);
-        }
-        HIPCHECK(hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(mask.size()), mask.data()));
-        cu_masked_ = true;
-      } else if (j > 0 || main_idle_) {
-        HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-      }
+      if (j > 0) HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
       cstreams_.push_back(s);
       hipEvent_t ev = nullptr;
       if (ncomms > 1) HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
       cjoin_.push_back(ev);
     }
     if (ncomms > 1) HIPCHECK(hipEventCreateWithFlags(&fork_, hipEventDisableTiming));
-    return cu_mask_mode;
   }
 
   // ncclUniqueIds from rank 0 through the bootstrap, then the communicators.
@@ -675,7 +493,7 @@ class RcclTransport final : public Transport {
     // Before anything of RCCL's runs in this process (ncclGetUniqueId
     // initialises its logging too): point its INFO log at our file, and pick
     // the kernels' unroll factor.
-    rccl_log();
+    rccl_log_file();
     if (!opt.rccl_stock) rccl_unroll_setup();
     // P2P_RCCL_DISTINCT_HOSTS=1 (tests on one GPU): every rank tells RCCL it
     // is on a host of its own (NCCL_HOSTID, read when RCCL first hashes the
@@ -697,16 +515,15 @@ class RcclTransport final : public Transport {
     boot.bcast(ids.data(), sizeof(ncclUniqueId) * ids.size(), 0);
 
     if (const char* sm = std::getenv("P2P_RCCL_SPLIT_MIN")) split_min_ = parse_size(sm);
-    if (const char* gp = std::getenv("P2P_RCCL_GROUP_PER_COMM")) group_per_comm_ = std::atoi(gp) != 0;
     if (const char* rg = std::getenv("P2P_RCCL_REGISTER")) register_ = std::atoi(rg);
     const char* blk = std::getenv("P2P_RCCL_BLOCKING");
     nonblocking_ = opt.nonblocking_init && !(blk && std::atoi(blk));
     comms_.assign(static_cast<size_t>(ncomms), nullptr);
     hook_ = push_abort_hook([this](int) { abort_all(); });
-    log_start_ = log_size();
+    log_start_ = rccl_log_size();
     // One communicator after the other, in the same order on every rank.
     for (int j = 0; j < ncomms; ++j) {
-      const size_t before = log_size();
+      const size_t before = rccl_log_size();
       if (nonblocking_) {
         ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
         cfg.blocking = 0;
@@ -715,7 +532,7 @@ class RcclTransport final : public Transport {
       } else {
         nccl_ok(ncclCommInitRank(&comms_[static_cast<size_t>(j)], n_, ids[static_cast<size_t>(j)], rank_), "ncclCommInitRank");
       }
-      comm_info_.push_back(parse_rccl_init(log_since(before)));
+      comm_info_.push_back(parse_rccl_init(rccl_log_since(before)));
     }
     derive_op_limits(boot);
   }
@@ -813,7 +630,7 @@ class RcclTransport final : public Transport {
   std::vector<RcclPeerLink> our_links() const {
     std::vector<std::string> ours;
     for (auto c : comms_) ours.push_back(strfmt("%p", static_cast<void*>(c)));
-    return rccl_peer_links(connections_of(parse_rccl_connections(log_since(log_start_)), ours), rank_, n_);
+    return rccl_peer_links(connections_of(parse_rccl_connections(rccl_log_since(log_start_)), ours), rank_, n_);
   }
 
  public:
@@ -836,8 +653,30 @@ class RcclTransport final : public Transport {
       peer_limit_[i] = kRcclBytesPerChannel * static_cast<size_t>(std::max(agreed[i], 1));
     }
     ++refinements_;
+    find_unparsed_peers(forced);
     return boot.allreduce_max(changed ? 1.0 : 0.0) > 0.0;
   }
+
+ private:
+  // A same-host peer this rank has exchanged messages with but whose
+  // connection lines the parser found none of: RCCL's format changed under
+  // us, and that peer's ops stay at the 2-channel default (VERDICT r4 item
+  // 5).  Recorded with its raw lines in link_report (unparsed_peers) and
+  // named once on stderr.
+  void find_unparsed_peers(bool forced) {
+    if (forced || rccl_log_file().path.empty() || init_channels_.empty()) return;
+    unparsed_ = rccl_unparsed_peers(rccl_log_since(log_start_), our_links(), net_peer_, touched_, rank_);
+    if (unparsed_.empty() || warned_unparsed_) return;
+    warned_unparsed_ = true;
+    std::string peers;
+    for (const auto& u : unparsed_) peers += strfmt("%s%d", peers.empty() ? "" : ",", u.peer);
+    std::fprintf(stderr,
+                 "p2p WARN rank %d: RCCL connected peer(s) %s but none of its connection lines parsed; their ops "
+                 "stay at the unconnected 2-channel limit (raw lines: link_report unparsed_peers)\n",
+                 rank_, peers.c_str());
+  }
+
+ public:
 
  private:
   // link_report(): the communicators' channel counts, and per peer the
@@ -846,12 +685,19 @@ class RcclTransport final : public Transport {
   std::string peers_json() const {
     const auto links = our_links();
     std::string o = strfmt("{\"rank\":%d,\"log\":%s,\"op_limit_source\":\"%s\",\"refinements\":%d,\"comms\":[",
-                           rank_, rccl_log().path.empty() ? "null" : "true", json_escape(limit_source_).c_str(),
+                           rank_, rccl_log_file().path.empty() ? "null" : "true", json_escape(limit_source_).c_str(),
                            refinements_);
     for (size_t j = 0; j < comm_info_.size(); ++j)
       o += strfmt("%s{\"p2p_channels\":%d,\"p2p_channels_per_peer\":%d,\"nnodes\":%d,\"from_rank\":%d,\"unroll\":%d}",
                   j ? "," : "", comm_info_[j].p2p_channels, comm_info_[j].p2p_per_peer, comm_info_[j].nnodes,
                   comm_info_[j].from_rank < 0 ? rank_ : comm_info_[j].from_rank, comm_info_[j].unroll);
+    o += "],\"unparsed_peers\":[";
+    for (size_t i = 0; i < unparsed_.size(); ++i) {
+      o += strfmt("%s{\"peer\":%d,\"lines\":[", i ? "," : "", unparsed_[i].peer);
+      for (size_t k = 0; k < unparsed_[i].lines.size(); ++k)
+        o += strfmt("%s\"%s\"", k ? "," : "", json_escape(unparsed_[i].lines[k]).c_str());
+      o += "]}";
+    }
     o += "],\"peers\":[";
     for (int p = 0; p < n_; ++p) {
       const auto& l = links[static_cast<size_t>(p)];
@@ -865,7 +711,7 @@ class RcclTransport final : public Transport {
     return o + "]}";
   }
 
-  void describe(int ncomms, int cu_mask_mode) {
+  void describe(int ncomms) {
     hipDeviceProp_t prop;
     HIPCHECK(hipGetDeviceProperties(&prop, device_));
     char pci[64] = {0};
@@ -875,7 +721,6 @@ class RcclTransport final : public Transport {
     desc_ = strfmt("hip:%d %s (%s, %d CUs, %.0f GiB, pci %s) rccl %d", device_, prop.name, prop.gcnArchName,
                    prop.multiProcessorCount, static_cast<double>(prop.totalGlobalMem) / (1ull << 30), pci, ver);
     if (ncomms > 1) desc_ += strfmt(" x%d comms", ncomms);
-    if (cu_masked_) desc_ += cu_mask_mode == 1 ? " cu-mask:contig" : cu_mask_mode == 2 ? " cu-mask:stride" : " cu-mask:full";
   }
 
   static constexpr int kMaxComms = 16;
@@ -973,7 +818,7 @@ class RcclTransport final : public Transport {
     }
     ncclComm_t c = comms_.empty() ? nullptr : comms_[0];
     std::string msg = strfmt("rank %d: %s failed: %s (%s)", rank_, what, ncclGetErrorString(r), c ? ncclGetLastError(c) : "") +
-                      log_warnings(log_start_);
+                      rccl_log_warnings(log_start_);
     abort_all();  // a communicator that returned an error is not used again
     P2P_FATAL(msg);
   }
@@ -1009,7 +854,7 @@ class RcclTransport final : public Transport {
     }
     if (r != ncclSuccess) {
       abort_all();
-      P2P_FATAL(strfmt("rank %d: %s failed: %s", rank_, what, ncclGetErrorString(r)) + log_warnings(log_start_));
+      P2P_FATAL(strfmt("rank %d: %s failed: %s", rank_, what, ncclGetErrorString(r)) + rccl_log_warnings(log_start_));
     }
   }
 
@@ -1052,10 +897,8 @@ class RcclTransport final : public Transport {
     return (c && bytes > c) ? c : bytes;
   }
   std::vector<ncclComm_t> comms_;      // comms_[0] on stream_
-  std::vector<hipStream_t> cstreams_;  // stream of each communicator (cstreams_[0] == stream_ unless main_idle_)
+  std::vector<hipStream_t> cstreams_;  // stream of each communicator (cstreams_[0] == stream_)
   std::vector<hipEvent_t> cjoin_;      // per communicator with a side stream: joins it into stream_
-  bool main_idle_ = false;             // P2P_RCCL_MAIN_IDLE=1: communicator 0 on a side stream too
-  bool cu_masked_ = false;             // P2P_RCCL_CU_MASK: communicator streams own disjoint CU sets
   hipEvent_t fork_ = nullptr;          // recorded on stream_ when a stale side stream is first used
   bool forked_ = false;                // fork_ covers the main stream's latest buffer work
   std::vector<bool> stale_;            // side stream j has not waited for the latest buffer work
@@ -1063,8 +906,10 @@ class RcclTransport final : public Transport {
   std::vector<bool> used_;             // side communicators used by the open group
   bool in_group_ = false;              // between group_begin and group_end
   std::vector<Op> deferred_;           // the open group's ops (several communicators)
-  bool group_per_comm_ = false;        // P2P_RCCL_GROUP_PER_COMM=1: one RCCL group per communicator at group_end
   std::vector<unsigned long long> send_seq_, recv_seq_;  // messages posted to / from each peer
+  std::vector<char> touched_;                            // per peer: any message posted to / from it
+  std::vector<RcclUnparsedPeer> unparsed_;               // find_unparsed_peers
+  bool warned_unparsed_ = false;
   struct RegSet {
     void* send = nullptr;
     std::vector<std::pair<ncclComm_t, void*>> handles;

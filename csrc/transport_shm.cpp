@@ -237,6 +237,7 @@ class ShmTransport final : public Transport {
           const double now = now_seconds();
           if (deadline == 0) deadline = now + timeout_;
           if (now > deadline) P2P_FATAL("shm transport: message timed out (peer hung or dead)");
+          if (abort_requested()) abort_wait("shm transport");
           std::this_thread::yield();
         } else {
           cpu_relax();
@@ -290,6 +291,7 @@ class ShmTransport final : public Transport {
       const double now = now_seconds();
       if (deadline == 0) deadline = now + timeout_;
       if (now > deadline) P2P_FATAL("shm transport: group timed out (peer hung or dead)");
+      if (abort_requested()) abort_wait("shm transport");
       std::this_thread::yield();
     }
     ops_.clear();

@@ -48,7 +48,7 @@ def main():
         del d
         lat = json.loads(s.latency(8, 300, 30))["pairs"][0]["one_way_us"]["p50"]
         rows.append({"comms": k, "graph": a.graph, "gbs": round(best, 1), "host_post_us_per_step": round(post, 1),
-                     "lat8_p50_us": round(lat, 2), "main_idle": os.environ.get("P2P_RCCL_MAIN_IDLE", "0"),
+                     "lat8_p50_us": round(lat, 2),
                      "gpu_us_per_step": round(size * a.msgs / best / 1e3, 1),
                      "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default")})
         print(json.dumps(rows[-1]), flush=True)

@@ -53,12 +53,9 @@ def main():
         buf = torch.empty(sz, dtype=torch.uint8, device="cuda")
         ptr = buf.data_ptr()
         t_fill = timed(lambda: nat.fill(ptr, sz, 7, stream, 1), a.reps)
-        t_fill_nt = timed(lambda: nat.fill(ptr, sz, 7, stream, 2), a.reps)
-        t_fill_stride = timed(lambda: nat.fill(ptr, sz, 7, stream, 3), a.reps)
-        t_fill_xcd = timed(lambda: nat.fill(ptr, sz, 7, stream, 4), a.reps)
         res = {}
-        for name, impl, check in [("verify_reg", 1, True), ("verify_stride", 3, True), ("verify_lds", 2, True), ("verify_lds8", 4, True), ("verify_ldspipe", 6, True), ("verify_lds8span", 7, True),
-                                  ("checksum_reg", 1, False), ("checksum_lds", 2, False)]:
+        for name, impl, check in [("verify_lds8", 1, True), ("verify_stride", 2, True),
+                                  ("checksum_lds8", 1, False), ("checksum_stride", 2, False)]:
             # Kernel time only: reset + verify + finalize launches, no readback.
             t = timed(lambda: nat.verify_launch(ptr, sz, 7, impl, check, stream), a.reps)
             res[name] = t
@@ -74,8 +71,7 @@ def main():
             res["verify_multi32m"] = timed(lambda: nat.verify_many_launch(jobs, stream), a.reps)
             assert all(m == 0 for m, _, _ in nat.verify_many(jobs, stream))
             nat.fill(ptr, sz, 7, stream)
-        row = {"bytes": sz, "fill_tbs": sz / t_fill / 1e12, "fill_nt_tbs": sz / t_fill_nt / 1e12,
-               "fill_stride_tbs": sz / t_fill_stride / 1e12, "fill_xcd_tbs": sz / t_fill_xcd / 1e12}
+        row = {"bytes": sz, "fill_tbs": sz / t_fill / 1e12}
         # Roofs measured the same way: torch zero_() (write-only) and copy_()
         # (read + write, counted once like ours), and our IPC copy kernel.
         dst = torch.empty_like(buf)
@@ -96,16 +92,15 @@ def main():
         for k, t in res.items():
             row[k + "_tbs"] = sz / t / 1e12
         row["fill_geom"] = nat.fill_geometry(sz)
-        row["verify_reg_geom"] = nat.verify_geometry(sz, 1)
-        row["verify_lds_geom"] = nat.verify_geometry(sz, 2)
+        row["verify_lds8_geom"] = nat.verify_geometry(sz, 1)
+        row["verify_stride_geom"] = nat.verify_geometry(sz, 2)
         rows.append(row)
-        print("%6s  fill %.2f (nt %.2f, stride %.2f, xcd %.2f)  verify grid %.2f / stride %.2f / lds %.2f / lds8 %.2f / lds-pipe %.2f  checksum reg %.2f / lds %.2f TB/s"
+        print("%6s  fill %.2f  verify lds8 %.2f / stride %.2f  checksum lds8 %.2f / stride %.2f TB/s"
               "  (HBM measured roof %.2f)"
-              % (nat.format_size(sz), row["fill_tbs"], row["fill_nt_tbs"], row["fill_stride_tbs"], row["fill_xcd_tbs"], row["verify_reg_tbs"], row["verify_stride_tbs"],
-                 row["verify_lds_tbs"], row["verify_lds8_tbs"], row["verify_ldspipe_tbs"], row["checksum_reg_tbs"], row["checksum_lds_tbs"], HBM_MEASURED_TBS), flush=True)
+              % (nat.format_size(sz), row["fill_tbs"], row["verify_lds8_tbs"], row["verify_stride_tbs"],
+                 row["checksum_lds8_tbs"], row["checksum_stride_tbs"], HBM_MEASURED_TBS), flush=True)
         print("        roofs: torch zero_ %.2f  torch copy_ %.2f  ours copy %.2f TB/s (copy counts bytes once)"
               % (row["torch_zero_tbs"], row["torch_copy_tbs"], row["copy_kernel_tbs"]), flush=True)
-        print("        lds8 contiguous spans per workgroup: %.2f TB/s" % row["verify_lds8span_tbs"], flush=True)
         if "verify_multi32m_tbs" in row:
             print("        batched verify, 32 MiB slots: %.2f TB/s" % row["verify_multi32m_tbs"], flush=True)
         del buf

@@ -254,6 +254,7 @@ class Reporter:
 
 
 ABORT_GRACE_S = 3.0
+ABORT_LINGER_S = 1.0
 
 
 def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> threading.Event:
@@ -264,9 +265,12 @@ def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> thread
     The abort is requested, not performed, here: the main thread may be inside
     RCCL, and aborting a communicator from this thread meanwhile crashed it
     (SIGSEGV on 3 of 8 ranks, profiles/r4_rehearsal/).  Every bounded wait of
-    the transports polls the request and aborts on its own thread; after up to
-    ABORT_GRACE_S the process ends either way (process exit tears the GPU
-    queues down)."""
+    the transports polls the request and aborts on its own thread; should the
+    main thread be outside the engine (no native call open: a gloo barrier, a
+    torch sync), the watchdog aborts the communicators itself
+    (nat.abort_if_idle).  After up to ABORT_GRACE_S the process ends either
+    way (process exit tears the GPU queues down); the line says which
+    happened."""
     stop = threading.Event()
 
     def run():
@@ -281,13 +285,27 @@ def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> thread
             errors[state["section"]] = "deadline reached while running"
         reporter.emit(deadline_hit=True, untimed_skipped=state.get("skipped") or None, section_errors=errors or None)
         kill_children(state)
+        how = "not aborted within %.1f s" % ABORT_GRACE_S
         try:
             nat.request_abort()
             t_end = time.monotonic() + ABORT_GRACE_S
-            while not nat.abort_done() and time.monotonic() < t_end:
+            while time.monotonic() < t_end:
+                if nat.abort_done():
+                    how = "aborted by the main thread's wait"
+                    break
+                # The main thread outside the engine (a gloo barrier, a torch
+                # sync, Python): no RCCL call can be running, abort from here.
+                if nat.abort_if_idle():
+                    how = "aborted by the watchdog (engine idle)"
+                    break
                 time.sleep(0.02)
-        except Exception:  # noqa: BLE001 -- the process ends either way
-            pass
+        except Exception as e:  # noqa: BLE001 -- the process ends either way
+            how = "abort failed: %s" % e
+        log("bench: communicators %s" % how)
+        # Every rank's watchdog fires within about a second of the others; a
+        # launcher (torchrun) SIGTERMs the other ranks as soon as one exits,
+        # which would cut a peer's own abort short.  Linger a moment first.
+        time.sleep(ABORT_LINGER_S)
         sys.stderr.flush()
         os._exit(0 if reporter.result is not None else 4)
 
@@ -378,6 +396,17 @@ def link_check(rank_links, matrix_transport):
     return {"direct_xgmi_pairs": direct, "not_p2p": wrong, "ok": not wrong}
 
 
+def unparsed_peers(reports):
+    """"rank->peer" for every remote peer on the same host whose RCCL
+    connection lines were not parsed although the rank exchanged messages
+    with it (link_report unparsed_peers, csrc/rccl_log.hpp
+    rccl_unparsed_peers): RCCL's log format changed and those peers' ops stay
+    at the 2-channel default.  None without RCCL link reports."""
+    if not isinstance(reports, list) or not any(reports):
+        return None
+    return ["%d->%d" % (r["rank"], u["peer"]) for r in reports if r for u in r.get("unparsed_peers") or []]
+
+
 def default_device(local_rank: int) -> int:
     """LOCAL_RANK, modulo the visible GPUs: a launcher that gives each rank
     one visible GPU (HIP_VISIBLE_DEVICES per process) leaves every rank on
@@ -393,23 +422,30 @@ def hang_requested(section: str, rank: int) -> bool:
     return bool(spec) and spec == "%s@%d" % (section, rank)
 
 
-def candidate_hang_requested(transport: str, comms: int, batch: int, phase: str, rank: int) -> bool:
-    """Test hook: P2P_BENCH_HANG="candidate:[<transport>:]<comms>,<batch>[:connect]@<rank>"
-    makes that rank stop making progress in that posting candidate's first
-    tuning pass (or its connect), as a peer whose transfer never completes:
-    it posts nothing, and its own wait ends only at its session's timeout."""
-    spec = os.environ.get("P2P_BENCH_HANG", "")
-    if not spec.startswith("candidate:") or "@" not in spec:
-        return False
-    what, at = spec[len("candidate:"):].rsplit("@", 1)
-    parts = what.split(":")
-    want_phase = "tuning"
-    if parts and parts[-1] in ("connect", "tuning"):
-        want_phase = parts.pop()
-    if len(parts) == 2:
-        if parts[0] != transport:
-            return False
-        parts = parts[1:]
-    return len(parts) == 1 and parts[0] == "%d,%d" % (comms, batch) and phase == want_phase and at == str(rank)
-
-
+def candidate_hang(transport: str, comms: int, batch: int, rank: int):
+    """Test hook: P2P_BENCH_HANG="candidate:[<transport>:]<comms>,<batch>[:<how>]@<rank>"
+    (several, separated by ';') makes that rank misbehave in that posting
+    candidate.  Returns <how> for this rank and candidate, else None:
+      tuning (default): in the first tuning pass it posts nothing, as a peer
+                whose transfer never completes, and its own wait ends only at
+                its session's timeout (the candidate's budget);
+      connect:  the same in the candidate's connect;
+      stall:    in the first tuning pass it stops in Python, outside the
+                engine (the deadline watchdog aborts the communicators
+                itself, abort_if_idle);
+      unbounded: its session's timeout is lifted for the first tuning pass,
+                which it runs as usual: next to a stalled peer it waits
+                inside the transport until the watchdog's cooperative abort."""
+    for spec in os.environ.get("P2P_BENCH_HANG", "").split(";"):
+        if not spec.startswith("candidate:") or "@" not in spec:
+            continue
+        what, at = spec[len("candidate:"):].rsplit("@", 1)
+        parts = what.split(":")
+        how = parts.pop() if parts and parts[-1] in ("tuning", "connect", "stall", "unbounded") else "tuning"
+        if len(parts) == 2:
+            if parts[0] != transport:
+                continue
+            parts = parts[1:]
+        if len(parts) == 1 and parts[0] == "%d,%d" % (comms, batch) and at == str(rank):
+            return how
+    return None

@@ -14,15 +14,20 @@ import torch
 import torch.distributed as dist
 
 from test_nccl_p2p_amd.bench.core import (BASELINE_VALUE, METRIC, RESERVE_S, TUNING_SHARE, candidate_budget,
-                                          candidate_hang_requested, cell_matrix, first_candidate_budget, first_comms,
+                                          candidate_hang, cell_matrix, first_candidate_budget, first_comms,
                                           headline_stats, link_check, log, pick_depth, posting_candidates,
-                                          tuning_steps)
+                                          tuning_steps, unparsed_peers)
 
 
-def emulate_hang(seconds: float):
-    """The P2P_BENCH_HANG candidate hook: this rank posts nothing and waits
-    as a transport wait that never completes does, until its session's
-    timeout (the candidate's budget), then fails."""
+def emulate_hang(seconds: float, how: str = "tuning"):
+    """The P2P_BENCH_HANG candidate hook (core.candidate_hang): this rank
+    posts nothing and waits as a transport wait that never completes does,
+    until its session's timeout (the candidate's budget), then fails; or
+    ("stall") stops outside the engine for good."""
+    if how == "stall":
+        log("bench: injected stall outside the engine")
+        while True:
+            time.sleep(1.0)
     log("bench: injected hang for the candidate's budget (%.1f s)" % seconds)
     time.sleep(seconds)
     raise RuntimeError("injected hang: no progress within %.1f s" % seconds)
@@ -132,13 +137,14 @@ class HeadlineMixin:
                     wait_s = first_budget
                 budgets[key] = round(wait_s, 2)
                 d, err, connect_s = None, None, 0.0
+                hang = candidate_hang(transport, c, b, self.env.rank)
                 t_phase = time.monotonic()
                 tl.begin("%stuning/%s/init" % (pre, key))
                 try:
                     s_c = session_for(c, wait_s)
                     tl.begin("%stuning/%s/connect" % (pre, key))
                     t_conn = time.monotonic()
-                    if candidate_hang_requested(transport, c, b, "connect", self.env.rank):
+                    if hang == "connect":
                         emulate_hang(wait_s)
                     d = nat.StepDriver(s_c, mode, "bi", size, args.msgs, False, bool(b), bool(args.graph))
                     d.connect()
@@ -162,8 +168,10 @@ class HeadlineMixin:
                         t_phase = time.monotonic()
                         w0 = time.perf_counter()
                         try:
-                            if p == 0 and candidate_hang_requested(transport, c, b, "tuning", self.env.rank):
-                                emulate_hang(wait_s)
+                            if p == 0 and hang == "unbounded":
+                                s_c.set_timeout(3600.0)
+                            elif p == 0 and hang in ("tuning", "stall"):
+                                emulate_hang(wait_s, hang)
                             d.run_steps(0, tune_k)
                             d.sync()
                             if (os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d,tuning" % (c, b)
@@ -472,6 +480,9 @@ class HeadlineMixin:
             "provenance": dict(h.provenance, rccl_peers=h.rccl_peers),
             "matrix_transport": h.matrix_transport,
             "link_check": link_check(h.provenance.get("rank_links"), h.matrix_transport),
+            # Peers whose RCCL connection lines did not parse:
+            # [] when every connected peer's lines were read.
+            "unparsed_peers": unparsed_peers(h.rccl_peers),
             "reference_semantics": None,
             "reference_semantics_stock": None,
             "pair_serial_events": None,

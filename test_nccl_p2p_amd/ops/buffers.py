@@ -19,7 +19,13 @@ import torch
 from .._native import require_native
 
 M32 = 0xFFFFFFFF
-IMPLS = {"auto": 0, "reg": 1, "register": 1, "grid": 1, "lds": 2, "stride": 3, "lds8": 4, "lds-cached": 5, "lds-pipe": 6, "lds8-span": 7}
+
+
+def impl_number(name: str) -> int:
+    """Verify kernel name -> the native impl number: auto, lds8 (alias lds),
+    stride (alias reg); a variant round 5 removed raises ValueError saying so
+    (csrc/app.cpp parse_verify_impl, shared with p2p_matrix --verify-impl)."""
+    return require_native().parse_verify_impl(name)
 
 
 class VerifyResult(NamedTuple):
@@ -57,14 +63,14 @@ def fill_(t: torch.Tensor, seed: int, stream: Optional[torch.cuda.Stream] = None
 def verify(t: torch.Tensor, seed: int, impl: str = "auto", stream: Optional[torch.cuda.Stream] = None) -> VerifyResult:
     """Compares ``t`` with PRNG stream ``seed`` on the device (blocking)."""
     nbytes = _check_tensor(t)
-    r = require_native().verify(t.data_ptr(), nbytes, seed & (2**64 - 1), IMPLS[impl], True, _stream(stream))
+    r = require_native().verify(t.data_ptr(), nbytes, seed & (2**64 - 1), impl_number(impl), True, _stream(stream))
     return VerifyResult(*r)
 
 
 def checksum(t: torch.Tensor, impl: str = "auto", stream: Optional[torch.cuda.Stream] = None) -> int:
     """Sum of the tensor's 32-bit words mod 2**64 (no PRNG compare)."""
     nbytes = _check_tensor(t)
-    return int(require_native().verify(t.data_ptr(), nbytes, 0, IMPLS[impl], False, _stream(stream))[1])
+    return int(require_native().verify(t.data_ptr(), nbytes, 0, impl_number(impl), False, _stream(stream))[1])
 
 
 # ---------------------------------------------------------------- reference --

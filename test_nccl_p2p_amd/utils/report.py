@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import json
 import re
+import statistics
 from typing import Dict, Iterable, List, Optional
 
 UNI_TITLE = "Evaluating the Uni-Directional NCCL P2P Bandwidth (Gbps)"
@@ -66,6 +67,47 @@ def parse_compat(text: str) -> Dict[str, List[List[float]]]:
 
 def gbps_to_gbs(m: List[List[float]]) -> List[List[float]]:
     return [[v / 8.0 for v in row] for row in m]
+
+
+def offdiag(m: List[List[float]]) -> List[float]:
+    return [m[i][j] for i in range(len(m)) for j in range(len(m[i])) if i != j]
+
+
+def fabric_findings(tournament: Optional[List[List[float]]] = None, uni: Optional[List[List[float]]] = None,
+                    bi: Optional[List[List[float]]] = None, link_check: Optional[dict] = None,
+                    unparsed: Optional[List[str]] = None, min_ratio: float = 0.5) -> List[str]:
+    """What is wrong with a node's fabric by checks that need no hardware
+    number; [] when all pass.  On a fully connected xGMI
+    node every link is alike, so
+      * no off-diagonal cell of the bench's tournament matrix (GB/s) or of
+        the reference's uni matrix (p2p_matrix.cc:177, Gbps) is below
+        min_ratio x the median cell: a degraded link or a mis-posted
+        communicator shows up as one slow cell;
+      * every bi cell (both directions summed, :258) is at least its uni cell;
+      * RCCL carried every direct xGMI pair over its P2P transport
+        (link_check) and parsed every connected peer's lines (unparsed).
+    Missing inputs are not judged."""
+    out = []
+    for name, m in (("tournament matrix_gbs", tournament), ("compat uni", uni)):
+        cells = offdiag(m) if m else []
+        if len(cells) < 2:
+            continue
+        med = statistics.median(cells)
+        for i in range(len(m)):
+            for j in range(len(m)):
+                if i != j and m[i][j] < min_ratio * med:
+                    out.append("%s: cell %d->%d %.2f < %.2f x median %.2f" % (name, i, j, m[i][j], min_ratio, med))
+    if uni and bi:
+        for i in range(min(len(uni), len(bi))):
+            for j in range(min(len(uni[i]), len(bi[i]))):
+                if i != j and bi[i][j] < uni[i][j]:
+                    out.append("compat bi cell %d<->%d %.2f below its uni cell %.2f" % (i, j, bi[i][j], uni[i][j]))
+    if link_check is not None and not link_check.get("ok", True):
+        out.append("link_check: %d direct xGMI pair(s) not on RCCL's P2P transport: %s"
+                   % (len(link_check.get("not_p2p") or []), ", ".join((link_check.get("not_p2p") or [])[:16])))
+    if unparsed:
+        out.append("RCCL connection lines not parsed for %s" % ", ".join(unparsed[:16]))
+    return out
 
 
 def read_json_lines(path: str) -> List[dict]:

@@ -15,6 +15,8 @@
 #include <thread>
 #include <vector>
 
+#include <unistd.h>
+
 #include "app.hpp"
 #include "bootstrap.hpp"
 #include "common.hpp"
@@ -446,6 +448,7 @@ TEST(test_cli_defaults_match_reference) {
   EXPECT(c2.sizes.size() == 3);
   EXPECT(c2.iters_auto);
   EXPECT(c2.run.timing == Timing::Wallclock && c2.run.warmup == 0 && !c2.warm_connections);
+  EXPECT(c2.reference_buffers && !cfg.reference_buffers);  // one send / receive region, like p2p_matrix.cc:124-130
   EXPECT(c2.dirs.size() == 1 && c2.dirs[0] == Direction::Bi);
   EXPECT(auto_iters(32u << 20, 4ull << 30) == 128);  // the reference's 128 x 32 MiB
   EXPECT(auto_iters(4096, 4ull << 30) == 1000);
@@ -453,8 +456,10 @@ TEST(test_cli_defaults_match_reference) {
 }
 
 TEST(test_cli_verify_impl_names) {
-  const std::pair<const char*, int> known[] = {{"auto", 0}, {"reg", 1},        {"lds", 2},      {"stride", 3},
-                                               {"lds8", 4}, {"lds-cached", 5}, {"lds-pipe", 6}, {"lds8-span", 7}};
+  // Round 5 kept the LDS-DMA (lds8) and the register (stride) verify: the
+  // older names of each staging are aliases.
+  const std::pair<const char*, int> known[] = {{"auto", 0}, {"lds8", 1},   {"lds", 1},     {"stride", 2},
+                                               {"reg", 2},  {"register", 2}};
   for (const auto& [name, impl] : known) {
     std::vector<std::string> args{"--verify-impl", name};
     std::vector<char*> argv;
@@ -470,6 +475,20 @@ TEST(test_cli_verify_impl_names) {
   AppConfig cfg;
   int code = -1;
   EXPECT(!parse_cli(static_cast<int>(argv.size()), argv.data(), &cfg, &code) && code == 1);
+  // A removed variant says so (and which profile holds its numbers).
+  for (const char* gone : {"lds-cached", "lds-pipe", "lds8-span", "grid"}) {
+    std::string note;
+    EXPECT(parse_verify_impl(gone, &note) == -2 && note.find("removed in round 5") != std::string::npos &&
+           note.find("profiles/") != std::string::npos);
+    std::vector<std::string> a2{"--verify-impl", gone};
+    std::vector<char*> v2;
+    for (auto& x : a2) v2.push_back(&x[0]);
+    AppConfig c2;
+    int code2 = -1;
+    EXPECT(!parse_cli(static_cast<int>(v2.size()), v2.data(), &c2, &code2) && code2 == 1);
+  }
+  std::string note;
+  EXPECT(parse_verify_impl("lds8span", &note) == -1 && note.find("unknown") != std::string::npos);
 }
 
 // ------------------------------------------- multi-rank engine (threads) ----
@@ -948,6 +967,60 @@ TEST(test_rccl_op_limits_from_connection_lines) {
   auto nl = rccl_peer_links(parse_rccl_connections(net), 1, 4);
   const int ninit = rccl_op_channels(parse_rccl_init(net), true, 2);
   EXPECT((proposed_op_channels({ninit, 0, ninit, ninit}, nl, 1) == std::vector<int>{2, 0, 2, 2}));
+}
+
+TEST(test_rccl_unparsed_peers_keep_their_raw_lines) {
+  // connection lines in a layout parse_rccl_connections
+  // does not know (peer 2 here) leave a connected same-host peer with no
+  // channels; rccl_unparsed_peers names it with its raw lines, connection-like
+  // lines first.  Peer 1's line is in the known layout.
+  const std::string text =
+      "node:4711:4711 [0] NCCL INFO comm 0x5a5a0100 rank 0 nRanks 4 nNodes 1 localRanks 4 localRank 0 MNNVL 0\n"
+      "node:4711:4711 [0] NCCL INFO 64 coll channels, 0 collnet channels, 0 nvls channels, 64 p2p channels, 8 p2p "
+      "channels per peer\n"
+      "node:4711:4711 [0] NCCL INFO comm 0x5a5a0100 rank 0 nranks 4 cudaDev 0 busId 2d000 - Init COMPLETE\n"
+      "node:4711:4730 [0] NCCL INFO Channel 00/1 : 0[0] -> 1[1] via P2P/IPC comm 0x5a5a0100 nRanks 04\n"
+      "node:4711:4731 [0] NCCL INFO peer 2 proxy progress thread started\n"
+      "node:4711:4731 [0] NCCL INFO P2P channel 04: rank 0 => peer 2 over xGMI (IPC read) comm 0x5a5a0100\r\n"
+      "node:4711:4731 [0] NCCL INFO P2P channel 12: rank 0 => peer 2 over xGMI (IPC read) comm 0x5a5a0100\n"
+      "node:4711:4731 [0] NCCL INFO busId 2d000 cudaDev 2 nothing about the peer\n";
+  auto links = rccl_peer_links(parse_rccl_connections(text), 0, 4);
+  EXPECT(links[1].channels_connected == 1 && links[2].channels_connected == 0 && links[3].channels_connected == 0);
+  // Peers 1 and 2 were exchanged with; 3 was not (no connection expected).
+  auto u = rccl_unparsed_peers(text, links, {0, 0, 0, 0}, {0, 1, 1, 0}, 0);
+  EXPECT(u.size() == 1 && u[0].peer == 2 && u[0].lines.size() == 3);
+  if (u.size() == 1 && u[0].lines.size() == 3) {
+    EXPECT(u[0].lines[0].find("P2P channel 04: rank 0 => peer 2") != std::string::npos);
+    EXPECT(u[0].lines[1].find("channel 12") != std::string::npos && u[0].lines[1].back() != '\r');
+    EXPECT(u[0].lines[2].find("proxy progress") != std::string::npos);
+  }
+  // A peer RCCL reaches over its network transport is judged by the init
+  // line, and the line budget holds.
+  EXPECT(rccl_unparsed_peers(text, links, {0, 0, 1, 0}, {0, 1, 1, 0}, 0).empty());
+  auto capped = rccl_unparsed_peers(text, links, {0, 0, 0, 0}, {0, 1, 1, 0}, 0, 2);
+  EXPECT(capped.size() == 1 && capped[0].lines.size() == 2);
+  // Every peer parsed: nothing to report.
+  const std::string known = read_file(std::string(P2P_TEST_DATA) + "/rccl_info_4rank_p2p_rank1_canned.txt");
+  auto kl = rccl_peer_links(connections_of(parse_rccl_connections(known), {"0x5a5a0100", "0x5a5a0900"}), 1, 4);
+  EXPECT(rccl_unparsed_peers(known, kl, {0, 0, 0, 0}, {1, 0, 1, 0}, 1).empty());
+}
+
+TEST(test_rccl_log_warnings_and_env_ownership) {
+  // The private log's WARN extraction (the text RCCL errors carry) on a file
+  // this test owns: NCCL_DEBUG_FILE set by the user is read as it is.
+  const std::string path = "/tmp/p2p_host_test_rccl_log_" + std::to_string(static_cast<int>(getpid())) + ".txt";
+  {
+    std::ofstream f(path);
+    for (int i = 0; i < 6; ++i) f << "x NCCL WARN problem " << i << "\nx NCCL INFO fine\n";
+  }
+  setenv("NCCL_DEBUG_FILE", path.c_str(), 1);
+  EXPECT(rccl_log_file().path == path && !rccl_log_file().ours);
+  const std::string w = rccl_log_warnings(0);
+  EXPECT(w.find("problem 2") != std::string::npos && w.find("problem 5") != std::string::npos &&
+         w.find("problem 1") == std::string::npos && w.find("fine") == std::string::npos);
+  EXPECT(rccl_log_size() > 0 && rccl_log_since(rccl_log_size()).empty());
+  unsetenv("NCCL_DEBUG_FILE");
+  std::remove(path.c_str());
 }
 
 TEST(test_link_transport_mismatch) {

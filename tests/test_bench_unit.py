@@ -253,17 +253,17 @@ def test_candidate_budgets():
 
 
 def test_candidate_hang_hook(monkeypatch):
-    from test_nccl_p2p_amd.bench.core import candidate_hang_requested as hang
+    from test_nccl_p2p_amd.bench.core import candidate_hang as hang
 
     monkeypatch.setenv("P2P_BENCH_HANG", "candidate:4,1@3")
-    assert hang("rccl", 4, 1, "tuning", 3) and hang("host", 4, 1, "tuning", 3)
-    assert not hang("rccl", 4, 1, "tuning", 2) and not hang("rccl", 4, 0, "tuning", 3)
-    assert not hang("rccl", 4, 1, "connect", 3)
+    assert hang("rccl", 4, 1, 3) == "tuning" and hang("host", 4, 1, 3) == "tuning"
+    assert hang("rccl", 4, 1, 2) is None and hang("rccl", 4, 0, 3) is None
     monkeypatch.setenv("P2P_BENCH_HANG", "candidate:host:1,0:connect@0")
-    assert hang("host", 1, 0, "connect", 0)
-    assert not hang("shm", 1, 0, "connect", 0) and not hang("host", 1, 0, "tuning", 0)
+    assert hang("host", 1, 0, 0) == "connect" and hang("shm", 1, 0, 0) is None
+    monkeypatch.setenv("P2P_BENCH_HANG", "candidate:rccl:1,0:stall@1;candidate:rccl:1,0:unbounded@0")
+    assert hang("rccl", 1, 0, 1) == "stall" and hang("rccl", 1, 0, 0) == "unbounded" and hang("ipc", 1, 0, 0) is None
     monkeypatch.setenv("P2P_BENCH_HANG", "latency@3")
-    assert not hang("rccl", 1, 0, "tuning", 3)
+    assert hang("rccl", 1, 0, 3) is None
 
 
 def test_timeline_entries_are_contiguous():
@@ -284,3 +284,12 @@ def test_timeline_entries_are_contiguous():
     assert abs(sum(s for _, s in snap["entries"]) - snap["total_s"]) < 1e-3
     assert dict(snap["entries"])["a"] >= 0.019
     assert snap["total_s"] >= process_age() - 0.05 and snap["deadline_left_s"] > 0
+
+
+def test_unparsed_peers_summary():
+    from test_nccl_p2p_amd.bench.core import unparsed_peers
+
+    assert unparsed_peers(None) is None and unparsed_peers({"error": "x"}) is None and unparsed_peers([None]) is None
+    reps = [{"rank": 0, "unparsed_peers": []}, {"rank": 1, "unparsed_peers": [{"peer": 3, "lines": ["x"]}]}, None]
+    assert unparsed_peers(reps) == ["1->3"]
+    assert unparsed_peers([{"rank": 0, "unparsed_peers": []}]) == []

@@ -47,8 +47,8 @@ def test_copy_kernel_matches_torch(nbytes, coherent):
     assert torch.all(dst[nbytes:] == 0xAB), "copy wrote past the end"
 
 
-# grid, non-temporal, grid-stride, XCD-ordered grid, grid with 2 / 4 stores per lane
-@pytest.mark.parametrize("fill_impl", [1, 2, 3, 4, 5, 6])
+# auto and the full grid (the one fill kernel since round 5)
+@pytest.mark.parametrize("fill_impl", [0, 1])
 @pytest.mark.parametrize("nbytes", SIZES + [(64 << 20) + 4])
 def test_fill_variants_match_reference(fill_impl, nbytes):
     from test_nccl_p2p_amd import require_native
@@ -59,7 +59,7 @@ def test_fill_variants_match_reference(fill_impl, nbytes):
     assert torch.all(buf[nbytes:] == 0xAB), "fill wrote past the end"
 
 
-@pytest.mark.parametrize("impl", ["reg", "lds", "stride", "lds8", "lds-cached", "lds-pipe", "lds8-span"])
+@pytest.mark.parametrize("impl", ["lds8", "stride"])
 @pytest.mark.parametrize("nbytes", SIZES)
 def test_verify_clean_and_checksum(impl, nbytes):
     buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
@@ -73,7 +73,7 @@ def test_verify_clean_and_checksum(impl, nbytes):
     assert wrong.mismatches == reference_verify(buf, 78).mismatches > 0
 
 
-@pytest.mark.parametrize("impl", ["reg", "lds", "stride", "lds8", "lds-cached", "lds-pipe", "lds8-span"])
+@pytest.mark.parametrize("impl", ["lds8", "stride"])
 def test_verify_counts_exact_bitflips(impl):
     nbytes = (8 << 20) + 5
     buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
@@ -119,9 +119,24 @@ def test_batched_verify_matches_reference_per_buffer(native):
 def test_lds_and_register_agree_on_random_data():
     g = torch.Generator(device="cuda").manual_seed(0)
     buf = torch.randint(0, 256, (3 << 20,), dtype=torch.uint8, device="cuda", generator=g)
-    a = verify(buf, 5, impl="reg")
-    b = verify(buf, 5, impl="lds")
+    a = verify(buf, 5, impl="stride")
+    b = verify(buf, 5, impl="lds8")
     assert a == b == reference_verify(buf, 5)
+
+
+def test_removed_kernel_variants_fail_loudly(native):
+    """Round 5 removed the fill / verify variants that lost their A/B: asking
+    for one is an error that says so, never a silent fall-back."""
+    buf = dev_bytes(4096)
+    stream = torch.cuda.current_stream().cuda_stream
+    for impl in (2, 3, 4, 5, 6):
+        with pytest.raises(ValueError, match="removed in round 5"):
+            native.fill(buf.data_ptr(), 4096, 1, stream, impl)
+    for name in ("lds-cached", "lds-pipe", "lds8-span", "grid"):
+        with pytest.raises(ValueError, match="removed in round 5"):
+            verify(buf, 1, impl=name)
+    with pytest.raises(ValueError):
+        native.verify(buf.data_ptr(), 4096, 1, 7, True, stream)
 
 
 def test_int32_tensor_and_alignment_checks():

@@ -60,7 +60,7 @@ def test_copy_many_matches_torch(arena, group):
 
 
 @GPU_SETTINGS
-@given(st.integers(1, 3 << 20), st.integers(0, (1 << 64) - 1), st.sampled_from([1, 2, 3, 4, 5, 6]))
+@given(st.integers(1, 3 << 20), st.integers(0, (1 << 64) - 1), st.sampled_from([0, 1]))
 def test_fill_matches_reference_any_size(arena, nbytes, seed, impl):
     native, _ = arena
     buf = torch.full((nbytes + 64,), 0xAB, dtype=torch.uint8, device="cuda")
@@ -72,7 +72,7 @@ def test_fill_matches_reference_any_size(arena, nbytes, seed, impl):
 
 @GPU_SETTINGS
 @given(st.integers(16, 3 << 20), st.integers(0, (1 << 63) - 1),
-       st.sampled_from(["reg", "lds", "stride", "lds8", "lds-cached", "lds-pipe", "lds8-span"]), st.data())
+       st.sampled_from(["lds8", "stride"]), st.data())
 def test_verify_matches_reference_on_corruption(arena, nbytes, seed, impl, data):
     """Any set of corrupted bytes: every verify kernel reports the reference's
     mismatching-word count, first bad offset and checksum."""

@@ -22,8 +22,8 @@ import sys
 
 import pytest
 
-from conftest import MPIRUN, ROOT, ensure_built, free_port
-from test_nccl_p2p_amd.utils.report import parse_compat
+from conftest import MPIRUN, PERF_RECORDS, ROOT, ensure_built, free_port
+from test_nccl_p2p_amd.utils.report import fabric_findings, offdiag, parse_compat
 
 
 # P2P_REHEARSE_MULTI_GPU=N: run this tier with N ranks on the one GPU of a
@@ -69,7 +69,21 @@ BUDGET_S = {
     "test_fuzz_all_gpus": 35,
     "test_cli_fuzz_relay_all_gpus": 35,
     "test_bench_two_gpus_pair_sweep": 95,
+    "test_fabric_is_uniform": 5,
 }
+
+# What the correctness tests measured, for test_fabric_is_uniform (the
+# session's memory; also written under $P2P_TEST_LOG_DIR when set).
+FABRIC = {}
+
+
+def _keep(name, value):
+    FABRIC[name] = value
+    d = os.environ.get("P2P_TEST_LOG_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "fabric_%s.json" % name), "w") as f:
+            json.dump(value, f)
 
 
 @pytest.fixture(scope="module")
@@ -100,6 +114,7 @@ def test_reference_matrix_all_gpus(exe, tmp_path):
             for j in range(n):
                 assert (m[key][i][j] == 0.0) == (i == j)
     assert "verification: OK" in out.stdout
+    _keep("compat", m)
     recs = [json.loads(l) for l in js.read_text().splitlines()]
     assert all(r["verify_coverage"] == 1 for r in recs if r["type"] == "run")
     # Which RCCL transport carried each pair (RCCL's INFO log); --min-gbs
@@ -132,6 +147,8 @@ def test_bench_all_gpus():
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=BUDGET_S["test_bench_all_gpus"], cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    _keep("bench", {k: r.get(k) for k in ("matrix_gbs", "link_check", "unparsed_peers", "matrix_transport", "value",
+                                          "aggregate_gbs", "timeline_s")})
     assert r["n_gpus"] == n and r["verify_mismatches"] == 0 and r["value"] > 0
     assert r["matrix_cells"] == "%d/%d" % (n * (n - 1), n * (n - 1))
     assert len(r["matrix_transport"]) == n
@@ -198,3 +215,28 @@ def test_bench_two_gpus_pair_sweep():
     assert sw is not None, (r["untimed_skipped"], out.stderr[-2000:])
     assert sw["emulated"] == ("rccl" if REHEARSAL else None) and sw["rows"]["rccl-comms1"]["rc"] == 0, sw
     assert sw["best"] and sw["best_rccl"], sw
+
+
+@pytest.mark.perf
+def test_fabric_is_uniform():
+    """the links the correctness tests above measured,
+    checked for what a healthy fully connected xGMI node must show, with no
+    hardware number: no off-diagonal cell of the bench's tournament matrix or
+    of the reference's uni matrix below half the median cell (a degraded link,
+    a mis-posted communicator), every bi cell (both directions summed,
+    p2p_matrix.cc:258) at least its uni cell (:177), RCCL's P2P transport on
+    every direct pair and every connected peer's RCCL lines parsed.  Reads
+    what they kept and runs nothing; ordered with the perf floors."""
+    if not FABRIC:
+        pytest.skip("no multi-GPU measurement kept (those tests did not run or failed)")
+    bench = FABRIC.get("bench") or {}
+    compat = FABRIC.get("compat") or {}
+    tour = bench.get("matrix_gbs")
+    if tour:
+        cells = offdiag(tour)
+        PERF_RECORDS.update(xgmi_cell_min=round(min(cells), 2), xgmi_cell_mean=round(sum(cells) / len(cells), 2))
+    findings = fabric_findings(tour, compat.get("uni"), compat.get("bi"), bench.get("link_check"),
+                               bench.get("unparsed_peers"))
+    assert not findings, "\n".join(findings + ["tournament GB/s: %s" % tour, "compat uni Gbps: %s" % compat.get("uni"),
+                                               "compat bi Gbps: %s" % compat.get("bi"),
+                                               "transports: %s" % bench.get("matrix_transport")])

@@ -113,3 +113,32 @@ def test_child_dies_with_its_parent():
     else:
         os.kill(pid, 9)
         raise AssertionError("the child outlived its parent")
+
+
+def test_fabric_findings_catch_one_slow_link():
+    """a node whose links are alike passes; one slow link,
+    a bi cell below its uni cell, a wrong transport or unparsed RCCL lines
+    each fail, by name."""
+    from test_nccl_p2p_amd.utils.report import fabric_findings
+
+    n = 4
+    even = [[0.0 if i == j else 48.0 + (i + j) % 3 for j in range(n)] for i in range(n)]
+    uni = [[0.0 if i == j else 390.0 for j in range(n)] for i in range(n)]
+    bi = [[0.0 if i == j else 770.0 for j in range(n)] for i in range(n)]
+    ok = {"direct_xgmi_pairs": 12, "not_p2p": [], "ok": True}
+    assert fabric_findings(even, uni, bi, ok, []) == []
+    assert fabric_findings(None, None, None, None, None) == []
+    slow = [row[:] for row in even]
+    slow[2][1] = 9.5
+    f = fabric_findings(slow, uni, bi, ok, [])
+    assert len(f) == 1 and f[0].startswith("tournament matrix_gbs: cell 2->1 9.50"), f
+    slow_uni = [row[:] for row in uni]
+    slow_uni[0][3] = 150.0
+    f = fabric_findings(even, slow_uni, bi, ok, [])
+    assert len(f) == 1 and "compat uni: cell 0->3" in f[0], f
+    low_bi = [row[:] for row in bi]
+    low_bi[1][0] = 380.0
+    assert fabric_findings(even, uni, low_bi, ok, []) == ["compat bi cell 1<->0 380.00 below its uni cell 390.00"]
+    bad = {"direct_xgmi_pairs": 12, "not_p2p": ["0->1 SHM"], "ok": False}
+    assert "0->1 SHM" in fabric_findings(even, uni, bi, bad, [])[0]
+    assert fabric_findings(even, uni, bi, ok, ["1->3"]) == ["RCCL connection lines not parsed for 1->3"]

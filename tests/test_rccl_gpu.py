@@ -171,15 +171,12 @@ def test_message_larger_than_4gib(session):
     assert ph["op_bytes"] == 1 << 30 and ph["warmup_mismatches"] == 0 and not r["rechunked"], ph
 
 
-@pytest.mark.parametrize("comms,per_comm", [(2, "0"), (4, "0"), (4, "1"), (8, "1")])
-def test_several_communicators(native, monkeypatch, comms, per_comm):
+@pytest.mark.parametrize("comms", [2, 4, 8])
+def test_several_communicators(native, comms):
     """K communicators per rank (messages of >= 1 MiB spread over them, each on
     its own stream, joined back per group): verified step driver, verified
     runs incl. a > 1 GiB message (chunks stay on their message's
-    communicator), small-message latency on the first communicator.  With
-    P2P_RCCL_GROUP_PER_COMM=1 every communicator's ops go to RCCL as a group
-    of their own."""
-    monkeypatch.setenv("P2P_RCCL_GROUP_PER_COMM", per_comm)
+    communicator), small-message latency on the first communicator."""
     s = native.Session(0, 1, device=0, transport="rccl:%d" % comms, timeout_s=120)
     assert ("x%d comms" % comms) in s.device_desc
     d = native.StepDriver(s, "self", "bi", 8 << 20, 8, True, True, False)
@@ -214,16 +211,13 @@ def test_buffer_registration_knob(native, monkeypatch, mode):
     del s
 
 
-@pytest.mark.parametrize("transport,chunk,per_comm", [("rccl", "0", "0"), ("rccl:4", "0", "0"), ("rccl:4", "1M", "0"),
-                                                     ("rccl:4", "1M", "1")])
-def test_fuzz_random_groups(native, monkeypatch, transport, chunk, per_comm):
+@pytest.mark.parametrize("transport,chunk", [("rccl", "0"), ("rccl:4", "0"), ("rccl:4", "1M")])
+def test_fuzz_random_groups(native, monkeypatch, transport, chunk):
     """Random groups of self messages (1 B .. 4 MiB, several per group)
     through one or four communicators; with P2P_RCCL_MAX_CHUNK=1M the larger
-    messages go out as several chunks on their message's communicator; with
-    P2P_RCCL_GROUP_PER_COMM=1 as one RCCL group per communicator."""
+    messages go out as several chunks on their message's communicator."""
     if chunk != "0":
         monkeypatch.setenv("P2P_RCCL_MAX_CHUNK", chunk)
-    monkeypatch.setenv("P2P_RCCL_GROUP_PER_COMM", per_comm)
     s = native.Session(0, 1, device=0, transport=transport, timeout_s=120)
     assert s.fuzz(rounds=30, seed=7, max_bytes=4 << 20) == 0
     del s

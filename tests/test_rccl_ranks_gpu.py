@@ -102,6 +102,32 @@ def test_bench_four_rccl_ranks(tmp_path):
             else:
                 assert p["op_limit_source"] == "connection lines" and p["channels_connected"] == 2, p
                 assert p["op_limit"] == 32 << 20, p
+    # Every connected peer's RCCL lines were parsed.
+    assert r["unparsed_peers"] == [], r["unparsed_peers"]
+
+
+@pytest.mark.emulated
+def test_bench_deadline_aborts_rccl_inside_and_outside_the_engine(tmp_path):
+    """the deadline watchdog gets the RCCL communicators of every
+    rank aborted wherever its main thread is.  Rank 1 stalls in Python during
+    the first posting candidate (outside the engine: the watchdog aborts them
+    from its own thread, abort_if_idle); rank 0, its session's timeout lifted,
+    sits in the transport's wait for rank 1's messages (the wait sees the
+    request and aborts them on the main thread).  Both end with exit 4
+    (nothing measured) and neither crashes."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2", "--device", "0", "--size", "4M",
+           "--msgs", "4", "--ipc-extra", "0", "--timeout", "60", "--deadline", "40"]
+    env = dict(ENV, P2P_BENCH_HANG="candidate:rccl:1,0:stall@1;candidate:rccl:1,0:unbounded@0")
+    out = run_logged(cmd, 120, "bench_deadline_abort", cwd=ROOT, env=env)
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert out.returncode != 0 and len(lines) == 1, out.stderr[-3000:]
+    r = json.loads(lines[0])
+    assert r["value"] is None and r["deadline_hit"] is True, r
+    assert r["timeline_s"]["open"] == "tuning/comms1_per_message/pass0", r["timeline_s"]
+    assert "communicators aborted by the main thread's wait" in out.stderr, out.stderr[-3000:]
+    assert "communicators aborted by the watchdog (engine idle)" in out.stderr, out.stderr[-3000:]
+    assert "Signal 11" not in out.stderr and "SIGSEGV" not in out.stderr, out.stderr[-3000:]
 
 
 @pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")

@@ -203,6 +203,32 @@ def test_bench_hung_first_candidate_falls_back_within_the_deadline(native):
     assert "tuning/comms1_per_message/pass0" in names and "fallback/headline/timed" in names, names
 
 
+def test_bench_deadline_aborts_inside_and_outside_the_engine(native):
+    """at the deadline the watchdog gets every rank's
+    communicators aborted wherever its main thread is.  Rank 1 stalls in
+    Python (outside the engine: the watchdog aborts from its own thread,
+    abort_if_idle); rank 0, its session's timeout lifted, waits inside the
+    transport for rank 1's messages (its wait sees the request and aborts on
+    the main thread).  Both exit 4: nothing was measured."""
+    t0 = time.monotonic()
+    args = ["bench.py", "--gpus", "2", "--steps", "3", "--warmup", "2", "--transport", "host", "--size", "64K",
+            "--msgs", "2", "--latency-iters", "10", "--sweep", "0", "--extras", "0", "--ref-iters", "0",
+            "--ipc-extra", "0", "--deadline", "30"]
+    out = torchrun(2, args,
+                   env={"P2P_BENCH_HANG": "candidate:host:1,0:stall@1;candidate:host:1,0:unbounded@0"}, timeout=120)
+    wall = time.monotonic() - t0
+    assert out.returncode != 0 and wall < 60, (wall, out.stderr[-3000:])
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stderr[-3000:]
+    r = json.loads(lines[0])
+    assert r["value"] is None and r["deadline_hit"] is True and "did not finish" in r["error"], r
+    assert r["timeline_s"]["open"] == "tuning/comms1_per_message/pass0", r["timeline_s"]
+    assert "communicators aborted by the main thread's wait" in out.stderr, out.stderr[-3000:]
+    assert "communicators aborted by the watchdog (engine idle)" in out.stderr, out.stderr[-3000:]
+    assert "exitcode  : 4" in out.stderr or "exitcode: 4" in out.stderr or "exit code 4" in out.stderr, \
+        out.stderr[-3000:]
+
+
 def test_fuzz_session_over_shm_and_host(native):
     """Random verified message groups, 3 processes, over the shared-memory and
     TCP transports through the Python session."""
