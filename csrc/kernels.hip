@@ -541,8 +541,7 @@ struct CopyArgs {
   uint32_t coherent;  // bit i: op i moves between GPUs (system-coherent accesses)
   int nops;
   // Workgroup -> op lookup: > 0 every op has this many blocks (one division);
-  // 0 binary search of block_begin; -1 the linear scan (A/B only,
-  // P2P_COPY_LOOKUP=linear).
+  // 0 binary search of block_begin.
   int32_t uniform;
 };
 
@@ -563,15 +562,13 @@ __global__ __launch_bounds__(kBlock) void multi_copy_kernel(const CopyArgs a) {
   int op = 0;
   if (a.uniform > 0) {
     op = min(static_cast<int>(blockIdx.x / static_cast<uint32_t>(a.uniform)), a.nops - 1);
-  } else if (a.uniform == 0) {
+  } else {
     int lo = 0, hi = a.nops - 1;  // largest op with block_begin[op] <= blockIdx.x
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
       if (blockIdx.x >= a.block_begin[mid]) lo = mid; else hi = mid - 1;
     }
     op = lo;
-  } else {
-    while (op + 1 < a.nops && blockIdx.x >= a.block_begin[op + 1]) ++op;
   }
   const uint32_t b = blockIdx.x - a.block_begin[op];
   const uint32_t nb = a.block_begin[op + 1] - a.block_begin[op];
@@ -645,31 +642,17 @@ void launch_copy_group(const CopyOp* ops, int cnt, hipStream_t stream, int max_b
   a.uniform = static_cast<int32_t>(a.block_begin[1] - a.block_begin[0]);
   for (int i = 1; i < cnt; ++i)
     if (a.block_begin[i + 1] - a.block_begin[i] != static_cast<uint32_t>(a.uniform)) a.uniform = 0;
-  static const bool linear = [] {
-    const char* e = std::getenv("P2P_COPY_LOOKUP");
-    return e && std::strcmp(e, "linear") == 0;
-  }();
-  if (linear) a.uniform = -1;
   multi_copy_kernel<<<acc, kBlock, 0, stream>>>(a);
   HIP_OK(hipGetLastError());
 }
 
 uint64_t copy_blocks(size_t bytes) { return std::max<uint64_t>(1, (bytes / 16 + kBlockVecs - 1) / kBlockVecs); }
 
-// Ops per launch: kMaxCopyOps, or fewer with P2P_COPY_MAX_OPS (A/B only).
-int copy_max_ops() {
-  static const int m = [] {
-    const char* e = std::getenv("P2P_COPY_MAX_OPS");
-    const int v = e ? std::atoi(e) : kMaxCopyOps;
-    return std::max(1, std::min(kMaxCopyOps, v));
-  }();
-  return m;
-}
 
 }  // namespace
 
 void launch_multi_copy(const CopyOp* ops, int nops, hipStream_t stream, int max_blocks) {
-  const int max_ops = copy_max_ops();
+  constexpr int max_ops = kMaxCopyOps;
   if (max_blocks > 0) {  // explicit grid cap (grid-shape experiments): the ops share it
     for (int first = 0; first < nops; first += max_ops)
       launch_copy_group(ops + first, std::min(max_ops, nops - first), stream, max_blocks);

@@ -5,7 +5,8 @@ multi-copy grid (kernels.hip multi_copy_kernel); a bench step at the default
 shape is 32 receives of 32 MiB = two launches of 16 ops.
 
     python scripts/probes/copy_ops_probe.py            # current lookup
-    P2P_COPY_LOOKUP=linear python scripts/probes/copy_ops_probe.py   # the old scan
+    (round 2's A/B; its P2P_COPY_LOOKUP=linear / P2P_COPY_MAX_OPS knobs were
+    removed from the kernel in round 5, profiles/r2_copy_lookup/ keeps the numbers)
 """
 import argparse
 import json

@@ -41,6 +41,13 @@ CONFIGS = [
     ("q4_seq_k1x6_k4", {"GPU_MAX_HW_QUEUES": "4"}, "1+1+1+1+1+1+4", 8),
     ("q4_seq_k8_k4", {"GPU_MAX_HW_QUEUES": "4"}, "8+4", 8),
     ("q8_seq_k1_k4", {"GPU_MAX_HW_QUEUES": "8"}, "1+4", 8),
+    # Work on the null stream first ("t": a torch kernel on the current,
+    # i.e. default, stream; "f": the fill kernel on stream 0), as the kernel
+    # tests do before the GPU tier's floor (profiles/r5_floor_bisect/).
+    ("q4_null_torch_k4", {"GPU_MAX_HW_QUEUES": "4"}, "t+4", 8),
+    ("q4_null_fill_k4", {"GPU_MAX_HW_QUEUES": "4"}, "f+4", 8),
+    ("q8_null_fill_k4", {"GPU_MAX_HW_QUEUES": "8"}, "f+4", 8),
+    ("q4_null_fill_k1", {"GPU_MAX_HW_QUEUES": "4"}, "f+1", 8),
 ]
 
 
@@ -51,11 +58,24 @@ def child(seq: str, msgs: int) -> None:
     import test_nccl_p2p_amd
 
     nat = test_nccl_p2p_amd.require_native()
-    counts = [int(c) for c in str(seq).split("+")]
+    steps = str(seq).split("+")
     rec = None
-    for comms in counts:
-        rec = one_session(nat, comms, msgs)
-    print(json.dumps(dict(rec, earlier=counts[:-1])))
+    for st in steps:
+        if st == "t":
+            import torch
+
+            torch.ones(1 << 20, device="cuda").mul_(2)
+            torch.cuda.synchronize()
+        elif st == "f":
+            import torch
+
+            buf = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
+            nat.fill(buf.data_ptr(), 64 << 20, 1, 0)
+            torch.cuda.synchronize()
+            del buf
+        else:
+            rec = one_session(nat, int(st), msgs)
+    print(json.dumps(dict(rec, earlier=steps[:-1])))
 
 
 def one_session(nat, comms: int, msgs: int) -> dict:

@@ -117,9 +117,9 @@ def test_bench_deadline_aborts_rccl_inside_and_outside_the_engine(tmp_path):
     (nothing measured) and neither crashes."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2", "--device", "0", "--size", "4M",
-           "--msgs", "4", "--ipc-extra", "0", "--timeout", "60", "--deadline", "40"]
+           "--msgs", "4", "--ipc-extra", "0", "--timeout", "60", "--deadline", "25"]
     env = dict(ENV, P2P_BENCH_HANG="candidate:rccl:1,0:stall@1;candidate:rccl:1,0:unbounded@0")
-    out = run_logged(cmd, 120, "bench_deadline_abort", cwd=ROOT, env=env)
+    out = run_logged(cmd, 90, "bench_deadline_abort", cwd=ROOT, env=env)
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert out.returncode != 0 and len(lines) == 1, out.stderr[-3000:]
     r = json.loads(lines[0])

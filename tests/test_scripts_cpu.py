@@ -86,13 +86,31 @@ def test_pair_sweep_resume_keeps_finished_rows(mpirun, host_build, tmp_path):
     assert json.loads((tmp_path / "summary.json").read_text())["rows_run"] == 1
 
 
+def emulated_tests():
+    """Names of the tests marked `emulated` (several ranks on one GPU): on a
+    node with >= 2 GPUs conftest skips them, the multi-GPU tier runs the
+    same flows across the real GPUs instead."""
+    import ast
+    import glob
+
+    names = set()
+    for path in glob.glob(os.path.join(ROOT, "tests", "test_*.py")):
+        for f in ast.parse(open(path).read()).body:
+            if isinstance(f, ast.FunctionDef) and any("emulated" in ast.dump(d) for d in f.decorator_list):
+                names.add(f.name)
+    return names
+
+
 def measured_single_gpu_tier_s():
-    """Duration of the single-GPU tier as measured on a one-GPU MI355X box:
-    the final line of every profiles/r<k>*/pytest_gpu*.log of the latest
-    round k that has one (a whole tier, not a failed run), worst case."""
+    """Duration of the single-GPU tier on a multi-GPU node, from the runs on
+    one-GPU MI355X boxes: the final line of every profiles/r<k>*/pytest_gpu*.log
+    of the latest round k that has one (a whole tier, not a failed run), less
+    the `emulated` tests' durations its --durations table lists (skipped on a
+    node), worst case."""
     import glob
     import re
 
+    emulated = emulated_tests()
     runs = []
     for path in glob.glob(os.path.join(ROOT, "profiles", "r*", "pytest_gpu*.log")):
         rnd = re.match(r"r(\d+)", os.path.basename(os.path.dirname(path)))
@@ -100,7 +118,9 @@ def measured_single_gpu_tier_s():
             lines = [l for l in f.read().splitlines() if l.strip()]
         m = re.search(r"(\d+) passed.* in ([\d.]+)s", lines[-1] if lines else "")
         if rnd and m and "failed" not in lines[-1]:
-            runs.append((int(rnd.group(1)), float(m.group(2)), path))
+            skipped_on_node = sum(float(d.group(1)) for d in (re.match(r"([\d.]+)s call\s+\S+::(\w+)", l) for l in lines)
+                                  if d and d.group(2) in emulated)
+            runs.append((int(rnd.group(1)), float(m.group(2)) - skipped_on_node, path))
     assert runs, "no measured GPU-tier log under profiles/"
     latest = max(r[0] for r in runs)
     return max((r[1], r[2]) for r in runs if r[0] == latest)

@@ -129,11 +129,14 @@ def test_kernel_bandwidth_floors(native):
     assert rates["copy"] > 2.5, msg  # payload bytes (read once + written once)
 
 
-def _self_step_gbs(native, transport):
-    """Median GB/s of the bench's step shape (32 MiB x 8 self messages in one
-    group) over 20 steps after 5 warm ones, and the per-step times."""
-    s = native.Session(0, 1, device=0, transport=transport, timeout_s=120)
-    d = native.StepDriver(s, "self", "bi", 32 << 20, 8, False, True, False)
+SELF_STEP_CHILD = """
+import json, statistics, sys
+from test_nccl_p2p_amd import require_native
+nat = require_native()
+out = {}
+for transport in ("rccl", "rccl:4"):
+    s = nat.Session(0, 1, device=0, transport=transport, timeout_s=120)
+    d = nat.StepDriver(s, "self", "bi", 32 << 20, 8, False, True, False)
     d.connect()
     d.run_steps(0, 5)
     d.sync()
@@ -142,23 +145,37 @@ def _self_step_gbs(native, transport):
     d.sync()
     ms = d.step_ms()
     del d, s
-    return 8 * (32 << 20) / (statistics.median(ms) * 1e-3) / 1e9, ms
+    out[transport] = {"gbs_median": 8 * (32 << 20) / (statistics.median(ms) * 1e-3) / 1e9, "step_ms": ms}
+print("RESULT " + json.dumps(out))
+"""
 
 
 def test_self_copy_rate_floors(native):
-    """The RCCL self step through one and four communicators: absolute floors
-    at about 2/3 of the rates this tier measured (one: 1206-1250 GB/s, four:
-    1886-1966 GB/s, profiles/r4_gpu_tier/, profiles/r4_tier2/), and four at
-    least 1.3x one measured in the same process (1.51-1.63x measured): a lost
-    multi-communicator speedup or a slower RCCL posting fails here, a slower
-    box alone does not."""
-    one, ms1 = _self_step_gbs(native, "rccl")
-    four, ms4 = _self_step_gbs(native, "rccl:4")
-    rec = {"rccl": {"gbs_median": one, "step_ms": ms1}, "rccl:4": {"gbs_median": four, "step_ms": ms4},
-           "ratio": four / one}
+    """The RCCL self step (32 MiB x 8 self messages in one group, median of
+    20 steps after 5) through one and four communicators, measured in a
+    fresh process with the environment's hardware queues (4 on the box), as
+    bench.py's ranks run.  Inside the tier's process the four-communicator
+    rate fell to ~1800-1970 GB/s: the kernel tests before it launch work on
+    HIP's null stream, which then holds one of the process's 4 hardware
+    queues, so two of the transport's four streams share one (ADVICE r4;
+    profiles/r5_floor_bisect/: 2177-2381 fresh, 1876-1976 after a fill on the
+    null stream, 2410-2582 with 8 queues).  Floors at ~80% of the fresh
+    rates measured (one: 1172-1238, four: 2177-2451 GB/s, profiles/r5_tier1/,
+    r5_floor_bisect/), and four at least 1.5x one (1.84-2.03x): a lost
+    multi-communicator speedup or a slower RCCL posting fails here."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", SELF_STEP_CHILD], capture_output=True, text=True, timeout=240,
+                         cwd=root)
+    assert out.returncode == 0, out.stderr[-3000:]
+    res = json.loads([l for l in out.stdout.splitlines() if l.startswith("RESULT ")][-1][len("RESULT "):])
+    one, four = res["rccl"]["gbs_median"], res["rccl:4"]["gbs_median"]
+    rec = {"rccl": res["rccl"], "rccl:4": res["rccl:4"], "ratio": four / one, "process": "fresh child"}
     _record("self_copy_rate_floors", rec)
     PERF_RECORDS.update(rccl=round(one, 1), rccl4=round(four, 1))
     print("rccl %.1f  rccl:4 %.1f GB/s  ratio %.2f" % (one, four, four / one))
-    assert one > 800.0, rec
-    assert four > 1300.0, rec
-    assert four >= 1.3 * one, rec
+    assert one > 950.0, rec
+    assert four > 1750.0, rec
+    assert four >= 1.5 * one, rec
