@@ -75,7 +75,8 @@ def offdiag(m: List[List[float]]) -> List[float]:
 
 def fabric_findings(tournament: Optional[List[List[float]]] = None, uni: Optional[List[List[float]]] = None,
                     bi: Optional[List[List[float]]] = None, link_check: Optional[dict] = None,
-                    unparsed: Optional[List[str]] = None, min_ratio: float = 0.5) -> List[str]:
+                    unparsed: Optional[List[str]] = None, min_ratio: float = 0.5,
+                    bi_at_least_uni: bool = True) -> List[str]:
     """What is wrong with a node's fabric by checks that need no hardware
     number; [] when all pass.  On a fully connected xGMI
     node every link is alike, so
@@ -86,7 +87,9 @@ def fabric_findings(tournament: Optional[List[List[float]]] = None, uni: Optiona
       * every bi cell (both directions summed, :258) is at least its uni cell;
       * RCCL carried every direct xGMI pair over its P2P transport
         (link_check) and parsed every connected peer's lines (unparsed).
-    Missing inputs are not judged."""
+    Missing inputs are not judged.  (A rehearsal on one GPU, over loopback
+    sockets that share one CPU, asks less: a lower min_ratio and no bi >= uni,
+    tests/test_multi_gpu.py.)"""
     out = []
     for name, m in (("tournament matrix_gbs", tournament), ("compat uni", uni)):
         cells = offdiag(m) if m else []
@@ -97,7 +100,7 @@ def fabric_findings(tournament: Optional[List[List[float]]] = None, uni: Optiona
             for j in range(len(m)):
                 if i != j and m[i][j] < min_ratio * med:
                     out.append("%s: cell %d->%d %.2f < %.2f x median %.2f" % (name, i, j, m[i][j], min_ratio, med))
-    if uni and bi:
+    if uni and bi and bi_at_least_uni:
         for i in range(min(len(uni), len(bi))):
             for j in range(min(len(uni[i]), len(bi[i]))):
                 if i != j and bi[i][j] < uni[i][j]:

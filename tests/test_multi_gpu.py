@@ -42,6 +42,8 @@ CONCURRENT_SIZES = "1M,16M" if REHEARSAL >= 8 else "1M,64M"
 # setting for the concurrent modes, and the reference's matrices 60 s of
 # their 60 (profiles/r4_reh8/); a node's xGMI takes seconds.
 CONCURRENT_TIMEOUT_S = 150 if REHEARSAL >= 8 else None
+# test_fabric_is_uniform's cell bound in a rehearsal (a node: 0.5 x the median).
+REHEARSAL_MIN_RATIO = 0.25
 # 8 ranks on one GPU plus a comparison child per rank would pass the test
 # box's 16 processes per GPU; on a node each rank has a GPU of its own.
 ISOLATE = ["--isolate", "0"] if REHEARSAL >= 8 else []
@@ -235,8 +237,12 @@ def test_fabric_is_uniform():
     if tour:
         cells = offdiag(tour)
         PERF_RECORDS.update(xgmi_cell_min=round(min(cells), 2), xgmi_cell_mean=round(sum(cells) / len(cells), 2))
+    # A rehearsal's "links" are RCCL sockets over loopback, 4-8 ranks sharing
+    # one box's CPU: cells spread 2-4x and a bi cell can come in below its uni
+    # cell (profiles/r5_reh8/), so it checks the flow with looser bounds.
     findings = fabric_findings(tour, compat.get("uni"), compat.get("bi"), bench.get("link_check"),
-                               bench.get("unparsed_peers"))
+                               bench.get("unparsed_peers"), min_ratio=REHEARSAL_MIN_RATIO if REHEARSAL else 0.5,
+                               bi_at_least_uni=not REHEARSAL)
     assert not findings, "\n".join(findings + ["tournament GB/s: %s" % tour, "compat uni Gbps: %s" % compat.get("uni"),
                                                "compat bi Gbps: %s" % compat.get("bi"),
                                                "transports: %s" % bench.get("matrix_transport")])

@@ -142,3 +142,23 @@ def test_fabric_findings_catch_one_slow_link():
     bad = {"direct_xgmi_pairs": 12, "not_p2p": ["0->1 SHM"], "ok": False}
     assert "0->1 SHM" in fabric_findings(even, uni, bi, bad, [])[0]
     assert fabric_findings(even, uni, bi, ok, ["1->3"]) == ["RCCL connection lines not parsed for 1->3"]
+
+
+def test_fabric_findings_on_the_rehearsals():
+    """The matrices the one-GPU rehearsals kept (RCCL over loopback sockets,
+    profiles/r5_reh4/, r5_reh8/) pass the rehearsal's bounds; the 8-rank one
+    would fail a node's (slow socket pairs, bi below uni), which is why a
+    rehearsal asks less."""
+    import json
+
+    from test_nccl_p2p_amd.utils.report import fabric_findings
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_multi_gpu import REHEARSAL_MIN_RATIO
+
+    for d, node_ok in (("r5_reh4", True), ("r5_reh8", False)):
+        b = json.load(open(os.path.join(ROOT, "profiles", d, "fabric_bench.json")))
+        c = json.load(open(os.path.join(ROOT, "profiles", d, "fabric_compat.json")))
+        args = (b["matrix_gbs"], c["uni"], c["bi"], b["link_check"], b["unparsed_peers"])
+        assert fabric_findings(*args, min_ratio=REHEARSAL_MIN_RATIO, bi_at_least_uni=False) == [], d
+        assert (fabric_findings(*args) == []) == node_ok, d
