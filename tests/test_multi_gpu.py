@@ -150,7 +150,7 @@ def test_bench_all_gpus():
     assert out.returncode == 0, out.stderr[-3000:]
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     _keep("bench", {k: r.get(k) for k in ("matrix_gbs", "link_check", "unparsed_peers", "matrix_transport", "value",
-                                          "aggregate_gbs", "timeline_s")})
+                                          "aggregate_gbs", "timeline_s", "posting")})
     assert r["n_gpus"] == n and r["verify_mismatches"] == 0 and r["value"] > 0
     assert r["matrix_cells"] == "%d/%d" % (n * (n - 1), n * (n - 1))
     assert len(r["matrix_transport"]) == n
