@@ -113,10 +113,11 @@ from test_nccl_p2p_amd.bench import core  # noqa: E402
 core.set_start(T0)
 # Re-exported: the pure functions the unit tests pin (tests/test_bench_unit.py).
 from test_nccl_p2p_amd.bench.compare import child_main, steps_through  # noqa: E402,F401
-from test_nccl_p2p_amd.bench.core import (METRIC, Deadline, Reporter, Timeline, candidate_budget,  # noqa: E402,F401
-                                          cell_matrix, claim_stdout, default_device, first_candidate_budget,
-                                          first_comms, free_port, headline_stats, link_check, log, pick_depth,
-                                          posting_candidates, process_age, start_watchdog, tuning_steps)
+from test_nccl_p2p_amd.bench.core import (METRIC, Deadline, Reporter, Timeline, bench_fabric_findings,  # noqa: E402,F401
+                                          candidate_budget, cell_matrix, claim_stdout, default_device,
+                                          first_candidate_budget, first_comms, free_port, headline_stats, link_check,
+                                          log, pick_depth, posting_candidates, process_age, start_watchdog,
+                                          tuning_steps)
 from test_nccl_p2p_amd.bench.headline import HeadlineMixin  # noqa: E402
 from test_nccl_p2p_amd.bench.sections import SectionsMixin  # noqa: E402
 
@@ -313,6 +314,11 @@ class BenchRun(HeadlineMixin, SectionsMixin):
         self.timeline.begin("report")
         self.reporter.update(untimed_skipped=self.state["skipped"] or None,
                              section_errors=self.state["errors"] or None)
+        if self.env.rank == 0:
+            ff = bench_fabric_findings(self.reporter.result, self.n)
+            self.reporter.update(fabric_findings=ff)
+            for f in ff or []:
+                log("bench: fabric: " + f)
         if self.env.rank == 0:
             log("bench: GB/s matrix (row=src, col=dst), median over steps:")
             for r in range(self.n):

@@ -407,6 +407,23 @@ def unparsed_peers(reports):
     return ["%d->%d" % (r["rank"], u["peer"]) for r in reports if r for u in r.get("unparsed_peers") or []]
 
 
+def bench_fabric_findings(result: dict, n: int):
+    """The multi-GPU tier's fabric checks (utils/report.py fabric_findings)
+    on what one bench line holds: the tournament matrix, the serial-pair uni
+    and bi matrices of pair_serial_events (our method: warmup, events; else
+    the reference's method), link_check and unparsed_peers.  [] when all
+    pass; None at N = 1.  Informational: the line never fails on it."""
+    from test_nccl_p2p_amd.utils.report import fabric_findings
+
+    if n < 2:
+        return None
+    ser = next((result.get(k) for k in ("pair_serial_events", "reference_semantics")
+                if isinstance(result.get(k), dict) and "error" not in result[k]), None) or {}
+    uni = (ser.get("uni") or {}).get("matrix_gbs")
+    bi = (ser.get("bi") or {}).get("matrix_gbs")
+    return fabric_findings(result.get("matrix_gbs"), uni, bi, result.get("link_check"), result.get("unparsed_peers"))
+
+
 def default_device(local_rank: int) -> int:
     """LOCAL_RANK, modulo the visible GPUs: a launcher that gives each rank
     one visible GPU (HIP_VISIBLE_DEVICES per process) leaves every rank on

@@ -483,6 +483,7 @@ class HeadlineMixin:
             # Peers whose RCCL connection lines did not parse:
             # [] when every connected peer's lines were read.
             "unparsed_peers": unparsed_peers(h.rccl_peers),
+            "fabric_findings": None,
             "reference_semantics": None,
             "reference_semantics_stock": None,
             "pair_serial_events": None,

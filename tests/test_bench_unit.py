@@ -293,3 +293,20 @@ def test_unparsed_peers_summary():
     reps = [{"rank": 0, "unparsed_peers": []}, {"rank": 1, "unparsed_peers": [{"peer": 3, "lines": ["x"]}]}, None]
     assert unparsed_peers(reps) == ["1->3"]
     assert unparsed_peers([{"rank": 0, "unparsed_peers": []}]) == []
+
+
+def test_bench_fabric_findings():
+    from test_nccl_p2p_amd.bench.core import bench_fabric_findings
+
+    assert bench_fabric_findings({"matrix_gbs": [[0.0]]}, 1) is None
+    even = [[0.0, 50.0, 51.0], [49.0, 0.0, 50.0], [50.0, 52.0, 0.0]]
+    uni = {"matrix_gbs": [[0.0, 48.0, 48.0], [48.0, 0.0, 48.0], [48.0, 48.0, 0.0]]}
+    bi = {"matrix_gbs": [[0.0, 96.0, 96.0], [96.0, 0.0, 96.0], [96.0, 96.0, 0.0]]}
+    r = {"matrix_gbs": even, "pair_serial_events": {"uni": uni, "bi": bi}, "link_check": None, "unparsed_peers": []}
+    assert bench_fabric_findings(r, 3) == []
+    slow = dict(r, matrix_gbs=[[0.0, 50.0, 51.0], [49.0, 0.0, 50.0], [50.0, 12.0, 0.0]])
+    assert bench_fabric_findings(slow, 3) == ["tournament matrix_gbs: cell 2->1 12.00 < 0.50 x median 50.00"]
+    # The reference's method stands in when our serial run failed or is missing.
+    low_bi = {"matrix_gbs": [[0.0, 40.0, 96.0], [96.0, 0.0, 96.0], [96.0, 96.0, 0.0]]}
+    ref = dict(r, pair_serial_events={"error": "x"}, reference_semantics={"uni": uni, "bi": low_bi})
+    assert bench_fabric_findings(ref, 3) == ["compat bi cell 0<->1 40.00 below its uni cell 48.00"]

@@ -66,6 +66,7 @@ def test_bench_cpu_two_ranks(native):
     assert [d["rank"] for d in prov["rank_devices"]] == [0, 1] and len(prov["rank_links"]) == 2
     assert r["extras"]["ring_hop"]["hop_us_p50"] > 0 and r["matrix_samples"] == [[0, 4], [4, 0]]
     assert r["xgmi_pair_sweep"] is None  # auto: only at N = 2 on two distinct GPUs
+    assert isinstance(r["fabric_findings"], list) and r["unparsed_peers"] is None  # (host transport: no RCCL log)
 
 
 @pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
