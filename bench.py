@@ -115,9 +115,9 @@ core.set_start(T0)
 from test_nccl_p2p_amd.bench.compare import child_main, steps_through  # noqa: E402,F401
 from test_nccl_p2p_amd.bench.core import (METRIC, Deadline, Reporter, Timeline, bench_fabric_findings,  # noqa: E402,F401
                                           candidate_budget, cell_matrix, claim_stdout, default_device,
-                                          first_candidate_budget, first_comms, free_port, headline_stats, link_check,
-                                          log, pick_depth, posting_candidates, process_age, start_watchdog,
-                                          tuning_steps)
+                                          first_candidate_budget, first_comms, free_port, hang_requested,
+                                          headline_stats, link_check, log, pick_depth, posting_candidates,
+                                          process_age, start_watchdog, tuning_steps)
 from test_nccl_p2p_amd.bench.headline import HeadlineMixin  # noqa: E402
 from test_nccl_p2p_amd.bench.sections import SectionsMixin  # noqa: E402
 
@@ -325,10 +325,21 @@ class BenchRun(HeadlineMixin, SectionsMixin):
                 log("  " + " ".join("%8.2f" % h.matrix[r][c] for c in range(self.n)))
         self.reporter.emit()
         # The watchdog stays armed: should the teardown below hang, it ends the
-        # process at the deadline (the line is out already, so it exits 0).
-        self.barrier()
-        if self.n > 1 and dist.is_initialized():
-            dist.destroy_process_group()
+        # process at the deadline (the line is out already, so it exits 0).  A
+        # peer whose watchdog ended it first breaks this barrier; that is no
+        # error of the measurement either.
+        self.timeline.begin("teardown")
+        if hang_requested("teardown", self.env.rank):
+            # Test hook: this rank ends here, as a rank whose watchdog fired a
+            # little earlier than the others' (its process started earlier).
+            log("bench: injected exit in the teardown on rank %d" % self.env.rank)
+            os._exit(0)
+        try:
+            self.barrier()
+            if self.n > 1 and dist.is_initialized():
+                dist.destroy_process_group()
+        except Exception as e:  # noqa: BLE001 -- the line is out
+            log("bench: teardown: %s (the result line is out)" % str(e)[:200])
         # The timeline ends at the JSON line; this is the whole process (a
         # test holds the timeline's total against it).
         self.log0("bench: process wall %.3f s" % process_age())

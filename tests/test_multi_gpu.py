@@ -22,7 +22,7 @@ import sys
 
 import pytest
 
-from conftest import MPIRUN, PERF_RECORDS, ROOT, ensure_built, free_port
+from conftest import MPIRUN, PERF_RECORDS, ROOT, ensure_built, free_port, run_logged
 from test_nccl_p2p_amd.utils.report import fabric_findings, offdiag, parse_compat
 
 
@@ -146,9 +146,13 @@ def test_bench_all_gpus():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
            "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", str(n), "--steps", "14",
            "--warmup", "7", "--deadline", "80", "--sweep-max", "256M", "--timeout", "45"] + BENCH_MSGS + ISOLATE
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=BUDGET_S["test_bench_all_gpus"], cwd=ROOT)
-    assert out.returncode == 0, out.stderr[-3000:]
-    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    out = run_logged(cmd, BUDGET_S["test_bench_all_gpus"], "bench_all_gpus", cwd=ROOT)
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    r = json.loads(lines[0]) if lines else {}
+    progress = "\n".join(l for l in out.stderr.splitlines() if "bench:" in l or "fatal" in l or "Error" in l
+                         or "Traceback" in l or "exitcode" in l)
+    assert out.returncode == 0, (progress[-3000:], {k: r.get(k) for k in ("deadline_hit", "section_errors",
+                                                                          "untimed_skipped", "verify_mismatches")})
     _keep("bench", {k: r.get(k) for k in ("matrix_gbs", "link_check", "unparsed_peers", "matrix_transport", "value",
                                           "aggregate_gbs", "timeline_s", "posting")})
     assert r["n_gpus"] == n and r["verify_mismatches"] == 0 and r["value"] > 0

@@ -230,6 +230,21 @@ def test_bench_deadline_aborts_inside_and_outside_the_engine(native):
         out.stderr[-3000:]
 
 
+def test_bench_teardown_after_the_line_never_fails_the_run(native):
+    """A rank that ends during the teardown (its watchdog fired a little
+    before the others': its process started earlier) breaks their final
+    barrier; the line is out by then, so every rank still exits 0 (the
+    8-rank rehearsal exited 1, profiles/r5_reh8b/)."""
+    args = ["bench.py", "--gpus", "2", "--steps", "3", "--warmup", "2", "--transport", "host", "--size", "64K",
+            "--msgs", "2", "--latency-iters", "10", "--sweep", "0", "--extras", "0", "--ref-iters", "0",
+            "--ipc-extra", "0", "--deadline", "25"]
+    out = torchrun(2, args, env={"P2P_BENCH_HANG": "teardown@1"}, timeout=120)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and json.loads(lines[0])["value"] > 0, out.stdout[-2000:]
+    assert "injected exit in the teardown on rank 1" in out.stderr
+
+
 def test_fuzz_session_over_shm_and_host(native):
     """Random verified message groups, 3 processes, over the shared-memory and
     TCP transports through the Python session."""
