@@ -190,7 +190,17 @@ class SectionsMixin:
             for d in dirs:
                 left = self.slice_remaining() / (len(dirs) - len(out))
                 fit = int((left / cells - 0.01) / per_iter) - warmup
-                iters = int(self.agreed_min(min(args.ref_iters, max(min(8, args.ref_iters), fit))))
+                # The fewest iterations a matrix is worth (8) must fit too: at
+                # a slow link rate the minimum alone can take many times the
+                # slice (8 ranks over loopback sockets: 88 s in a 6 s slice,
+                # the deadline hit, profiles/r5_reh8c/).  Agreed on every rank.
+                least = min(8, args.ref_iters)
+                need = cells * ((warmup + least) * per_iter + 0.01)
+                if not self.agree(need <= 1.5 * left):
+                    out[d] = {"skipped": "the fewest iterations (%d + %d warmup) would take ~%.1f s, %.1f s left"
+                                         % (least, warmup, need, left)}
+                    break
+                iters = int(self.agreed_min(min(args.ref_iters, max(least, fit))))
                 t0 = time.monotonic()
                 r = json.loads(session.run(mode="pair" if n > 1 else "self", dir=d, bytes=self.size, iters=iters,
                                            warmup=warmup, timing=timing, verify=verify, warm=warmup > 0))
@@ -203,7 +213,7 @@ class SectionsMixin:
 
         def reference_semantics():
             out = matrices(h.ref_sess or h.sess, "wallclock", 0, False, 4.0)
-            uni = out["uni"]["gbs_mean"]
+            uni = (out.get("uni") or {}).get("gbs_mean")
             return dict(out, size=self.size, comms=1,
                         method="reference semantics: serial ordered pairs, wall clock, stream sync per message, no "
                                "warmup" + ("" if n > 1 else " (applied to the self cell)"),
@@ -222,7 +232,7 @@ class SectionsMixin:
             # stock RCCL / HIP settings: the headline's process runs RCCL's
             # kernels at unroll 4, 8 HW queues and RCCL's INFO log, which the
             # reference's stock setup would not.
-            iters = {d: v["iters"] for d, v in ref.items() if d in dirs and isinstance(v, dict)}
+            iters = {d: v["iters"] for d, v in ref.items() if d in dirs and isinstance(v, dict) and "iters" in v}
             r = self.child_job(REF_STOCK, ["--child-ref-iters", json.dumps(iters), "--hw-queues", "0"],
                                env=stock_env())
             if r is None or "error" in r:
