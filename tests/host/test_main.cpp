@@ -1034,6 +1034,29 @@ TEST(test_link_transport_mismatch) {
   EXPECT(!link_transport_mismatch("n/a", "NET"));
 }
 
+TEST(test_abort_if_idle_waits_for_native_calls) {
+  // the watchdog aborts the communicators itself only when no
+  // engine call is open, then takes no more calls.  (Closes the engine for
+  // the rest of this process: the last test.)
+  int ran = 0;
+  push_abort_hook([&ran](int) { ++ran; });
+  {
+    NativeCall in_engine;
+    EXPECT(!abort_if_idle() && ran == 0 && !abort_done());
+  }
+  EXPECT(abort_if_idle() && ran == 1 && abort_done());
+  set_throw_on_fatal(true);
+  bool refused = false;
+  try {
+    NativeCall late;
+  } catch (const Error& e) {
+    refused = std::string(e.what()).find("aborted") != std::string::npos;
+  }
+  set_throw_on_fatal(false);
+  EXPECT(refused);
+  EXPECT(abort_if_idle() && ran == 1);  // the hooks ran once
+}
+
 int main(int argc, char** argv) {
   const char* only = argc > 1 ? argv[1] : nullptr;
   int ran = 0;
