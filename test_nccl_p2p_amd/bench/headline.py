@@ -450,6 +450,7 @@ class HeadlineMixin:
             "p50_latency_preposted_us": None,
             "latency_preposted_p50_us_matrix": None,
             "latency_bytes": nat.parse_size(args.latency_size),
+            "latency_iters": None,
             "per_gpu_gbs": round(h.aggregate / n, 3),
             "rank0_step_ms_p50": round(statistics.median(h.my_ms) if h.my_ms else 0.0, 4),
             # Every timed step's GPU time on rank 0, and what the wall-clock

@@ -138,16 +138,28 @@ class SectionsMixin:
         nbytes = self.nat.parse_size(args.latency_size)
 
         def ping(preposted):
+            # Exchanges that fit the section's slice: a short calibration pass
+            # first (on xGMI a few ms; 8 ranks over loopback sockets took 18 s
+            # for the full 300, profiles/r5_reh8/), agreed on every rank.
+            iters = args.latency_iters
+            if iters > 20:
+                t0 = time.monotonic()
+                sess.latency(nbytes, 10, 2, preposted)
+                per = max(1e-6, (time.monotonic() - t0) / 12)
+                fit = int(self.slice_remaining() / per) - min(50, iters)
+                iters = int(self.agreed_min(max(20, min(iters, fit))))
             m = [[0.0] * n for _ in range(n)]
-            lat = json.loads(sess.latency(nbytes, args.latency_iters, min(50, args.latency_iters), preposted))
+            lat = json.loads(sess.latency(nbytes, iters, min(50, iters), preposted))
             for p in lat["pairs"]:  # a < b; the ping-pong's one-way time holds for both directions
                 m[p["a"]][p["b"]] = m[p["b"]][p["a"]] = round(p["one_way_us"]["p50"], 3)
             p50s = [p["one_way_us"]["p50"] for p in lat["pairs"]]
-            return {"p50": float(statistics.median(p50s)) if p50s else None, "matrix": m, "method": lat["method"]}
+            return {"p50": float(statistics.median(p50s)) if p50s else None, "matrix": m, "method": lat["method"],
+                    "iters": iters}
 
         r = self.section("latency", lambda: ping(0), budgeted=False)
         if isinstance(r, dict) and r.get("p50") is not None:
-            self.reporter.update(p50_latency_us=round(r["p50"], 3), latency_p50_us_matrix=r["matrix"])
+            self.reporter.update(p50_latency_us=round(r["p50"], 3), latency_p50_us_matrix=r["matrix"],
+                                 latency_iters=r["iters"])
         if args.latency_preposted > 0:
             r = self.section("latency_preposted", lambda: ping(args.latency_preposted), budgeted=False)
             if isinstance(r, dict) and r.get("p50") is not None and r.get("method") == "preposted":
