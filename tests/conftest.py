@@ -102,24 +102,26 @@ def pytest_runtest_setup(item):
 
 def run_logged(cmd, timeout, name="child", **kw):
     """subprocess.run(cmd, capture_output=True, text=True, timeout=...) whose
-    stderr also lands, as it is written, in $P2P_TEST_LOG_DIR/<name>.log when
-    that is set (the GPU sessions set it under gpurun_out/): a long bench run
-    inside a test shows its progress there instead of looking silent."""
+    stderr and stdout also land, as they are written, in
+    $P2P_TEST_LOG_DIR/<name>.log and <name>.out when that is set (the GPU
+    sessions set it under gpurun_out/): a long run inside a test shows its
+    progress there instead of looking silent."""
     log_dir = os.environ.get("P2P_TEST_LOG_DIR")
     if not log_dir:
         return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, **kw)
     os.makedirs(log_dir, exist_ok=True)
-    path = os.path.join(log_dir, "%s.log" % name)
-    with open(path, "w") as err:
-        proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=err, text=True, **kw)
+    err_path = os.path.join(log_dir, "%s.log" % name)
+    out_path = os.path.join(log_dir, "%s.out" % name)
+    with open(err_path, "w") as err, open(out_path, "w") as out:
+        proc = subprocess.Popen(cmd, stdout=out, stderr=err, text=True, **kw)
         try:
-            out, _ = proc.communicate(timeout=timeout)
+            proc.wait(timeout=timeout)
         except subprocess.TimeoutExpired:
             proc.kill()
-            proc.communicate()
+            proc.wait()
             raise
-    with open(path) as f:
-        return subprocess.CompletedProcess(cmd, proc.returncode, out, f.read())
+    with open(err_path) as fe, open(out_path) as fo:
+        return subprocess.CompletedProcess(cmd, proc.returncode, fo.read(), fe.read())
 
 
 def ensure_built(target: str) -> None:

@@ -17,7 +17,6 @@ then the concurrent modes, bench.py, the hand-written data plane and the
 fuzzers."""
 import json
 import os
-import subprocess
 import sys
 
 import pytest
@@ -106,9 +105,9 @@ def test_reference_matrix_all_gpus(exe, tmp_path):
     xGMI link carried by anything but RCCL's P2P transport fails."""
     n = _n()
     js = tmp_path / "r.json"
-    out = subprocess.run([MPIRUN, "-n", str(n), exe, "--verify", "-n", "16", "--json", str(js), "--timeout", "45",
-                          "--min-gbs", MIN_GBS], capture_output=True, text=True,
-                         timeout=BUDGET_S["test_reference_matrix_all_gpus"] * (2 if REHEARSAL >= 8 else 1))
+    out = run_logged([MPIRUN, "-n", str(n), exe, "--verify", "-n", "16", "--json", str(js), "--timeout", "45",
+                      "--min-gbs", MIN_GBS], BUDGET_S["test_reference_matrix_all_gpus"] * (2 if REHEARSAL >= 8 else 1),
+                     "reference_matrix_all_gpus")
     assert out.returncode == 0, out.stderr[-3000:]
     m = parse_compat(out.stdout)
     for key in ("uni", "bi"):
@@ -133,10 +132,11 @@ def test_concurrent_modes_all_gpus(exe):
     synchronised only around buffer work)."""
     n = _n()
     for comms in ("1", "4"):
-        out = subprocess.run([MPIRUN, "-n", str(n), exe, "--comms", comms, "--mode", "tournament,ring,allpairs",
-                              "--sizes", CONCURRENT_SIZES, "-n", "8", "--verify", "--latency", "--no-compat", "--timeout",
-                              "60" if CONCURRENT_TIMEOUT_S else "20"], capture_output=True, text=True,
-                             timeout=CONCURRENT_TIMEOUT_S or BUDGET_S["test_concurrent_modes_all_gpus"] / 2)
+        out = run_logged([MPIRUN, "-n", str(n), exe, "--comms", comms, "--mode", "tournament,ring,allpairs",
+                          "--sizes", CONCURRENT_SIZES, "-n", "8", "--verify", "--latency", "--no-compat", "--timeout",
+                          "60" if CONCURRENT_TIMEOUT_S else "20"],
+                         CONCURRENT_TIMEOUT_S or BUDGET_S["test_concurrent_modes_all_gpus"] / 2,
+                         "concurrent_modes_comms%s" % comms)
         assert out.returncode == 0, out.stderr[-3000:]
         assert "verification: OK" in out.stdout and "FAILED" not in out.stdout
 
@@ -169,10 +169,10 @@ def test_ipc_engines_all_gpus(exe):
     n = _n()
     for engine in ("kernel", "push", "relay"):
         modes = "tournament,allpairs,pair" if engine == "relay" else "tournament,allpairs"
-        out = subprocess.run([MPIRUN, "-n", str(n), exe, "--transport", "ipc", "--ipc-engine", engine,
-                              "--mode", modes, "--sizes", "1M,64M", "-n", "4", "--verify",
-                              "--device-latency", "--latency-iters", "200", "--no-compat", "--timeout", "15"],
-                             capture_output=True, text=True, timeout=BUDGET_S["test_ipc_engines_all_gpus"] / 3)
+        out = run_logged([MPIRUN, "-n", str(n), exe, "--transport", "ipc", "--ipc-engine", engine,
+                          "--mode", modes, "--sizes", "1M,64M", "-n", "4", "--verify",
+                          "--device-latency", "--latency-iters", "200", "--no-compat", "--timeout", "15"],
+                         BUDGET_S["test_ipc_engines_all_gpus"] / 3, "ipc_engines_%s" % engine)
         assert out.returncode == 0, (engine, out.stderr[-3000:])
         assert "verification: OK" in out.stdout and "FAILED" not in out.stdout
         assert "device-initiated ping-pong" in out.stdout
@@ -185,7 +185,7 @@ def test_fuzz_all_gpus():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "tests/scripts/fuzz_session.py",
            "rccl:4", "20"]
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=BUDGET_S["test_fuzz_all_gpus"], cwd=ROOT)
+    out = run_logged(cmd, BUDGET_S["test_fuzz_all_gpus"], "fuzz_all_gpus", cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     assert "FUZZ rccl:4 mismatches 0" in out.stdout
 
@@ -195,9 +195,9 @@ def test_cli_fuzz_relay_all_gpus(exe):
     """p2p_matrix --fuzz across every GPU over the relay engine, whose stripes
     cross third GPUs: random groups (random pairs incl. self, 1 B .. 16 MiB)."""
     n = _n()
-    out = subprocess.run([MPIRUN, "-n", str(n), exe, "--transport", "ipc", "--ipc-engine", "relay", "--mode", "pair",
-                          "--size", "16M", "-n", "2", "--fuzz", "30", "--no-compat", "--timeout", "25"],
-                         capture_output=True, text=True, timeout=BUDGET_S["test_cli_fuzz_relay_all_gpus"])
+    out = run_logged([MPIRUN, "-n", str(n), exe, "--transport", "ipc", "--ipc-engine", "relay", "--mode", "pair",
+                      "--size", "16M", "-n", "2", "--fuzz", "30", "--no-compat", "--timeout", "25"],
+                     BUDGET_S["test_cli_fuzz_relay_all_gpus"], "cli_fuzz_relay_all_gpus")
     assert out.returncode == 0, out.stderr[-3000:]
     assert "all verified" in out.stdout
 
@@ -213,8 +213,7 @@ def test_bench_two_gpus_pair_sweep():
            "--deadline", "75", "--xgmi-sweep-sizes", "32M", "--ipc-extra", "0", "--extras", "0", "--sweep", "0",
            "--ref-iters", "0", "--latency-preposted", "0", "--latency-iters", "50",
            "--timeout", "45"] + BENCH_MSGS + (["--xgmi-sweep", "1"] if REHEARSAL else [])
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=BUDGET_S["test_bench_two_gpus_pair_sweep"],
-                         cwd=ROOT)
+    out = run_logged(cmd, BUDGET_S["test_bench_two_gpus_pair_sweep"], "bench_two_gpus_pair_sweep", cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     sw = r["xgmi_pair_sweep"]
