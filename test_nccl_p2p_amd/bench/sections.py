@@ -282,6 +282,15 @@ class SectionsMixin:
             return
 
         def concurrent_config(mode_x, dir_x, nbytes, iters):
+            # Iterations the slice holds, at the headline's per-flow rate with
+            # every rank's flows sharing it (a rank sends to up to N - 1 peers
+            # at once): on xGMI a few ms each; over 8 loopback ranks an
+            # all-pairs iteration at 1 GiB took ~4 s (profiles/r5_reh8d/).
+            # At least one; agreed on every rank.
+            flows = (n - 1) if mode_x == "allpairs" else 1
+            per_iter = flows * nbytes / (max(h.value or 1.0, 1e-3) * 1e9) + 0.01
+            fit = int(self.slice_remaining() / per_iter) - 1
+            iters = int(self.agreed_min(max(1, min(iters, fit))))
             r = json.loads(h.sess.run(mode=mode_x, dir=dir_x, bytes=nbytes, iters=iters, warmup=1, timing="events",
                                       verify=not args.no_verify, warm=True))
             ph = r["phases"][0]
