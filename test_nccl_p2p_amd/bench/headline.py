@@ -93,13 +93,8 @@ class HeadlineMixin:
         # slot, up to this much memory per rank (ranks sharing a GPU split it).
         budget = self.recv_budget(provenance)
 
-        # ---- posting selection: whole untimed laps of the schedule per
-        # candidate (one group per step vs one per message; RCCL: one
-        # communicator vs several whose send/recv kernels run side by side,
-        # posting_candidates), timed by the slowest rank, before the W warmup
-        # steps of the chosen one.  Every wait of a candidate is bounded by its
-        # budget (first_candidate_budget / candidate_budget), so one that hangs
-        # on some rank is dropped on every rank in seconds, not at --timeout.
+        # ---- posting selection (select_posting), before the W warmup steps
+        # of the chosen candidate.
         self.state["section"] = "tuning"
         choices = posting_candidates(transport, args.comms, args.batch, n, hw_queues=hw_queues())
         c0 = first_comms(transport, args.comms)
@@ -113,115 +108,9 @@ class HeadlineMixin:
                 sessions[c].set_timeout(timeout_s)
             return sessions[c]
 
-        tuning, tuning_passes, failed, skipped, budgets = {}, {}, {}, {}, {}
         phases = len(nat.schedule(mode, "bi", n))
-        tune_k = tuning_steps(phases) * args.tune_laps
-        first_cost = None
-        if args.tune_laps > 0 and len(choices) > 1:
-            tuning_t0 = time.monotonic()
-            tuning_cap = TUNING_SHARE * max(0.0, self.deadline.left() - RESERVE_S)
-            for i, (c, b) in enumerate(choices):
-                key = "comms%d_%s" % (c, "batch" if b else "per_message")
-                # The headline session's first candidate must work; anything else
-                # (another communicator count, another posting) may be dropped.
-                droppable = i > 0 or c != c0
-                if droppable and first_cost is not None:
-                    wait_s = candidate_budget(first_cost, self.deadline.left() - RESERVE_S, args.timeout)
-                    used = time.monotonic() - tuning_t0
-                    if not self.agree(wait_s >= 1.0 and used + wait_s <= tuning_cap):
-                        skipped[key] = "no time left: budget %.1f s, tuning used %.1f of %.1f s" % (
-                            wait_s, used, tuning_cap)
-                        self.log0("bench: posting candidate %s skipped: %s" % ((c, b), skipped[key]))
-                        continue
-                else:
-                    wait_s = first_budget
-                budgets[key] = round(wait_s, 2)
-                d, err, connect_s = None, None, 0.0
-                hang = candidate_hang(transport, c, b, self.env.rank)
-                t_phase = time.monotonic()
-                tl.begin("%stuning/%s/init" % (pre, key))
-                try:
-                    s_c = session_for(c, wait_s)
-                    tl.begin("%stuning/%s/connect" % (pre, key))
-                    t_conn = time.monotonic()
-                    if hang == "connect":
-                        emulate_hang(wait_s)
-                    d = nat.StepDriver(s_c, mode, "bi", size, args.msgs, False, bool(b), bool(args.graph))
-                    d.connect()
-                    connect_s = time.monotonic() - t_conn
-                    # Test hook: P2P_BENCH_FAIL_CANDIDATE="<comms>,<batch>" fails
-                    # that candidate on the last rank only.
-                    if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d" % (c, b) and self.env.rank == n - 1:
-                        raise RuntimeError("injected candidate failure")
-                except Exception as e:  # noqa: BLE001 -- reported, and the candidate is skipped everywhere
-                    err = str(e)[:200]
-                if self.agree(err is None):
-                    # --tune-passes timed passes back to back; the fastest counts.
-                    # The first pass carries the candidate's first-use costs, and
-                    # one short pass is noisy: with a single 4-step pass, 2 of 16
-                    # one-GPU runs picked 4 communicators over 8 and lost 15%
-                    # (profiles/r3b_nt_ab/).
-                    passes = []
-                    for p in range(max(1, args.tune_passes)):
-                        self.barrier()
-                        tl.begin("%stuning/%s/pass%d" % (pre, key, p))
-                        t_phase = time.monotonic()
-                        w0 = time.perf_counter()
-                        try:
-                            if p == 0 and hang == "unbounded":
-                                s_c.set_timeout(3600.0)
-                            elif p == 0 and hang in ("tuning", "stall"):
-                                emulate_hang(wait_s, hang)
-                            d.run_steps(0, tune_k)
-                            d.sync()
-                            if (os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d,tuning" % (c, b)
-                                    and self.env.rank == n - 1):
-                                raise RuntimeError("injected tuning failure")
-                        except Exception as e:  # noqa: BLE001 -- same agreement as above
-                            err = str(e)[:200]
-                        w = time.perf_counter() - w0
-                        if not self.agree(err is None):
-                            # Failed on some rank: dropped on every rank alike.
-                            err = err or "failed on another rank"
-                            break
-                        passes.append(self.allmax(w) / tune_k)
-                    if err is None:
-                        tuning[(c, b)] = min(passes)
-                        tuning_passes[(c, b)] = passes
-                        if first_cost is None:
-                            first_cost = self.allmax(connect_s) + min(passes) * tune_k
-                        del d
-                        # Only the best communicator count so far, the headline
-                        # session and the single communicator (kept for the
-                        # reference-method comparison) stay open.
-                        best_c = min(tuning, key=tuning.get)[0]
-                        for cc in [cc for cc in sessions if cc not in (c0, 1, best_c)]:
-                            if not any(cc == c2 for (c2, _) in choices[i + 1:]):
-                                del sessions[cc]
-                        continue
-                # Failed (on every rank alike).  A wait that ran out its budget
-                # on the slowest rank is reported as a timeout.
-                tl.begin("%stuning/%s/dropped" % (pre, key))
-                timed_out = self.allmax(time.monotonic() - t_phase) >= 0.9 * wait_s
-                err = err or "failed on another rank"
-                if timed_out:
-                    err = "timed out (waits bounded at %.1f s): %s" % (wait_s, err)
-                if not droppable:
-                    raise RuntimeError("first posting candidate %s: %s" % (key, err))
-                failed[key] = err
-                self.log0("bench: posting candidate %s dropped: %s" % ((c, b), failed[key]))
-                del d
-                # Its session may be out of step across ranks (an aborted
-                # communicator, a transfer cut off mid-message): closed on every
-                # rank, and opened afresh should the headline need it.
-                sessions.pop(c, None)
-            comms, batch = min(tuning, key=tuning.get)
-            reason = "fastest of %d candidate(s): best of %d pass(es) of %d untimed step(s) each (%s lap(s) of %d " \
-                     "round(s)), slowest rank's clock" % (len(tuning), max(1, args.tune_passes), tune_k, args.tune_laps,
-                                                         phases)
-        else:
-            comms, batch = choices[0]
-            reason = "single candidate" if len(choices) == 1 else "no tuning laps (--tune-laps 0): first candidate"
+        sel = self.select_posting(transport, choices, c0, sessions, session_for, first_budget, phases, pre)
+        comms, batch = sel.comms, sel.batch
         tl.begin(pre + "headline/session")
         sess = session_for(comms, args.timeout)
         # A single-communicator session stays for the reference-method comparison
@@ -295,11 +184,129 @@ class HeadlineMixin:
         del drv
         return types.SimpleNamespace(
             sess=sess, ref_sess=ref_sess, sessions=sessions, provenance=provenance, comms=comms, batch=batch,
-            failed=failed, skipped=skipped, budgets=budgets, first_cost=first_cost, reason=reason, tuning=tuning, tuning_passes=tuning_passes, elapsed=elapsed, flows_total=flows_total, value=value,
+            failed=sel.failed, skipped=sel.skipped, budgets=sel.budgets, first_cost=sel.first_cost, reason=sel.reason,
+            tuning=sel.tuning, tuning_passes=sel.tuning_passes, elapsed=elapsed, flows_total=flows_total, value=value,
             aggregate=aggregate, my_ms=my_ms, matrix=matrix, samples=samples, cells=cells, offdiag=offdiag,
             expected=n * (n - 1) if n > 1 else 1, vr=vr, mismatches=vr["mismatches"] if vr else -1, depth=depth,
             recv_bytes=recv_bytes, chunking=chunking, rccl_peers=rccl_peers, matrix_transport=matrix_transport,
             host_post_ms=(t_posted - t0) * 1e3, post_ms=post_ms)
+
+    def select_posting(self, transport, choices, c0, sessions, session_for, first_budget, phases, pre):
+        """Posting selection: whole untimed laps of the schedule per candidate
+        (one group per step vs one per message; RCCL: one communicator vs
+        several whose send/recv kernels run side by side, posting_candidates),
+        timed by the slowest rank.  Every wait of a candidate is bounded by its
+        budget (first_candidate_budget / candidate_budget), so one that hangs
+        on some rank is dropped on every rank in seconds, not at --timeout; the
+        first candidate (the headline session's) must work, or this raises.
+        `sessions` (communicator count -> session) is pruned as it goes."""
+        args = self.args
+        out = types.SimpleNamespace(tuning={}, tuning_passes={}, failed={}, skipped={}, budgets={}, first_cost=None)
+        tune_k = tuning_steps(phases) * args.tune_laps
+        if args.tune_laps <= 0 or len(choices) == 1:
+            out.comms, out.batch = choices[0]
+            out.reason = "single candidate" if len(choices) == 1 else "no tuning laps (--tune-laps 0): first candidate"
+            return out
+        tuning_t0 = time.monotonic()
+        tuning_cap = TUNING_SHARE * max(0.0, self.deadline.left() - RESERVE_S)
+        for i, (c, b) in enumerate(choices):
+            key = "comms%d_%s" % (c, "batch" if b else "per_message")
+            droppable = i > 0 or c != c0
+            if droppable and out.first_cost is not None:
+                wait_s = candidate_budget(out.first_cost, self.deadline.left() - RESERVE_S, args.timeout)
+                used = time.monotonic() - tuning_t0
+                if not self.agree(wait_s >= 1.0 and used + wait_s <= tuning_cap):
+                    out.skipped[key] = "no time left: budget %.1f s, tuning used %.1f of %.1f s" % (
+                        wait_s, used, tuning_cap)
+                    self.log0("bench: posting candidate %s skipped: %s" % ((c, b), out.skipped[key]))
+                    continue
+            else:
+                wait_s = first_budget
+            out.budgets[key] = round(wait_s, 2)
+            passes, connect_s, err, t_phase = self.try_candidate(transport, c, b, key, wait_s, session_for, tune_k, pre)
+            if err is None:
+                out.tuning[(c, b)] = min(passes)
+                out.tuning_passes[(c, b)] = passes
+                if out.first_cost is None:
+                    out.first_cost = self.allmax(connect_s) + min(passes) * tune_k
+                # Only the best communicator count so far, the headline session
+                # and the single communicator (kept for the reference-method
+                # comparison) stay open.
+                best_c = min(out.tuning, key=out.tuning.get)[0]
+                for cc in [cc for cc in sessions if cc not in (c0, 1, best_c)]:
+                    if not any(cc == c2 for (c2, _) in choices[i + 1:]):
+                        del sessions[cc]
+                continue
+            # Failed (on every rank alike).  A wait that ran out its budget on
+            # the slowest rank is reported as a timeout.
+            self.timeline.begin("%stuning/%s/dropped" % (pre, key))
+            if self.allmax(time.monotonic() - t_phase) >= 0.9 * wait_s:
+                err = "timed out (waits bounded at %.1f s): %s" % (wait_s, err)
+            if not droppable:
+                raise RuntimeError("first posting candidate %s: %s" % (key, err))
+            out.failed[key] = err
+            self.log0("bench: posting candidate %s dropped: %s" % ((c, b), err))
+            # Its session may be out of step across ranks (an aborted
+            # communicator, a transfer cut off mid-message): closed on every
+            # rank, and opened afresh should the headline need it.
+            sessions.pop(c, None)
+        out.comms, out.batch = min(out.tuning, key=out.tuning.get)
+        out.reason = ("fastest of %d candidate(s): best of %d pass(es) of %d untimed step(s) each (%s lap(s) of %d "
+                      "round(s)), slowest rank's clock" % (len(out.tuning), max(1, args.tune_passes), tune_k,
+                                                          args.tune_laps, phases))
+        return out
+
+    def try_candidate(self, transport, c, b, key, wait_s, session_for, tune_k, pre):
+        """One posting candidate (c communicators, batch b) on every rank: its
+        session (waits bounded at wait_s), connect, then --tune-passes timed
+        passes back to back, the fastest counting: the first pass carries the
+        candidate's first-use costs, and one short pass is noisy (with a
+        single 4-step pass, 2 of 16 one-GPU runs picked 4 communicators over 8
+        and lost 15%, profiles/r3b_nt_ab/).  Every outcome is agreed on every
+        rank.  Returns (seconds per step of each pass, connect seconds, error
+        or None, when the failing phase began)."""
+        args, nat, n, tl = self.args, self.nat, self.n, self.timeline
+        d, err, connect_s, passes = None, None, 0.0, []
+        hang = candidate_hang(transport, c, b, self.env.rank)
+        t_phase = time.monotonic()
+        tl.begin("%stuning/%s/init" % (pre, key))
+        try:
+            s_c = session_for(c, wait_s)
+            tl.begin("%stuning/%s/connect" % (pre, key))
+            if hang == "connect":
+                emulate_hang(wait_s)
+            d = nat.StepDriver(s_c, self.mode, "bi", self.size, args.msgs, False, bool(b), bool(args.graph))
+            d.connect()
+            connect_s = time.monotonic() - t_phase
+            # Test hook: P2P_BENCH_FAIL_CANDIDATE="<comms>,<batch>" fails that
+            # candidate on the last rank only.
+            if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d" % (c, b) and self.env.rank == n - 1:
+                raise RuntimeError("injected candidate failure")
+        except Exception as e:  # noqa: BLE001 -- reported, and the candidate is skipped everywhere
+            err = str(e)[:200]
+        if not self.agree(err is None):
+            return passes, connect_s, err or "failed on another rank", t_phase
+        for p in range(max(1, args.tune_passes)):
+            self.barrier()
+            tl.begin("%stuning/%s/pass%d" % (pre, key, p))
+            t_phase = time.monotonic()
+            w0 = time.perf_counter()
+            try:
+                if p == 0 and hang == "unbounded":
+                    s_c.set_timeout(3600.0)
+                elif p == 0 and hang in ("tuning", "stall"):
+                    emulate_hang(wait_s, hang)
+                d.run_steps(0, tune_k)
+                d.sync()
+                if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d,tuning" % (c, b) and self.env.rank == n - 1:
+                    raise RuntimeError("injected tuning failure")
+            except Exception as e:  # noqa: BLE001 -- same agreement as above
+                err = str(e)[:200]
+            w = time.perf_counter() - w0
+            if not self.agree(err is None):
+                return passes, connect_s, err or "failed on another rank", t_phase
+            passes.append(self.allmax(w) / tune_k)
+        return passes, connect_s, None, t_phase
 
     def verify_warmup(self, drv, sessions):
         """RCCL 2.26 / 2.27 deliver only the first half of an op whose share
