@@ -518,6 +518,7 @@ void write_reports(const AppConfig& cfg, const Transport& t, const Bootstrap& bo
     if (t.name() != "host" && t.name() != "shm") std::fprintf(out, "%s", topology_report().c_str());
     print_transport_matrix(out, res, n);
     for (const auto& rec : res.runs) print_extended(out, rec, n);
+    print_fabric_check(out, res.runs, n);
     print_latency(out, res.latency, n);
     print_latency(out, res.preposted_latency, n);
     print_latency(out, res.device_latency, n);

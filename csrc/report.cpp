@@ -75,6 +75,56 @@ void print_matrix(FILE* out, const std::string& title, const std::vector<double>
   }
 }
 
+std::vector<std::string> fabric_findings(const std::vector<double>& uni, const std::vector<double>* bi, int n,
+                                         double min_ratio) {
+  std::vector<std::string> out;
+  std::vector<double> cells;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j)
+      if (i != j && uni[static_cast<size_t>(i) * n + j] > 0) cells.push_back(uni[static_cast<size_t>(i) * n + j]);
+  if (cells.size() >= 2) {
+    std::sort(cells.begin(), cells.end());
+    const size_t h = cells.size() / 2;
+    const double med = cells.size() % 2 ? cells[h] : 0.5 * (cells[h - 1] + cells[h]);
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) {
+        const double v = uni[static_cast<size_t>(i) * n + j];
+        if (i != j && v > 0 && v < min_ratio * med)
+          out.push_back(strfmt("cell %d->%d %.2f GB/s < %.2f x median %.2f", i, j, v, min_ratio, med));
+      }
+  }
+  if (bi)
+    for (int i = 0; i < n; ++i)
+      for (int j = i + 1; j < n; ++j) {
+        const double total = (*bi)[static_cast<size_t>(i) * n + j] + (*bi)[static_cast<size_t>(j) * n + i];
+        for (const auto& [a, b] : {std::pair<int, int>{i, j}, std::pair<int, int>{j, i}}) {
+          const double u = uni[static_cast<size_t>(a) * n + b];
+          if (total > 0 && u > 0 && total < u)
+            out.push_back(strfmt("pair %d<->%d both directions %.2f GB/s < its uni cell %d->%d %.2f", i, j, total, a,
+                                 b, u));
+        }
+      }
+  return out;
+}
+
+void print_fabric_check(FILE* out, const std::vector<RunRecord>& runs, int n) {
+  if (n < 2) return;
+  for (const auto& u : runs) {
+    if (u.mode != Mode::Pair || u.dir != Direction::Uni) continue;
+    const RunRecord* b = nullptr;
+    for (const auto& r : runs)
+      if (r.mode == Mode::Pair && r.dir == Direction::Bi && r.bytes == u.bytes) b = &r;
+    const auto ug = flow_matrix_gbs(u, n);
+    std::vector<double> bg;
+    if (b) bg = flow_matrix_gbs(*b, n);
+    const auto f = fabric_findings(ug, b ? &bg : nullptr, n);
+    std::fprintf(out, "\n== fabric check, pair %s: %s ==\n", format_size(u.bytes).c_str(),
+                 f.empty() ? "every link alike (no cell below half the median, bi >= uni)" : "FINDINGS");
+    for (const auto& line : f) std::fprintf(out, "  %s\n", line.c_str());
+  }
+  std::fflush(out);
+}
+
 void print_extended(FILE* out, const RunRecord& rec, int n) {
   std::string head = strfmt("[%s %s | %s x %d | timing=%s warmup=%d%s]", mode_name(rec.mode), direction_name(rec.dir),
                             format_size(rec.bytes).c_str(), rec.cfg.iters, timing_name(rec.cfg.timing), rec.cfg.warmup,

@@ -47,8 +47,21 @@ struct RunRecord {
 std::vector<double> flow_matrix_gbs(const RunRecord& rec, int n);
 std::vector<double> flow_matrix_p50_us(const RunRecord& rec, int n);
 
+// Fabric checks of one node's matrices (GB/s per direction, row = sender;
+// the multi-GPU tier's test_fabric_is_uniform and bench.py fabric_findings
+// carry the same rules): on a fully connected xGMI node every link is alike,
+// so an off-diagonal cell of `uni` below min_ratio x the median cell, or a
+// pair whose bi-directional total (bi[a][b] + bi[b][a], p2p_matrix.cc:258)
+// is below its uni cell (:177), is reported.  Cells never measured (0) are
+// not judged; `bi` may be null.  One line per finding, [] when all pass.
+std::vector<std::string> fabric_findings(const std::vector<double>& uni, const std::vector<double>* bi, int n,
+                                         double min_ratio = 0.5);
+
 // Human-readable tables appended after the compat section.
 void print_extended(FILE* out, const RunRecord& rec, int n);
+// The fabric lines of every pair-mode size with both a uni and a bi run
+// (fabric_findings), after the extended tables.
+void print_fabric_check(FILE* out, const std::vector<RunRecord>& runs, int n);
 void print_latency(FILE* out, const std::vector<LatencyResult>& lat, int n);
 void print_matrix(FILE* out, const std::string& title, const std::vector<double>& m, int n, const char* fmt,
                   bool blank_diag);

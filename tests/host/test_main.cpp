@@ -1034,6 +1034,29 @@ TEST(test_link_transport_mismatch) {
   EXPECT(!link_transport_mismatch("n/a", "NET"));
 }
 
+TEST(test_fabric_findings_cli) {
+  // The CLI's fabric check (report.cpp fabric_findings): alike links pass;
+  // one slow cell, or a pair whose both directions together are below a uni
+  // cell, are named.  GB/s per direction, row = sender.
+  const int n = 3;
+  std::vector<double> uni = {0, 50, 51, 49, 0, 50, 50, 52, 0};
+  std::vector<double> bi = {0, 45, 46, 44, 0, 45, 45, 47, 0};
+  EXPECT(fabric_findings(uni, &bi, n).empty());
+  EXPECT(fabric_findings(uni, nullptr, n).empty());
+  std::vector<double> slow = uni;
+  slow[2 * n + 1] = 12.0;
+  auto f = fabric_findings(slow, &bi, n);
+  EXPECT(f.size() == 1 && f[0].find("cell 2->1 12.00") != std::string::npos);
+  std::vector<double> weak_bi = bi;
+  weak_bi[0 * n + 1] = 20.0;
+  weak_bi[1 * n + 0] = 20.0;  // 40 both ways < 50 and < 49
+  f = fabric_findings(uni, &weak_bi, n);
+  EXPECT(f.size() == 2 && f[0].find("pair 0<->1 both directions 40.00") != std::string::npos);
+  // Unmeasured cells (0) are not judged.
+  std::vector<double> partial = {0, 50, 0, 0, 0, 0, 0, 0, 0};
+  EXPECT(fabric_findings(partial, nullptr, n).empty());
+}
+
 TEST(test_abort_if_idle_waits_for_native_calls) {
   // the watchdog aborts the communicators itself only when no
   // engine call is open, then takes no more calls.  (Closes the engine for
