@@ -350,7 +350,20 @@ def main(argv=None) -> int:
     args = parse_args(argv)
     if args.child:
         return child_main(args)
-    return BenchRun(args, claim_stdout()).run()
+    try:
+        rc = BenchRun(args, claim_stdout()).run()
+    except BaseException:
+        if not core.WATCHDOG_FIRED.is_set():
+            raise
+        rc = None
+    if core.WATCHDOG_FIRED.is_set():
+        # The deadline's watchdog printed the line and ends the process with
+        # its own status (0 with a result, 4 without) once the communicators
+        # are aborted; a main thread that got here meanwhile -- e.g. through a
+        # peer whose exit broke a gloo collective -- must not end it first.
+        while True:
+            time.sleep(1.0)
+    return rc
 
 
 if __name__ == "__main__":

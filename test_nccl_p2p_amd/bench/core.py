@@ -255,6 +255,9 @@ class Reporter:
 
 ABORT_GRACE_S = 3.0
 ABORT_LINGER_S = 1.0
+# Set once the watchdog has fired: from then on it owns the process's exit
+# status (bench.py main waits for it instead of returning or raising).
+WATCHDOG_FIRED = threading.Event()
 
 
 def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> threading.Event:
@@ -279,35 +282,43 @@ def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> thread
                 break
         if stop.is_set():
             return
-        log("bench: deadline reached during %s; printing what is done" % state.get("section"))
-        errors = dict(state.get("errors") or {})
-        if state.get("section"):
-            errors[state["section"]] = "deadline reached while running"
-        reporter.emit(deadline_hit=True, untimed_skipped=state.get("skipped") or None, section_errors=errors or None)
-        kill_children(state)
-        how = "not aborted within %.1f s" % ABORT_GRACE_S
+        WATCHDOG_FIRED.set()
         try:
-            nat.request_abort()
-            t_end = time.monotonic() + ABORT_GRACE_S
-            while time.monotonic() < t_end:
-                if nat.abort_done():
-                    how = "aborted by the main thread's wait"
-                    break
-                # The main thread outside the engine (a gloo barrier, a torch
-                # sync, Python): no RCCL call can be running, abort from here.
-                if nat.abort_if_idle():
-                    how = "aborted by the watchdog (engine idle)"
-                    break
-                time.sleep(0.02)
-        except Exception as e:  # noqa: BLE001 -- the process ends either way
-            how = "abort failed: %s" % e
-        log("bench: communicators %s" % how)
-        # Every rank's watchdog fires within about a second of the others; a
-        # launcher (torchrun) SIGTERMs the other ranks as soon as one exits,
-        # which would cut a peer's own abort short.  Linger a moment first.
-        time.sleep(ABORT_LINGER_S)
-        sys.stderr.flush()
-        os._exit(0 if reporter.result is not None else 4)
+            log("bench: deadline reached during %s; printing what is done" % state.get("section"))
+            errors = dict(state.get("errors") or {})
+            if state.get("section"):
+                errors[state["section"]] = "deadline reached while running"
+            reporter.emit(deadline_hit=True, untimed_skipped=state.get("skipped") or None,
+                          section_errors=errors or None)
+            kill_children(state)
+            how = "not aborted within %.1f s" % ABORT_GRACE_S
+            try:
+                nat.request_abort()
+                t_end = time.monotonic() + ABORT_GRACE_S
+                while time.monotonic() < t_end:
+                    if nat.abort_done():
+                        how = "aborted by the main thread's wait"
+                        break
+                    # The main thread outside the engine (a gloo barrier, a torch
+                    # sync, Python): no RCCL call can be running, abort from here.
+                    if nat.abort_if_idle():
+                        how = "aborted by the watchdog (engine idle)"
+                        break
+                    time.sleep(0.02)
+            except Exception as e:  # noqa: BLE001 -- the process ends either way
+                how = "abort failed: %s" % e
+            log("bench: communicators %s" % how)
+            # Every rank's watchdog fires within about a second of the others; a
+            # launcher (torchrun) SIGTERMs the other ranks as soon as one exits,
+            # which would cut a peer's own abort short.  Linger a moment first.
+            time.sleep(ABORT_LINGER_S)
+        finally:
+            # Whatever happened above, the process ends here (bench.py's main
+            # thread waits for it once WATCHDOG_FIRED is set).
+            try:
+                sys.stderr.flush()
+            finally:
+                os._exit(0 if reporter.result is not None else 4)
 
     threading.Thread(target=run, name="bench-watchdog", daemon=True).start()
     return stop

@@ -128,6 +128,8 @@ def test_bench_deadline_aborts_rccl_inside_and_outside_the_engine(tmp_path):
     assert "communicators aborted by the main thread's wait" in out.stderr, out.stderr[-3000:]
     assert "communicators aborted by the watchdog (engine idle)" in out.stderr, out.stderr[-3000:]
     assert "Signal 11" not in out.stderr and "SIGSEGV" not in out.stderr, out.stderr[-3000:]
+    # Both ranks ended through their watchdogs with exit status 4 (nothing measured).
+    assert out.stderr.count("exitcode  : 4") == 2, out.stderr[-3000:]
 
 
 @pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
