@@ -308,10 +308,12 @@ def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> thread
             except Exception as e:  # noqa: BLE001 -- the process ends either way
                 how = "abort failed: %s" % e
             log("bench: communicators %s" % how)
-            # Every rank's watchdog fires within about a second of the others; a
-            # launcher (torchrun) SIGTERMs the other ranks as soon as one exits,
-            # which would cut a peer's own abort short.  Linger a moment first.
-            time.sleep(ABORT_LINGER_S)
+            # Every rank's watchdog fires at about the same time; a launcher
+            # (torchrun) SIGTERMs the other ranks as soon as one exits, which
+            # would cut a peer's own abort short.  Linger until a common point
+            # (ABORT_LINGER_S past the deadline, at least that long after the
+            # abort), so the ranks end together.
+            time.sleep(max(ABORT_LINGER_S, deadline.end + ABORT_GRACE_S - time.monotonic()))
         finally:
             # Whatever happened above, the process ends here (bench.py's main
             # thread waits for it once WATCHDOG_FIRED is set).

@@ -12,6 +12,7 @@ what the driver's multi-GPU run executes, minus the link.
 """
 import json
 import os
+import re
 import subprocess
 import sys
 
@@ -128,8 +129,10 @@ def test_bench_deadline_aborts_rccl_inside_and_outside_the_engine(tmp_path):
     assert "communicators aborted by the main thread's wait" in out.stderr, out.stderr[-3000:]
     assert "communicators aborted by the watchdog (engine idle)" in out.stderr, out.stderr[-3000:]
     assert "Signal 11" not in out.stderr and "SIGSEGV" not in out.stderr, out.stderr[-3000:]
-    # Both ranks ended through their watchdogs with exit status 4 (nothing measured).
-    assert out.stderr.count("exitcode  : 4") == 2, out.stderr[-3000:]
+    # Every rank ended through its watchdog with exit status 4 (nothing measured), or was stopped by
+    # torchrun's SIGTERM (-15) once a peer had; none by an exception (1) or a crash.
+    codes = re.findall(r"exitcode\s*:\s*(-?\d+)", out.stderr.split("Failures:")[-1])
+    assert codes and set(codes) <= {"4", "-15"} and "4" in codes, (codes, out.stderr[-3000:])
 
 
 @pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")

@@ -226,8 +226,10 @@ def test_bench_deadline_aborts_inside_and_outside_the_engine(native):
     assert r["timeline_s"]["open"] == "tuning/comms1_per_message/pass0", r["timeline_s"]
     assert "communicators aborted by the main thread's wait" in out.stderr, out.stderr[-3000:]
     assert "communicators aborted by the watchdog (engine idle)" in out.stderr, out.stderr[-3000:]
-    # Both ranks ended through their watchdogs with exit status 4 (torchrun's failure table).
-    assert out.stderr.count("exitcode  : 4") == 2, out.stderr[-3000:]
+    # Every rank ended through its watchdog with exit status 4 (nothing measured), or was stopped by
+    # torchrun's SIGTERM (-15) once a peer had; none by an exception (1) or a crash.
+    codes = re.findall(r"exitcode\s*:\s*(-?\d+)", out.stderr.split("Failures:")[-1])
+    assert codes and set(codes) <= {"4", "-15"} and "4" in codes, (codes, out.stderr[-3000:])
 
 
 def test_bench_teardown_after_the_line_never_fails_the_run(native):
