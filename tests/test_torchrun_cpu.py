@@ -298,7 +298,8 @@ def test_bench_skipped_transfers_fail_verification(native):
     assert r["verify_mismatches"] == 3 * 2 * (64 << 10) // 4, r["verify_detail"]
 
 
-def test_bench_deadline_with_a_hung_section(native):
+@pytest.mark.parametrize("hung", [3, 0])
+def test_bench_deadline_with_a_hung_section(native, hung):
     """A rank that stops responding inside an untimed section: the others' waits
     are bounded by the time left, and at the deadline the watchdog prints the
     headline with the section reported; nothing waits for the driver's kill."""
@@ -307,7 +308,7 @@ def test_bench_deadline_with_a_hung_section(native):
     t0 = _time.monotonic()
     out = torchrun(4, ["bench.py", "--gpus", "4", "--steps", "3", "--warmup", "2", "--transport", "host",
                        "--size", "64K", "--msgs", "1", "--latency-iters", "10", "--sweep", "0", "--ipc-extra", "0",
-                       "--deadline", "80"], env={"P2P_BENCH_HANG": "latency@3"}, timeout=200)
+                       "--deadline", "80"], env={"P2P_BENCH_HANG": "latency@%d" % hung}, timeout=200)
     wall = _time.monotonic() - t0
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stderr[-3000:]
@@ -318,11 +319,16 @@ def test_bench_deadline_with_a_hung_section(native):
     assert r["value"] is not None and r["value"] > 0 and r["deadline_hit"] is True, (r, out.stderr[-2000:])
     assert "latency" in (r["section_errors"] or {}), r["section_errors"]
     assert wall < 80 + 30, wall
-    # The watchdog's line carries the timeline: rank 0's latency section ran
-    # until its waits gave up (their bound is the time left), and the open
-    # entry is its wait for the others to agree on the next section.
+    # The watchdog's line carries rank 0's timeline.
     tl = r["timeline_s"]
-    assert dict(tl["entries"])["section:latency"] > 10 and tl["open"] == "agree:latency_preposted", tl
+    if hung == 0:
+        # Rank 0 itself hung there: the section is the open entry.
+        assert tl["open"] == "section:latency" and tl["entries"][-1][1] > 30, tl
+    else:
+        # Rank 0's latency section ran until its waits gave up (their bound
+        # is the time left); the open entry is its wait for the others to
+        # agree on the next section.
+        assert dict(tl["entries"])["section:latency"] > 10 and tl["open"] == "agree:latency_preposted", tl
     assert tl["entries"][-1][0] == tl["open"] and tl["deadline_left_s"] <= 0.5, tl
 
 
