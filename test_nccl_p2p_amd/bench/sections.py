@@ -245,6 +245,8 @@ class SectionsMixin:
             # kernels at unroll 4, 8 HW queues and RCCL's INFO log, which the
             # reference's stock setup would not.
             iters = {d: v["iters"] for d, v in ref.items() if d in dirs and isinstance(v, dict) and "iters" in v}
+            if not iters:
+                return {"skipped": "the reference-method matrices it repeats were skipped"}
             r = self.child_job(REF_STOCK, ["--child-ref-iters", json.dumps(iters), "--hw-queues", "0"],
                                env=stock_env())
             if r is None or "error" in r:
