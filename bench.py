@@ -319,7 +319,6 @@ class BenchRun(HeadlineMixin, SectionsMixin):
             self.reporter.update(fabric_findings=ff)
             for f in ff or []:
                 log("bench: fabric: " + f)
-        if self.env.rank == 0:
             log("bench: GB/s matrix (row=src, col=dst), median over steps:")
             for r in range(self.n):
                 log("  " + " ".join("%8.2f" % h.matrix[r][c] for c in range(self.n)))
