@@ -397,6 +397,25 @@ std::vector<RcclUnparsedPeer> rccl_unparsed_peers(const std::string& text, const
   return out;
 }
 
+std::vector<std::string> rccl_log_sample(const std::string& text, size_t max_conn) {
+  std::string version, channels;
+  std::vector<std::string> conns;
+  std::istringstream in(text);
+  for (std::string line; std::getline(in, line);) {
+    if (!line.empty() && line.back() == '\r') line.pop_back();
+    if (version.empty() && line.find("RCCL version") != std::string::npos) version = line;
+    if (line.find(" p2p channels per peer") != std::string::npos) channels = line;
+    const size_t ch = line.find("Channel ");
+    if (conns.size() < max_conn && ch != std::string::npos && line.find(" via ", ch) != std::string::npos)
+      conns.push_back(line);
+  }
+  std::vector<std::string> out;
+  if (!version.empty()) out.push_back(version);
+  if (!channels.empty()) out.push_back(channels);
+  out.insert(out.end(), conns.begin(), conns.end());
+  return out;
+}
+
 bool link_transport_mismatch(const std::string& link, const std::string& transport) {
   const bool direct_xgmi = link.rfind("XGMI/1", 0) == 0 && link.size() == 6;
   return direct_xgmi && !transport.empty() && transport != "?" && transport != "P2P" && transport != "self";

@@ -110,6 +110,13 @@ std::vector<RcclUnparsedPeer> rccl_unparsed_peers(const std::string& text, const
                                                   const std::vector<char>& net_peer, const std::vector<char>& touched,
                                                   int me, size_t max_lines = 20);
 
+// Raw lines of `text` for the record (link_report log_sample): RCCL's version
+// line, the last line that states the p2p channel counts, and the first
+// `max_conn` connection lines ("Channel .. via .."), so a node run keeps the
+// real format its parser was checked against (the fixtures in tests/data are
+// hand-written in RCCL 2.26's layout).
+std::vector<std::string> rccl_log_sample(const std::string& text, size_t max_conn = 4);
+
 // ---- this process's RCCL environment and INFO log file -----------------
 // RCCL's INFO log, which this process reads to learn the p2p channels and
 // transports RCCL set up.  Unless the user asked for RCCL's log themselves

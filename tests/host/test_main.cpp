@@ -1005,6 +1005,21 @@ TEST(test_rccl_unparsed_peers_keep_their_raw_lines) {
   EXPECT(rccl_unparsed_peers(known, kl, {0, 0, 0, 0}, {1, 0, 1, 0}, 1).empty());
 }
 
+TEST(test_rccl_log_sample) {
+  // What a node run keeps of RCCL's real log: version, channel counts, the
+  // first connection lines, in that order.
+  const std::string text = read_file(std::string(P2P_TEST_DATA) + "/rccl_info_4rank_p2p_rank1_canned.txt");
+  auto s = rccl_log_sample(text, 3);
+  EXPECT(s.size() == 5);
+  if (s.size() == 5) {
+    EXPECT(s[0].find("RCCL version : 2.26.6") != std::string::npos);
+    EXPECT(s[1].find("8 p2p channels per peer") != std::string::npos);
+    EXPECT(s[2].find("Channel 00/0 : 1[1] -> 2[2] via P2P/IPC") != std::string::npos);
+    EXPECT(s[4].find("Channel 00/1 : 1[1] -> 0[0]") != std::string::npos);
+  }
+  EXPECT(rccl_log_sample("", 4).empty());
+}
+
 TEST(test_rccl_log_warnings_and_env_ownership) {
   // The private log's WARN extraction (the text RCCL errors carry) on a file
   // this test owns: NCCL_DEBUG_FILE set by the user is read as it is.

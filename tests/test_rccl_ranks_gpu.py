@@ -105,6 +105,11 @@ def test_bench_four_rccl_ranks(tmp_path):
                 assert p["op_limit"] == 32 << 20, p
     # Every connected peer's RCCL lines were parsed.
     assert r["unparsed_peers"] == [], r["unparsed_peers"]
+    # And every rank keeps a sample of RCCL's real log: version, channel
+    # counts, connection lines (here over its socket transport).
+    for rep in r["provenance"]["rccl_peers"]:
+        sample = rep["log_sample"]
+        assert any("RCCL version" in l for l in sample) and any(" via NET" in l for l in sample), sample
 
 
 @pytest.mark.emulated
