@@ -692,7 +692,9 @@ class RcclTransport final : public Transport {
                   j ? "," : "", comm_info_[j].p2p_channels, comm_info_[j].p2p_per_peer, comm_info_[j].nnodes,
                   comm_info_[j].from_rank < 0 ? rank_ : comm_info_[j].from_rank, comm_info_[j].unroll);
     o += "],\"log_sample\":[";
-    const auto sample = rccl_log_sample(rccl_log_since(log_start_));
+    // (From the start of the process's log: rank 0's ncclGetUniqueId prints
+    // RCCL's version before this transport's part begins.)
+    const auto sample = rccl_log_sample(rccl_log_since(0));
     for (size_t k = 0; k < sample.size(); ++k) o += strfmt("%s\"%s\"", k ? "," : "", json_escape(sample[k]).c_str());
     o += "],\"unparsed_peers\":[";
     for (size_t i = 0; i < unparsed_.size(); ++i) {
