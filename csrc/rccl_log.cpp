@@ -399,20 +399,24 @@ std::vector<RcclUnparsedPeer> rccl_unparsed_peers(const std::string& text, const
 
 std::vector<std::string> rccl_log_sample(const std::string& text, size_t max_conn) {
   std::string version, channels;
-  std::vector<std::string> conns;
+  std::vector<std::string> p2p, other;  // connection lines of p2p ops ("Channel xx/1") first
   std::istringstream in(text);
   for (std::string line; std::getline(in, line);) {
     if (!line.empty() && line.back() == '\r') line.pop_back();
     if (version.empty() && line.find("RCCL version") != std::string::npos) version = line;
     if (line.find(" p2p channels per peer") != std::string::npos) channels = line;
     const size_t ch = line.find("Channel ");
-    if (conns.size() < max_conn && ch != std::string::npos && line.find(" via ", ch) != std::string::npos)
-      conns.push_back(line);
+    if (ch == std::string::npos || line.find(" via ", ch) == std::string::npos) continue;
+    const size_t slash = line.find('/', ch), colon = line.find(" : ", ch);
+    const bool is_p2p = slash != std::string::npos && slash < colon && std::atoi(line.c_str() + slash + 1) > 0;
+    auto& v = is_p2p ? p2p : other;
+    if (v.size() < max_conn) v.push_back(line);
   }
   std::vector<std::string> out;
   if (!version.empty()) out.push_back(version);
   if (!channels.empty()) out.push_back(channels);
-  out.insert(out.end(), conns.begin(), conns.end());
+  for (size_t i = 0; i < other.size() && p2p.size() < max_conn; ++i) p2p.push_back(other[i]);
+  out.insert(out.end(), p2p.begin(), p2p.end());
   return out;
 }
 

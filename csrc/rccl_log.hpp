@@ -112,7 +112,8 @@ std::vector<RcclUnparsedPeer> rccl_unparsed_peers(const std::string& text, const
 
 // Raw lines of `text` for the record (link_report log_sample): RCCL's version
 // line, the last line that states the p2p channel counts, and the first
-// `max_conn` connection lines ("Channel .. via .."), so a node run keeps the
+// `max_conn` connection lines ("Channel .. via .."; those of p2p connections,
+// "Channel xx/1", before the collectives' "xx/0"), so a node run keeps the
 // real format its parser was checked against (the fixtures in tests/data are
 // hand-written in RCCL 2.26's layout).
 std::vector<std::string> rccl_log_sample(const std::string& text, size_t max_conn = 4);

@@ -1014,10 +1014,14 @@ TEST(test_rccl_log_sample) {
   if (s.size() == 5) {
     EXPECT(s[0].find("RCCL version : 2.26.6") != std::string::npos);
     EXPECT(s[1].find("8 p2p channels per peer") != std::string::npos);
-    EXPECT(s[2].find("Channel 00/0 : 1[1] -> 2[2] via P2P/IPC") != std::string::npos);
-    EXPECT(s[4].find("Channel 00/1 : 1[1] -> 0[0]") != std::string::npos);
+    // p2p connection lines ("xx/1") before the collectives' ("xx/0").
+    EXPECT(s[2].find("Channel 00/1 : 1[1] -> 0[0] via P2P/IPC") != std::string::npos);
+    EXPECT(s[4].find("Channel 32/1 : 1[1] -> 0[0]") != std::string::npos);
   }
   EXPECT(rccl_log_sample("", 4).empty());
+  // Only collective lines: they fill the sample.
+  auto c = rccl_log_sample("x NCCL INFO Channel 00/0 : 3[0] -> 0[0] [receive] via NET/Socket/0 comm 0x1\n", 4);
+  EXPECT(c.size() == 1 && c[0].find("via NET/Socket/0") != std::string::npos);
 }
 
 TEST(test_rccl_log_warnings_and_env_ownership) {
