@@ -448,8 +448,10 @@ class IpcTransport final : public Transport {
     const size_t bytes = kPingSlot * static_cast<size_t>(n_ + 1);
     Export me{};
     page_ = exportable(bytes, &me.handle, [&](void** q) { return alloc_signal_page(q, bytes); });
-    HIPCHECK(hipMemset(page_, 0, bytes));
-    HIPCHECK(hipDeviceSynchronize());
+    // Stream-ordered and waited for with the bounded sync(): a device-wide
+    // synchronize would also wait, unbounded, for any other session's work.
+    HIPCHECK(hipMemsetAsync(page_, 0, bytes, stream_));
+    sync();
     me.bytes = bytes;
     me.host_hash = host_hash(real_hostname());
     me.device = device_;
@@ -719,8 +721,8 @@ class IpcTransport final : public Transport {
     const size_t bytes = kSyncLine * 2 * static_cast<size_t>(n_);
     Export me{};
     sync_page_ = exportable(bytes, &me.handle, [&](void** q) { return alloc_signal_page(q, bytes); });
-    HIPCHECK(hipMemset(sync_page_, 0, bytes));
-    HIPCHECK(hipDeviceSynchronize());
+    HIPCHECK(hipMemsetAsync(sync_page_, 0, bytes, stream_));
+    sync();  // bounded (see pingpong_setup)
     HIPCHECK(hipHostMalloc(&sig_status_, 64, hipHostMallocMapped));
     *sig_status_ = 0;
     me.host_hash = host_hash(real_hostname());
