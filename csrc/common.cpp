@@ -72,9 +72,18 @@ NativeCall::NativeCall() {
   std::lock_guard<std::mutex> lk(g_call_mu);
   if (g_closed) P2P_FATAL("the engine was aborted (the run's deadline passed)");
   ++g_calls;
+  entered_ = true;
+}
+
+NativeCall::NativeCall(std::nothrow_t) {
+  std::lock_guard<std::mutex> lk(g_call_mu);
+  if (g_closed) return;
+  ++g_calls;
+  entered_ = true;
 }
 
 NativeCall::~NativeCall() {
+  if (!entered_) return;
   std::lock_guard<std::mutex> lk(g_call_mu);
   --g_calls;
 }

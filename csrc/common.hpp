@@ -12,6 +12,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <functional>
+#include <new>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -48,10 +49,16 @@ bool abort_done();
 // while a call is in flight.
 class NativeCall {
  public:
-  NativeCall();
+  NativeCall();  // fatal (throws under the bindings) once the engine is closed
+  // Never throws (destructors): entered() is false once the engine is closed.
+  explicit NativeCall(std::nothrow_t);
   ~NativeCall();
+  bool entered() const { return entered_; }
   NativeCall(const NativeCall&) = delete;
   NativeCall& operator=(const NativeCall&) = delete;
+
+ private:
+  bool entered_ = false;
 };
 bool abort_if_idle();
 // A CPU transport's wait that saw abort_requested(): nothing to abort but the

@@ -35,6 +35,22 @@ using namespace p2p;
 
 namespace {
 
+// Teardown of an engine object from Python's deallocation: the transports'
+// waits (buffers freed, streams drained) run without the GIL, so bench.py's
+// deadline watchdog keeps running meanwhile, and inside a NativeCall, so the
+// watchdog does not abort these communicators from its thread (the drain
+// honours its abort request instead).
+template <class Fn>
+void teardown_outside_gil(Fn&& fn) {
+  NativeCall in_engine(std::nothrow);
+  if (PyGILState_Check()) {
+    py::gil_scoped_release nogil;
+    fn();
+  } else {
+    fn();
+  }
+}
+
 class Session {
  public:
   Session(int rank, int world, const std::string& host, int port, int device, const std::string& transport,
@@ -62,6 +78,13 @@ class Session {
       t_ = make_shm_transport(*boot_, opt);
     else
       P2P_FATAL("transport must be 'rccl[:K]', 'ipc[:kernel|:sdma|:push|:relay]', 'host' or 'shm'");
+  }
+
+  ~Session() {
+    teardown_outside_gil([this] {
+      t_.reset();
+      boot_.reset();
+    });
   }
 
   int rank() const { return boot_->rank(); }
@@ -131,6 +154,17 @@ class Session {
     return "";
   }
 
+  // Test hook for teardown: a receive from `peer` that no send matches,
+  // posted and left pending (no sync); the session's destructor must still
+  // end, bounded by its timeout (RcclTransport::drain_quietly).  The buffer is
+  // leaked on purpose: an aborted transfer may not have let go of it.
+  void post_unmatched_recv(size_t bytes, int peer) {
+    void* p = t_->alloc(bytes);
+    t_->group_begin();
+    t_->recv(p, bytes, peer);
+    t_->group_end();
+  }
+
   // Test hook for the stream gate: arm one, release it or not, wait for the
   // stream.  An unreleased gate must open by itself at its deadline.
   std::string gate_probe(double timeout_s, bool release) {
@@ -193,13 +227,24 @@ class PyStepDriver {
   PyStepDriver(std::shared_ptr<Session> s, const std::string& mode, const std::string& dir, size_t bytes, int msgs,
                bool verify, bool batch, bool graph, int depth, size_t recv_budget, uint64_t salt)
       : session_(std::move(s)),
-        d_(session_->t(), session_->boot(), make_schedule(parse_mode(mode), parse_direction(dir), session_->world()),
-           bytes, msgs, verify, salt, StepOptions{batch, graph, depth, recv_budget}) {}
-  StepDriver& d() { return d_; }
+        d_(std::make_unique<StepDriver>(session_->t(), session_->boot(),
+                                        make_schedule(parse_mode(mode), parse_direction(dir), session_->world()),
+                                        bytes, msgs, verify, salt, StepOptions{batch, graph, depth, recv_budget})) {}
+  ~PyStepDriver() {
+    teardown_outside_gil([this] {
+      // Drain first (bounded): the driver's buffers are freed next.
+      if (!session_->t().drain_quietly()) {
+        (void)d_.release();  // leaked: kernels may still use its buffers
+        return;
+      }
+      d_.reset();
+    });
+  }
+  StepDriver& d() { return *d_; }
 
  private:
   std::shared_ptr<Session> session_;  // keeps transport alive
-  StepDriver d_;
+  std::unique_ptr<StepDriver> d_;
 };
 
 hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
@@ -372,6 +417,9 @@ PYBIND11_MODULE(_p2pcore, m) {
            "each peer's transport, the op limit in use); JSON list.")
       .def("provenance", &Session::provenance, py::arg("device") = -1, py::call_guard<NativeCall, py::gil_scoped_release>(),
            "Collective: runtime, RCCL library, knobs, every rank's GPU and the links between them (JSON).")
+      .def("_post_unmatched_recv", &Session::post_unmatched_recv, py::arg("bytes"), py::arg("peer"),
+           py::call_guard<NativeCall, py::gil_scoped_release>(),
+           "Test hook: a receive no send matches, left pending; the session's teardown must still end.")
       .def("_unmatched_recv", &Session::unmatched_recv, py::arg("bytes") = size_t{1} << 20,
            py::call_guard<NativeCall, py::gil_scoped_release>(), "Test hook: a receive no send matches; returns the watchdog's error.");
 

@@ -112,6 +112,18 @@ class Transport {
   virtual int concurrency() const { return 1; }
   // Wait for all posted work (bounded by the transport's watchdog timeout).
   virtual void sync() = 0;
+  // Teardown's wait (destructors of buffers and drivers): like sync() but
+  // never throws.  False when the work did not finish; the caller then
+  // leaks rather than free memory under running kernels.  RCCL aborts its
+  // communicators past the timeout (or on an abort request) first.
+  virtual bool drain_quietly() {
+    try {
+      sync();
+      return true;
+    } catch (const std::exception&) {
+      return false;
+    }
+  }
 
   // A buffer set: one send buffer plus `nslots` receive slots of
   // `slot_bytes`, `stride` bytes apart in one receive arena (slot i at

@@ -108,9 +108,13 @@ class RcclTransport final : public Transport {
 
   ~RcclTransport() override {
     remove_abort_hook(hook_);
-    (void)hipStreamSynchronize(stream_);
-    for (auto cs : cstreams_)
-      if (cs != stream_) (void)hipStreamSynchronize(cs);
+    if (!drain_quietly()) {
+      // Kernels still run after the abort: free nothing under them (process
+      // exit tears the queues down).
+      std::fprintf(stderr, "p2p WARN rank %d: RCCL streams still busy after the abort; leaving them to exit\n",
+                   rank_);
+      return;
+    }
     // Graphs that captured RCCL work hold references to the communicator's
     // persistent resources: release them before the communicator, or
     // ncclCommDestroy waits for them forever.
@@ -429,6 +433,36 @@ class RcclTransport final : public Transport {
         }
         if (now - t0 > 20e-3) std::this_thread::sleep_for(std::chrono::microseconds(20));
       }
+    }
+  }
+
+  // Every stream idle, bounded like sync() but without throwing: past the
+  // timeout, or when the run's deadline asks for an abort, the communicators
+  // are aborted (RCCL's kernels poll the abort flag and exit) and the streams
+  // get 10 s more.  A destructor that waited unbounded here -- with the GIL
+  // held under the Python bindings -- could keep bench.py's deadline watchdog
+  // from ever printing its line.
+  bool drain_quietly() override {
+    double deadline = now_seconds() + timeout_;
+    bool aborted = false;
+    for (;;) {
+      bool busy = false;
+      for (hipStream_t s : {stream_, recv_stream_})
+        if (s && hipStreamQuery(s) == hipErrorNotReady) busy = true;
+      for (auto cs : cstreams_)
+        if (hipStreamQuery(cs) == hipErrorNotReady) busy = true;
+      if (!busy) return true;
+      const double now = now_seconds();
+      if (!aborted && (now > deadline || abort_requested())) {
+        const bool requested = abort_requested();
+        abort_all();
+        if (requested) note_abort_done();
+        aborted = true;
+        deadline = now + 10.0;
+      } else if (aborted && now > deadline) {
+        return false;
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
     }
   }
 

@@ -164,3 +164,19 @@ def test_cli_four_rccl_ranks_fuzz(exe, comms):
                          capture_output=True, text=True, timeout=300, env=ENV)
     assert out.returncode == 0, out.stderr[-3000:]
     assert "all verified" in out.stdout
+
+
+@pytest.mark.emulated
+def test_rccl_teardown_with_a_pending_receive_is_bounded():
+    """A session dropped while an RCCL receive is still pending (its peer never
+    sends) is torn down within its timeout: the transport's drain aborts the
+    communicators instead of waiting on the stream forever, and it runs
+    without the GIL, so another Python thread -- bench.py's deadline
+    watchdog -- keeps running meanwhile (tests/scripts/teardown_pending.py)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "tests/scripts/teardown_pending.py"]
+    out = run_logged(cmd, 90, "teardown_pending", cwd=ROOT, env=ENV)
+    assert out.returncode == 0, out.stderr[-3000:]
+    m = re.search(r"TEARDOWN ([0-9.]+) s, ticker ran (\d+) times", out.stdout)
+    assert m, out.stdout[-2000:]
+    assert 2.5 < float(m.group(1)) < 20 and int(m.group(2)) >= 5, m.group(0)
