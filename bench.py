@@ -95,11 +95,25 @@ def set_hw_queues(argv) -> None:
 STOCK_ENV_KEYS = ("GPU_MAX_HW_QUEUES", "RCCL_UNROLL_FACTOR", "NCCL_DEBUG", "NCCL_DEBUG_FILE", "NCCL_DEBUG_SUBSYS")
 
 
+def user_value(k, environ=None):
+    """`k` as the user set it.  A parent process whose native engine set
+    RCCL's variables (P2P_RCCL_ENV_OWNER: its pid) recorded what each one
+    replaced in P2P_RCCL_PREV_<k> ("=<value>", or "" for unset); this process
+    inherited its settings, not the user's (csrc/rccl_log.cpp
+    undo_inherited_rccl_env, which the native side applies the same way)."""
+    env = os.environ if environ is None else environ
+    owner = env.get("P2P_RCCL_ENV_OWNER")
+    prev = env.get("P2P_RCCL_PREV_" + k)
+    if owner and owner != str(os.getpid()) and prev is not None:
+        return prev[1:] if prev.startswith("=") else None
+    return env.get(k)
+
+
 def stash_stock_env() -> None:
     import json
 
     if "P2P_STOCK_ENV" not in os.environ:  # a child keeps its parent's record
-        os.environ["P2P_STOCK_ENV"] = json.dumps({k: os.environ.get(k) for k in STOCK_ENV_KEYS})
+        os.environ["P2P_STOCK_ENV"] = json.dumps({k: user_value(k) for k in STOCK_ENV_KEYS})
 
 
 if __name__ == "__main__":  # (not when tests import this module)

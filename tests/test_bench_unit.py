@@ -310,3 +310,18 @@ def test_bench_fabric_findings():
     low_bi = {"matrix_gbs": [[0.0, 40.0, 96.0], [96.0, 0.0, 96.0], [96.0, 96.0, 0.0]]}
     ref = dict(r, pair_serial_events={"error": "x"}, reference_semantics={"uni": uni, "bi": low_bi})
     assert bench_fabric_findings(ref, 3) == ["compat bi cell 0<->1 40.00 below its uni cell 48.00"]
+
+
+def test_stock_env_ignores_an_engine_parents_settings():
+    """A process started by one whose native engine set RCCL's variables (a
+    pytest process that ran RCCL tests, say) records the user's values for the
+    stock-settings reference, not the parent's (ran after in-process RCCL
+    tests, test_bench_contract_single_gpu saw RCCL_UNROLL_FACTOR=4)."""
+    env = {"RCCL_UNROLL_FACTOR": "4", "P2P_RCCL_PREV_RCCL_UNROLL_FACTOR": "", "NCCL_DEBUG": "INFO",
+           "P2P_RCCL_PREV_NCCL_DEBUG": "=VERSION", "P2P_RCCL_ENV_OWNER": "1", "GPU_MAX_HW_QUEUES": "4"}
+    assert bench.user_value("RCCL_UNROLL_FACTOR", env) is None
+    assert bench.user_value("NCCL_DEBUG", env) == "VERSION"
+    assert bench.user_value("GPU_MAX_HW_QUEUES", env) == "4"
+    own = dict(env, P2P_RCCL_ENV_OWNER=str(os.getpid()))  # this process's own settings stand
+    assert bench.user_value("RCCL_UNROLL_FACTOR", own) == "4"
+    assert bench.user_value("RCCL_UNROLL_FACTOR", {"RCCL_UNROLL_FACTOR": "2"}) == "2"
