@@ -13,7 +13,7 @@ strings of ROCm 7.2's librccl.so during the survey.
 from __future__ import annotations
 
 import os
-from typing import Dict
+from typing import Dict, List, Tuple
 
 P2P_KNOBS = (
     "NCCL_NCHANNELS_PER_PEER",
@@ -42,3 +42,36 @@ def capture() -> Dict[str, str]:
     for k in P2P_KNOBS:
         out.setdefault(k, "")
     return dict(sorted(out.items()))
+
+
+def linked_librccl() -> str:
+    """The librccl.so that csrc/ links against: the one torch bundles (Makefile RTDIR)."""
+    import torch
+
+    return os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+
+
+_FORMAT_RE = rb"(?:Channel|CollNet) %02d[^\x00\n]*? via [^\x00\n]*"
+
+
+def connection_formats(path: str) -> Tuple[str, List[str]]:
+    """(RCCL version, sorted connection-line printf formats) read from a librccl's bytes.
+
+    These are the formats of the INFO lines csrc/rccl_log.cpp parses
+    (``Channel cc/i : a[bus] -> b[bus] via P2P/IPC … comm 0x… nRanks NN``).  The
+    file is memory-mapped and searched; nothing in it is loaded or run.
+    """
+    import mmap
+    import re
+
+    with open(path, "rb") as f, mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ) as m:
+        found = re.search(rb"RCCL version : ([0-9][0-9.]*[0-9])", m)
+        ver = found.group(1).decode() if found else ""
+        fmts = sorted({x.decode() for x in re.findall(_FORMAT_RE, m)})
+    return ver, fmts
+
+
+def read_pinned_formats(path: str) -> List[str]:
+    """The formats of a tests/data/rccl_<version>_connection_formats.txt file."""
+    with open(path) as f:
+        return [line.rstrip("\n") for line in f if line.strip() and not line.startswith("#")]
