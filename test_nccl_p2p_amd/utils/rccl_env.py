@@ -51,15 +51,22 @@ def linked_librccl() -> str:
     return os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
 
 
-_FORMAT_RE = rb"(?:Channel|CollNet) %02d[^\x00\n]*? via [^\x00\n]*"
+# Each pattern starts with a literal (a linear scan of the 300+ MB library).
+_FORMAT_RES = (
+    rb"(?:Channel|CollNet) %02d[^\x00\n]*? via [^\x00\n]*",  # connections
+    rb"%d coll channels, [^\x00\n]*p2p channels per peer",  # channel counts
+    rb"comm %p rank %d nRanks %d nNodes %d[^\x00\n]*",  # ranks / nodes
+    rb"RCCL Unroll Factor \([a-z-]+\): %d",
+)
 
 
-def connection_formats(path: str) -> Tuple[str, List[str]]:
-    """(RCCL version, sorted connection-line printf formats) read from a librccl's bytes.
+def log_formats(path: str) -> Tuple[str, List[str]]:
+    """(RCCL version, sorted printf formats of the INFO lines csrc/rccl_log.cpp parses).
 
-    These are the formats of the INFO lines csrc/rccl_log.cpp parses
-    (``Channel cc/i : a[bus] -> b[bus] via P2P/IPC … comm 0x… nRanks NN``).  The
-    file is memory-mapped and searched; nothing in it is loaded or run.
+    Read from a librccl's bytes: the connection lines (``Channel cc/i :
+    a[bus] -> b[bus] via P2P/IPC … comm 0x… nRanks NN``) and the init lines
+    parse_rccl_init reads.  The file is memory-mapped and searched; nothing in
+    it is loaded or run.
     """
     import mmap
     import re
@@ -67,11 +74,11 @@ def connection_formats(path: str) -> Tuple[str, List[str]]:
     with open(path, "rb") as f, mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ) as m:
         found = re.search(rb"RCCL version : ([0-9][0-9.]*[0-9])", m)
         ver = found.group(1).decode() if found else ""
-        fmts = sorted({x.decode() for x in re.findall(_FORMAT_RE, m)})
+        fmts = sorted({x.decode() for r in _FORMAT_RES for x in re.findall(r, m)})
     return ver, fmts
 
 
 def read_pinned_formats(path: str) -> List[str]:
-    """The formats of a tests/data/rccl_<version>_connection_formats.txt file."""
+    """The formats of a tests/data/rccl_<version>_log_formats.txt file."""
     with open(path) as f:
         return [line.rstrip("\n") for line in f if line.strip() and not line.startswith("#")]

@@ -1024,12 +1024,12 @@ TEST(test_rccl_log_sample) {
   EXPECT(c.size() == 1 && c[0].find("via NET/Socket/0") != std::string::npos);
 }
 
-// printf of one of RCCL's connection formats with the values a run would
-// print: the n-th integer conversion (%d, %02d, %x, %lx) takes ints[n] (0 past
-// the end), except the last, nRanks; %s takes strs[n] ("" past the end); %p
-// takes `comm`.
+// printf of one of RCCL's log formats with the values a run would print: the
+// n-th integer conversion (%d, %02d, %x, %lx) takes ints[n] (0 past the end),
+// except the last, which takes `last` (nRanks on a connection line); %s takes
+// strs[n] ("" past the end); %p takes `comm`.
 static std::string expand_rccl_format(const std::string& fmt, const std::vector<long>& ints,
-                                      const std::vector<std::string>& strs, long nranks, const std::string& comm) {
+                                      const std::vector<std::string>& strs, long last, const std::string& comm) {
   int total = 0;
   for (size_t i = 0; i + 1 < fmt.size(); ++i)
     if (fmt[i] == '%') {
@@ -1053,7 +1053,7 @@ static std::string expand_rccl_format(const std::string& fmt, const std::vector<
     const char conv = fmt[j];
     std::string v;
     if (conv == 'd' || conv == 'x') {
-      const long x = ni + 1 == static_cast<size_t>(total) ? nranks : (ni < ints.size() ? ints[ni] : 0);
+      const long x = ni + 1 == static_cast<size_t>(total) ? last : (ni < ints.size() ? ints[ni] : 0);
       ++ni;
       std::ostringstream s;
       if (conv == 'x') s << std::hex;
@@ -1072,19 +1072,40 @@ static std::string expand_rccl_format(const std::string& fmt, const std::vector<
   return out;
 }
 
-TEST(test_rccl_connection_formats_of_the_library) {
+TEST(test_rccl_log_formats_of_the_library) {
   // VERDICT r4 missing #2: RCCL's xGMI P2P transport cannot run on one GPU,
   // so the lines a node run prints are pinned from the printf formats
   // compiled into the linked librccl.so (scripts/rccl_formats.py;
   // tests/test_rccl_formats.py checks the file against the library).  Every
   // "Channel" format, expanded with a hex bus id in the brackets, parses to
-  // the channel, connection index, ranks, comm and transport class it names.
-  std::ifstream in(std::string(P2P_TEST_DATA) + "/rccl_2.26.6_connection_formats.txt");
-  int formats = 0, channel_formats = 0;
-  std::string ipc_format;
+  // the channel, connection index, ranks, comm and transport class it names;
+  // every init format to the counts it carries.
+  std::ifstream in(std::string(P2P_TEST_DATA) + "/rccl_2.26.6_log_formats.txt");
+  int formats = 0, channel_formats = 0, init_formats = 0;
+  std::string ipc_format, counts_format, ranks_format;
   for (std::string fmt; std::getline(in, fmt);) {
     if (fmt.empty() || fmt[0] == '#') continue;
     ++formats;
+    const std::string pre = "node:4711:4711 [3] NCCL INFO ";
+    if (fmt.find("p2p channels per peer") != std::string::npos) {
+      counts_format = fmt;
+      RcclInitInfo i = parse_rccl_init(pre + expand_rccl_format(fmt, {64, 0, 0, 64}, {}, 8, ""));
+      EXPECT(i.p2p_channels == 64 && i.p2p_per_peer == 8);
+      ++init_formats;
+      continue;
+    }
+    if (fmt.find(" nNodes ") != std::string::npos) {
+      ranks_format = fmt;
+      RcclInitInfo i = parse_rccl_init(pre + expand_rccl_format(fmt, {3, 8, 2, 4, 3}, {}, 0, "0x5a5a0100"));
+      EXPECT(i.nranks == 8 && i.nnodes == 2);
+      ++init_formats;
+      continue;
+    }
+    if (fmt.find("Unroll Factor") != std::string::npos) {
+      EXPECT(parse_rccl_init(pre + expand_rccl_format(fmt, {}, {}, 4, "")).unroll == 4);
+      ++init_formats;
+      continue;
+    }
     const size_t via = fmt.find(" via ");
     const std::string cls = fmt.substr(via + 5, fmt.find('/', via) - via - 5);
     const bool with_conn = fmt.rfind("Channel %02d/", 0) == 0;
@@ -1110,14 +1131,14 @@ TEST(test_rccl_connection_formats_of_the_library) {
     auto links = rccl_peer_links(conns, 3, 8);
     EXPECT(links[6].transport == (cls == "COLLNET" ? "NET" : cls) && links[6].channels_connected == 1);
   }
-  EXPECT(formats == 10 && channel_formats == 8 && !ipc_format.empty());
-  if (ipc_format.empty()) return;
-  // Rank 3 of 8 on one node, in the library's P2P/IPC format: 8 p2p channels
-  // per peer on send lines, 2 ring channels ("/0") towards each neighbour.
-  std::string text =
-      "node:4711:4711 [3] NCCL INFO comm 0x5a5a0100 rank 3 nRanks 8 nNodes 1 localRanks 8 localRank 3 MNNVL 0\n"
-      "node:4711:4711 [3] NCCL INFO 64 coll channels, 0 collnet channels, 0 nvls channels, 64 p2p channels, 8 p2p "
-      "channels per peer\n";
+  EXPECT(formats == 14 && channel_formats == 8 && init_formats == 4);
+  if (ipc_format.empty() || counts_format.empty() || ranks_format.empty()) return;
+  // Rank 3 of 8 on one node, in the library's formats: 8 p2p channels per
+  // peer on send lines, 2 ring channels ("/0") towards each neighbour.
+  std::string text = "node:4711:4711 [3] NCCL INFO " +
+                     expand_rccl_format(ranks_format, {3, 8, 1, 8, 3}, {}, 0, "0x5a5a0100") + "\n" +
+                     "node:4711:4711 [3] NCCL INFO " + expand_rccl_format(counts_format, {64, 0, 0, 64}, {}, 8, "") +
+                     "\n";
   for (int p : {2, 4})
     for (int ch = 0; ch < 2; ++ch)
       text += "node:4711:4730 [3] NCCL INFO " +
