@@ -285,6 +285,34 @@ def summarize_compat(text: str) -> str:
     return "\n".join(lines)
 
 
+def _lines_in_text(text: str) -> list:
+    out = []
+    for line in text.splitlines():
+        if line.startswith('{"metric"'):
+            try:
+                out.append(json.loads(line))
+            except ValueError:
+                pass
+    return out
+
+
+def bench_lines_in(obj) -> list:
+    """Every bench line (a dict with `metric` and `n_gpus`) nested anywhere in
+    a JSON document, in document order; a line's own fields are not searched.
+    A record that keeps the run's stdout as text (the driver's `tail`) gives
+    the whole line from it, in preference to an abridged parsed copy."""
+    if isinstance(obj, dict):
+        if "metric" in obj and "n_gpus" in obj:
+            return [obj]
+        whole = [x for v in obj.values() if isinstance(v, str) for x in _lines_in_text(v)]
+        if whole:
+            return whole
+        return [x for v in obj.values() for x in bench_lines_in(v)]
+    if isinstance(obj, list):
+        return [x for v in obj for x in bench_lines_in(v)]
+    return []
+
+
 def main(argv=None) -> int:
     """python -m test_nccl_p2p_amd.utils.report FILE...
 
@@ -308,6 +336,13 @@ def main(argv=None) -> int:
                     recs.append(json.loads(line))
                 except ValueError:
                     pass
+        if not recs:
+            # A pretty-printed record that holds bench lines, such as the
+            # driver's BENCH_rNN.json ("parsed") or SCALE_rNN.json.
+            try:
+                recs = bench_lines_in(json.loads(text))
+            except ValueError:
+                pass
         bench = [r for r in recs if "metric" in r and "n_gpus" in r]
         runs = [r for r in recs if r.get("type") == "run"]
         if bench:

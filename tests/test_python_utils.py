@@ -162,3 +162,27 @@ def test_fabric_findings_on_the_rehearsals():
         args = (b["matrix_gbs"], c["uni"], c["bi"], b["link_check"], b["unparsed_peers"])
         assert fabric_findings(*args, min_ratio=REHEARSAL_MIN_RATIO, bi_at_least_uni=False) == [], d
         assert (fabric_findings(*args) == []) == node_ok, d
+
+
+def test_report_reads_the_drivers_pretty_printed_records(tmp_path, capsys):
+    """The driver keeps each bench run as a pretty-printed record: an abridged
+    `parsed` copy of the line plus the run's stdout tail.  The report tool
+    takes the whole line from the tail, and finds every line of a record
+    that holds several (one per GPU count)."""
+    from test_nccl_p2p_amd.utils.report import bench_lines_in
+
+    def line(n, v):
+        return {"metric": "m", "n_gpus": n, "value": v, "aggregate_gbs": v * n, "matrix_gbs_min": v, "steps": 20}
+
+    full = line(1, 2862.9)
+    bench = {"n": 1, "rc": 0, "parsed": {"metric": "m", "n_gpus": 1, "value": 2862.9},
+             "tail": "noise\n" + json.dumps(full) + "\n---- stderr ----\n"}
+    assert bench_lines_in(bench) == [full]
+    scale = {"runs": [{"parsed": line(1, 2800.0)}, {"parsed": line(2, 52.0)}, {"parsed": line(8, 50.0)}]}
+    assert [r["n_gpus"] for r in bench_lines_in(scale)] == [1, 2, 8]
+    assert bench_lines_in({"x": [1, "a", None]}) == []
+    f = tmp_path / "SCALE_rNN.json"
+    f.write_text(json.dumps(scale, indent=2))
+    assert report_main([str(f)]) == 0
+    out = capsys.readouterr().out
+    assert "| 8 | 50.0 |" in out and "== scaling" in out
