@@ -124,9 +124,10 @@ class RcclTransport final : public Transport {
       if (g) (void)hipGraphDestroy(g);
     execs_.clear();
     graphs_.clear();
+    // An aborted communicator took its registrations with it.
     for (auto& r : reg_sets_)
       for (auto& ch : r.handles)
-        if (ch.first) ncclCommDeregister(ch.first, ch.second);
+        if (live(ch.first)) ncclCommDeregister(ch.first, ch.second);
     reg_sets_.clear();
     try {
       release_discard_sink();
@@ -207,9 +208,12 @@ class RcclTransport final : public Transport {
     auto it = std::find_if(reg_sets_.begin(), reg_sets_.end(), [&](const RegSet& r) { return r.send == send; });
     if (it == reg_sets_.end()) return;
     sync();
-    for (auto& ch : it->handles) nccl_ok(ncclCommDeregister(ch.first, ch.second), "ncclCommDeregister");
+    for (auto& ch : it->handles)
+      if (live(ch.first)) nccl_ok(ncclCommDeregister(ch.first, ch.second), "ncclCommDeregister");
     reg_sets_.erase(it);
   }
+  // Not aborted (abort_all clears the communicator's slot).
+  bool live(ncclComm_t c) const { return c && std::find(comms_.begin(), comms_.end(), c) != comms_.end(); }
   void fill(void* p, size_t bytes, uint64_t seed) override {
     buffer_work();
     dev::launch_fill(p, bytes, seed, stream_);

@@ -211,6 +211,28 @@ def test_buffer_registration_knob(native, monkeypatch, mode):
     del s
 
 
+def test_registered_buffers_after_an_abort():
+    """A session whose communicators were aborted (the deadline watchdog's
+    abort_if_idle) with buffers still registered (P2P_RCCL_REGISTER=1): the
+    abort took the registrations with the communicators, so the teardown
+    deregisters nothing on them and the process ends cleanly.  In a child:
+    abort_if_idle closes the engine for the whole process."""
+    code = ("from test_nccl_p2p_amd import require_native\n"
+            "nat = require_native()\n"
+            "s = nat.Session(0, 1, device=0, transport='rccl:2', timeout_s=60)\n"
+            "d = nat.StepDriver(s, 'self', 'bi', 4 << 20, 4, True, True, False)\n"
+            "d.connect(); d.run_steps(0, 2); d.sync()\n"
+            "print('VERIFY', d.verify_last())\n"
+            "print('ABORTED', nat.abort_if_idle(), nat.abort_done())\n"
+            "del d, s\n"
+            "print('TORN DOWN')\n")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT,
+                         env=dict(os.environ, P2P_RCCL_REGISTER="1"))
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "VERIFY 0" in out.stdout and "ABORTED True True" in out.stdout, out.stdout + out.stderr[-2000:]
+    assert "TORN DOWN" in out.stdout, out.stderr[-3000:]
+
+
 @pytest.mark.parametrize("transport,chunk", [("rccl", "0"), ("rccl:4", "0"), ("rccl:4", "1M")])
 def test_fuzz_random_groups(native, monkeypatch, transport, chunk):
     """Random groups of self messages (1 B .. 4 MiB, several per group)
