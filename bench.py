@@ -132,6 +132,7 @@ from test_nccl_p2p_amd.bench.core import (METRIC, Deadline, Reporter, Timeline, 
                                           first_candidate_budget, first_comms, free_port, hang_requested,
                                           headline_stats, link_check, log, pick_depth, posting_candidates,
                                           process_age, start_watchdog, tuning_steps)
+from test_nccl_p2p_amd.bench.faults import Faults  # noqa: E402
 from test_nccl_p2p_amd.bench.headline import HeadlineMixin  # noqa: E402
 from test_nccl_p2p_amd.bench.sections import SectionsMixin  # noqa: E402
 
@@ -188,10 +189,15 @@ def parse_args(argv=None):
     ap.add_argument("--allpairs-size", default="1G", help="message size of the all-pairs extra (BASELINE config 4: 1 GiB)")
     ap.add_argument("--ring-size", default="256M", help="message size of the ring extra (BASELINE config 5: 256 MiB)")
     ap.add_argument("--sweep", type=int, default=1,
-                    help="1: also sweep the single pair 0 -> 1 over 4 KiB .. --sweep-max (N > 1, after the timed region)")
+                    help="1: also sweep the single pair 0 -> 1 (N > 1; the self cell at N = 1) over 4 KiB .. "
+                         "--sweep-max in powers of 4, verified, after the timed region")
     ap.add_argument("--sweep-max", default="4G", help="largest message of the pair sweep")
     ap.add_argument("--ref-iters", type=int, default=128,
                     help="iterations per cell of the reference-methodology comparison (0 = skip)")
+    ap.add_argument("--ref-runs", type=int, default=7,
+                    help="runs of each reference-method matrix (reference_semantics, its stock-settings child, "
+                         "pair_serial_events): all of them at N = 1 (a run is a few ms), at N >= 2 as many as the "
+                         "section's slice holds, at least one; the ratios use the median run")
     ap.add_argument("--fallback", type=int, default=1,
                     help="1: should the RCCL headline fail (setup, connection, stalled transfer), time the same steps "
                          "through the IPC data plane and keep that number in headline_fallback.value_gbs (value stays "
@@ -220,6 +226,7 @@ def parse_args(argv=None):
     ap.add_argument("--child-out", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--child-batch", type=int, default=1, help=argparse.SUPPRESS)
     ap.add_argument("--child-ref-iters", default="{}", help=argparse.SUPPRESS)  # ref-stock: {"uni": I, "bi": I}
+    ap.add_argument("--child-ref-runs", default="{}", help=argparse.SUPPRESS)  # ref-stock: {"uni": R, "bi": R}
     ap.add_argument("--ref-stock", type=int, default=1,
                     help="1: also run the reference's methodology in a child with the stock RCCL / HIP settings "
                          "(RCCL's own unroll, the environment's HW queues, no INFO log): reference_semantics_stock")
@@ -251,6 +258,7 @@ class BenchRun(HeadlineMixin, SectionsMixin):
         self.device = default_device(self.env.local_rank) if args.device is None else args.device
         if self.use_gpu:
             torch.cuda.set_device(self.device)
+        self.faults = Faults(self.env.rank, self.env.world)  # the test hooks, read once (bench/faults.py)
         self.reporter = Reporter(self.env.rank, real_stdout, args.json_out, self.timeline, self.deadline)
         self.state = {"section": "setup", "skipped": [], "errors": {}}
         start_watchdog(self.deadline, self.reporter, self.nat, self.state)
@@ -342,11 +350,7 @@ class BenchRun(HeadlineMixin, SectionsMixin):
         # peer whose watchdog ended it first breaks this barrier; that is no
         # error of the measurement either.
         self.timeline.begin("teardown")
-        if hang_requested("teardown", self.env.rank):
-            # Test hook: this rank ends here, as a rank whose watchdog fired a
-            # little earlier than the others' (its process started earlier).
-            log("bench: injected exit in the teardown on rank %d" % self.env.rank)
-            os._exit(0)
+        self.faults.teardown()
         try:
             self.barrier()
             if self.n > 1 and dist.is_initialized():

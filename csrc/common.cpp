@@ -89,10 +89,17 @@ NativeCall::~NativeCall() {
 }
 
 bool abort_if_idle() {
-  std::lock_guard<std::mutex> lk(g_call_mu);
-  if (g_calls > 0) return false;
-  g_closed = true;
-  run_abort_hooks(1);  // still holding g_call_mu: no call can enter meanwhile
+  {
+    std::lock_guard<std::mutex> lk(g_call_mu);
+    if (g_calls > 0) return false;
+    g_closed = true;  // from here on every call is refused: none can enter while the hooks run
+  }
+  // The hooks run without g_call_mu: one that blocks
+  // (ncclCommAbort on a kernel that never exits, a stuck proxy thread) must
+  // not also stall every thread that tries to enter the engine; those are
+  // refused at once.  The bindings release the GIL around this call, so the
+  // bench watchdog's hard exit does not wait for it either.
+  run_abort_hooks(1);
   note_abort_done();
   return true;
 }

@@ -133,25 +133,31 @@ __device__ void check_tail(const uint8_t* tail, uint32_t tail_bytes, uint64_t ta
 }
 
 // Reduction epilogue: wave64 butterfly, the 4 wave partials through LDS, then
-// one atomic per non-zero field into this block's shard.
-__device__ __forceinline__ void block_commit(Partial acc, VerifyAccum* out, uint32_t shard_key) {
+// one atomic per non-zero field into this block's shard.  Wave w's partial
+// goes to red + w * red_stride bytes: the stride kernel passes a small array
+// of its own, the LDS-staged kernels the first bytes of each wave's own
+// staging slots (free once that wave's loop is done), so those kernels use
+// exactly 32 KiB of LDS and 5 workgroups fit a CU's 160 KiB (a separate
+// 96-byte array made it 32,864 B: 4 per CU).
+__device__ __forceinline__ void block_commit(Partial acc, VerifyAccum* out, uint32_t shard_key, char* red,
+                                             uint32_t red_stride) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     acc.mism += __shfl_xor(acc.mism, off, 64);
     acc.sum += __shfl_xor(acc.sum, off, 64);
     acc.first = min(acc.first, __shfl_xor(acc.first, off, 64));
   }
-  __shared__ Partial red[kWaves];
   const int wave = threadIdx.x / 64;
-  if ((threadIdx.x & 63) == 0) red[wave] = acc;
+  if ((threadIdx.x & 63) == 0) *reinterpret_cast<Partial*>(red + wave * red_stride) = acc;
   __syncthreads();
   if (threadIdx.x == 0) {
-    Partial t = red[0];
+    Partial t = *reinterpret_cast<const Partial*>(red);
 #pragma unroll
     for (int w = 1; w < kWaves; ++w) {
-      t.mism += red[w].mism;
-      t.sum += red[w].sum;
-      t.first = min(t.first, red[w].first);
+      const Partial& r = *reinterpret_cast<const Partial*>(red + w * red_stride);
+      t.mism += r.mism;
+      t.sum += r.sum;
+      t.first = min(t.first, r.first);
     }
     VerifyAccum* s = out + (shard_key % kVerifyShards);
     if (t.sum) atomicAdd(&s->checksum, t.sum);
@@ -188,7 +194,8 @@ __global__ __launch_bounds__(kBlock) void verify_stride_kernel(const uint4* __re
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) check_tail<CHECK>(tail, tail_bytes, tail_offset, seed, acc);
-  block_commit(acc, out, blockIdx.x);
+  __shared__ Partial red[kWaves];
+  block_commit(acc, out, blockIdx.x, reinterpret_cast<char*>(red), sizeof(Partial));
 }
 
 // LDS-staged verify.  Wave g owns super-chunk g (kLdsStages consecutive KiB)
@@ -219,6 +226,20 @@ __device__ __forceinline__ void lds_read_stages(uint32_t addr, u32x4 (&r)[kLdsSt
       : "memory");
 }
 
+// The LDS-staged kernels' only LDS: 8 KiB of staging slots per wave (32 KiB
+// per workgroup), whose first bytes also carry the block_commit partials.
+typedef uint4 LdsSlots[kWaves][kLdsStages][64];
+static_assert(sizeof(LdsSlots) == 32768, "5 workgroups per CU need <= 32 KiB each");
+
+__device__ __forceinline__ LdsSlots& lds_slots() {
+  __shared__ LdsSlots slots;
+  return slots;
+}
+
+__device__ __forceinline__ void lds_block_commit(Partial acc, VerifyAccum* out, uint32_t shard_key) {
+  block_commit(acc, out, shard_key, reinterpret_cast<char*>(&lds_slots()[0][0][0]), sizeof(lds_slots()[0]));
+}
+
 // Blocks `block` of `nblocks` of one buffer: the LDS-staged loop below, with
 // the workgroup's own LDS slots (the single and the batched verify share it).
 // aux = 2 on the LDS-DMA: non-temporal (6.3-6.6 TB/s against 5.7-5.9 with the
@@ -227,9 +248,12 @@ template <bool CHECK>
 __device__ __forceinline__ Partial lds_verify_blocks(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
                                                      uint64_t block, uint64_t nblocks) {
   constexpr int STAGES = kLdsStages;
-  __shared__ uint4 slot[kWaves][STAGES][64];
+  LdsSlots& slot = lds_slots();
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x / 64;
+  // Wave-uniform by construction; readfirstlane tells the compiler, so the
+  // chunk walk below stays on the scalar unit (no per-lane 64-bit compares
+  // and exec branches around the DMAs).
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x / 64));
   const uint64_t sc_vecs = static_cast<uint64_t>(STAGES) * 64;
   const uint64_t n_sc = (nvec + sc_vecs - 1) / sc_vecs;
   const uint32_t lds_addr = static_cast<uint32_t>(
@@ -256,13 +280,62 @@ __device__ __forceinline__ Partial lds_verify_blocks(const uint4* __restrict__ p
   return acc;
 }
 
+// Span form of the same staging (experiment, impl 3): workgroup b walks the
+// contiguous super-chunks [b * per, (b + 1) * per), its 4 waves interleaved,
+// so the resident workgroups read far-apart regions of the buffer at once
+// (as the batched kernel over 32 MiB slots does) instead of one dense window
+// moving through it.
+template <bool CHECK>
+__device__ __forceinline__ Partial lds_verify_blocks_db(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
+                                                        uint64_t block, uint64_t nblocks) {
+  constexpr int STAGES = kLdsStages;
+  LdsSlots& slot = lds_slots();
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x / 64));
+  const uint64_t sc_vecs = static_cast<uint64_t>(STAGES) * 64;
+  const uint64_t n_sc = (nvec + sc_vecs - 1) / sc_vecs;
+  const uint64_t per = (n_sc + nblocks - 1) / nblocks;
+  const uint64_t end = min(n_sc, (block + 1) * per);
+  const uint32_t lds_addr = static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)(&slot[wave][0][lane])));
+  Partial acc{0, 0, ~0ull};
+  for (uint64_t sc = block * per + wave; sc < end; sc += kWaves) {
+#pragma unroll
+    for (int s = 0; s < STAGES; ++s) {
+      const uint64_t i = sc * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
+      if (i < nvec)
+        __builtin_amdgcn_global_load_lds(static_cast<const void*>(p + i),
+                                         (__attribute__((address_space(3))) void*)(&slot[wave][s][0]), 16, 0, 2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    u32x4 rv[STAGES];
+    lds_read_stages(lds_addr, rv);
+    const uint32_t key = prng_key(seed, sc * sc_vecs * 4);  // wave-uniform
+#pragma unroll
+    for (int s = 0; s < STAGES; ++s) {
+      const uint64_t i = sc * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
+      if (i < nvec) check_vec<CHECK>(make_uint4(rv[s].x, rv[s].y, rv[s].z, rv[s].w), key, i, acc);
+    }
+  }
+  return acc;
+}
+
+template <bool CHECK>
+__global__ __launch_bounds__(kBlock) void verify_lds_db_kernel(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
+                                                               const uint8_t* __restrict__ tail, uint32_t tail_bytes,
+                                                               uint64_t tail_offset, VerifyAccum* __restrict__ out) {
+  Partial acc = lds_verify_blocks_db<CHECK>(p, nvec, seed, blockIdx.x, gridDim.x);
+  if (blockIdx.x == 0 && threadIdx.x == 0) check_tail<CHECK>(tail, tail_bytes, tail_offset, seed, acc);
+  lds_block_commit(acc, out, blockIdx.x);
+}
+
 template <bool CHECK>
 __global__ __launch_bounds__(kBlock) void verify_lds_kernel(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
                                                             const uint8_t* __restrict__ tail, uint32_t tail_bytes,
                                                             uint64_t tail_offset, VerifyAccum* __restrict__ out) {
   Partial acc = lds_verify_blocks<CHECK>(p, nvec, seed, blockIdx.x, gridDim.x);
   if (blockIdx.x == 0 && threadIdx.x == 0) check_tail<CHECK>(tail, tail_bytes, tail_offset, seed, acc);
-  block_commit(acc, out, blockIdx.x);
+  lds_block_commit(acc, out, blockIdx.x);
 }
 
 // Batched verify: up to kMaxVerifyJobs buffers, each with
@@ -294,7 +367,7 @@ __global__ __launch_bounds__(kBlock) void multi_verify_lds_kernel(const MultiVer
   Partial acc = lds_verify_blocks<true>(a.p[job], nvec, a.seed[job], b, nb);
   if (b == 0 && threadIdx.x == 0)
     check_tail<true>(reinterpret_cast<const uint8_t*>(a.p[job] + nvec), a.tail[job], nvec * 16, a.seed[job], acc);
-  block_commit(acc, scratch + static_cast<size_t>(job) * kVerifyShards, b);
+  lds_block_commit(acc, scratch + static_cast<size_t>(job) * kVerifyShards, b);
 }
 
 // One workgroup (one wave) per job: reset its shards.
@@ -438,6 +511,8 @@ void launch_verify_t(const uint4* vp, uint64_t nvec, uint64_t seed, const uint8_
                      VerifyImpl impl, const LaunchGeom& g, hipStream_t stream) {
   if (impl == VerifyImpl::Stride)
     verify_stride_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
+  else if (impl == VerifyImpl::LdsDb)
+    verify_lds_db_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
   else
     verify_lds_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
 }

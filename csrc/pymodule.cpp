@@ -9,12 +9,15 @@
 // The fill / verify kernels are also exposed on raw device pointers so they
 // can be driven on torch tensors and checked against a PyTorch reference.
 #include <hip/hip_runtime.h>
+
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <chrono>
 #include <cstdlib>
 #include <memory>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -270,7 +273,7 @@ KernelScratch& scratch() {
 }
 
 dev::VerifyImpl verify_impl_arg(int impl) {
-  if (impl < 0 || impl > static_cast<int>(dev::VerifyImpl::Stride))
+  if (impl < 0 || impl > static_cast<int>(dev::VerifyImpl::LdsDb))
     throw py::value_error(strfmt("verify: impl %d is not 0 (auto), 1 (lds8) or 2 (stride); round 5 removed the "
                                  "other variants (parse_verify_impl names them)", impl));
   return static_cast<dev::VerifyImpl>(impl);
@@ -539,9 +542,14 @@ PYBIND11_MODULE(_p2pcore, m) {
   m.def("abort_requested", []() { return abort_requested(); });
   m.def("abort_done", []() { return abort_done(); },
         "True once a transport wait has aborted its communicators after request_abort().");
-  m.def("abort_if_idle", &abort_if_idle,
+  m.def("abort_if_idle", &abort_if_idle, py::call_guard<py::gil_scoped_release>(),
         "Watchdog: when no thread is inside the engine, abort every communicator from this thread, take no more "
-        "engine calls and note the abort done; False (nothing done) while a call is in flight.  Holds the GIL.");
+        "engine calls and note the abort done; False (nothing done) while a call is in flight.  Releases the GIL "
+        "(and holds no engine lock) while the aborts run, so a blocking abort stalls no other thread.");
+  m.def("_push_blocking_abort_hook", [](double seconds) {
+        push_abort_hook([seconds](int) { std::this_thread::sleep_for(std::chrono::duration<double>(seconds)); });
+      }, py::arg("seconds"),
+      "Test hook: an abort hook that blocks for `seconds` (an ncclCommAbort that does not return).");
   m.def("run_abort_hooks", []() { run_abort_hooks(1); }, py::call_guard<py::gil_scoped_release>(),
         "Aborts every live RCCL communicator / bootstrap (their kernels exit); for a watchdog about to end the "
         "process.");
@@ -611,6 +619,10 @@ PYBIND11_MODULE(_p2pcore, m) {
     AppConfig cfg;
     int code = 0;
     if (!parse_cli(static_cast<int>(argv.size()), argv.data(), &cfg, &code)) return code;
+    // In the engine for the whole app: a watchdog's abort_if_idle
+    // must not abort its communicators from another thread meanwhile.  Taken
+    // with the GIL held, like every binding's NativeCall.
+    NativeCall in_engine;
     py::gil_scoped_release nogil;
     std::string kind = cfg.bootstrap == "mpi" ? "env" : cfg.bootstrap;
     auto boot = make_bootstrap(kind, nullptr, nullptr);

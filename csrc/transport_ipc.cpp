@@ -121,15 +121,8 @@ class IpcTransport final : public Transport {
                    relayed_stripes_);
     for (auto& r : regs_) close_registration(r);
     regs_.clear();
-    for (size_t r = 0; r < peer_pages_.size(); ++r)
-      if (peer_pages_[r] && static_cast<int>(r) != rank_) (void)hipIpcCloseMemHandle(peer_pages_[r]);
-    if (page_) (void)hipFree(page_);
-    if (ping_scratch_) (void)hipFree(ping_scratch_);
-    for (size_t r = 0; r < sync_peer_.size(); ++r)
-      if (sync_peer_[r] && static_cast<int>(r) != rank_) (void)hipIpcCloseMemHandle(sync_peer_[r]);
-    if (sync_page_) (void)hipFree(sync_page_);
-    if (sig_status_) (void)hipHostFree(sig_status_);
-    if (ping_host_) (void)hipHostFree(ping_host_);
+    release_pingpong();
+    release_sync_pages();
     drain_pool();
     for (auto ex : execs_)
       if (ex) (void)hipGraphExecDestroy(ex);
@@ -444,7 +437,34 @@ class IpcTransport final : public Transport {
   bool gate_timed_out() override { return gate_.timed_out(); }
   bool supports_device_pingpong() const override { return true; }
   void pingpong_setup() override {
-    if (page_) return;  // same state on every rank: they all set up together
+    if (ping_ready_) return;  // same state on every rank: they all set up together
+    // Set only once everything below completed: a setup that
+    // failed half way (the bounded sync() timed out or was aborted) leaves no
+    // page_ behind that a later call would take for a finished setup.
+    try {
+      pingpong_setup_once();
+    } catch (...) {
+      release_pingpong();
+      throw;
+    }
+    ping_ready_ = true;
+  }
+
+  void release_pingpong() {
+    for (size_t r = 0; r < peer_pages_.size(); ++r)
+      if (peer_pages_[r] && static_cast<int>(r) != rank_) (void)hipIpcCloseMemHandle(peer_pages_[r]);
+    peer_pages_.clear();
+    if (page_) (void)hipFree(page_);
+    if (ping_scratch_) (void)hipFree(ping_scratch_);
+    if (ping_host_) (void)hipHostFree(ping_host_);
+    page_ = ping_scratch_ = nullptr;
+    ping_host_ = nullptr;
+    sent_.clear();
+    recvd_.clear();
+    ping_ready_ = false;
+  }
+
+  void pingpong_setup_once() {
     const size_t bytes = kPingSlot * static_cast<size_t>(n_ + 1);
     Export me{};
     page_ = exportable(bytes, &me.handle, [&](void** q) { return alloc_signal_page(q, bytes); });
@@ -582,7 +602,7 @@ class IpcTransport final : public Transport {
   }
   // A role with its timing buffers and bounds set; links and bases follow.
   dev::PingRole ping_role(size_t bytes, int iters) {
-    P2P_CHECK(page_, "pingpong_setup() first");
+    P2P_CHECK(ping_ready_, "pingpong_setup() first");
     P2P_CHECK(iters >= 1 && iters <= kPingMaxIters, strfmt("device ping-pong: 1..%d iterations", kPingMaxIters));
     P2P_CHECK(bytes <= kPingMaxBytes, strfmt("device ping-pong payload is at most %zu bytes", kPingMaxBytes));
     auto* stamps = static_cast<unsigned long long*>(ping_scratch_);
@@ -716,8 +736,29 @@ class IpcTransport final : public Transport {
   }
 
   // Collective (constructor): one signal page per rank, 2 x n flag lines
-  // (ready / done from every peer), exported to every peer.
+  // (ready / done from every peer), exported to every peer.  A setup that
+  // fails half way releases what it made (the constructor throws, so the
+  // destructor does not run).
   void setup_sync_pages() {
+    try {
+      setup_sync_pages_once();
+    } catch (...) {
+      release_sync_pages();
+      throw;
+    }
+  }
+
+  void release_sync_pages() {
+    for (size_t r = 0; r < sync_peer_.size(); ++r)
+      if (sync_peer_[r] && static_cast<int>(r) != rank_) (void)hipIpcCloseMemHandle(sync_peer_[r]);
+    sync_peer_.clear();
+    if (sync_page_) (void)hipFree(sync_page_);
+    if (sig_status_) (void)hipHostFree(sig_status_);
+    sync_page_ = nullptr;
+    sig_status_ = nullptr;
+  }
+
+  void setup_sync_pages_once() {
     const size_t bytes = kSyncLine * 2 * static_cast<size_t>(n_);
     Export me{};
     sync_page_ = exportable(bytes, &me.handle, [&](void** q) { return alloc_signal_page(q, bytes); });
@@ -900,6 +941,7 @@ class IpcTransport final : public Transport {
   static constexpr size_t kPingSlot = kPingHeader + kPingMaxBytes;
   static constexpr int kPingMaxIters = 100000;
   void* page_ = nullptr;
+  bool ping_ready_ = false;  // pingpong_setup completed
   std::vector<void*> peer_pages_;
   std::vector<unsigned long long> sent_, recvd_;  // ping messages written to / read from each rank
   double tick_hz_ = 1e8;

@@ -50,6 +50,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -247,6 +248,7 @@ class RcclTransport final : public Transport {
   }
 
   void group_begin() override {
+    check_live("group_begin");
     nccl_ok(ncclGroupStart(), "ncclGroupStart");
     in_group_ = true;
     if (cstreams_.size() > 1) {
@@ -262,6 +264,7 @@ class RcclTransport final : public Transport {
   // limit is 16 MiB x the channels RCCL splits an op to that peer over
   // (derive_op_limits).
   void send(const void* p, size_t bytes, int peer) override {
+    check_live("send");
     const int j = pick(&send_seq_, peer, bytes);
     touched_[static_cast<size_t>(peer)] = 1;
     const char* c = static_cast<const char*>(p);
@@ -273,6 +276,7 @@ class RcclTransport final : public Transport {
     } while (bytes);
   }
   void recv(void* p, size_t bytes, int peer) override {
+    check_live("recv");
     const int j = pick(&recv_seq_, peer, bytes);
     touched_[static_cast<size_t>(peer)] = 1;
     hipStream_t s = j == 0 && recv_stream_ ? recv_stream_ : cstreams_[static_cast<size_t>(j)];
@@ -408,6 +412,7 @@ class RcclTransport final : public Transport {
     // Bounded poll instead of hipStreamSynchronize: spins for the first 20 ms
     // (so per-message syncs in wallclock mode are not inflated by sleeps),
     // then backs off; checks RCCL's async error so a failed peer aborts.
+    check_live("sync");
     join_all();
     double t0 = now_seconds();
     double deadline = t0 + timeout_;
@@ -449,7 +454,7 @@ class RcclTransport final : public Transport {
   bool drain_quietly() override {
     double deadline = now_seconds() + timeout_;
     bool aborted = false;
-    for (;;) {
+    for (long it = 0;; ++it) {
       bool busy = false;
       for (hipStream_t s : {stream_, recv_stream_})
         if (s && hipStreamQuery(s) == hipErrorNotReady) busy = true;
@@ -457,7 +462,10 @@ class RcclTransport final : public Transport {
         if (hipStreamQuery(cs) == hipErrorNotReady) busy = true;
       if (!busy) return true;
       const double now = now_seconds();
-      if (!aborted && (now > deadline || abort_requested())) {
+      // RCCL's async error, as sync() checks it: work pending on
+      // a dead peer aborts now, not at the end of the session's timeout.
+      const bool failed = !aborted && (it & 255) == 0 && !async_error().empty();
+      if (!aborted && (failed || now > deadline || abort_requested())) {
         const bool requested = abort_requested();
         abort_all();
         if (requested) note_abort_done();
@@ -846,11 +854,24 @@ class RcclTransport final : public Transport {
   }
 
   void abort_all() {
+    aborted_.store(true, std::memory_order_release);
     for (auto& c : comms_)
       if (c) {
         ncclCommAbort(c);
         c = nullptr;
       }
+  }
+
+  // Every entry point that would post work first: once the
+  // communicators are aborted -- a wait that timed out, an RCCL error, the
+  // run's deadline, a driver's teardown drain -- a session that outlives its
+  // driver fails with this, not with an invalid-argument error from RCCL on a
+  // null communicator.
+  void check_live(const char* what) const {
+    if (aborted_.load(std::memory_order_acquire))
+      P2P_FATAL(strfmt("rank %d: %s on an aborted session: its RCCL communicators were aborted earlier (a wait that "
+                       "timed out, an RCCL error or the run's deadline); open a new session",
+                       rank_, what));
   }
 
   void nccl_ok(ncclResult_t r, const char* what) {
@@ -976,6 +997,7 @@ class RcclTransport final : public Transport {
   dev::VerifyImpl verify_impl_ = dev::VerifyImpl::Auto;
   std::string desc_;
   int hook_ = 0;
+  std::atomic<bool> aborted_{false};  // abort_all ran: check_live refuses new work
   StreamGate gate_;
 };
 

@@ -8,8 +8,8 @@ import os
 import statistics
 import time
 
-from test_nccl_p2p_amd.bench.core import (claim_stdout, default_device, headline_stats, log, pair_matrix_summary,
-                                          pick_depth)
+from test_nccl_p2p_amd.bench.core import (claim_stdout, combine_runs, default_device, headline_stats, log,
+                                          pair_matrix_summary, pick_depth)
 
 REF_STOCK = "ref-stock"  # --child: the reference's methodology with RCCL's and HIP's stock settings
 
@@ -31,17 +31,21 @@ def stock_env(environ=None) -> dict:
     return env
 
 
-def reference_stock(nat, sess, args, dirs, iters) -> dict:
+def reference_stock(nat, sess, args, dirs, iters, runs=None) -> dict:
     """--child ref-stock: the pair (self at N = 1) matrices by the reference's
     methodology -- one communicator, host clock, a stream sync per message, no
     warmup, no connection warm-up (p2p_matrix.cc:141-267) -- per direction
-    mode, `iters[d]` iterations per cell (those of reference_semantics)."""
+    mode, `iters[d]` iterations per cell and `runs[d]` runs (those of
+    reference_semantics), combined as there (combine_runs)."""
     n = sess.world
     out = {}
     for d in dirs:
-        r = json.loads(sess.run(mode="pair" if n > 1 else "self", dir=d, bytes=nat.parse_size(args.size),
-                                iters=int(iters[d]), warmup=0, timing="wallclock", verify=False, warm=False))
-        out[d] = dict(pair_matrix_summary(r, n), iters=int(iters[d]))
+        rs = []
+        for _ in range(max(1, int((runs or {}).get(d, 1)))):
+            r = json.loads(sess.run(mode="pair" if n > 1 else "self", dir=d, bytes=nat.parse_size(args.size),
+                                    iters=int(iters[d]), warmup=0, timing="wallclock", verify=False, warm=False))
+            rs.append(pair_matrix_summary(r, n))
+        out[d] = dict(combine_runs(rs, n), iters=int(iters[d]))
     out["env"] = {k: os.environ.get(k) for k in ("GPU_MAX_HW_QUEUES", "RCCL_UNROLL_FACTOR", "NCCL_DEBUG",
                                                  "P2P_RCCL_UNROLL", "P2P_RCCL_LOG")}
     return out
@@ -142,7 +146,8 @@ def child_main(args) -> int:
                            transport=transport, timeout_s=min(90.0, args.timeout))
         if args.child == REF_STOCK:
             iters = json.loads(args.child_ref_iters)
-            out = reference_stock(nat, sess, args, [d for d in ("uni", "bi") if d in iters], iters)
+            out = reference_stock(nat, sess, args, [d for d in ("uni", "bi") if d in iters], iters,
+                                  json.loads(args.child_ref_runs))
         else:
             budget = 0 if args.recv_budget.strip() in ("", "0") else nat.parse_size(args.recv_budget)
             out = steps_through(nat, sess, args, args.mode, size, args.child_batch, args.child, budget)

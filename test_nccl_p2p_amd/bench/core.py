@@ -15,6 +15,7 @@ import time
 
 import torch
 
+from test_nccl_p2p_amd.bench.faults import candidate_hang, hang_requested  # noqa: F401 (re-exported)
 from test_nccl_p2p_amd.utils.proc import kill_children
 
 METRIC = "pairwise P2P GB/s matrix (min/mean) + p50 latency at 1/2/4/8 MI355X"
@@ -270,10 +271,12 @@ def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> thread
     (SIGSEGV on 3 of 8 ranks, profiles/r4_rehearsal/).  Every bounded wait of
     the transports polls the request and aborts on its own thread; should the
     main thread be outside the engine (no native call open: a gloo barrier, a
-    torch sync), the watchdog aborts the communicators itself
-    (nat.abort_if_idle).  After up to ABORT_GRACE_S the process ends either
-    way (process exit tears the GPU queues down); the line says which
-    happened."""
+    torch sync), the communicators are aborted from here (nat.abort_if_idle).
+    That runs on a helper thread with the GIL released: an abort
+    that never returns (a kernel that never exits, a stuck proxy thread) holds
+    the helper, not this thread, which ends the process ABORT_GRACE_S after
+    the deadline whatever the abort is doing (process exit tears the GPU
+    queues down); the line says which happened."""
     stop = threading.Event()
 
     def run():
@@ -291,23 +294,35 @@ def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> thread
             reporter.emit(deadline_hit=True, untimed_skipped=state.get("skipped") or None,
                           section_errors=errors or None)
             kill_children(state)
-            how = "not aborted within %.1f s" % ABORT_GRACE_S
-            try:
-                nat.request_abort()
-                t_end = time.monotonic() + ABORT_GRACE_S
-                while time.monotonic() < t_end:
-                    if nat.abort_done():
-                        how = "aborted by the main thread's wait"
-                        break
-                    # The main thread outside the engine (a gloo barrier, a torch
-                    # sync, Python): no RCCL call can be running, abort from here.
-                    if nat.abort_if_idle():
-                        how = "aborted by the watchdog (engine idle)"
-                        break
-                    time.sleep(0.02)
-            except Exception as e:  # noqa: BLE001 -- the process ends either way
-                how = "abort failed: %s" % e
-            log("bench: communicators %s" % how)
+            outcome = {"how": "not aborted within %.1f s" % ABORT_GRACE_S}
+            done = threading.Event()
+
+            def aborter():
+                try:
+                    nat.request_abort()
+                    t_end = time.monotonic() + ABORT_GRACE_S
+                    while time.monotonic() < t_end:
+                        if nat.abort_done():
+                            outcome["how"] = "aborted by the main thread's wait"
+                            break
+                        # The main thread outside the engine (a gloo barrier, a
+                        # torch sync, Python): no RCCL call can be running, abort
+                        # from here.
+                        outcome["how"] = "abort from the watchdog (engine idle) still running after %.1f s" % (
+                            ABORT_GRACE_S)
+                        if nat.abort_if_idle():
+                            outcome["how"] = "aborted by the watchdog (engine idle)"
+                            break
+                        outcome["how"] = "not aborted within %.1f s" % ABORT_GRACE_S
+                        time.sleep(0.02)
+                except Exception as e:  # noqa: BLE001 -- the process ends either way
+                    outcome["how"] = "abort failed: %s" % e
+                finally:
+                    done.set()
+
+            threading.Thread(target=aborter, name="bench-aborter", daemon=True).start()
+            done.wait(ABORT_GRACE_S)
+            log("bench: communicators %s" % outcome["how"])
             # Every rank's watchdog fires at about the same time; a launcher
             # (torchrun) SIGTERMs the other ranks as soon as one exits, which
             # would cut a peer's own abort short.  Linger until a common point
@@ -332,11 +347,12 @@ def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> thread
 # and the ring hop, 2 the single-pair sweep -- and while one runs, the slices
 # of those after it stay free, so a slow section cannot crowd a later config
 # out.  The IPC comparisons and the xGMI pair sweep come after them and get
-# whatever is left.
+# whatever is left.  (self_sweep, config 2's sizes on the self cell, runs at
+# N = 1 only, pair_sweep_0_1 at N > 1 only.)
 SECTION_SLICES = (("latency", 5.0), ("latency_preposted", 5.0), ("reference_semantics", 12.0),
                   ("reference_semantics_stock", 12.0),
                   ("pair_serial_events", 12.0), ("allpairs_1g", 8.0), ("ring_256m", 5.0), ("ring_hop", 3.0),
-                  ("pair_sweep_0_1", 10.0))
+                  ("self_sweep", 4.0), ("pair_sweep_0_1", 10.0))
 
 
 def reserved_after(name: str, active) -> float:
@@ -366,16 +382,42 @@ def pair_matrix_summary(run: dict, n: int) -> dict:
             "mismatches": sum(ph["mismatches"] for ph in run["phases"]), "matrix_gbs": m}
 
 
+def combine_runs(runs, n: int) -> dict:
+    """R repeats of one reference-method matrix (pair_matrix_summary each,
+    VERDICT r5 item 1): the matrix is the per-cell median over the runs
+    (gbs_min / gbs_mean over its cells), `runs` each run's mean cell, and
+    median / min / max / spread of those; the ratios are taken from `median`.
+    One reference run (p2p_matrix.cc:153-177) is a single wall-clock shot per
+    cell; its spread across records was +-9% (686.7-819.0 GB/s on the self
+    cell in round 5)."""
+    per_run = [r["gbs_mean"] for r in runs if r.get("gbs_mean") is not None]
+    m = [[round(statistics.median([r["matrix_gbs"][a][b] for r in runs]), 3) for b in range(n)] for a in range(n)]
+    cells = [m[a][b] for a in range(n) for b in range(n) if (a != b or n == 1)]
+    med = statistics.median(per_run) if per_run else None
+    return {"gbs_min": round(min(cells), 3) if cells else None,
+            "gbs_mean": round(statistics.mean(cells), 3) if cells else None,
+            "cells": runs[0]["cells"] if runs else 0,
+            "mismatches": sum(r["mismatches"] for r in runs),
+            "matrix_gbs": m,
+            "runs": [round(x, 3) for x in per_run],
+            "median": round(med, 3) if med is not None else None,
+            "min": round(min(per_run), 3) if per_run else None,
+            "max": round(max(per_run), 3) if per_run else None,
+            "spread": round((max(per_run) - min(per_run)) / med, 4) if per_run and med else None}
+
+
 def method_ratios(ours: dict, ref: dict, value: float, n: int) -> dict:
     """method_ratio[dir]: our methodology over the reference's on the same
-    serial pair schedule (mean cells; warmup + hipEvents + pipelined
-    iterations vs host clock + a sync per message), per direction mode.
-    concurrency_ratio: the headline's tournament cell (per link and direction,
-    every disjoint pair at once) over our serial bi cell per direction (both
-    directions summed / 2) -- the schedule's gain alone; None at n == 1,
-    where there are no pairs."""
+    serial pair schedule (the median over repeats of each run's mean cell,
+    combine_runs; a record without repeats: its mean cell; warmup + hipEvents
+    + pipelined iterations vs host clock + a sync per message), per direction
+    mode.  concurrency_ratio: the headline's tournament cell (per link and
+    direction, every disjoint pair at once) over our serial bi cell per
+    direction (both directions summed / 2) -- the schedule's gain alone; None
+    at n == 1, where there are no pairs."""
     def mean(d, k):
-        return (d or {}).get(k, {}) and (d or {}).get(k, {}).get("gbs_mean")
+        x = (d or {}).get(k) or {}
+        return x.get("median") if x.get("median") is not None else x.get("gbs_mean")
 
     out = {"method_ratio": {}, "concurrency_ratio": None}
     for k in ("uni", "bi"):
@@ -443,39 +485,3 @@ def default_device(local_rank: int) -> int:
     its device 0.  torch.cuda.device_count() does not initialise the GPU."""
     count = torch.cuda.device_count()
     return local_rank % count if count > 0 else local_rank
-
-
-def hang_requested(section: str, rank: int) -> bool:
-    """Test hook: P2P_BENCH_HANG="<section>@<rank>" makes that rank stop
-    responding inside that untimed section."""
-    spec = os.environ.get("P2P_BENCH_HANG", "")
-    return bool(spec) and spec == "%s@%d" % (section, rank)
-
-
-def candidate_hang(transport: str, comms: int, batch: int, rank: int):
-    """Test hook: P2P_BENCH_HANG="candidate:[<transport>:]<comms>,<batch>[:<how>]@<rank>"
-    (several, separated by ';') makes that rank misbehave in that posting
-    candidate.  Returns <how> for this rank and candidate, else None:
-      tuning (default): in the first tuning pass it posts nothing, as a peer
-                whose transfer never completes, and its own wait ends only at
-                its session's timeout (the candidate's budget);
-      connect:  the same in the candidate's connect;
-      stall:    in the first tuning pass it stops in Python, outside the
-                engine (the deadline watchdog aborts the communicators
-                itself, abort_if_idle);
-      unbounded: its session's timeout is lifted for the first tuning pass,
-                which it runs as usual: next to a stalled peer it waits
-                inside the transport until the watchdog's cooperative abort."""
-    for spec in os.environ.get("P2P_BENCH_HANG", "").split(";"):
-        if not spec.startswith("candidate:") or "@" not in spec:
-            continue
-        what, at = spec[len("candidate:"):].rsplit("@", 1)
-        parts = what.split(":")
-        how = parts.pop() if parts and parts[-1] in ("tuning", "connect", "stall", "unbounded") else "tuning"
-        if len(parts) == 2:
-            if parts[0] != transport:
-                continue
-            parts = parts[1:]
-        if len(parts) == 1 and parts[0] == "%d,%d" % (comms, batch) and at == str(rank):
-            return how
-    return None

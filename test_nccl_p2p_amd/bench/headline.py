@@ -14,23 +14,11 @@ import torch
 import torch.distributed as dist
 
 from test_nccl_p2p_amd.bench.core import (BASELINE_VALUE, METRIC, RESERVE_S, TUNING_SHARE, candidate_budget,
-                                          candidate_hang, cell_matrix, first_candidate_budget, first_comms,
-                                          headline_stats, link_check, log, pick_depth, posting_candidates,
-                                          tuning_steps, unparsed_peers)
-
-
-def emulate_hang(seconds: float, how: str = "tuning"):
-    """The P2P_BENCH_HANG candidate hook (core.candidate_hang): this rank
-    posts nothing and waits as a transport wait that never completes does,
-    until its session's timeout (the candidate's budget), then fails; or
-    ("stall") stops outside the engine for good."""
-    if how == "stall":
-        log("bench: injected stall outside the engine")
-        while True:
-            time.sleep(1.0)
-    log("bench: injected hang for the candidate's budget (%.1f s)" % seconds)
-    time.sleep(seconds)
-    raise RuntimeError("injected hang: no progress within %.1f s" % seconds)
+                                          cell_matrix, first_candidate_budget, first_comms, headline_stats,
+                                          link_check, log, pick_depth, posting_candidates, tuning_steps,
+                                          unparsed_peers)
+from test_nccl_p2p_amd.bench.faults import emulate_hang
+from test_nccl_p2p_amd.utils.report import FALLBACK, SELF_COPY, XGMI_LINK
 
 
 def hw_queues() -> int:
@@ -80,11 +68,7 @@ class HeadlineMixin:
         tl.begin(pre + "session_init")
         sess = self.create_session(headline, device=self.device, timeout_s=first_budget)
         self.log0("bench: %d rank(s), %s, %s" % (n, sess.transport, sess.device_desc))
-        # Test hook: P2P_BENCH_FAIL_HEADLINE=<transport> fails the headline
-        # through that transport on every rank, as a communicator that cannot
-        # be set up does.
-        if os.environ.get("P2P_BENCH_FAIL_HEADLINE") == transport:
-            raise RuntimeError("injected headline failure")
+        self.faults.fail_headline(transport)
         tl.begin(pre + "provenance")
         provenance = json.loads(sess.provenance(self.device if self.use_gpu else -1))
         provenance.pop("type", None)
@@ -118,8 +102,12 @@ class HeadlineMixin:
         ref_sess = sessions.get(1)
         if ref_sess is not None:
             ref_sess.set_timeout(args.timeout)
-        for c in list(sessions):
-            if c not in (comms, 1):
+        closing = [c for c in sessions if c not in (comms, 1)]
+        if closing:
+            # Its own entry: closing a session is ncclCommDestroy per
+            # communicator (p2p_matrix.cc:270), not headline work.
+            tl.begin(pre + "headline/close_candidates")
+            for c in closing:
                 del sessions[c]
 
         # ---- the headline driver: W warmup steps, poison, K timed steps -------
@@ -233,8 +221,14 @@ class HeadlineMixin:
                 # and the single communicator (kept for the reference-method
                 # comparison) stay open.
                 best_c = min(out.tuning, key=out.tuning.get)[0]
-                for cc in [cc for cc in sessions if cc not in (c0, 1, best_c)]:
-                    if not any(cc == c2 for (c2, _) in choices[i + 1:]):
+                closing = [cc for cc in sessions if cc not in (c0, 1, best_c)
+                           and not any(cc == c2 for (c2, _) in choices[i + 1:])]
+                if closing:
+                    # The losers' teardown (ncclCommDestroy per communicator)
+                    # gets its own entry: charged to the pass it read as a slow
+                    # tuning pass.
+                    self.timeline.begin("%stuning/%s/close" % (pre, key))
+                    for cc in closing:
                         del sessions[cc]
                 continue
             # Failed (on every rank alike).  A wait that ran out its budget on
@@ -267,7 +261,7 @@ class HeadlineMixin:
         or None, when the failing phase began)."""
         args, nat, n, tl = self.args, self.nat, self.n, self.timeline
         d, err, connect_s, passes = None, None, 0.0, []
-        hang = candidate_hang(transport, c, b, self.env.rank)
+        hang = self.faults.candidate(transport, c, b)
         t_phase = time.monotonic()
         tl.begin("%stuning/%s/init" % (pre, key))
         try:
@@ -278,10 +272,7 @@ class HeadlineMixin:
             d = nat.StepDriver(s_c, self.mode, "bi", self.size, args.msgs, False, bool(b), bool(args.graph))
             d.connect()
             connect_s = time.monotonic() - t_phase
-            # Test hook: P2P_BENCH_FAIL_CANDIDATE="<comms>,<batch>" fails that
-            # candidate on the last rank only.
-            if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d" % (c, b) and self.env.rank == n - 1:
-                raise RuntimeError("injected candidate failure")
+            self.faults.candidate_fail(c, b, "connect")
         except Exception as e:  # noqa: BLE001 -- reported, and the candidate is skipped everywhere
             err = str(e)[:200]
         if not self.agree(err is None):
@@ -298,11 +289,13 @@ class HeadlineMixin:
                     emulate_hang(wait_s, hang)
                 d.run_steps(0, tune_k)
                 d.sync()
-                if os.environ.get("P2P_BENCH_FAIL_CANDIDATE") == "%d,%d,tuning" % (c, b) and self.env.rank == n - 1:
-                    raise RuntimeError("injected tuning failure")
+                self.faults.candidate_fail(c, b, "tuning")
             except Exception as e:  # noqa: BLE001 -- same agreement as above
                 err = str(e)[:200]
             w = time.perf_counter() - w0
+            # The ranks' agreement on the outcome (gloo collectives) gets an
+            # entry of its own, so the pass entry is the pass.
+            tl.begin("%stuning/%s/agree" % (pre, key))
             if not self.agree(err is None):
                 return passes, connect_s, err or "failed on another rank", t_phase
             passes.append(self.allmax(w) / tune_k)
@@ -405,6 +398,17 @@ class HeadlineMixin:
                            transport=args.transport, headline_fallback=self.fallback)
         return 5
 
+    def value_kind(self) -> str:
+        """SELF_COPY at N = 1 (no link: the diagonal the reference prints as
+        0.00, p2p_matrix.cc:147-151), XGMI_LINK from N = 2 on GPUs, FALLBACK
+        when the headline ran on the fallback data plane; a CPU transport's
+        link otherwise (tests)."""
+        if self.fallback:
+            return FALLBACK
+        if self.n == 1:
+            return SELF_COPY if self.use_gpu else "self-copy (host memory, not a GPU)"
+        return XGMI_LINK if self.use_gpu else "%s-link per direction (not xGMI)" % self.h.sess.transport
+
     def base_result(self) -> dict:
         """The JSON line as far as the timed steps go; the untimed sections
         fill in the rest (Reporter.update)."""
@@ -418,6 +422,9 @@ class HeadlineMixin:
         return {
             "metric": METRIC,
             "value": value,
+            # What `value` measures: utils/report.py
+            # scaling_table never puts two kinds in one ratio.
+            "value_kind": self.value_kind(),
             "unit": "GB/s",
             "n_gpus": n,
             "steps": args.steps,

@@ -18,7 +18,7 @@ import time
 import torch.distributed as dist
 
 from test_nccl_p2p_amd.bench.compare import REF_STOCK, steps_through, stock_env
-from test_nccl_p2p_amd.bench.core import (RESERVE_S, SECTION_SLICES, free_port, hang_requested, log, method_ratios,
+from test_nccl_p2p_amd.bench.core import (RESERVE_S, SECTION_SLICES, combine_runs, free_port, log, method_ratios,
                                           pair_matrix_summary, reserved_after)
 from test_nccl_p2p_amd.utils.proc import run_child
 
@@ -70,10 +70,7 @@ class SectionsMixin:
             s.set_timeout(max(1.0, min(self.args.timeout, wait_left)))
         self.state["section"] = name
         self.timeline.begin("section:" + name)
-        if hang_requested(name, self.env.rank):
-            log("bench: injected hang in %s on rank %d" % (name, self.env.rank))
-            while True:
-                time.sleep(1)
+        self.faults.section(name)
         try:
             return fn()
         except Exception as e:  # noqa: BLE001 -- reported in the JSON
@@ -109,6 +106,8 @@ class SectionsMixin:
             active |= {"allpairs_1g", "ring_256m", "ring_hop"}
         if n > 1 and args.sweep:
             active.add("pair_sweep_0_1")
+        if n == 1 and args.sweep:
+            active.add("self_sweep")
         self.active_sections = active
         self.slice_left, self.slice_t0 = 0.0, time.monotonic()
         self.broken = None
@@ -197,7 +196,11 @@ class SectionsMixin:
             # the first at the headline's rate (slowed by `slowdown`) plus a
             # fixed 10 ms per cell (barriers, fill, verify), later ones at the
             # previous mode's measured time per cell and iteration.  Agreed on
-            # every rank.
+            # every rank.  Then the same matrix again, up to --ref-runs runs
+            # in all, while this mode's share of the slice holds one more
+            # (at N = 1 a run is ~6 ms, so all of them;
+            # at N = 8 over xGMI about one); combine_runs keeps each run's
+            # mean cell and the median the ratios use.
             out, per_iter = {}, self.size * slowdown / rate + 50e-6
             for d in dirs:
                 left = self.slice_remaining() / (len(dirs) - len(out))
@@ -213,19 +216,26 @@ class SectionsMixin:
                                          % (least, warmup, need, left)}
                     break
                 iters = int(self.agreed_min(min(args.ref_iters, max(least, fit))))
-                t0 = time.monotonic()
-                r = json.loads(session.run(mode="pair" if n > 1 else "self", dir=d, bytes=self.size, iters=iters,
-                                           warmup=warmup, timing=timing, verify=verify, warm=warmup > 0))
-                # Everything the mode took, charged to its iterations (conservative).
-                per_iter = max(1e-6, self.agreed_min(time.monotonic() - t0) / cells / (warmup + iters))
-                out[d] = dict(pair_matrix_summary(r, n), iters=iters)
+                runs = []
+                while True:
+                    t0 = time.monotonic()
+                    r = json.loads(session.run(mode="pair" if n > 1 else "self", dir=d, bytes=self.size, iters=iters,
+                                               warmup=warmup, timing=timing, verify=verify, warm=warmup > 0))
+                    run_s = self.allmax(time.monotonic() - t0)
+                    runs.append(pair_matrix_summary(r, n))
+                    # Everything the run took, charged to its iterations (conservative).
+                    per_iter = max(1e-6, run_s / cells / (warmup + iters))
+                    share = self.slice_remaining() / (len(dirs) - len(out))
+                    if len(runs) >= max(1, args.ref_runs) or not self.agree(1.2 * run_s + 0.05 <= share):
+                        break
+                out[d] = dict(combine_runs(runs, n), iters=iters)
                 if iters != args.ref_iters:
                     out[d]["iters_scaled_from"] = args.ref_iters
             return out
 
         def reference_semantics():
             out = matrices(h.ref_sess or h.sess, "wallclock", 0, False, 4.0)
-            uni = (out.get("uni") or {}).get("gbs_mean")
+            uni = (out.get("uni") or {}).get("median")
             return dict(out, size=self.size, comms=1,
                         method="reference semantics: serial ordered pairs, wall clock, stream sync per message, no "
                                "warmup" + ("" if n > 1 else " (applied to the self cell)"),
@@ -247,11 +257,14 @@ class SectionsMixin:
             iters = {d: v["iters"] for d, v in ref.items() if d in dirs and isinstance(v, dict) and "iters" in v}
             if not iters:
                 return {"skipped": "the reference-method matrices it repeats were skipped"}
-            r = self.child_job(REF_STOCK, ["--child-ref-iters", json.dumps(iters), "--hw-queues", "0"],
-                               env=stock_env())
+            # As many runs as the in-process matrices had, repeated inside the
+            # child: its start (~4.6 s) is paid once.
+            runs = {d: len(ref[d].get("runs") or [1]) for d in iters}
+            r = self.child_job(REF_STOCK, ["--child-ref-iters", json.dumps(iters), "--child-ref-runs",
+                                           json.dumps(runs), "--hw-queues", "0"], env=stock_env())
             if r is None or "error" in r:
                 return r
-            uni = (r.get("uni") or {}).get("gbs_mean")
+            uni = (r.get("uni") or {}).get("median")
             return dict(r, size=self.size, comms=1, method=ref["method"] + "; stock RCCL / HIP settings",
                         value_ratio=round(h.value / uni, 3) if uni else None)
 
@@ -280,8 +293,6 @@ class SectionsMixin:
         (0 -> 1) bandwidth sweep 4 KiB -> 4 GiB (config 2; only cell (0, 1) is
         scheduled, the other ranks just join the barriers)."""
         args, n, nat, h = self.args, self.n, self.nat, self.h
-        if n == 1:
-            return
 
         def concurrent_config(mode_x, dir_x, nbytes, iters):
             # Iterations the slice holds, at the headline's per-flow rate with
@@ -311,14 +322,17 @@ class SectionsMixin:
                               "receive completed (grouped send/recv on the stream); hop = lap / N, rank 0's hipEvents"}
 
         def pair_cell(session, nbytes, iters):
-            r = json.loads(session.run(mode="pair", dir="uni", bytes=nbytes, iters=iters, warmup=2, timing="events",
-                                       verify=not args.no_verify, warm=False, cells=[(0, 1)]))
+            # Cell 0 -> 1 alone (N > 1), or the self cell (N = 1).
+            cells = [(0, 1)] if n > 1 else []
+            r = json.loads(session.run(mode="pair" if n > 1 else "self", dir="uni", bytes=nbytes, iters=iters,
+                                       warmup=2, timing="events", verify=not args.no_verify, warm=False, cells=cells))
             fl = [f for ph in r["phases"] for f in ph["flows"]]
             return fl[0] if fl else None
 
-        def pair_sweep():
-            # Sizes while the slice lasts (the same decision on every rank);
-            # a size's cost is estimated at the rate the previous one ran.
+        def size_sweep():
+            # 4 KiB -> --sweep-max in powers of 4, every delivery verified,
+            # while the slice lasts (the same decision on every rank); a size's
+            # cost is estimated at the rate the previous one ran.
             sweep, rate = [], max(h.value or 1.0, 1e-3)
             for nbytes in [b for b in (4096 << (2 * k) for k in range(11)) if b <= nat.parse_size(args.sweep_max)]:
                 iters = max(4, min(200, (2 << 30) // nbytes))
@@ -326,7 +340,7 @@ class SectionsMixin:
                 if not self.agree(self.slice_remaining() > est + 1.0):
                     sweep.append({"bytes": nbytes, "skipped": "no time left in the section's slice"})
                     break
-                self.log0("bench: pair sweep %d B" % nbytes)
+                self.log0("bench: %s sweep %d B" % ("pair" if n > 1 else "self", nbytes))
                 f = pair_cell(h.sess, nbytes, iters)
                 if f:
                     rate = max(f["gbs"], 1e-3)
@@ -334,11 +348,25 @@ class SectionsMixin:
                                   "iter_us_p50": round(f["iter_us"]["p50"], 2), "mismatches": f.get("mismatches", -1)})
             return sweep
 
-        def pair_one_comm():
-            # The same single pair on one communicator (what the sweep ran with
-            # K of them), at the bench's message size and 256 MiB.
+        def one_comm():
+            # The same cell on one communicator (what the sweep ran with K of
+            # them), at the bench's message size and 256 MiB.
             return [{"bytes": nb, "gbs": round(f["gbs"], 2)}
                     for nb in (self.size, 256 << 20) for f in [pair_cell(h.ref_sess, nb, 16)] if f]
+
+        if n == 1:
+            # the sweep's code path on the self cell, so
+            # every driver record (N = 1) runs it; BASELINE config 2's sizes.
+            if args.sweep:
+                sw = self.section("self_sweep", size_sweep, 2.0)
+                if sw is not None:
+                    extras = {"self_sweep": sw, "self_sweep_rccl_comms": h.comms}
+                    if h.ref_sess is not None and h.ref_sess is not h.sess:
+                        oc = self.section("self_one_comm", one_comm)
+                        if oc is not None:
+                            extras["self_one_comm"] = oc
+                    self.reporter.update(extras=extras)
+            return
 
         extras = None
         if args.extras:
@@ -360,11 +388,11 @@ class SectionsMixin:
                 extras["ring_hop"] = v
             self.reporter.update(extras=extras)
         if args.sweep:
-            sw = self.section("pair_sweep_0_1", pair_sweep, 10.0)
+            sw = self.section("pair_sweep_0_1", size_sweep, 10.0)
             if sw is not None:
                 extras = dict(extras or {}, pair_sweep_0_1=sw, pair_sweep_rccl_comms=h.comms)
                 if h.ref_sess is not None and h.ref_sess is not h.sess:
-                    oc = self.section("pair_0_1_one_comm", pair_one_comm)
+                    oc = self.section("pair_0_1_one_comm", one_comm)
                     if oc is not None:
                         extras["pair_0_1_one_comm"] = oc
             self.reporter.update(extras=extras)

@@ -150,7 +150,9 @@ def _reference_cells(r: dict) -> str:
     single uni number of round-2 lines."""
     ref = r.get("reference_semantics") or {}
     if "uni" in ref:
-        return "%s / %s" % (_get(ref, "uni", "gbs_mean"), _get(ref, "bi", "gbs_mean"))
+        def cell(d):
+            return _get(ref, d, "median") if _get(ref, d, "median") != "-" else _get(ref, d, "gbs_mean")
+        return "%s / %s" % (cell("uni"), cell("bi"))
     return _get(r, "reference_semantics", "cell_gbs_mean")
 
 
@@ -161,17 +163,56 @@ def _ratios(r: dict) -> str:
     return "%s / %s / %s" % (m.get("uni", "-") or "-", m.get("bi", "-") or "-", _get(r, "concurrency_ratio"))
 
 
+SELF_COPY = "self-copy (on-GPU HBM)"
+XGMI_LINK = "xgmi-link per direction"
+FALLBACK = "fallback"
+
+
+def value_kind(r: dict) -> str:
+    """What a line's `value` measures (its `value_kind`):
+    the on-GPU self copy at N = 1 (the diagonal the reference prints as 0.00,
+    p2p_matrix.cc:147-151), the per-link, per-direction xGMI cell from N = 2,
+    or the fallback data plane's number.  Lines from before the field are
+    classed the same way from n_gpus and headline_fallback."""
+    if r.get("value_kind"):
+        return r["value_kind"]
+    if r.get("headline_fallback"):
+        return FALLBACK
+    return SELF_COPY if r.get("n_gpus") == 1 else XGMI_LINK
+
+
+def _kind_order(kind: str) -> int:
+    return {XGMI_LINK: 0, SELF_COPY: 2, FALLBACK: 3}.get(kind, 1)
+
+
 def scaling_table(results: Iterable[dict]) -> str:
-    """Markdown table of bench.py lines (one per GPU count): `value` (the
-    mean cell of the matrix, GB/s per direction), aggregate and per-GPU GB/s,
-    the cell rate kept relative to N = 2 (weak scaling: per-GPU work is fixed,
-    so an ideal fabric keeps every cell's rate; N = 1 is the on-GPU self path
-    and has no link), matrix min / mean, p50 latency, and the untimed
-    comparisons the line carries: the reference's methodology on the same
-    communicator, all-pairs aggregate, the ring token hop, the IPC engines and
-    the device ping-pong."""
+    """Markdown tables of bench.py lines (one per GPU count), one table per
+    value_kind: `value` (the mean cell of the matrix, GB/s per direction),
+    aggregate and per-GPU GB/s, the cell rate relative to N = 2 of the SAME
+    kind (weak scaling: per-GPU work is fixed, so an ideal fabric keeps every
+    cell's rate), matrix min / mean, p50 latency, and the untimed comparisons
+    the line carries: the reference's methodology on the same communicator,
+    all-pairs aggregate, the ring token hop, the IPC engines and the device
+    ping-pong.  The N = 1 self copy (HBM-bound, no link) and fallback lines
+    get tables of their own and never enter a ratio with the link rows: read
+    from `value` alone a 1 -> 8 curve would show a ~40x "drop" at N = 2."""
     rows = sorted((r for r in results if r.get("value") is not None), key=lambda r: r["n_gpus"])
-    base = next((r for r in rows if r["n_gpus"] == 2), None)
+    kinds = sorted({value_kind(r) for r in rows}, key=lambda k: (_kind_order(k), k))
+    out = []
+    for kind in kinds:
+        krows = [r for r in rows if value_kind(r) == kind]
+        base = next((r for r in krows if r["n_gpus"] == 2), None) if kind != SELF_COPY else None
+        if out:
+            out.append("")
+        out.append("value_kind: %s%s" % (kind, " (no link: not comparable with the link rows)" if kind == SELF_COPY
+                                          else " (not RCCL: the metric's value is null)" if kind == FALLBACK else ""))
+        out += _kind_table(krows, base)
+    for r in rows:
+        out += transport_lines(r) + pair_sweep_lines(r)
+    return "\n".join(out)
+
+
+def _kind_table(rows, base) -> List[str]:
     out = ["| GPUs | value: mean cell GB/s | aggregate GB/s | per-GPU GB/s | cell rate vs 2 GPUs | RCCL comms "
            "| matrix min / mean GB/s | p50 latency us | reference-method cell GB/s (uni / bi) "
            "| method ratio (uni / bi) / concurrency ratio | all-pairs 1 GiB aggregate GB/s "
@@ -197,9 +238,7 @@ def scaling_table(results: Iterable[dict]) -> str:
             _get(r, "ipc_transport", "relay", "value_gbs"), relay_pair.get("gbs", "-"),
             _get(r, "ipc_transport", "device_pingpong_p50_us", fmt="%.2f"),
             "%s -> %s" % (fb["from"], fb["to"]) if fb else "-"))
-    for r in rows:
-        out += transport_lines(r) + pair_sweep_lines(r)
-    return "\n".join(out)
+    return out
 
 
 def transport_lines(r: dict) -> List[str]:

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -1223,11 +1224,33 @@ TEST(test_abort_if_idle_waits_for_native_calls) {
   // the rest of this process: the last test.)
   int ran = 0;
   push_abort_hook([&ran](int) { ++ran; });
+  // a hook that blocks (ncclCommAbort on a kernel that never
+  // exits) must not hold the engine's lock: a thread entering meanwhile is
+  // refused at once instead of queueing behind the abort.
+  std::atomic<bool> in_hook{false}, release{false};
+  push_abort_hook([&](int) {
+    in_hook = true;
+    for (int i = 0; i < 10000 && !release; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  });
   {
     NativeCall in_engine;
     EXPECT(!abort_if_idle() && ran == 0 && !abort_done());
   }
-  EXPECT(abort_if_idle() && ran == 1 && abort_done());
+  std::atomic<bool> aborted{false};
+  std::thread watchdog([&] { aborted = abort_if_idle(); });
+  for (int i = 0; i < 5000 && !in_hook; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  EXPECT(in_hook && !aborted);
+  const auto t0 = std::chrono::steady_clock::now();
+  bool entered = true;
+  {
+    NativeCall probe(std::nothrow);
+    entered = probe.entered();
+  }
+  const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  EXPECT(!entered && waited < 0.5);
+  release = true;
+  watchdog.join();
+  EXPECT(aborted && ran == 1 && abort_done());
   set_throw_on_fatal(true);
   bool refused = false;
   try {

@@ -325,3 +325,70 @@ def test_stock_env_ignores_an_engine_parents_settings():
     own = dict(env, P2P_RCCL_ENV_OWNER=str(os.getpid()))  # this process's own settings stand
     assert bench.user_value("RCCL_UNROLL_FACTOR", own) == "4"
     assert bench.user_value("RCCL_UNROLL_FACTOR", {"RCCL_UNROLL_FACTOR": "2"}) == "2"
+
+
+def test_combine_runs_and_median_ratios():
+    """R repeats of a reference-method matrix keep each
+    run's mean cell, their median / min / max / spread, and a per-cell median
+    matrix; the method ratios come from the medians (not one noisy shot)."""
+    from test_nccl_p2p_amd.bench.core import combine_runs, method_ratios, pair_matrix_summary
+
+    def run(v01, v10):
+        return pair_matrix_summary({"phases": [{"row": 0, "col": 1, "compat_gbps": 8 * v01, "mismatches": 0},
+                                               {"row": 1, "col": 0, "compat_gbps": 8 * v10, "mismatches": 1}]}, 2)
+
+    c = combine_runs([run(50, 70), run(40, 60), run(90, 90), run(45, 55), run(52, 68)], 2)
+    assert c["runs"] == [60.0, 50.0, 90.0, 50.0, 60.0]
+    assert c["median"] == 60.0 and c["min"] == 50.0 and c["max"] == 90.0 and c["spread"] == round(40 / 60, 4)
+    assert c["matrix_gbs"] == [[0.0, 50.0], [68.0, 0.0]] and c["gbs_mean"] == 59.0 and c["gbs_min"] == 50.0
+    assert c["cells"] == 2 and c["mismatches"] == 5
+    # One GPU: the self cell on the diagonal.
+    one = combine_runs([pair_matrix_summary({"phases": [{"row": -1, "col": -1, "compat_gbps": 8 * v,
+                                                         "mismatches": 0}]}, 1) for v in (686.7, 751.6, 819.0)], 1)
+    assert one["median"] == 751.6 and one["matrix_gbs"] == [[751.6]] and one["gbs_mean"] == 751.6
+    # The ratios use the medians: an outlier run moves neither.
+    ours = {"uni": combine_runs([run(100, 100), run(120, 120), run(500, 500)], 2)}
+    ref = {"uni": combine_runs([run(50, 50), run(10, 10), run(60, 60)], 2)}
+    assert method_ratios(ours, ref, 1.0, 2)["method_ratio"]["uni"] == round(120 / 50, 3)
+    # Records without repeats still use their mean cell.
+    assert method_ratios({"uni": {"gbs_mean": 6.0}}, {"uni": {"gbs_mean": 2.0}}, 1.0, 2)["method_ratio"]["uni"] == 3.0
+
+
+WATCHDOG_CHILD = r"""
+import sys, time
+sys.path.insert(0, %r)
+from test_nccl_p2p_amd import require_native
+from test_nccl_p2p_amd.bench import core
+nat = require_native()
+nat._push_blocking_abort_hook(120.0)  # an ncclCommAbort that never returns
+t0 = time.monotonic()
+core.set_start(t0)
+dl = core.Deadline(1.0)
+rep = core.Reporter(0, 1, None, core.Timeline(t0), dl)
+rep.result = {"metric": core.METRIC, "value": 1.0}
+core.start_watchdog(dl, rep, nat, {"section": "latency", "skipped": [], "errors": {}})
+while True:  # the main thread in Python, outside the engine: the watchdog aborts from its helper
+    time.sleep(1.0)
+"""
+
+
+def test_watchdog_ends_the_process_when_the_abort_blocks(native):
+    """the watchdog's own abort (abort_if_idle, main thread outside
+    the engine) runs on a helper thread with the GIL released, so an abort
+    hook that never returns cannot keep the process alive: it prints the line
+    and exits at the deadline + ABORT_GRACE_S (+ the linger), not when the
+    launcher kills it."""
+    import json
+    import subprocess
+    import time
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    t0 = time.monotonic()
+    out = subprocess.run([sys.executable, "-c", WATCHDOG_CHILD % root], capture_output=True, text=True, timeout=60)
+    wall = time.monotonic() - t0
+    from test_nccl_p2p_amd.bench.core import ABORT_GRACE_S, ABORT_LINGER_S
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert wall < 1.0 + ABORT_GRACE_S + ABORT_LINGER_S + 15.0, wall
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["deadline_hit"] is True and line["section_errors"] == {"latency": "deadline reached while running"}
+    assert "abort from the watchdog (engine idle) still running after" in out.stderr, out.stderr[-2000:]

@@ -256,10 +256,18 @@ def test_unmatched_receive_is_reported(transport):
     the next communicator created on that thread."""
     code = ("from test_nccl_p2p_amd import require_native\n"
             "s = require_native().Session(0, 1, device=0, transport=%r, timeout_s=5)\n"
-            "print('ERR:', s._unmatched_recv(1 << 20))\n" % transport)
+            "print('ERR:', s._unmatched_recv(1 << 20))\n"
+            "try:\n"
+            "    s.run(mode='self', dir='uni', bytes=1 << 20, iters=2, warmup=0)\n"
+            "    print('AGAIN: ran')\n"
+            "except Exception as e:\n"
+            "    print('AGAIN:', e)\n" % transport)
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     assert "ERR: " in out.stdout and ("ncclGroupEnd failed" in out.stdout or "did not finish" in out.stdout), out.stdout
+    # ADVICE r5: the session outlives its aborted communicators; using it
+    # again fails with that said, not with RCCL's error on a null communicator.
+    assert "AGAIN: " in out.stdout and "on an aborted session" in out.stdout, out.stdout
 
 
 def test_chunk_sizes_follow_the_channel_knobs():

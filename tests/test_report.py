@@ -62,7 +62,8 @@ def test_scaling_table_comparisons_and_cli(tmp_path, capsys):
           "reference_semantics": {"uni": {"gbs_mean": 20.0}, "bi": {"gbs_mean": 38.0}},
           "method_ratio": {"uni": 2.5, "bi": 2.4}, "concurrency_ratio": 1.3}
     assert "| 20.0 / 38.0 | 2.5 / 2.4 / 1.3 |" in scaling_table([r3])
-    assert "| 8 | 95.0 | 760.0 | 95.0 | 95.0% | - |" in t and "- / - / - / - | - | - | rccl -> ipc |" in t
+    # A fallback line is its own kind: no ratio against the RCCL rows.
+    assert "| 8 | 95.0 | 760.0 | 95.0 |  | - |" in t and "- / - / - / - | - | - | rccl -> ipc |" in t
     assert not any(l.startswith("| 4 |") for l in t.splitlines())  # a line without a value is left out
     files = []
     for r in rows:
@@ -124,3 +125,36 @@ def test_bench_compat_text_round_trips():
     m = parse_compat(txt)
     assert m["uni"] == [[0.0, 388.0], [378.0, 0.0]] and m["bi"] == [[0.0, 760.0], [760.0, 0.0]]
     assert bench_compat_text({"reference_semantics": None}) == ""
+
+
+def test_scaling_table_never_mixes_value_kinds():
+    """the N = 1 self copy (HBM-bound, no link), the xGMI
+    link rows and a fallback line each get a table of their own, and no ratio
+    is ever taken across two kinds (1 -> 8 from `value` alone would read as a
+    ~40x drop at N = 2)."""
+    from test_nccl_p2p_amd.utils.report import FALLBACK, SELF_COPY, XGMI_LINK, value_kind
+    rows = [{"n_gpus": 1, "value": 2800.0, "aggregate_gbs": 2800.0, "value_kind": SELF_COPY},
+            {"n_gpus": 2, "value": 70.0, "aggregate_gbs": 140.0, "value_kind": XGMI_LINK},
+            {"n_gpus": 4, "value": 66.5, "aggregate_gbs": 266.0, "value_kind": XGMI_LINK},
+            {"n_gpus": 8, "value": 63.0, "aggregate_gbs": 504.0, "value_kind": XGMI_LINK}]
+    t = scaling_table(rows)
+    lines = t.splitlines()
+    x, s = lines.index("value_kind: " + XGMI_LINK), [i for i, l in enumerate(lines) if l.startswith(
+        "value_kind: " + SELF_COPY)][0]
+    assert x < s  # the link rows first, the self copy apart below them
+    link_rows = [l for l in lines[x:s] if l.startswith("| ") and l[2].isdigit()]
+    assert [l.split("|")[1].strip() for l in link_rows] == ["2", "4", "8"]
+    assert "| 2 | 70.0 | 140.0 | 70.0 | 100.0% |" in t and "| 4 | 66.5 | 266.0 | 66.5 | 95.0% |" in t
+    assert "| 8 | 63.0 | 504.0 | 63.0 | 90.0% |" in t
+    # The self-copy row has no ratio at all, and nothing is ever relative to it.
+    assert "| 1 | 2800.0 | 2800.0 | 2800.0 |  |" in t and "4000.0%" not in t and "2.5%" not in t
+    # Without an N = 2 line of its own kind a row gets no ratio (never one against N = 1).
+    t2 = scaling_table([rows[0], rows[3]])
+    assert "| 8 | 63.0 | 504.0 | 63.0 |  |" in t2
+    fb = {"n_gpus": 2, "value": 90.0, "aggregate_gbs": 180.0, "value_kind": FALLBACK,
+          "headline_fallback": {"from": "rccl", "to": "ipc", "error": "e"}}
+    t3 = scaling_table([fb, rows[2]])
+    assert "| 4 | 66.5 | 266.0 | 66.5 |  |" in t3 and "value_kind: fallback" in t3
+    # Lines from before the field are classed from n_gpus and headline_fallback.
+    assert value_kind({"n_gpus": 1}) == SELF_COPY and value_kind({"n_gpus": 8}) == XGMI_LINK
+    assert value_kind({"n_gpus": 8, "headline_fallback": {"from": "rccl"}}) == FALLBACK

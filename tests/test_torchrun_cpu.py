@@ -376,6 +376,17 @@ def test_bench_eight_ranks_with_the_driver_step_counts(native):
     for n in ("tuning/comms1_per_message/connect", "tuning/comms1_batch/pass1", "headline/timed",
               "section:reference_semantics", "section:allpairs_1g", "section:host"):
         assert n in names, names
+    # a pass entry is the pass (the slowest rank's clock
+    # around its steps), with any candidate teardown in entries of its own.
+    spent = dict(tl["entries"])
+    steps = 7  # one lap of the 7 tournament rounds per pass
+    for key, passes in r["posting"]["tuning_passes_ms_per_step"].items():
+        for i, ms in enumerate(passes):
+            entry, timed = spent["tuning/%s/pass%d" % (key, i)], ms * steps / 1e3
+            assert abs(entry - timed) <= max(0.2 * timed, 0.010), (key, i, entry, timed, tl)
+    # The reference-method matrices ran more than once per direction (item 1).
+    for key in ("reference_semantics", "pair_serial_events"):
+        assert all(len(r[key][d]["runs"]) >= 2 and r[key][d]["median"] > 0 for d in ("uni", "bi")), r[key]
 
 
 def test_bench_headline_fallback(native):
@@ -446,3 +457,50 @@ def test_bench_baseline_configs_land_at_xgmi_speed(native):
     ref = [r[k][d] for k in ("reference_semantics", "pair_serial_events") for d in ("uni", "bi") if r[k]]
     assert ref and all(x["iters"] <= 128 for x in ref)
     assert any(x.get("iters_scaled_from") == 128 for x in ref), ref
+
+
+def test_bench_four_ranks_repeat_the_reference_matrices(native):
+    """at N = 4 every reference-method matrix (the
+    reference's methodology and ours on its serial pair schedule, uni and bi)
+    runs more than once in its slice; the line keeps each run's mean cell and
+    their median / min / max, and the method ratio is the ratio of the
+    medians."""
+    out = torchrun(4, ["bench.py", "--gpus", "4", "--steps", "3", "--warmup", "2", "--transport", "host",
+                       "--size", "64K", "--msgs", "2", "--latency-iters", "10", "--sweep", "0", "--extras", "0",
+                       "--ref-iters", "8", "--ipc-extra", "0"])
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert r["value_kind"] == "host-link per direction (not xGMI)", r["value_kind"]
+    for key in ("reference_semantics", "pair_serial_events"):
+        for d in ("uni", "bi"):
+            x = r[key][d]
+            assert len(x["runs"]) >= 2 and x["cells"] == 12 and x["iters"] == 8, (key, d, x)
+            assert x["min"] <= x["median"] <= x["max"] and x["median"] == sorted(x["runs"])[(len(x["runs"]) - 1) // 2] \
+                or len(x["runs"]) % 2 == 0, x
+    for d in ("uni", "bi"):
+        want = round(r["pair_serial_events"][d]["median"] / r["reference_semantics"][d]["median"], 3)
+        assert abs(r["method_ratio"][d] - want) <= 0.002, (d, r["method_ratio"], want)
+    assert r["pair_serial_events"]["bi"]["mismatches"] == 0
+
+
+def test_bench_one_rank_self_sweep(native):
+    """at N = 1 the size sweep runs on the self cell (the
+    driver's N = 1 record then executes the sweep's code every round): 4 KiB
+    in powers of 4 up to --sweep-max, every size verified; here over the CPU
+    host transport.  The reference-method matrices repeat --ref-runs times
+    (each run is milliseconds at N = 1)."""
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--steps", "3", "--warmup", "2",
+                          "--transport", "host", "--size", "64K", "--msgs", "2", "--latency-iters", "10",
+                          "--sweep-max", "1M", "--ref-iters", "8", "--ipc-extra", "0"],
+                         capture_output=True, text=True, timeout=240, cwd=ROOT,
+                         env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert r["value_kind"] == "self-copy (host memory, not a GPU)"
+    sw = r["extras"]["self_sweep"]
+    assert [p["bytes"] for p in sw] == [4096 << (2 * k) for k in range(5)], sw
+    assert all(p["gbs"] > 0 and p["iter_us_p50"] > 0 and p["mismatches"] == 0 for p in sw), sw
+    assert r["extras"]["self_sweep_rccl_comms"] == 1
+    for key in ("reference_semantics", "pair_serial_events"):
+        assert len(r[key]["uni"]["runs"]) == 7 and r[key]["uni"]["median"] > 0, r[key]
+    assert r["untimed_skipped"] is None and r.get("section_errors") is None
