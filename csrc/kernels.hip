@@ -207,59 +207,85 @@ __global__ __launch_bounds__(kBlock) void verify_stride_kernel(const uint4* __re
 // wrote.  The four ds_read_b128 live in one asm statement: hipcc cannot tell
 // which LDS-DMA a ds_read aliases and would put a vmcnt(0) in front of each
 // one; the asm drains its own reads (lgkmcnt(0)).
-// Reads this lane's 16 B of each of the 8 consecutive 1 KiB LDS pieces in
-// one asm statement and drains them (lgkmcnt(0)) before returning.
-__device__ __forceinline__ void lds_read_stages(uint32_t addr, u32x4 (&r)[kLdsStages]) {
-  static_assert(kLdsStages == 8, "one ds_read_b128 per stage below");
-  asm volatile(
-      "ds_read_b128 %0, %8\n\t"
-      "ds_read_b128 %1, %8 offset:1024\n\t"
-      "ds_read_b128 %2, %8 offset:2048\n\t"
-      "ds_read_b128 %3, %8 offset:3072\n\t"
-      "ds_read_b128 %4, %8 offset:4096\n\t"
-      "ds_read_b128 %5, %8 offset:5120\n\t"
-      "ds_read_b128 %6, %8 offset:6144\n\t"
-      "ds_read_b128 %7, %8 offset:7168\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3]), "=v"(r[4]), "=v"(r[5]), "=v"(r[6]), "=v"(r[7])
-      : "v"(addr)
-      : "memory");
+// Reads this lane's 16 B of each of the STAGES consecutive 1 KiB LDS pieces
+// in one asm statement and drains them (lgkmcnt(0)) before returning.
+template <int STAGES>
+__device__ __forceinline__ void lds_read_stages(uint32_t addr, u32x4 (&r)[STAGES]) {
+  static_assert(STAGES == 8 || STAGES == 4, "one ds_read_b128 per stage below");
+  if constexpr (STAGES == 8) {
+    asm volatile(
+        "ds_read_b128 %0, %8\n\t"
+        "ds_read_b128 %1, %8 offset:1024\n\t"
+        "ds_read_b128 %2, %8 offset:2048\n\t"
+        "ds_read_b128 %3, %8 offset:3072\n\t"
+        "ds_read_b128 %4, %8 offset:4096\n\t"
+        "ds_read_b128 %5, %8 offset:5120\n\t"
+        "ds_read_b128 %6, %8 offset:6144\n\t"
+        "ds_read_b128 %7, %8 offset:7168\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3]), "=v"(r[4]), "=v"(r[5]), "=v"(r[6]), "=v"(r[7])
+        : "v"(addr)
+        : "memory");
+  } else {
+    asm volatile(
+        "ds_read_b128 %0, %4\n\t"
+        "ds_read_b128 %1, %4 offset:1024\n\t"
+        "ds_read_b128 %2, %4 offset:2048\n\t"
+        "ds_read_b128 %3, %4 offset:3072\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3])
+        : "v"(addr)
+        : "memory");
+  }
 }
 
-// The LDS-staged kernels' only LDS: 8 KiB of staging slots per wave (32 KiB
-// per workgroup), whose first bytes also carry the block_commit partials.
-typedef uint4 LdsSlots[kWaves][kLdsStages][64];
-static_assert(sizeof(LdsSlots) == 32768, "5 workgroups per CU need <= 32 KiB each");
+// The LDS-staged kernels' only LDS: STAGES KiB of staging slots per wave
+// (8: 32 KiB per workgroup), whose first bytes also carry the block_commit
+// partials.
+template <int STAGES>
+struct LdsSlots {
+  uint4 s[kWaves][STAGES][64];
+};
+static_assert(sizeof(LdsSlots<kLdsStages>) == 32768, "5 workgroups per CU need <= 32 KiB each");
 
-__device__ __forceinline__ LdsSlots& lds_slots() {
-  __shared__ LdsSlots slots;
+template <int STAGES>
+__device__ __forceinline__ LdsSlots<STAGES>& lds_slots() {
+  __shared__ LdsSlots<STAGES> slots;
   return slots;
 }
 
+template <int STAGES>
 __device__ __forceinline__ void lds_block_commit(Partial acc, VerifyAccum* out, uint32_t shard_key) {
-  block_commit(acc, out, shard_key, reinterpret_cast<char*>(&lds_slots()[0][0][0]), sizeof(lds_slots()[0]));
+  block_commit(acc, out, shard_key, reinterpret_cast<char*>(&lds_slots<STAGES>().s[0][0][0]),
+               sizeof(lds_slots<STAGES>().s[0]));
 }
 
 // Blocks `block` of `nblocks` of one buffer: the LDS-staged loop below, with
 // the workgroup's own LDS slots (the single and the batched verify share it).
 // aux = 2 on the LDS-DMA: non-temporal (6.3-6.6 TB/s against 5.7-5.9 with the
 // default cache policy; MI355X_MICROARCH.md ldsdma-fill row agrees).
-template <bool CHECK>
+//
+// Pipelined (PIPE): as soon as a chunk's ds_reads have drained into VGPRs
+// its slots are free, so the wave issues the NEXT chunk's DMAs into them
+// before it checks this one: its loads stay in flight through the PRNG
+// compare instead of stopping while it computes.  Without it the check's
+// VALU work cost the LDS path 4% (6.55 -> 6.30 TB/s, checksum-only vs
+// check, profiles/r5_prof/pmc_summary.txt) against 0.75% for register
+// staging at 32 waves per CU; LDS staging runs 20.
+template <bool CHECK, int STAGES = kLdsStages, bool PIPE = true>
 __device__ __forceinline__ Partial lds_verify_blocks(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
-                                                     uint64_t block, uint64_t nblocks) {
-  constexpr int STAGES = kLdsStages;
-  LdsSlots& slot = lds_slots();
+                                                     uint64_t block, uint64_t nblocks, uint64_t vbase = 0) {
+  auto& slot = lds_slots<STAGES>().s;
   const int lane = threadIdx.x & 63;
   // Wave-uniform by construction; readfirstlane tells the compiler, so the
-  // chunk walk below stays on the scalar unit (no per-lane 64-bit compares
-  // and exec branches around the DMAs).
+  // chunk walk below stays on the scalar unit.
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x / 64));
   const uint64_t sc_vecs = static_cast<uint64_t>(STAGES) * 64;
   const uint64_t n_sc = (nvec + sc_vecs - 1) / sc_vecs;
+  const uint64_t step = nblocks * kWaves;
   const uint32_t lds_addr = static_cast<uint32_t>(
       reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)(&slot[wave][0][lane])));
-  Partial acc{0, 0, ~0ull};
-  for (uint64_t sc = block * kWaves + wave; sc < n_sc; sc += nblocks * kWaves) {
+  auto issue = [&](uint64_t sc) {
 #pragma unroll
     for (int s = 0; s < STAGES; ++s) {
       const uint64_t i = sc * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
@@ -267,75 +293,60 @@ __device__ __forceinline__ Partial lds_verify_blocks(const uint4* __restrict__ p
         __builtin_amdgcn_global_load_lds(static_cast<const void*>(p + i),
                                          (__attribute__((address_space(3))) void*)(&slot[wave][s][0]), 16, 0, 2);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    u32x4 rv[STAGES];
-    lds_read_stages(lds_addr, rv);
-    const uint32_t key = prng_key(seed, sc * sc_vecs * 4);  // wave-uniform
-#pragma unroll
-    for (int s = 0; s < STAGES; ++s) {
-      const uint64_t i = sc * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
-      if (i < nvec) check_vec<CHECK>(make_uint4(rv[s].x, rv[s].y, rv[s].z, rv[s].w), key, i, acc);
-    }
-  }
-  return acc;
-}
-
-// Span form of the same staging (experiment, impl 3): workgroup b walks the
-// contiguous super-chunks [b * per, (b + 1) * per), its 4 waves interleaved,
-// so the resident workgroups read far-apart regions of the buffer at once
-// (as the batched kernel over 32 MiB slots does) instead of one dense window
-// moving through it.
-template <bool CHECK>
-__device__ __forceinline__ Partial lds_verify_blocks_db(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
-                                                        uint64_t block, uint64_t nblocks) {
-  constexpr int STAGES = kLdsStages;
-  LdsSlots& slot = lds_slots();
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x / 64));
-  const uint64_t sc_vecs = static_cast<uint64_t>(STAGES) * 64;
-  const uint64_t n_sc = (nvec + sc_vecs - 1) / sc_vecs;
-  const uint64_t per = (n_sc + nblocks - 1) / nblocks;
-  const uint64_t end = min(n_sc, (block + 1) * per);
-  const uint32_t lds_addr = static_cast<uint32_t>(
-      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)(&slot[wave][0][lane])));
+  };
   Partial acc{0, 0, ~0ull};
-  for (uint64_t sc = block * per + wave; sc < end; sc += kWaves) {
-#pragma unroll
-    for (int s = 0; s < STAGES; ++s) {
-      const uint64_t i = sc * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
-      if (i < nvec)
-        __builtin_amdgcn_global_load_lds(static_cast<const void*>(p + i),
-                                         (__attribute__((address_space(3))) void*)(&slot[wave][s][0]), 16, 0, 2);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  uint64_t sc = block * kWaves + wave;
+  if (PIPE && sc < n_sc) issue(sc);
+  for (; sc < n_sc; sc += step) {
+    if (!PIPE) issue(sc);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this chunk's DMAs (the only ones in flight)
     u32x4 rv[STAGES];
-    lds_read_stages(lds_addr, rv);
-    const uint32_t key = prng_key(seed, sc * sc_vecs * 4);  // wave-uniform
+    lds_read_stages<STAGES>(lds_addr, rv);  // drained (lgkmcnt(0)): the slots are free again
+    if (PIPE && sc + step < n_sc) issue(sc + step);
+    const uint32_t key = prng_key(seed, (vbase + sc * sc_vecs) * 4);  // wave-uniform
 #pragma unroll
     for (int s = 0; s < STAGES; ++s) {
       const uint64_t i = sc * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
-      if (i < nvec) check_vec<CHECK>(make_uint4(rv[s].x, rv[s].y, rv[s].z, rv[s].w), key, i, acc);
+      if (i < nvec) check_vec<CHECK>(make_uint4(rv[s].x, rv[s].y, rv[s].z, rv[s].w), key, vbase + i, acc);
     }
   }
   return acc;
 }
 
+// Experiment (impl 3): the buffer as kSlices equal slices, each walked by a
+// contiguous range of the workgroups (the batched kernel's layout over 32 MiB
+// slots, which reads at the register kernel's rate where one grid-stride walk
+// over the whole buffer trails it).
+constexpr int kSlices = 32;
+
 template <bool CHECK>
-__global__ __launch_bounds__(kBlock) void verify_lds_db_kernel(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
-                                                               const uint8_t* __restrict__ tail, uint32_t tail_bytes,
-                                                               uint64_t tail_offset, VerifyAccum* __restrict__ out) {
-  Partial acc = lds_verify_blocks_db<CHECK>(p, nvec, seed, blockIdx.x, gridDim.x);
+__global__ __launch_bounds__(kBlock) void verify_lds_sliced_kernel(const uint4* __restrict__ p, uint64_t nvec,
+                                                                   uint64_t seed, const uint8_t* __restrict__ tail,
+                                                                   uint32_t tail_bytes, uint64_t tail_offset,
+                                                                   VerifyAccum* __restrict__ out) {
+  // Slices of whole super-chunks (8 KiB); the last one takes the rest.
+  constexpr uint64_t sc_vecs = static_cast<uint64_t>(kLdsStages) * 64;
+  const uint64_t n_sc = (nvec + sc_vecs - 1) / sc_vecs;
+  const uint32_t nb = gridDim.x / kSlices;  // grid is a multiple of kSlices (launch_verify_t)
+  const uint32_t slice = blockIdx.x / nb;
+  const uint64_t per = (n_sc + kSlices - 1) / kSlices;
+  const uint64_t begin = min(n_sc, static_cast<uint64_t>(slice) * per);
+  const uint64_t end_sc = min(n_sc, begin + per);
+  const uint64_t v0 = begin * sc_vecs;
+  const uint64_t v1 = min(nvec, end_sc * sc_vecs);
+  Partial acc{0, 0, ~0ull};
+  if (v1 > v0) acc = lds_verify_blocks<CHECK, kLdsStages, true>(p + v0, v1 - v0, seed, blockIdx.x % nb, nb, v0);
   if (blockIdx.x == 0 && threadIdx.x == 0) check_tail<CHECK>(tail, tail_bytes, tail_offset, seed, acc);
-  lds_block_commit(acc, out, blockIdx.x);
+  lds_block_commit<kLdsStages>(acc, out, blockIdx.x);
 }
 
-template <bool CHECK>
+template <bool CHECK, int STAGES, bool PIPE = true>
 __global__ __launch_bounds__(kBlock) void verify_lds_kernel(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
                                                             const uint8_t* __restrict__ tail, uint32_t tail_bytes,
                                                             uint64_t tail_offset, VerifyAccum* __restrict__ out) {
-  Partial acc = lds_verify_blocks<CHECK>(p, nvec, seed, blockIdx.x, gridDim.x);
+  Partial acc = lds_verify_blocks<CHECK, STAGES, PIPE>(p, nvec, seed, blockIdx.x, gridDim.x);
   if (blockIdx.x == 0 && threadIdx.x == 0) check_tail<CHECK>(tail, tail_bytes, tail_offset, seed, acc);
-  lds_block_commit(acc, out, blockIdx.x);
+  lds_block_commit<STAGES>(acc, out, blockIdx.x);
 }
 
 // Batched verify: up to kMaxVerifyJobs buffers, each with
@@ -367,7 +378,7 @@ __global__ __launch_bounds__(kBlock) void multi_verify_lds_kernel(const MultiVer
   Partial acc = lds_verify_blocks<true>(a.p[job], nvec, a.seed[job], b, nb);
   if (b == 0 && threadIdx.x == 0)
     check_tail<true>(reinterpret_cast<const uint8_t*>(a.p[job] + nvec), a.tail[job], nvec * 16, a.seed[job], acc);
-  lds_block_commit(acc, scratch + static_cast<size_t>(job) * kVerifyShards, b);
+  lds_block_commit<kLdsStages>(acc, scratch + static_cast<size_t>(job) * kVerifyShards, b);
 }
 
 // One workgroup (one wave) per job: reset its shards.
@@ -512,9 +523,10 @@ void launch_verify_t(const uint4* vp, uint64_t nvec, uint64_t seed, const uint8_
   if (impl == VerifyImpl::Stride)
     verify_stride_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
   else if (impl == VerifyImpl::LdsDb)
-    verify_lds_db_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
+    verify_lds_sliced_kernel<CHECK><<<std::max<unsigned>(kSlices, g.grid / kSlices * kSlices), kBlock, 0, stream>>>(
+        vp, nvec, seed, tp, tail, nvec * 16, acc);
   else
-    verify_lds_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
+    verify_lds_kernel<CHECK, kLdsStages><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
 }
 }  // namespace
 

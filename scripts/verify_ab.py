@@ -39,7 +39,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--grids", default="2048,3072,4096,6144,8192", help="lds8 max_grid variants")
-    ap.add_argument("--db", type=int, default=0, help="1: also the double-buffered LDS verify (impl 3)")
+    ap.add_argument("--db", type=int, default=0, help="1: also the experimental LDS verify (impl 3: 32 slices, each walked by its own workgroups)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     nat = test_nccl_p2p_amd.require_native()
@@ -57,7 +57,7 @@ def main():
             "multi_1job": lambda: nat.verify_many_launch([(ptr, sz, 7)], stream),
         }
         if a.db:
-            variants["lds_db"] = lambda: nat.verify_launch(ptr, sz, 7, 3, True, stream)
+            variants["lds8_sliced"] = lambda: nat.verify_launch(ptr, sz, 7, 3, True, stream)
         for g in [int(x) for x in a.grids.split(",") if x]:
             variants["lds8_g%d" % g] = (lambda g=g: nat.verify_launch(ptr, sz, 7, 1, True, stream, g))
             variants["stride_g%d" % g] = (lambda g=g: nat.verify_launch(ptr, sz, 7, 2, True, stream, g))

@@ -129,6 +129,54 @@ def test_kernel_bandwidth_floors(native):
     assert rates["copy"] > 2.5, msg  # payload bytes (read once + written once)
 
 
+def test_verify_staging_ab(native):
+    """VERDICT r5 item 3 (LDS staging must be shown not to cost
+    bandwidth): the LDS-DMA verify (lds8, the default) and register staging
+    (stride) timed alternately in one process on the same buffer -- 12
+    rounds per size, each round 5 event-timed launches of each (the order
+    reversed every other round), the median per kernel -- at 1 GiB and 4
+    GiB.  lds_over_stride = the stride kernel's time over the LDS kernel's,
+    summed over both sizes (>= 1: LDS staging costs nothing); per size too.
+    Floor 0.97 on the sum, 0.95 per size.  (scripts/verify_ab.py runs the
+    same A/B with the grid-cap and batched-kernel variants.)"""
+    stream = torch.cuda.current_stream().cuda_stream
+    ms = {}
+    for gib in (1, 4):
+        nbytes = gib * GIB
+        buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        ptr = buf.data_ptr()
+        native.fill(ptr, nbytes, 3, stream, 0)
+        assert verify(buf, 3).ok
+
+        def lds():
+            native.verify_launch(ptr, nbytes, 3, 1, True, stream)
+
+        def stride():
+            native.verify_launch(ptr, nbytes, 3, 2, True, stream)
+
+        warm(lds, 0.2)
+        runs = {"lds8": [], "stride": []}
+        for r in range(12):
+            for name, fn in ((("lds8", lds), ("stride", stride)) if r % 2 == 0 else
+                             (("stride", stride), ("lds8", lds))):
+                runs[name].append(statistics.median(per_launch_ms(fn, 5)))
+        ms[gib] = {k: statistics.median(v) for k, v in runs.items()}
+        ms[gib]["rounds"] = runs
+        del buf
+        torch.cuda.empty_cache()
+    per_size = {"%dg" % g: round(m["stride"] / m["lds8"], 4) for g, m in ms.items()}
+    total = round(sum(m["stride"] for m in ms.values()) / sum(m["lds8"] for m in ms.values()), 4)
+    rates = {"%dg_%s" % (g, k): round(g * GIB / (m[k] * 1e-3) / 1e12, 3) for g, m in ms.items() for k in ("lds8", "stride")}
+    rec = {"lds_over_stride": total, "per_size": per_size, "tbs": rates,
+           "rounds_ms": {"%dg" % g: m["rounds"] for g, m in ms.items()}}
+    _record("verify_staging_ab", rec)
+    PERF_RECORDS["lds_over_stride"] = total
+    PERF_RECORDS.update({"lds_over_stride_" + k: v for k, v in per_size.items()})
+    print(json.dumps(rec))
+    assert total >= 0.97, rec
+    assert min(per_size.values()) >= 0.95, rec
+
+
 SELF_STEP_CHILD = """
 import json, statistics, sys
 from test_nccl_p2p_amd import require_native
