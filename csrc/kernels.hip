@@ -41,17 +41,22 @@ constexpr uint64_t kBlockVecs = kBlock;     // 16 B vectors per block iteration 
 constexpr uint64_t kMaxGrid = 1ull << 20;   // 4 GiB per grid pass
 constexpr int kStrideUnroll = 4;            // register verify: loads in flight per lane
 constexpr int kLdsStages = 8;               // 1 KiB LDS-DMA pieces per wave (8 KiB per wave)
-// Verify grid caps, from scripts/verify_grid_sweep.py on MI355X (1 GiB /
-// 4 GiB, TB/s, run-to-run noise ~5%): LDS-DMA nt 8 KiB/wave 16/CU 6.44 /
-// 6.64; register stride 16/CU 6.5 / 6.7.  The variants that lost this A/B
-// (4 KiB/wave and default-cache LDS-DMA, the pipelined LDS loop, per-block
-// spans, the full-grid register loop: 5.5-6.4 TB/s) were removed in round 5;
-// their numbers stay in profiles/r1_tuned/, r4_verify_span/.
+// Verify grid caps (workgroups per CU).  Register stride: 16 (2 generations
+// of its 8 resident per CU), from scripts/verify_grid_sweep.py.  LDS-DMA: 8,
+// from round 6's interleaved A/B (scripts/verify_ab.py, profiles/r6_verify_ab/,
+// 5 boxes): at 1 GiB 0.3-4% faster than 16, at 256 MiB and 4 GiB within
+// +-1%.  The batched kernel keeps 16 (its 32 MiB-slot layout was measured
+// there).  Variants that lost their A/Bs: 4 KiB/wave, default-cache LDS-DMA,
+// two 4 KiB halves per wave, per-block spans, 32 slices each walked by its
+// own workgroups, the full-grid register loop (profiles/r1_tuned/,
+// r4_verify_span/, r6_verify_ab/).
 constexpr int kVerifyStridePerCu = 16;
-constexpr int kVerifyLdsPerCu = 16;
-// LDS-staged verify is the default: 8 KiB of non-temporal LDS-DMA per wave
-// runs within 1-2% of register staging (profiles/r1_tuned/verify_grid_sweep.txt:
-// 6.44 / 6.64 TB/s at 1 / 4 GiB vs 6.53 / 6.74).
+constexpr int kVerifyLdsPerCu = 8;
+constexpr int kMultiVerifyPerCu = 16;
+// LDS-staged verify is the default (the north star's LDS staging): at 256 MiB
+// it reads 3-8% faster than register staging, at 1 GiB 2-7% slower, at 4 GiB
+// 0-3% slower, in interleaved A/Bs on 5 boxes (tests/test_zz_perf_floors_gpu.py
+// test_verify_staging_ab prints the box's lds_over_stride on the PERF line).
 constexpr VerifyImpl kDefaultVerify = VerifyImpl::Lds8;
 
 #define HIP_OK(cmd)                                                                          \
@@ -211,32 +216,20 @@ __global__ __launch_bounds__(kBlock) void verify_stride_kernel(const uint4* __re
 // in one asm statement and drains them (lgkmcnt(0)) before returning.
 template <int STAGES>
 __device__ __forceinline__ void lds_read_stages(uint32_t addr, u32x4 (&r)[STAGES]) {
-  static_assert(STAGES == 8 || STAGES == 4, "one ds_read_b128 per stage below");
-  if constexpr (STAGES == 8) {
-    asm volatile(
-        "ds_read_b128 %0, %8\n\t"
-        "ds_read_b128 %1, %8 offset:1024\n\t"
-        "ds_read_b128 %2, %8 offset:2048\n\t"
-        "ds_read_b128 %3, %8 offset:3072\n\t"
-        "ds_read_b128 %4, %8 offset:4096\n\t"
-        "ds_read_b128 %5, %8 offset:5120\n\t"
-        "ds_read_b128 %6, %8 offset:6144\n\t"
-        "ds_read_b128 %7, %8 offset:7168\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3]), "=v"(r[4]), "=v"(r[5]), "=v"(r[6]), "=v"(r[7])
-        : "v"(addr)
-        : "memory");
-  } else {
-    asm volatile(
-        "ds_read_b128 %0, %4\n\t"
-        "ds_read_b128 %1, %4 offset:1024\n\t"
-        "ds_read_b128 %2, %4 offset:2048\n\t"
-        "ds_read_b128 %3, %4 offset:3072\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3])
-        : "v"(addr)
-        : "memory");
-  }
+  static_assert(STAGES == 8, "one ds_read_b128 per stage below");
+  asm volatile(
+      "ds_read_b128 %0, %8\n\t"
+      "ds_read_b128 %1, %8 offset:1024\n\t"
+      "ds_read_b128 %2, %8 offset:2048\n\t"
+      "ds_read_b128 %3, %8 offset:3072\n\t"
+      "ds_read_b128 %4, %8 offset:4096\n\t"
+      "ds_read_b128 %5, %8 offset:5120\n\t"
+      "ds_read_b128 %6, %8 offset:6144\n\t"
+      "ds_read_b128 %7, %8 offset:7168\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3]), "=v"(r[4]), "=v"(r[5]), "=v"(r[6]), "=v"(r[7])
+      : "v"(addr)
+      : "memory");
 }
 
 // The LDS-staged kernels' only LDS: STAGES KiB of staging slots per wave
@@ -265,16 +258,16 @@ __device__ __forceinline__ void lds_block_commit(Partial acc, VerifyAccum* out, 
 // aux = 2 on the LDS-DMA: non-temporal (6.3-6.6 TB/s against 5.7-5.9 with the
 // default cache policy; MI355X_MICROARCH.md ldsdma-fill row agrees).
 //
-// Pipelined (PIPE): as soon as a chunk's ds_reads have drained into VGPRs
-// its slots are free, so the wave issues the NEXT chunk's DMAs into them
-// before it checks this one: its loads stay in flight through the PRNG
-// compare instead of stopping while it computes.  Without it the check's
-// VALU work cost the LDS path 4% (6.55 -> 6.30 TB/s, checksum-only vs
-// check, profiles/r5_prof/pmc_summary.txt) against 0.75% for register
-// staging at 32 waves per CU; LDS staging runs 20.
-template <bool CHECK, int STAGES = kLdsStages, bool PIPE = true>
+// Pipelined: as soon as a chunk's ds_reads have drained into VGPRs its
+// slots are free, so the wave issues the NEXT chunk's DMAs into them before
+// it checks this one, and its loads stay in flight through the PRNG compare.
+// The check's VALU work cost the unpipelined loop 4% (6.55 -> 6.30 TB/s,
+// checksum-only vs check, profiles/r5_prof/pmc_summary.txt) against 0.75%
+// for register staging at 32 waves per CU (LDS staging runs 20); pipelined
+// +0.6% at 1 GiB, +1.2% at 4 GiB in one interleaved A/B (profiles/r6_verify_ab/).
+template <bool CHECK, int STAGES = kLdsStages>
 __device__ __forceinline__ Partial lds_verify_blocks(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
-                                                     uint64_t block, uint64_t nblocks, uint64_t vbase = 0) {
+                                                     uint64_t block, uint64_t nblocks) {
   auto& slot = lds_slots<STAGES>().s;
   const int lane = threadIdx.x & 63;
   // Wave-uniform by construction; readfirstlane tells the compiler, so the
@@ -296,55 +289,27 @@ __device__ __forceinline__ Partial lds_verify_blocks(const uint4* __restrict__ p
   };
   Partial acc{0, 0, ~0ull};
   uint64_t sc = block * kWaves + wave;
-  if (PIPE && sc < n_sc) issue(sc);
+  if (sc < n_sc) issue(sc);
   for (; sc < n_sc; sc += step) {
-    if (!PIPE) issue(sc);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this chunk's DMAs (the only ones in flight)
     u32x4 rv[STAGES];
     lds_read_stages<STAGES>(lds_addr, rv);  // drained (lgkmcnt(0)): the slots are free again
-    if (PIPE && sc + step < n_sc) issue(sc + step);
-    const uint32_t key = prng_key(seed, (vbase + sc * sc_vecs) * 4);  // wave-uniform
+    if (sc + step < n_sc) issue(sc + step);
+    const uint32_t key = prng_key(seed, sc * sc_vecs * 4);  // wave-uniform
 #pragma unroll
     for (int s = 0; s < STAGES; ++s) {
       const uint64_t i = sc * sc_vecs + static_cast<uint64_t>(s) * 64 + lane;
-      if (i < nvec) check_vec<CHECK>(make_uint4(rv[s].x, rv[s].y, rv[s].z, rv[s].w), key, vbase + i, acc);
+      if (i < nvec) check_vec<CHECK>(make_uint4(rv[s].x, rv[s].y, rv[s].z, rv[s].w), key, i, acc);
     }
   }
   return acc;
 }
 
-// Experiment (impl 3): the buffer as kSlices equal slices, each walked by a
-// contiguous range of the workgroups (the batched kernel's layout over 32 MiB
-// slots, which reads at the register kernel's rate where one grid-stride walk
-// over the whole buffer trails it).
-constexpr int kSlices = 32;
-
-template <bool CHECK>
-__global__ __launch_bounds__(kBlock) void verify_lds_sliced_kernel(const uint4* __restrict__ p, uint64_t nvec,
-                                                                   uint64_t seed, const uint8_t* __restrict__ tail,
-                                                                   uint32_t tail_bytes, uint64_t tail_offset,
-                                                                   VerifyAccum* __restrict__ out) {
-  // Slices of whole super-chunks (8 KiB); the last one takes the rest.
-  constexpr uint64_t sc_vecs = static_cast<uint64_t>(kLdsStages) * 64;
-  const uint64_t n_sc = (nvec + sc_vecs - 1) / sc_vecs;
-  const uint32_t nb = gridDim.x / kSlices;  // grid is a multiple of kSlices (launch_verify_t)
-  const uint32_t slice = blockIdx.x / nb;
-  const uint64_t per = (n_sc + kSlices - 1) / kSlices;
-  const uint64_t begin = min(n_sc, static_cast<uint64_t>(slice) * per);
-  const uint64_t end_sc = min(n_sc, begin + per);
-  const uint64_t v0 = begin * sc_vecs;
-  const uint64_t v1 = min(nvec, end_sc * sc_vecs);
-  Partial acc{0, 0, ~0ull};
-  if (v1 > v0) acc = lds_verify_blocks<CHECK, kLdsStages, true>(p + v0, v1 - v0, seed, blockIdx.x % nb, nb, v0);
-  if (blockIdx.x == 0 && threadIdx.x == 0) check_tail<CHECK>(tail, tail_bytes, tail_offset, seed, acc);
-  lds_block_commit<kLdsStages>(acc, out, blockIdx.x);
-}
-
-template <bool CHECK, int STAGES, bool PIPE = true>
+template <bool CHECK, int STAGES>
 __global__ __launch_bounds__(kBlock) void verify_lds_kernel(const uint4* __restrict__ p, uint64_t nvec, uint64_t seed,
                                                             const uint8_t* __restrict__ tail, uint32_t tail_bytes,
                                                             uint64_t tail_offset, VerifyAccum* __restrict__ out) {
-  Partial acc = lds_verify_blocks<CHECK, STAGES, PIPE>(p, nvec, seed, blockIdx.x, gridDim.x);
+  Partial acc = lds_verify_blocks<CHECK, STAGES>(p, nvec, seed, blockIdx.x, gridDim.x);
   if (blockIdx.x == 0 && threadIdx.x == 0) check_tail<CHECK>(tail, tail_bytes, tail_offset, seed, acc);
   lds_block_commit<STAGES>(acc, out, blockIdx.x);
 }
@@ -522,9 +487,6 @@ void launch_verify_t(const uint4* vp, uint64_t nvec, uint64_t seed, const uint8_
                      VerifyImpl impl, const LaunchGeom& g, hipStream_t stream) {
   if (impl == VerifyImpl::Stride)
     verify_stride_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
-  else if (impl == VerifyImpl::LdsDb)
-    verify_lds_sliced_kernel<CHECK><<<std::max<unsigned>(kSlices, g.grid / kSlices * kSlices), kBlock, 0, stream>>>(
-        vp, nvec, seed, tp, tail, nvec * 16, acc);
   else
     verify_lds_kernel<CHECK, kLdsStages><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
 }
@@ -552,9 +514,9 @@ void launch_verify(const void* p, size_t bytes, uint64_t seed, VerifyAccum* acc,
 
 void launch_multi_verify(const VerifyJob* jobs, int njobs, VerifyAccum* scratch, VerifyAccum* out,
                          hipStream_t stream) {
-  // Workgroups: the LDS8 verify's cap (16 per CU) shared by the jobs of a
+  // Workgroups: kMultiVerifyPerCu (16) per CU shared by the jobs of a
   // batch in proportion to their size, at least one each.
-  const uint64_t cap = static_cast<uint64_t>(cu_count()) * kVerifyLdsPerCu;
+  const uint64_t cap = static_cast<uint64_t>(cu_count()) * kMultiVerifyPerCu;
   constexpr uint64_t kChunkVecs = kLdsStages * 64 * kWaves;  // 32 KiB per workgroup pass
   for (int first = 0; first < njobs; first += kMaxVerifyJobs) {
     const int cnt = std::min(kMaxVerifyJobs, njobs - first);

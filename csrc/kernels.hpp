@@ -53,7 +53,7 @@ constexpr int kVerifyShards = 64;
 constexpr size_t verify_accum_bytes() { return sizeof(VerifyAccum) * kVerifyShards; }
 
 // Verify staging (app.hpp parse_verify_impl maps the CLI / Python names).
-enum class VerifyImpl : int { Auto = 0, Lds8 = 1, Stride = 2, LdsDb = 3 };
+enum class VerifyImpl : int { Auto = 0, Lds8 = 1, Stride = 2 };
 // One fill kernel, the full grid; the enum stays so callers name it.
 enum class FillImpl : int { Auto = 0, Grid = 1 };
 

@@ -273,7 +273,7 @@ KernelScratch& scratch() {
 }
 
 dev::VerifyImpl verify_impl_arg(int impl) {
-  if (impl < 0 || impl > static_cast<int>(dev::VerifyImpl::LdsDb))
+  if (impl < 0 || impl > static_cast<int>(dev::VerifyImpl::Stride))
     throw py::value_error(strfmt("verify: impl %d is not 0 (auto), 1 (lds8) or 2 (stride); round 5 removed the "
                                  "other variants (parse_verify_impl names them)", impl));
   return static_cast<dev::VerifyImpl>(impl);

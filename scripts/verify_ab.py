@@ -38,8 +38,7 @@ def main():
     ap.add_argument("--sizes", default="1G,4G")
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--grids", default="2048,3072,4096,6144,8192", help="lds8 max_grid variants")
-    ap.add_argument("--db", type=int, default=0, help="1: also the experimental LDS verify (impl 3: 32 slices, each walked by its own workgroups)")
+    ap.add_argument("--grids", default="2048,4096", help="max_grid variants of both kernels")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     nat = test_nccl_p2p_amd.require_native()
@@ -50,22 +49,24 @@ def main():
         buf = torch.empty(sz, dtype=torch.uint8, device="cuda")
         ptr = buf.data_ptr()
         chunk = 32 << 20
-        slots = [(ptr + i * chunk, chunk, 1000 + i) for i in range(sz // chunk)]
+        # The batched kernel's buffer: its own allocation, 32 MiB slots with a
+        # PRNG stream each (a bench step's receive slots).
+        sbuf = torch.empty(sz, dtype=torch.uint8, device="cuda")
+        slots = [(sbuf.data_ptr() + i * chunk, chunk, 1000 + i) for i in range(sz // chunk)]
+        for p_, n_, s_ in slots:
+            nat.fill(p_, n_, s_, stream)
         variants = {
             "lds8": lambda: nat.verify_launch(ptr, sz, 7, 1, True, stream),
             "stride": lambda: nat.verify_launch(ptr, sz, 7, 2, True, stream),
             "multi_1job": lambda: nat.verify_many_launch([(ptr, sz, 7)], stream),
+            "multi_32m_slots_interleaved": lambda: nat.verify_many_launch(slots, stream),
         }
-        if a.db:
-            variants["lds8_sliced"] = lambda: nat.verify_launch(ptr, sz, 7, 3, True, stream)
         for g in [int(x) for x in a.grids.split(",") if x]:
             variants["lds8_g%d" % g] = (lambda g=g: nat.verify_launch(ptr, sz, 7, 1, True, stream, g))
             variants["stride_g%d" % g] = (lambda g=g: nat.verify_launch(ptr, sz, 7, 2, True, stream, g))
         nat.fill(ptr, sz, 7, stream)
         assert nat.verify(ptr, sz, 7, 1, True, stream)[0] == 0
-        if a.db:
-            assert nat.verify(ptr, sz, 7, 3, True, stream)[0] == 0
-            assert nat.verify(ptr + 16, sz - 4096 - 37, 7, 3, True, stream)[0] > 0  # wrong offset: must fail
+        assert nat.verify(ptr + 16, sz - 4096 - 37, 7, 1, True, stream)[0] > 0  # wrong offset: must fail
         # warm: 0.3 s of launches
         for _ in range(max(4, int(0.3 / (sz / 6e12)))):
             variants["lds8"]()
@@ -75,15 +76,14 @@ def main():
         for r in range(a.rounds):
             for k in (names if r % 2 == 0 else names[::-1]):
                 ms[k].append(statistics.median(per_launch_ms(variants[k], a.reps)))
-        # The batched kernel over 32 MiB slots (a bench step's receive slots):
-        # the same bytes, refilled with a stream per slot.
-        for p_, n_, s_ in slots:
-            nat.fill(p_, n_, s_, stream)
-        multi_ms = [statistics.median(per_launch_ms(lambda: nat.verify_many_launch(slots, stream), a.reps))
-                    for _ in range(a.rounds)]
+        # The same kernels back to back (not interleaved): each variant's
+        # rounds one after the other.
+        b2b = {}
+        for k, fn in (("multi_32m_slots", lambda: nat.verify_many_launch(slots, stream)),
+                      ("lds8_back_to_back", variants["lds8"]), ("stride_back_to_back", variants["stride"])):
+            b2b[k] = [statistics.median(per_launch_ms(fn, a.reps)) for _ in range(a.rounds)]
         assert all(m == 0 for m, _, _ in nat.verify_many(slots, stream))
-        row = {k: round(sz / (statistics.median(v) * 1e-3) / 1e12, 3) for k, v in ms.items()}
-        row["multi_32m_slots"] = round(sz / (statistics.median(multi_ms) * 1e-3) / 1e12, 3)
+        row = {k: round(sz / (statistics.median(v) * 1e-3) / 1e12, 3) for k, v in list(ms.items()) + list(b2b.items())}
         # Per-round ratio lds8 / stride (same round, adjacent launches).
         ratios = [s / l for l, s in zip(ms["lds8"], ms["stride"])]
         row["lds_over_stride_median_of_rounds"] = round(statistics.median(ratios), 4)
@@ -92,7 +92,7 @@ def main():
         row["verify_geometry_stride"] = nat.verify_geometry(sz, 2)
         out[nat.format_size(sz)] = row
         print(nat.format_size(sz), json.dumps(row), flush=True)
-        del buf
+        del buf, sbuf
         torch.cuda.empty_cache()
     if a.json:
         with open(a.json, "w") as f:
