@@ -407,7 +407,15 @@ class HeadlineMixin:
             return FALLBACK
         if self.n == 1:
             return SELF_COPY if self.use_gpu else "self-copy (host memory, not a GPU)"
-        return XGMI_LINK if self.use_gpu else "%s-link per direction (not xGMI)" % self.h.sess.transport
+        if not self.use_gpu:
+            return "%s-link per direction (not xGMI)" % self.h.sess.transport
+        # Ranks sharing a GPU (the emulated node of the tests: PCI bus ids
+        # repeat) move bytes within one GPU's memory, not over a link.
+        devs = (self.h.provenance or {}).get("rank_devices") or []
+        pcis = [d.get("pci") for d in devs]
+        if len(pcis) == self.n and all(pcis) and len(set(pcis)) < self.n:
+            return "emulated: %d ranks on %d GPU(s), per direction (not xGMI)" % (self.n, len(set(pcis)))
+        return XGMI_LINK
 
     def base_result(self) -> dict:
         """The JSON line as far as the timed steps go; the untimed sections

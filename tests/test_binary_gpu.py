@@ -85,6 +85,15 @@ def test_bench_contract_single_gpu():
     assert stock["env"]["P2P_RCCL_UNROLL"] == "0" and stock["env"]["RCCL_UNROLL_FACTOR"] is None, stock
     assert stock["env"]["GPU_MAX_HW_QUEUES"] in (None, "4"), stock
     assert r["method_ratio_stock"]["uni"] > 0 and r["method_ratio"]["uni"] > 0
+    # >= 5 runs of each reference-method matrix (in
+    # the stock child too), ratios of the medians; the size sweep on the self
+    # cell, every size verified; value labelled as the on-GPU self copy.
+    for x in (ref, stock, r["pair_serial_events"]):
+        assert len(x["uni"]["runs"]) >= 5 and x["uni"]["min"] <= x["uni"]["median"] <= x["uni"]["max"], x
+    assert abs(r["method_ratio"]["uni"] - r["pair_serial_events"]["uni"]["median"] / ref["uni"]["median"]) < 0.002
+    sw = r["extras"]["self_sweep"]
+    assert len(sw) >= 10 and all(p["mismatches"] == 0 and p["gbs"] > 0 for p in sw), sw
+    assert r["value_kind"] == "self-copy (on-GPU HBM)"
 
 
 def test_topology_probe(exe):

@@ -239,6 +239,7 @@ def test_bench_emulated_node(nranks):
     assert out.returncode == 0, progress
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert r["n_gpus"] == nranks and r["verify_mismatches"] == 0
+    assert r["value_kind"] == "emulated: %d ranks on 1 GPU(s), per direction (not xGMI)" % nranks, r["value_kind"]
     assert r["matrix_cells"] == "%d/%d" % (nranks * (nranks - 1), nranks * (nranks - 1))
     m, lat = r["matrix_gbs"], r["latency_p50_us_matrix"]
     assert len(m) == nranks and all(m[a][b] > 0 for a in range(nranks) for b in range(nranks) if a != b)

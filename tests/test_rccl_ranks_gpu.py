@@ -78,6 +78,10 @@ def test_bench_four_rccl_ranks(tmp_path):
     assert out.returncode == 0, progress[-3000:]
     r = json.loads(out_json.read_text())
     assert r["transport"] == "rccl" and r["headline_fallback"] is None
+    assert r["value_kind"].startswith("emulated: 4 ranks on 1 GPU"), r["value_kind"]
+    # The reference-method matrices repeat, in-process and in the stock child.
+    for key in ("reference_semantics", "reference_semantics_stock", "pair_serial_events"):
+        assert all(len(r[key][d]["runs"]) >= 2 for d in ("uni", "bi")), r[key]
     assert r["verify_mismatches"] == 0 and r["verify_coverage"] == 1.0 and r["matrix_cells"] == "12/12"
     tuned = r["posting"]["tuning_ms_per_step"]
     assert set(tuned) == {"comms1_per_message", "comms1_batch", "comms2_batch", "comms4_batch", "comms8_batch"}, tuned
