@@ -41,6 +41,14 @@ constexpr uint64_t kBlockVecs = kBlock;     // 16 B vectors per block iteration 
 constexpr uint64_t kMaxGrid = 1ull << 20;   // 4 GiB per grid pass
 constexpr int kStrideUnroll = 4;            // register verify: loads in flight per lane
 constexpr int kLdsStages = 8;               // 1 KiB LDS-DMA pieces per wave (8 KiB per wave)
+// Below this size the single-buffer LDS verify stages 4 KiB per wave (16 KiB
+// of LDS per workgroup: 8 workgroups, 32 waves per CU, the register kernel's
+// occupancy) instead of 8 KiB (20 waves).  Interleaved A/B (scripts/verify_ab.py
+// --impl3, profiles/r6_verify_ab/r6_vab11-12): 4 KiB per wave read 2.4% faster
+// at 512 MiB, 1.7-2.4% at 1 GiB (= register staging), equal at 2 GiB and 4.6%
+// slower at 4 GiB.
+constexpr uint64_t kLds4Below = 2ull << 30;
+constexpr int lds_stages_for(uint64_t bytes) { return bytes < kLds4Below ? 4 : kLdsStages; }
 // Verify grid caps (workgroups per CU).  Register stride: 16 (2 generations
 // of its 8 resident per CU), from scripts/verify_grid_sweep.py.  LDS-DMA: 8,
 // from round 6's interleaved A/B (scripts/verify_ab.py, profiles/r6_verify_ab/,
@@ -53,10 +61,11 @@ constexpr int kLdsStages = 8;               // 1 KiB LDS-DMA pieces per wave (8 
 constexpr int kVerifyStridePerCu = 16;
 constexpr int kVerifyLdsPerCu = 8;
 constexpr int kMultiVerifyPerCu = 16;
-// LDS-staged verify is the default (the north star's LDS staging): at 256 MiB
-// it reads 3-8% faster than register staging, at 1 GiB 2-7% slower, at 4 GiB
-// 0-3% slower, in interleaved A/Bs on 5 boxes (tests/test_zz_perf_floors_gpu.py
-// test_verify_staging_ab prints the box's lds_over_stride on the PERF line).
+// LDS-staged verify is the default (the north star's LDS staging).  Against
+// register staging in interleaved A/Bs (profiles/r6_verify_ab/): 3-8% faster
+// at 256 MiB, 0.97-1.0x at 1 GiB (4 KiB per wave), 0.98-1.0x at 2-4 GiB (8 KiB
+// per wave); tests/test_zz_perf_floors_gpu.py test_verify_staging_ab puts the
+// box's lds_over_stride on the PERF line (0.991: 1 GiB 0.973, 4 GiB 0.996).
 constexpr VerifyImpl kDefaultVerify = VerifyImpl::Lds8;
 
 #define HIP_OK(cmd)                                                                          \
@@ -203,8 +212,8 @@ __global__ __launch_bounds__(kBlock) void verify_stride_kernel(const uint4* __re
   block_commit(acc, out, blockIdx.x, reinterpret_cast<char*>(red), sizeof(Partial));
 }
 
-// LDS-staged verify.  Wave g owns super-chunk g (kLdsStages consecutive KiB)
-// of each grid pass: it issues kLdsStages LDS-DMA pieces
+// LDS-staged verify.  Wave g owns super-chunk g (STAGES consecutive KiB: 4 or
+// 8, lds_stages_for) of each grid pass: it issues STAGES LDS-DMA pieces
 // (global_load_lds_dwordx4: the wave's 64 lanes x 16 B land contiguously at
 // the LDS address in M0), waits for its own DMAs (vmcnt(0)), reads each lane's
 // 16 B back with ds_read_b128 (contiguous per lane: bank-conflict free) and
@@ -216,20 +225,32 @@ __global__ __launch_bounds__(kBlock) void verify_stride_kernel(const uint4* __re
 // in one asm statement and drains them (lgkmcnt(0)) before returning.
 template <int STAGES>
 __device__ __forceinline__ void lds_read_stages(uint32_t addr, u32x4 (&r)[STAGES]) {
-  static_assert(STAGES == 8, "one ds_read_b128 per stage below");
-  asm volatile(
-      "ds_read_b128 %0, %8\n\t"
-      "ds_read_b128 %1, %8 offset:1024\n\t"
-      "ds_read_b128 %2, %8 offset:2048\n\t"
-      "ds_read_b128 %3, %8 offset:3072\n\t"
-      "ds_read_b128 %4, %8 offset:4096\n\t"
-      "ds_read_b128 %5, %8 offset:5120\n\t"
-      "ds_read_b128 %6, %8 offset:6144\n\t"
-      "ds_read_b128 %7, %8 offset:7168\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3]), "=v"(r[4]), "=v"(r[5]), "=v"(r[6]), "=v"(r[7])
-      : "v"(addr)
-      : "memory");
+  static_assert(STAGES == 8 || STAGES == 4, "one ds_read_b128 per stage below (lds_stages_for)");
+  if constexpr (STAGES == 8) {
+    asm volatile(
+        "ds_read_b128 %0, %8\n\t"
+        "ds_read_b128 %1, %8 offset:1024\n\t"
+        "ds_read_b128 %2, %8 offset:2048\n\t"
+        "ds_read_b128 %3, %8 offset:3072\n\t"
+        "ds_read_b128 %4, %8 offset:4096\n\t"
+        "ds_read_b128 %5, %8 offset:5120\n\t"
+        "ds_read_b128 %6, %8 offset:6144\n\t"
+        "ds_read_b128 %7, %8 offset:7168\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3]), "=v"(r[4]), "=v"(r[5]), "=v"(r[6]), "=v"(r[7])
+        : "v"(addr)
+        : "memory");
+  } else {
+    asm volatile(
+        "ds_read_b128 %0, %4\n\t"
+        "ds_read_b128 %1, %4 offset:1024\n\t"
+        "ds_read_b128 %2, %4 offset:2048\n\t"
+        "ds_read_b128 %3, %4 offset:3072\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3])
+        : "v"(addr)
+        : "memory");
+  }
 }
 
 // The LDS-staged kernels' only LDS: STAGES KiB of staging slots per wave
@@ -447,11 +468,12 @@ LaunchGeom verify_geometry(size_t bytes, VerifyImpl impl, unsigned max_grid) {
     const uint64_t tiles = (nvec + kBlock * kStrideUnroll - 1) / (kBlock * kStrideUnroll);
     g.grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min(tiles, cap)));
   } else {
-    // Waves of 8 KiB chunks, and the 8 KiB of LDS each wave owns.
-    const uint64_t sc_vecs = static_cast<uint64_t>(kLdsStages) * 64;
+    // Waves of 4 or 8 KiB chunks (lds_stages_for), and the LDS each wave owns.
+    const int stages = lds_stages_for(bytes);
+    const uint64_t sc_vecs = static_cast<uint64_t>(stages) * 64;
     const uint64_t waves = (nvec + sc_vecs - 1) / sc_vecs;
     g.grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min((waves + kWaves - 1) / kWaves, cap)));
-    g.lds_bytes = sizeof(uint4) * kWaves * kLdsStages * 64;
+    g.lds_bytes = sizeof(uint4) * kWaves * stages * 64;
   }
   return g;
 }
@@ -487,6 +509,8 @@ void launch_verify_t(const uint4* vp, uint64_t nvec, uint64_t seed, const uint8_
                      VerifyImpl impl, const LaunchGeom& g, hipStream_t stream) {
   if (impl == VerifyImpl::Stride)
     verify_stride_kernel<CHECK><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
+  else if (lds_stages_for(nvec * 16) == 4)
+    verify_lds_kernel<CHECK, 4><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
   else
     verify_lds_kernel<CHECK, kLdsStages><<<g.grid, kBlock, 0, stream>>>(vp, nvec, seed, tp, tail, nvec * 16, acc);
 }

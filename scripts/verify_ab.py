@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--grids", default="2048,4096", help="max_grid variants of both kernels")
+    ap.add_argument("--impl3", type=int, default=0, help="1: also verify impl 3 (an experiment under A/B, if built)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     nat = test_nccl_p2p_amd.require_native()
@@ -61,12 +62,19 @@ def main():
             "multi_1job": lambda: nat.verify_many_launch([(ptr, sz, 7)], stream),
             "multi_32m_slots_interleaved": lambda: nat.verify_many_launch(slots, stream),
         }
+        if a.impl3:  # an experiment under A/B, when the build has one (round 6: 4 KiB per wave)
+            variants["impl3"] = lambda: nat.verify_launch(ptr, sz, 7, 3, True, stream)
+            for g in [int(x) for x in a.grids.split(",") if x]:
+                variants["impl3_g%d" % g] = (lambda g=g: nat.verify_launch(ptr, sz, 7, 3, True, stream, g))
         for g in [int(x) for x in a.grids.split(",") if x]:
             variants["lds8_g%d" % g] = (lambda g=g: nat.verify_launch(ptr, sz, 7, 1, True, stream, g))
             variants["stride_g%d" % g] = (lambda g=g: nat.verify_launch(ptr, sz, 7, 2, True, stream, g))
         nat.fill(ptr, sz, 7, stream)
         assert nat.verify(ptr, sz, 7, 1, True, stream)[0] == 0
         assert nat.verify(ptr + 16, sz - 4096 - 37, 7, 1, True, stream)[0] > 0  # wrong offset: must fail
+        if a.impl3:
+            assert nat.verify(ptr, sz, 7, 3, True, stream)[0] == 0
+            assert nat.verify(ptr + 16, sz - 4096 - 37, 7, 3, True, stream)[0] > 0
         # warm: 0.3 s of launches
         for _ in range(max(4, int(0.3 / (sz / 6e12)))):
             variants["lds8"]()
