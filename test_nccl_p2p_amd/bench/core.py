@@ -406,6 +406,20 @@ def combine_runs(runs, n: int) -> dict:
             "spread": round((max(per_run) - min(per_run)) / med, 4) if per_run and med else None}
 
 
+def child_runs(ref: dict, iters: dict, slice_left: float, start_s: float) -> dict:
+    """Runs per direction mode for the stock-settings child: as many as the
+    in-process matrices had (ref[d]["runs"]), or as many as the slice left
+    holds after the child's start at their measured time per run
+    (ref[d]["run_s"], with 20% margin) -- at least one."""
+    per_dir = max(0.0, slice_left - start_s) / max(1, len(iters))
+    out = {}
+    for d in iters:
+        have = len(ref[d].get("runs") or [1])
+        fit = int(per_dir / (1.2 * max(ref[d].get("run_s") or 0.0, 1e-3)))
+        out[d] = max(1, min(have, fit))
+    return out
+
+
 def method_ratios(ours: dict, ref: dict, value: float, n: int) -> dict:
     """method_ratio[dir]: our methodology over the reference's on the same
     serial pair schedule (the median over repeats of each run's mean cell,

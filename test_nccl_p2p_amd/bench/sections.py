@@ -18,11 +18,12 @@ import time
 import torch.distributed as dist
 
 from test_nccl_p2p_amd.bench.compare import REF_STOCK, steps_through, stock_env
-from test_nccl_p2p_amd.bench.core import (RESERVE_S, SECTION_SLICES, combine_runs, free_port, log, method_ratios,
-                                          pair_matrix_summary, reserved_after)
+from test_nccl_p2p_amd.bench.core import (RESERVE_S, SECTION_SLICES, child_runs, combine_runs, free_port, log,
+                                          method_ratios, pair_matrix_summary, reserved_after)
 from test_nccl_p2p_amd.utils.proc import run_child
 
 HERE = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # the repository root
+CHILD_START_S = 6.0  # a bench.py child's start to its first RCCL run (~4.6 s on the box, profiles/r5_final/)
 
 
 class SectionsMixin:
@@ -216,19 +217,20 @@ class SectionsMixin:
                                          % (least, warmup, need, left)}
                     break
                 iters = int(self.agreed_min(min(args.ref_iters, max(least, fit))))
-                runs = []
+                runs, run_secs = [], []
                 while True:
                     t0 = time.monotonic()
                     r = json.loads(session.run(mode="pair" if n > 1 else "self", dir=d, bytes=self.size, iters=iters,
                                                warmup=warmup, timing=timing, verify=verify, warm=warmup > 0))
                     run_s = self.allmax(time.monotonic() - t0)
                     runs.append(pair_matrix_summary(r, n))
+                    run_secs.append(run_s)
                     # Everything the run took, charged to its iterations (conservative).
                     per_iter = max(1e-6, run_s / cells / (warmup + iters))
                     share = self.slice_remaining() / (len(dirs) - len(out))
                     if len(runs) >= max(1, args.ref_runs) or not self.agree(1.2 * run_s + 0.05 <= share):
                         break
-                out[d] = dict(combine_runs(runs, n), iters=iters)
+                out[d] = dict(combine_runs(runs, n), iters=iters, run_s=round(statistics.median(run_secs), 4))
                 if iters != args.ref_iters:
                     out[d]["iters_scaled_from"] = args.ref_iters
             return out
@@ -258,8 +260,10 @@ class SectionsMixin:
             if not iters:
                 return {"skipped": "the reference-method matrices it repeats were skipped"}
             # As many runs as the in-process matrices had, repeated inside the
-            # child: its start (~4.6 s) is paid once.
-            runs = {d: len(ref[d].get("runs") or [1]) for d in iters}
+            # child (its start, ~4.6 s, is paid once), or as many as this
+            # section's slice holds at their measured time per run, at least
+            # one; agreed (the same numbers on every rank: ref is collective).
+            runs = child_runs(ref, iters, -self.allmax(-self.slice_remaining()), CHILD_START_S)
             r = self.child_job(REF_STOCK, ["--child-ref-iters", json.dumps(iters), "--child-ref-runs",
                                            json.dumps(runs), "--hw-queues", "0"], env=stock_env())
             if r is None or "error" in r:

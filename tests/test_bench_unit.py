@@ -392,3 +392,20 @@ def test_watchdog_ends_the_process_when_the_abort_blocks(native):
     line = json.loads(out.stdout.strip().splitlines()[-1])
     assert line["deadline_hit"] is True and line["section_errors"] == {"latency": "deadline reached while running"}
     assert "abort from the watchdog (engine idle) still running after" in out.stderr, out.stderr[-2000:]
+
+
+def test_child_runs_fit_the_slice():
+    """The stock-settings child repeats as many runs as the in-process
+    reference matrices had, unless the section's slice (less the child's
+    start) holds fewer at their measured time per run; at least one."""
+    from test_nccl_p2p_amd.bench.core import child_runs
+
+    ref = {"uni": {"runs": [1.0] * 7, "run_s": 0.006}, "bi": {"runs": [1.0] * 3, "run_s": 1.0}}
+    # N = 1: 7 runs of 6 ms fit easily.
+    assert child_runs(ref, {"uni": 128}, 12.0, 6.0) == {"uni": 7}
+    # 6 s left for two modes: 3 s each, 1.2 s per bi run with the margin -> 2 of its 3.
+    assert child_runs(ref, {"uni": 128, "bi": 128}, 12.0, 6.0) == {"uni": 7, "bi": 2}
+    # No time left: still one run each.
+    assert child_runs(ref, {"uni": 128, "bi": 128}, 3.0, 6.0) == {"uni": 1, "bi": 1}
+    # Records without run_s (or runs) fall back to one run per mode, bounded the same way.
+    assert child_runs({"uni": {}}, {"uni": 8}, 60.0, 6.0) == {"uni": 1}
