@@ -66,6 +66,11 @@ class SectionsMixin:
                                                   else "no time left (or another rank's sessions failed)"))
             return None
         self.slice_left = left
+        # Its own slice (SECTION_SLICES), for work that is optional: the
+        # reference matrices' repeats stop there rather than take the slack
+        # the sections after the BASELINE ones (the IPC comparisons, the
+        # xGMI pair sweep) would otherwise get.
+        self.slice_own = min(left, mine) if mine else left
         self.slice_t0 = time.monotonic()
         for s in self.live:
             s.set_timeout(max(1.0, min(self.args.timeout, wait_left)))
@@ -92,6 +97,11 @@ class SectionsMixin:
         """Seconds the running section has left of its slice."""
         return self.slice_left - (time.monotonic() - self.slice_t0)
 
+    def own_slice_remaining(self) -> float:
+        """Seconds the running section has left of its own SECTION_SLICES
+        share (slice_own)."""
+        return self.slice_own - (time.monotonic() - self.slice_t0)
+
     def plan_sections(self):
         """The SECTION_SLICES sections this run will attempt (their slices are
         reserved while the ones before them run)."""
@@ -110,7 +120,7 @@ class SectionsMixin:
         if n == 1 and args.sweep:
             active.add("self_sweep")
         self.active_sections = active
-        self.slice_left, self.slice_t0 = 0.0, time.monotonic()
+        self.slice_left, self.slice_own, self.slice_t0 = 0.0, 0.0, time.monotonic()
         self.broken = None
 
     # At most this many processes may hold one GPU (the test boxes' limit is
@@ -198,10 +208,10 @@ class SectionsMixin:
             # fixed 10 ms per cell (barriers, fill, verify), later ones at the
             # previous mode's measured time per cell and iteration.  Agreed on
             # every rank.  Then the same matrix again, up to --ref-runs runs
-            # in all, while this mode's share of the slice holds one more
-            # (at N = 1 a run is ~6 ms, so all of them;
-            # at N = 8 over xGMI about one); combine_runs keeps each run's
-            # mean cell and the median the ratios use.
+            # in all, while this mode's share of the section's own slice
+            # holds one more (at N = 1 a run is ~6 ms, so
+            # all of them; at N = 8 over xGMI about one); combine_runs keeps
+            # each run's mean cell and the median the ratios use.
             out, per_iter = {}, self.size * slowdown / rate + 50e-6
             for d in dirs:
                 left = self.slice_remaining() / (len(dirs) - len(out))
@@ -227,7 +237,7 @@ class SectionsMixin:
                     run_secs.append(run_s)
                     # Everything the run took, charged to its iterations (conservative).
                     per_iter = max(1e-6, run_s / cells / (warmup + iters))
-                    share = self.slice_remaining() / (len(dirs) - len(out))
+                    share = self.own_slice_remaining() / (len(dirs) - len(out))
                     if len(runs) >= max(1, args.ref_runs) or not self.agree(1.2 * run_s + 0.05 <= share):
                         break
                 out[d] = dict(combine_runs(runs, n), iters=iters, run_s=round(statistics.median(run_secs), 4))
@@ -263,7 +273,7 @@ class SectionsMixin:
             # child (its start, ~4.6 s, is paid once), or as many as this
             # section's slice holds at their measured time per run, at least
             # one; agreed (the same numbers on every rank: ref is collective).
-            runs = child_runs(ref, iters, -self.allmax(-self.slice_remaining()), CHILD_START_S)
+            runs = child_runs(ref, iters, -self.allmax(-self.own_slice_remaining()), CHILD_START_S)
             r = self.child_job(REF_STOCK, ["--child-ref-iters", json.dumps(iters), "--child-ref-runs",
                                            json.dumps(runs), "--hw-queues", "0"], env=stock_env())
             if r is None or "error" in r:
