@@ -218,11 +218,10 @@ __global__ __launch_bounds__(kBlock) void verify_stride_kernel(const uint4* __re
 // the LDS address in M0), waits for its own DMAs (vmcnt(0)), reads each lane's
 // 16 B back with ds_read_b128 (contiguous per lane: bank-conflict free) and
 // compares.  No workgroup barrier: a wave only reads bytes its own DMAs
-// wrote.  The four ds_read_b128 live in one asm statement: hipcc cannot tell
+// wrote.  The ds_read_b128s live in one asm statement: hipcc cannot tell
 // which LDS-DMA a ds_read aliases and would put a vmcnt(0) in front of each
-// one; the asm drains its own reads (lgkmcnt(0)).
-// Reads this lane's 16 B of each of the STAGES consecutive 1 KiB LDS pieces
-// in one asm statement and drains them (lgkmcnt(0)) before returning.
+// one.  lds_read_stages reads this lane's 16 B of each of the STAGES
+// consecutive 1 KiB LDS pieces and drains them (lgkmcnt(0)) before returning.
 template <int STAGES>
 __device__ __forceinline__ void lds_read_stages(uint32_t addr, u32x4 (&r)[STAGES]) {
   static_assert(STAGES == 8 || STAGES == 4, "one ds_read_b128 per stage below (lds_stages_for)");
