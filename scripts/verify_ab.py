@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Interleaved A/B of the verify staging: the LDS-DMA
-verify (lds8) against register staging (stride) on one buffer, plus the
-variants that could explain a gap between them -- the lds8 grid cap
-(max_grid) and the batched kernel over the same bytes as one job or as 32 MiB
-slots.  Every round times every variant (`reps` launches, each on its own
+verify (lds8; 4 KiB per wave below 2 GiB, 8 KiB from 2 GiB) against register
+staging (stride) on one buffer, plus the variants that could explain a gap
+between them -- the grid cap (max_grid) and the batched kernel over the same
+bytes as one job or as 32 MiB slots.  (Round 6's experiments ran here as a
+temporary impl 3: profiles/r6_verify_ab/.)  Every round times every variant (`reps` launches, each on its own
 event pair, median), the order reversed on alternate rounds, so drift of the
 clock or the HBM temperature hits all variants alike; the result per variant
 is the median over rounds.
@@ -39,7 +40,6 @@ def main():
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--grids", default="2048,4096", help="max_grid variants of both kernels")
-    ap.add_argument("--impl3", type=int, default=0, help="1: also verify impl 3 (an experiment under A/B, if built)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     nat = test_nccl_p2p_amd.require_native()
@@ -62,19 +62,12 @@ def main():
             "multi_1job": lambda: nat.verify_many_launch([(ptr, sz, 7)], stream),
             "multi_32m_slots_interleaved": lambda: nat.verify_many_launch(slots, stream),
         }
-        if a.impl3:  # an experiment under A/B, when the build has one (round 6: 4 KiB per wave)
-            variants["impl3"] = lambda: nat.verify_launch(ptr, sz, 7, 3, True, stream)
-            for g in [int(x) for x in a.grids.split(",") if x]:
-                variants["impl3_g%d" % g] = (lambda g=g: nat.verify_launch(ptr, sz, 7, 3, True, stream, g))
         for g in [int(x) for x in a.grids.split(",") if x]:
             variants["lds8_g%d" % g] = (lambda g=g: nat.verify_launch(ptr, sz, 7, 1, True, stream, g))
             variants["stride_g%d" % g] = (lambda g=g: nat.verify_launch(ptr, sz, 7, 2, True, stream, g))
         nat.fill(ptr, sz, 7, stream)
         assert nat.verify(ptr, sz, 7, 1, True, stream)[0] == 0
         assert nat.verify(ptr + 16, sz - 4096 - 37, 7, 1, True, stream)[0] > 0  # wrong offset: must fail
-        if a.impl3:
-            assert nat.verify(ptr, sz, 7, 3, True, stream)[0] == 0
-            assert nat.verify(ptr + 16, sz - 4096 - 37, 7, 3, True, stream)[0] > 0
         # warm: 0.3 s of launches
         for _ in range(max(4, int(0.3 / (sz / 6e12)))):
             variants["lds8"]()
