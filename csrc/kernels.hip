@@ -45,9 +45,8 @@ constexpr int kLdsStages = 8;               // 1 KiB LDS-DMA pieces per wave (8 
 // of LDS per workgroup: 8 workgroups, 32 waves per CU, the register kernel's
 // occupancy) instead of 8 KiB (20 waves).  Interleaved A/B (scripts/verify_ab.py
 // with 4 KiB per wave as a temporary impl 3, profiles/r6_verify_ab/r6_vab11-12):
-// 4 KiB per wave read 2.4% faster
-// at 512 MiB, 1.7-2.4% at 1 GiB (= register staging), equal at 2 GiB and 4.6%
-// slower at 4 GiB.
+// 4 KiB per wave read 2.4% faster at 512 MiB, 1.7-2.4% at 1 GiB (= register
+// staging), equal at 2 GiB and 4.6% slower at 4 GiB.
 constexpr uint64_t kLds4Below = 2ull << 30;
 constexpr int lds_stages_for(uint64_t bytes) { return bytes < kLds4Below ? 4 : kLdsStages; }
 // Verify grid caps (workgroups per CU).  Register stride: 16 (2 generations
