@@ -294,7 +294,7 @@ def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> thread
             reporter.emit(deadline_hit=True, untimed_skipped=state.get("skipped") or None,
                           section_errors=errors or None)
             kill_children(state)
-            outcome = {"how": "not aborted within %.1f s" % ABORT_GRACE_S}
+            outcome = {"how": None, "aborting": False}
             done = threading.Event()
 
             def aborter():
@@ -308,12 +308,12 @@ def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> thread
                         # The main thread outside the engine (a gloo barrier, a
                         # torch sync, Python): no RCCL call can be running, abort
                         # from here.
-                        outcome["how"] = "abort from the watchdog (engine idle) still running after %.1f s" % (
-                            ABORT_GRACE_S)
-                        if nat.abort_if_idle():
+                        outcome["aborting"] = True
+                        idle = nat.abort_if_idle()
+                        outcome["aborting"] = False
+                        if idle:
                             outcome["how"] = "aborted by the watchdog (engine idle)"
                             break
-                        outcome["how"] = "not aborted within %.1f s" % ABORT_GRACE_S
                         time.sleep(0.02)
                 except Exception as e:  # noqa: BLE001 -- the process ends either way
                     outcome["how"] = "abort failed: %s" % e
@@ -322,7 +322,9 @@ def start_watchdog(deadline: Deadline, reporter: Reporter, nat, state) -> thread
 
             threading.Thread(target=aborter, name="bench-aborter", daemon=True).start()
             done.wait(ABORT_GRACE_S)
-            log("bench: communicators %s" % outcome["how"])
+            how = outcome["how"] or ("abort from the watchdog (engine idle) still running after %.1f s"
+                                     if outcome["aborting"] else "not aborted within %.1f s") % ABORT_GRACE_S
+            log("bench: communicators %s" % how)
             # Every rank's watchdog fires at about the same time; a launcher
             # (torchrun) SIGTERMs the other ranks as soon as one exits, which
             # would cut a peer's own abort short.  Linger until a common point

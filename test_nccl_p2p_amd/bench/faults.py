@@ -97,10 +97,6 @@ class Faults:
         self.fail_candidate = env.get("P2P_BENCH_FAIL_CANDIDATE") or None
         self.hang_spec = env.get("P2P_BENCH_HANG", "")
 
-    @property
-    def any(self) -> bool:
-        return bool(self.headline_transport or self.fail_candidate or self.hang_spec)
-
     def fail_headline(self, transport: str):
         """The headline through `transport` fails on every rank, as a
         communicator that cannot be set up does."""

@@ -409,3 +409,29 @@ def test_child_runs_fit_the_slice():
     assert child_runs(ref, {"uni": 128, "bi": 128}, 3.0, 6.0) == {"uni": 1, "bi": 1}
     # Records without run_s (or runs) fall back to one run per mode, bounded the same way.
     assert child_runs({"uni": {}}, {"uni": 8}, 60.0, 6.0) == {"uni": 1}
+
+
+def test_faults_read_once_and_fire_at_named_points():
+    """VERDICT r5 item 6: bench/faults.py reads every P2P_BENCH_* hook once;
+    the measured flow only calls its named points."""
+    import pytest
+
+    from test_nccl_p2p_amd.bench.faults import Faults
+
+    env = {"P2P_BENCH_FAIL_HEADLINE": "rccl", "P2P_BENCH_FAIL_CANDIDATE": "4,1,tuning",
+           "P2P_BENCH_HANG": "candidate:rccl:1,0:stall@1;latency@3"}
+    last, first = Faults(3, 4, env), Faults(1, 4, env)
+    with pytest.raises(RuntimeError, match="injected headline failure"):
+        last.fail_headline("rccl")
+    last.fail_headline("ipc")  # other transports: nothing
+    with pytest.raises(RuntimeError, match="injected tuning failure"):
+        last.candidate_fail(4, 1, "tuning")
+    last.candidate_fail(4, 1, "connect")  # that spec names the tuning pass
+    first.candidate_fail(4, 1, "tuning")  # only the last rank fails
+    assert first.candidate("rccl", 1, 0) == "stall" and last.candidate("rccl", 1, 0) is None
+    first.section("latency")  # rank 3's hang, not rank 1's
+    first.teardown()
+    # Read once: a later change of the environment does not reach the object.
+    quiet = Faults(0, 1, {})
+    assert quiet.candidate("rccl", 1, 0) is None and quiet.fail_candidate is None
+    quiet.fail_headline("rccl")
