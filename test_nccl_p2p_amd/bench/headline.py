@@ -293,10 +293,13 @@ class HeadlineMixin:
             except Exception as e:  # noqa: BLE001 -- same agreement as above
                 err = str(e)[:200]
             w = time.perf_counter() - w0
-            # The ranks' agreement on the outcome (gloo collectives) gets an
-            # entry of its own, so the pass entry is the pass.
+            # The pass entry ends once every rank has finished it (the
+            # agreement on its outcome returns then), so it is the slowest
+            # rank's pass as tuning_passes_ms_per_step records it; the
+            # bookkeeping after it gets an entry of its own.
+            ok = self.agree(err is None)
             tl.begin("%stuning/%s/agree" % (pre, key))
-            if not self.agree(err is None):
+            if not ok:
                 return passes, connect_s, err or "failed on another rank", t_phase
             passes.append(self.allmax(w) / tune_k)
         return passes, connect_s, None, t_phase

@@ -340,8 +340,11 @@ def test_bench_eight_ranks_with_the_driver_step_counts(native):
     The extras' sizes are lowered to fit the CPU container (all-pairs holds
     7 receive slots per rank)."""
     t0 = time.monotonic()
+    # (2 MiB x 8 messages: a tuning pass takes ~75-110 ms here, long enough
+    # for the timeline check below; at 256 KiB x 4 a 10 ms pass drowned in
+    # the scheduling noise of 8 processes on 8 CPUs.)
     out = torchrun(8, ["bench.py", "--gpus", "8", "--steps", "20", "--warmup", "5", "--transport", "shm",
-                       "--size", "256K", "--msgs", "4", "--sweep-max", "4M", "--ref-iters", "8",
+                       "--size", "2M", "--msgs", "8", "--recv-budget", "512M", "--sweep-max", "4M", "--ref-iters", "8",
                        "--latency-iters", "50", "--allpairs-size", "16M", "--ring-size", "4M"], timeout=300)
     wall = time.monotonic() - t0
     assert out.returncode == 0, out.stderr[-3000:]
