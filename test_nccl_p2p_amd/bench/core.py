@@ -357,6 +357,15 @@ SECTION_SLICES = (("latency", 5.0), ("latency_preposted", 5.0), ("reference_sema
                   ("self_sweep", 4.0), ("pair_sweep_0_1", 10.0))
 
 
+# Share of the slack beyond a section's own slice that its optional work (the
+# reference-method matrices' repeats, sections.py section()) may use.  At N = 8
+# at xGMI-like speed (tests/test_torchrun_cpu.py's rehearsal: one run of a
+# direction mode ~6-8 s) 0.2 gives each mode of the reference matrices ~4 runs
+# and ours ~2, and leaves the IPC comparisons across the links their time;
+# 0.3 gave 5-6 and 3-4 but left the comparisons ~40 s less.
+REPEAT_SLACK_SHARE = 0.2
+
+
 def reserved_after(name: str, active) -> float:
     """Seconds the sections after `name` (those of SECTION_SLICES in
     `active`) keep reserved while `name` runs; 0 for sections not planned."""

@@ -18,8 +18,8 @@ import time
 import torch.distributed as dist
 
 from test_nccl_p2p_amd.bench.compare import REF_STOCK, steps_through, stock_env
-from test_nccl_p2p_amd.bench.core import (RESERVE_S, SECTION_SLICES, child_runs, combine_runs, free_port, log,
-                                          method_ratios, pair_matrix_summary, reserved_after)
+from test_nccl_p2p_amd.bench.core import (REPEAT_SLACK_SHARE, RESERVE_S, SECTION_SLICES, child_runs, combine_runs,
+                                          free_port, log, method_ratios, pair_matrix_summary, reserved_after)
 from test_nccl_p2p_amd.utils.proc import run_child
 
 HERE = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # the repository root
@@ -66,11 +66,14 @@ class SectionsMixin:
                                                   else "no time left (or another rank's sessions failed)"))
             return None
         self.slice_left = left
-        # Its own slice (SECTION_SLICES), for work that is optional: the
-        # reference matrices' repeats stop there rather than take the slack
-        # the sections after the BASELINE ones (the IPC comparisons, the
-        # xGMI pair sweep) would otherwise get.
-        self.slice_own = min(left, mine) if mine else left
+        # Its own share, for work that is optional (the reference matrices'
+        # repeats): its SECTION_SLICES slice plus REPEAT_SLACK_SHARE of the
+        # slack beyond it, so repeats cannot take all the time the sections
+        # after the BASELINE ones (the IPC comparisons, the xGMI pair sweep)
+        # would get, yet a node's 300 s deadline still leaves the N = 8
+        # reference matrices room for a few runs each (one run of both
+        # direction modes there is ~12 s over xGMI).
+        self.slice_own = min(left, mine + REPEAT_SLACK_SHARE * max(0.0, left - mine)) if mine else left
         self.slice_t0 = time.monotonic()
         for s in self.live:
             s.set_timeout(max(1.0, min(self.args.timeout, wait_left)))
@@ -227,6 +230,9 @@ class SectionsMixin:
                                          % (least, warmup, need, left)}
                     break
                 iters = int(self.agreed_min(min(args.ref_iters, max(least, fit))))
+                # This mode's share of the section's own slice, fixed when it
+                # starts (what an earlier mode left unused carries over).
+                d_t0, d_share = time.monotonic(), self.own_slice_remaining() / (len(dirs) - len(out))
                 runs, run_secs = [], []
                 while True:
                     t0 = time.monotonic()
@@ -237,8 +243,8 @@ class SectionsMixin:
                     run_secs.append(run_s)
                     # Everything the run took, charged to its iterations (conservative).
                     per_iter = max(1e-6, run_s / cells / (warmup + iters))
-                    share = self.own_slice_remaining() / (len(dirs) - len(out))
-                    if len(runs) >= max(1, args.ref_runs) or not self.agree(1.2 * run_s + 0.05 <= share):
+                    left_d = d_share - (time.monotonic() - d_t0)
+                    if len(runs) >= max(1, args.ref_runs) or not self.agree(1.2 * run_s + 0.05 <= left_d):
                         break
                 out[d] = dict(combine_runs(runs, n), iters=iters, run_s=round(statistics.median(run_secs), 4))
                 if iters != args.ref_iters:
