@@ -450,6 +450,9 @@ def test_bench_baseline_configs_land_at_xgmi_speed(native):
     for key in ("reference_semantics", "pair_serial_events"):
         for d in ("uni", "bi"):
             assert r[key][d]["iters"] == 128 and r[key][d]["cells"] == 56 and r[key][d]["gbs_mean"] > 0, r[key]
+    # VERDICT r5 item 1 at N = 8: the reference's method repeats in both
+    # direction modes (each run ~6 s here), within its share of the slack.
+    assert all(len(r["reference_semantics"][d]["runs"]) >= 2 for d in ("uni", "bi")), r["reference_semantics"]
     assert r["pair_serial_events"]["bi"]["mismatches"] == 0 and r["p50_latency_us"] > 0
     ex = r["extras"]
     assert {"allpairs_1g", "ring_256m", "ring_hop", "pair_sweep_0_1"} <= set(ex)
