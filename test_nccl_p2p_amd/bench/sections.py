@@ -355,7 +355,7 @@ class SectionsMixin:
             # cost is estimated at the rate the previous one ran.
             sweep, rate = [], max(h.value or 1.0, 1e-3)
             for nbytes in [b for b in (4096 << (2 * k) for k in range(11)) if b <= nat.parse_size(args.sweep_max)]:
-                iters = max(4, min(200, (2 << 30) // nbytes))
+                iters = max(8, min(200, (2 << 30) // nbytes))  # >= 8 samples for the p50
                 est = (iters + 2) * (nbytes / (rate * 1e9) + 50e-6)
                 if not self.agree(self.slice_remaining() > est + 1.0):
                     sweep.append({"bytes": nbytes, "skipped": "no time left in the section's slice"})
