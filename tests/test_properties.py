@@ -136,3 +136,28 @@ def test_block_placement(native, hosts, per_host, data):
 @given(st.one_of(st.integers(1, 1 << 48), st.integers(0, 40).map(lambda k: 1 << k)))
 def test_size_format_round_trips(native, size):
     assert native.parse_size(native.format_size(size)) == size
+
+
+@SETTINGS
+@given(st.integers(1, 4), st.lists(st.lists(st.floats(0.5, 5000.0), min_size=16, max_size=16), min_size=1, max_size=9))
+def test_combine_runs_summarises_every_run(n, cells):
+    """bench/core.py combine_runs (the reference-method repeats, VERDICT r5
+    item 1): one `runs` entry per run (its mean cell), median / min / max in
+    order, a spread of (max - min) / median, every cell of the combined matrix
+    the median of that cell over the runs, and mismatches summed."""
+    import statistics
+
+    from test_nccl_p2p_amd.bench.core import combine_runs, pair_matrix_summary
+
+    pairs = [(a, b) for a in range(n) for b in range(n) if a != b] if n > 1 else [(-1, -1)]
+    runs = [pair_matrix_summary({"phases": [{"row": a, "col": b, "compat_gbps": 8 * v[i], "mismatches": i % 2}
+                                            for i, (a, b) in enumerate(pairs)]}, n) for v in cells]
+    c = combine_runs(runs, n)
+    assert c["runs"] == [round(r["gbs_mean"], 3) for r in runs]
+    assert c["min"] <= c["median"] <= c["max"] and c["spread"] >= 0
+    assert abs(c["median"] - statistics.median(r["gbs_mean"] for r in runs)) < 1e-3
+    for i, (a, b) in enumerate(pairs):
+        a, b = (0, 0) if a < 0 else (a, b)
+        per_run = [r["matrix_gbs"][a][b] for r in runs]
+        assert min(per_run) - 1e-3 <= c["matrix_gbs"][a][b] <= max(per_run) + 1e-3
+    assert c["mismatches"] == sum(r["mismatches"] for r in runs) and c["cells"] == len(pairs)
