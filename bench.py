@@ -129,7 +129,7 @@ core.set_start(T0)
 from test_nccl_p2p_amd.bench.compare import child_main, steps_through  # noqa: E402,F401
 from test_nccl_p2p_amd.bench.core import (METRIC, Deadline, Reporter, Timeline, bench_fabric_findings,  # noqa: E402,F401
                                           candidate_budget, cell_matrix, claim_stdout, default_device,
-                                          first_candidate_budget, first_comms, free_port, hang_requested,
+                                          first_candidate_budget, first_comms, free_port,
                                           headline_stats, link_check, log, pick_depth, posting_candidates,
                                           process_age, start_watchdog, tuning_steps)
 from test_nccl_p2p_amd.bench.faults import Faults  # noqa: E402
