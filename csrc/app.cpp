@@ -63,6 +63,10 @@ schedule
 timing
   -n, --iters N|auto     iterations per cell (auto: ~4 GiB per cell, 8..1000) [128]
   -w, --warmup N         untimed iterations per cell                          [8]
+      --repeat R         run every (mode, dir, size) R times; the reference matrices print
+                         the first run as it goes, then a repeat summary gives every run's
+                         mean cell and their median / min / max (one wall-clock run of
+                         the reference's method is a single noisy shot)       [1]
       --timing MODE      events    hipEvents, back-to-back messages, 1 sync  [events]
                          wallclock reference semantics: host clock, sync per message
       --reference        = --timing wallclock --warmup 0 --no-warm --two-streams, and RCCL's
@@ -205,7 +209,7 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
     static const char* kValued[] = {"-m", "--mode", "-d", "--dir", "-b", "--size", "--sizes", "-n", "--iters", "-w",
                                     "--warmup", "--timing", "--latency-size", "--latency-iters", "--latency-preposted", "--verify-impl",
                                     "--transport", "--ipc-engine", "--bootstrap", "--device", "--timeout", "--min-gbs", "--json",
-                                    "--csv", "--trace", "--cells", "--comms", "--fuzz"};
+                                    "--csv", "--trace", "--cells", "--comms", "--fuzz", "--repeat"};
     for (const char* v : kValued)
       if (a == v && !has_eq && i + 1 >= argc) {
         missing = true;
@@ -265,6 +269,13 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
       cfg->latency = true;
     } else if (a == "--fuzz") {
       cfg->fuzz_rounds = std::atoi(next().c_str());
+    } else if (a == "--repeat") {
+      cfg->repeat = std::atoi(next().c_str());
+      if (cfg->repeat < 1) {
+        std::fprintf(stderr, "p2p_matrix: --repeat needs a count >= 1\n");
+        *exit_code = 1;
+        return false;
+      }
     } else if (a == "--latency-size") {
       cfg->latency_bytes = parse_size(next());
       cfg->latency = true;
@@ -455,31 +466,35 @@ void run_all(const AppConfig& cfg, Transport& t, Bootstrap& boot, const std::vec
         if (root) P2P_INFO("resume: skipping %s", run_key(s.mode, s.dir, cfg.sizes[si]).c_str());
         continue;
       }
-      RunRecord rec;
-      rec.mode = s.mode;
-      rec.dir = s.dir;
-      rec.bytes = cfg.sizes[si];
-      rec.cfg = cfg.run;
-      rec.cfg.bytes = rec.bytes;
-      rec.cfg.salt = static_cast<uint64_t>(res.runs.size());
-      if (cfg.iters_auto) rec.cfg.iters = auto_iters(rec.bytes, cfg.target_bytes);
-      const bool compat = cfg.compat && s.mode == Mode::Pair && root;
-      CompatPrinter cp(out, n);
-      if (compat) {
-        if (cfg.sizes.size() > 1)
-          std::fprintf(out, "%s# message size %s\n", printed_compat ? "\n" : "", format_size(rec.bytes).c_str());
-        cp.begin(s.dir, printed_compat && s.dir == Direction::Uni && cfg.sizes.size() == 1);
-        printed_compat = true;
+      for (int rep = 0; rep < std::max(1, cfg.repeat); ++rep) {
+        RunRecord rec;
+        rec.mode = s.mode;
+        rec.dir = s.dir;
+        rec.bytes = cfg.sizes[si];
+        rec.cfg = cfg.run;
+        rec.cfg.bytes = rec.bytes;
+        rec.cfg.salt = static_cast<uint64_t>(res.runs.size());
+        rec.repeat = rep;
+        if (cfg.iters_auto) rec.cfg.iters = auto_iters(rec.bytes, cfg.target_bytes);
+        // The reference matrices print the first run only, cell by cell.
+        const bool compat = cfg.compat && s.mode == Mode::Pair && root && rep == 0;
+        CompatPrinter cp(out, n);
+        if (compat) {
+          if (cfg.sizes.size() > 1)
+            std::fprintf(out, "%s# message size %s\n", printed_compat ? "\n" : "", format_size(rec.bytes).c_str());
+          cp.begin(s.dir, printed_compat && s.dir == Direction::Uni && cfg.sizes.size() == 1);
+          printed_compat = true;
+        }
+        rec.phases = run_schedule(t, boot, s, rec.cfg, bufs, [&](const PhaseResult& r) {
+          if (compat) cp.on_phase(r);
+        });
+        for (const auto& ph : rec.phases) res.mismatches += ph.total_mismatches;
+        if (js.is_open()) {
+          js << run_to_json(rec, n) << "\n";
+          js.flush();
+        }
+        res.runs.push_back(std::move(rec));
       }
-      rec.phases = run_schedule(t, boot, s, rec.cfg, bufs, [&](const PhaseResult& r) {
-        if (compat) cp.on_phase(r);
-      });
-      for (const auto& ph : rec.phases) res.mismatches += ph.total_mismatches;
-      if (js.is_open()) {
-        js << run_to_json(rec, n) << "\n";
-        js.flush();
-      }
-      res.runs.push_back(std::move(rec));
     }
   }
 }
@@ -517,8 +532,14 @@ void write_reports(const AppConfig& cfg, const Transport& t, const Bootstrap& bo
     for (int r = 0; r < n; ++r) std::fprintf(out, "  rank %d: %s\n", r, &all_desc[static_cast<size_t>(r) * desc_len]);
     if (t.name() != "host" && t.name() != "shm") std::fprintf(out, "%s", topology_report().c_str());
     print_transport_matrix(out, res, n);
-    for (const auto& rec : res.runs) print_extended(out, rec, n);
-    print_fabric_check(out, res.runs, n);
+    // The tables of the first run of each (mode, dir, size); with --repeat
+    // the others are summarised below.
+    std::vector<RunRecord> firsts;
+    for (const auto& rec : res.runs)
+      if (rec.repeat == 0) firsts.push_back(rec);
+    for (const auto& rec : firsts) print_extended(out, rec, n);
+    print_fabric_check(out, firsts, n);
+    if (cfg.repeat > 1) print_repeat_summary(out, repeat_summaries(res.runs, n));
     print_latency(out, res.latency, n);
     print_latency(out, res.preposted_latency, n);
     print_latency(out, res.device_latency, n);
@@ -530,6 +551,8 @@ void write_reports(const AppConfig& cfg, const Transport& t, const Bootstrap& bo
                             : "all verified");
   }
   if (js.is_open()) {
+    if (cfg.repeat > 1)
+      for (const auto& rs : repeat_summaries(res.runs, n)) js << repeat_summary_json(rs) << "\n";
     js << links_to_json(res, n) << "\n";
     if (!res.latency.empty()) js << latency_to_json(res.latency, n) << "\n";
     if (!res.preposted_latency.empty()) js << latency_to_json(res.preposted_latency, n) << "\n";

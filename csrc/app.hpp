@@ -55,6 +55,7 @@ struct AppConfig {
   bool two_streams = false;  // RCCL receives on a second stream (reference layout)
   bool rccl_stock = false;   // --reference: RCCL's own kernel unroll (no P2P_RCCL_UNROLL)
   int comms = 1;             // RCCL communicators per rank (messages spread round-robin)
+  int repeat = 1;            // --repeat R: every (mode, dir, size) run R times; repeat summary (median)
   int verbose = 0;
 };
 

@@ -125,6 +125,57 @@ void print_fabric_check(FILE* out, const std::vector<RunRecord>& runs, int n) {
   std::fflush(out);
 }
 
+std::vector<RepeatSummary> repeat_summaries(const std::vector<RunRecord>& runs, int n) {
+  std::vector<RepeatSummary> out;
+  for (const auto& r : runs) {
+    double v = 0;
+    if (r.mode == Mode::Pair) {
+      double sum = 0;
+      size_t cells = 0;
+      for (const auto& ph : r.phases)
+        if (!ph.idle) {
+          sum += compat_cell_gbps(ph) / 8.0;
+          ++cells;
+        }
+      v = cells ? sum / static_cast<double>(cells) : 0.0;
+    } else {
+      v = summarize_offdiag(flow_matrix_gbs(r, n), n).mean;
+    }
+    auto it = std::find_if(out.begin(), out.end(), [&](const RepeatSummary& s) {
+      return s.mode == r.mode && s.dir == r.dir && s.bytes == r.bytes;
+    });
+    if (it == out.end()) {
+      out.push_back(RepeatSummary{r.mode, r.dir, r.bytes, {}, 0, 0, 0});
+      it = out.end() - 1;
+    }
+    it->runs.push_back(v);
+  }
+  for (auto& s : out) {
+    std::vector<double> v = s.runs;
+    std::sort(v.begin(), v.end());
+    const size_t k = v.size();
+    s.median = k % 2 ? v[k / 2] : 0.5 * (v[k / 2 - 1] + v[k / 2]);
+    s.min = v.front();
+    s.max = v.back();
+  }
+  return out;
+}
+
+void print_repeat_summary(FILE* out, const std::vector<RepeatSummary>& sums) {
+  if (sums.empty()) return;
+  std::fprintf(out, "\n== repeats: mean cell GB/s of every run (pair: the compat cell / 8, bi both directions) ==\n");
+  std::fprintf(out, "  %-10s %-4s %8s  %5s %10s %10s %10s %7s  runs\n", "mode", "dir", "size", "n", "median", "min", "max",
+               "spread");
+  for (const auto& s : sums) {
+    std::string runs;
+    for (double v : s.runs) runs += strfmt(" %.2f", v);
+    std::fprintf(out, "  %-10s %-4s %8s  %5zu %10.2f %10.2f %10.2f %6.1f%% %s\n", mode_name(s.mode),
+                 direction_name(s.dir), format_size(s.bytes).c_str(), s.runs.size(), s.median, s.min, s.max,
+                 s.median > 0 ? 100.0 * (s.max - s.min) / s.median : 0.0, runs.c_str());
+  }
+  std::fflush(out);
+}
+
 void print_extended(FILE* out, const RunRecord& rec, int n) {
   std::string head = strfmt("[%s %s | %s x %d | timing=%s warmup=%d%s]", mode_name(rec.mode), direction_name(rec.dir),
                             format_size(rec.bytes).c_str(), rec.cfg.iters, timing_name(rec.cfg.timing), rec.cfg.warmup,
@@ -235,6 +286,15 @@ std::string matrix_json(const std::vector<double>& m, int n) {
 }
 }  // namespace
 
+std::string repeat_summary_json(const RepeatSummary& s) {
+  std::string runs = "[";
+  for (size_t i = 0; i < s.runs.size(); ++i) runs += (i ? "," : "") + num(s.runs[i]);
+  return strfmt("{\"type\":\"repeats\",\"mode\":\"%s\",\"dir\":\"%s\",\"bytes\":%zu,\"runs\":%s],"
+                "\"median\":%s,\"min\":%s,\"max\":%s}",
+                mode_name(s.mode), direction_name(s.dir), s.bytes, runs.c_str(), num(s.median).c_str(),
+                num(s.min).c_str(), num(s.max).c_str());
+}
+
 std::string run_to_json(const RunRecord& rec, int n) {
   auto gbs = flow_matrix_gbs(rec, n);
   MatrixSummary ms = summarize_offdiag(gbs, n);
@@ -247,7 +307,7 @@ std::string run_to_json(const RunRecord& rec, int n) {
     rechunked = rechunked || !ph.rechunked_to.empty();
   }
   o << "{\"type\":\"run\",\"mode\":\"" << mode_name(rec.mode) << "\",\"dir\":\"" << direction_name(rec.dir)
-    << "\",\"bytes\":" << rec.bytes << ",\"iters\":" << rec.cfg.iters << ",\"warmup\":" << rec.cfg.warmup
+    << "\",\"bytes\":" << rec.bytes << ",\"repeat\":" << rec.repeat << ",\"iters\":" << rec.cfg.iters << ",\"warmup\":" << rec.cfg.warmup
     << ",\"timing\":\"" << timing_name(rec.cfg.timing) << "\",\"nranks\":" << n << ",\"verify\":"
     << (rec.cfg.verify ? "true" : "false") << ",\"timed_msgs\":" << timed << ",\"verified_msgs\":" << checked
     << ",\"verify_coverage\":" << (rec.cfg.verify && timed ? num(static_cast<double>(checked) / static_cast<double>(timed)) : "null")

@@ -41,6 +41,7 @@ struct RunRecord {
   size_t bytes;
   RunConfig cfg;
   std::vector<PhaseResult> phases;
+  int repeat = 0;  // --repeat: which run of this (mode, dir, size), 0-based
 };
 
 // N x N (row = src, col = dst) matrices built from all flows of a run.
@@ -62,6 +63,24 @@ void print_extended(FILE* out, const RunRecord& rec, int n);
 // The fabric lines of every pair-mode size with both a uni and a bi run
 // (fabric_findings), after the extended tables.
 void print_fabric_check(FILE* out, const std::vector<RunRecord>& runs, int n);
+
+// --repeat: per (mode, dir, size), every run's mean cell and their median /
+// min / max.  A run's value is its mean compat cell in GB/s for pair mode
+// (the reference's printed cell / 8: bi = both directions summed,
+// p2p_matrix.cc:258) and its mean off-diagonal flow (per direction) for the
+// other modes.  One wall-clock run of the reference's method varied by +-9%
+// between records on one GPU, so the median is the number to
+// compare.
+struct RepeatSummary {
+  Mode mode;
+  Direction dir;
+  size_t bytes;
+  std::vector<double> runs;
+  double median = 0, min = 0, max = 0;
+};
+std::vector<RepeatSummary> repeat_summaries(const std::vector<RunRecord>& runs, int n);
+void print_repeat_summary(FILE* out, const std::vector<RepeatSummary>& sums);
+std::string repeat_summary_json(const RepeatSummary& s);
 void print_latency(FILE* out, const std::vector<LatencyResult>& lat, int n);
 void print_matrix(FILE* out, const std::string& title, const std::vector<double>& m, int n, const char* fmt,
                   bool blank_diag);

@@ -430,6 +430,36 @@ TEST(test_json_escape) {
   EXPECT(json_escape("a\"b\\c\n") == "a\\\"b\\\\c\\n");
 }
 
+TEST(test_repeat_summaries) {
+  // --repeat: per (mode, dir, size) every run's mean cell (pair: the compat
+  // cell / 8, bi both directions summed) and their median / min / max.
+  auto pair_run = [](Direction d, double gbps01, double gbps10, int rep) {
+    RunRecord r;
+    r.mode = Mode::Pair;
+    r.dir = d;
+    r.bytes = 1 << 20;
+    r.repeat = rep;
+    for (int i = 0; i < 2; ++i) {
+      PhaseResult ph;
+      ph.row = i;
+      ph.col = 1 - i;
+      ph.seconds_per_iter = 1.0;
+      ph.bytes_per_iter = (i == 0 ? gbps01 : gbps10) * 1e9 / 8.0;
+      r.phases.push_back(ph);
+    }
+    return r;
+  };
+  std::vector<RunRecord> runs = {pair_run(Direction::Uni, 80, 160, 0), pair_run(Direction::Uni, 40, 40, 1),
+                                 pair_run(Direction::Bi, 200, 200, 0), pair_run(Direction::Uni, 800, 800, 2)};
+  auto s = repeat_summaries(runs, 2);
+  EXPECT(s.size() == 2 && s[0].dir == Direction::Uni && s[1].dir == Direction::Bi);
+  EXPECT(s[0].runs.size() == 3 && std::fabs(s[0].runs[0] - 15.0) < 1e-9 && std::fabs(s[0].runs[1] - 5.0) < 1e-9);
+  EXPECT(std::fabs(s[0].median - 15.0) < 1e-9 && std::fabs(s[0].min - 5.0) < 1e-9 && std::fabs(s[0].max - 100.0) < 1e-9);
+  EXPECT(s[1].runs.size() == 1 && std::fabs(s[1].median - 25.0) < 1e-9);
+  const std::string js = repeat_summary_json(s[0]);
+  EXPECT(js.find("\"type\":\"repeats\"") != std::string::npos && js.find("\"median\":15") != std::string::npos);
+}
+
 TEST(test_cli_defaults_match_reference) {
   AppConfig cfg;
   int code = -1;

@@ -305,3 +305,30 @@ def test_fuzz_option(mpirun, host_build, tmp_path):
         assert "== fuzz: 12 groups of random messages (1 B .. 256K" in out.stdout and "all verified" in out.stdout
         rec = [json.loads(l) for l in js.read_text().splitlines() if '"fuzz"' in l]
         assert rec == [{"type": "fuzz", "rounds": 12, "max_bytes": 262144, "mismatches": 0}]
+
+
+def test_repeat_runs_summarised(mpirun, host_build, tmp_path):
+    """--repeat R (the binary's side of VERDICT r5 item 1): every (mode, dir,
+    size) runs R times; the reference matrices print once (the first run, as
+    it goes), the repeat summary gives every run's mean cell and their
+    median / min / max, and --json keeps each run (with its index) and one
+    "repeats" record per configuration."""
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    js = tmp_path / "rep.json"
+    out = run(mpirun, exe, 2, ["--transport", "host", "--size", "64K", "-n", "4", "--repeat", "3", "--json", str(js)])
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.count("Evaluating the Uni-Directional NCCL P2P Bandwidth (Gbps)") == 1
+    assert out.stdout.count("Evaluating the Bi-Directional NCCL P2P Bandwidth (Gbps)") == 1
+    assert out.stdout.count("== [pair uni | 64K") == 1  # the extended tables of the first run only
+    lines = out.stdout.split("== repeats:")[1].splitlines()
+    rows = [l.split() for l in lines if l.strip().startswith("pair")]
+    assert [(r[0], r[1], r[3]) for r in rows] == [("pair", "uni", "3"), ("pair", "bi", "3")], lines
+    recs = [json.loads(l) for l in js.read_text().splitlines()]
+    runs = [r for r in recs if r["type"] == "run"]
+    assert sorted((r["dir"], r["repeat"]) for r in runs) == [(d, i) for d in ("bi", "uni") for i in range(3)]
+    reps = {r["dir"]: r for r in recs if r["type"] == "repeats"}
+    for d in ("uni", "bi"):
+        x = reps[d]
+        assert len(x["runs"]) == 3 and x["min"] <= x["median"] <= x["max"] and x["median"] == sorted(x["runs"])[1]
+    bad = run(mpirun, exe, 1, ["--transport", "host", "--repeat", "0"])
+    assert bad.returncode != 0 and "--repeat needs a count >= 1" in bad.stderr
