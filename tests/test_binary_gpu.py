@@ -54,6 +54,21 @@ def test_reference_invocation_from_repo_root(exe):
     assert "Evaluating the Bi-Directional NCCL P2P Bandwidth (Gbps)" in out.stdout
 
 
+def test_repeat_self_summary(exe, tmp_path):
+    """--repeat 4: the self cell measured four times on the card, summarised
+    (median / min / max) and recorded as one repeats record per size."""
+    js = tmp_path / "r.json"
+    out = subprocess.run([exe, "--mode", "self", "--size", "64M", "-n", "8", "--repeat", "4", "--verify",
+                          "--json", str(js)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert "== repeats" in out.stdout and "verification: OK" in out.stdout
+    recs = [json.loads(l) for l in js.read_text().splitlines()]
+    assert sum(1 for r in recs if r["type"] == "run") == 4
+    rep = [r for r in recs if r["type"] == "repeats"]
+    assert len(rep) == 1 and len(rep[0]["runs"]) == 4
+    assert rep[0]["min"] <= rep[0]["median"] <= rep[0]["max"] and rep[0]["min"] > 10
+
+
 def test_bench_contract_single_gpu():
     out = subprocess.run([sys.executable, "bench.py", "--steps", "6", "--warmup", "2", "--latency-iters", "50"],
                          capture_output=True, text=True, timeout=600, cwd=ROOT)
