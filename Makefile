@@ -5,6 +5,7 @@
 #   make test         host unit tests + CPU pytest tier
 #   make test-gpu     pytest -m gpu (run on an MI355X, e.g. via gpurun)
 #   make asan         host unit tests under AddressSanitizer/UBSan (host code only)
+#   make tsan         host unit tests under ThreadSanitizer (host code only)
 #   make clean        removes build/ and the extension (the reference's clean
 #                     target removes the misspelled "p2pmatrix", Makefile:5)
 #
@@ -61,7 +62,7 @@ PY_INC    := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_paths()[
 PYBIND    := $(shell $(PYTHON) -c "import pybind11;print(pybind11.get_include())")
 EXT       := test_nccl_p2p_amd/_p2pcore$(PY_EXT)
 
-.PHONY: all gpu host ext tools test test-host test-gpu asan clean
+.PHONY: all gpu host ext tools test test-host test-gpu asan tsan clean
 
 all: gpu host ext tools
 
@@ -74,7 +75,7 @@ ext: $(EXT)
 tools: $(BUILD)/fill_probe $(BUILD)/copy_probe $(BUILD)/ipc_export_probe $(BUILD)/rccl_half_repro $(BUILD)/rccl_half_repro_rocm \
        $(BUILD)/rccl_net_repro
 
-$(BUILD)/gpu $(BUILD)/host $(BUILD)/asan:
+$(BUILD)/gpu $(BUILD)/host $(BUILD)/asan $(BUILD)/tsan:
 	mkdir -p $@
 
 $(RTDIR)/.stamp:
@@ -172,6 +173,21 @@ $(BUILD)/asan/p2p_host_tests: $(ASAN_SRCS) tests/host/test_main.cpp $(HEADERS) |
 $(BUILD)/asan/p2p_matrix_host: $(ASAN_SRCS) csrc/bootstrap_mpi.cpp csrc/main.cpp $(HEADERS) $(MPILIB)/.stamp | $(BUILD)/asan
 	$(CXX_HOST) $(CXXSTD) $(WARN) $(ASAN) -Icsrc $(MPI_INC) -pthread $(ASAN_SRCS) csrc/bootstrap_mpi.cpp csrc/main.cpp \
 	    -o $@ -L$(MPILIB) -lmpi -Wl,-rpath,'$$ORIGIN/../mpilib'
+
+# ThreadSanitizer on the same host code: the unit tests run every rank of a
+# multi-rank case as a thread (TCP / shm transports, bootstrap collectives,
+# the abort path against in-flight native calls), so a data race between
+# ranks, the watchdog's abort and the logging is reported; any report fails.
+TSAN      := -fsanitize=thread -fno-omit-frame-pointer -g -O1
+tsan: $(BUILD)/tsan/p2p_host_tests $(BUILD)/tsan/p2p_matrix_host
+	TSAN_OPTIONS=halt_on_error=1 $(BUILD)/tsan/p2p_host_tests
+
+$(BUILD)/tsan/p2p_matrix_host: $(ASAN_SRCS) csrc/bootstrap_mpi.cpp csrc/main.cpp $(HEADERS) $(MPILIB)/.stamp | $(BUILD)/tsan
+	$(CXX_HOST) $(CXXSTD) $(WARN) $(TSAN) -Icsrc $(MPI_INC) -pthread $(ASAN_SRCS) csrc/bootstrap_mpi.cpp csrc/main.cpp \
+	    -o $@ -L$(MPILIB) -lmpi -Wl,-rpath,'$$ORIGIN/../mpilib'
+
+$(BUILD)/tsan/p2p_host_tests: $(ASAN_SRCS) tests/host/test_main.cpp $(HEADERS) | $(BUILD)/tsan
+	$(CXX_HOST) $(CXXSTD) $(WARN) $(TSAN) $(TEST_DATA) -Icsrc -pthread $(ASAN_SRCS) tests/host/test_main.cpp -o $@
 
 test-host: $(BUILD)/p2p_host_tests
 	$(BUILD)/p2p_host_tests

@@ -26,7 +26,7 @@ int g_next_hook = 1;
 bool g_throw = false;
 std::atomic<bool> g_abort_requested{false};
 std::atomic<bool> g_abort_done{false};
-int g_log_level = -1;
+std::atomic<int> g_log_level{-1};  // read by every thread that logs
 }  // namespace
 
 int push_abort_hook(AbortHook hook) {
@@ -143,14 +143,17 @@ std::string strfmt(const char* fmt, ...) {
 }
 
 int log_level() {
-  if (g_log_level < 0) {
+  int level = g_log_level.load(std::memory_order_relaxed);
+  if (level < 0) {
     const char* e = std::getenv("P2P_LOG");
-    g_log_level = e ? std::atoi(e) : 0;
+    int env_level = e ? std::atoi(e) : 0;
+    // First caller wins; set_log_level may have run in between.
+    if (g_log_level.compare_exchange_strong(level, env_level, std::memory_order_relaxed)) level = env_level;
   }
-  return g_log_level;
+  return level;
 }
 
-void set_log_level(int level) { g_log_level = level; }
+void set_log_level(int level) { g_log_level.store(level, std::memory_order_relaxed); }
 
 void logf(int level, const char* fmt, ...) {
   if (log_level() < level) return;

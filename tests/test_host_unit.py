@@ -29,3 +29,25 @@ def test_host_code_under_asan_ubsan(mpirun):
         assert run.returncode == 0, run.stderr[-4000:]
         assert "AddressSanitizer" not in run.stderr and "runtime error" not in run.stderr
         assert "verification: OK" in run.stdout
+
+
+def test_host_code_under_tsan(mpirun):
+    """Host code under ThreadSanitizer (SURVEY.md §5 race detection row): the
+    unit tests run every rank of a multi-rank case as a thread of one process
+    (bootstrap collectives, the TCP and shared-memory transports, abort_if_idle
+    against in-flight native calls), so a race between ranks, the abort path
+    and the logging fails the run (halt_on_error); then 3-rank MPI jobs of the
+    host binary over both CPU transports."""
+    from conftest import ROOT
+    out = subprocess.run(["make", "-j2", "tsan"], cwd=ROOT, capture_output=True, text=True, timeout=900)
+    assert out.returncode == 0, out.stdout[-4000:] + out.stderr[-4000:]
+    assert " 0 failures" in out.stdout and "ThreadSanitizer" not in out.stdout + out.stderr
+    exe = os.path.join(ROOT, "build", "tsan", "p2p_matrix_host")
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1")
+    for transport in ("host", "shm"):
+        run = subprocess.run([mpirun, "-n", "3", exe, "--transport", transport, "--mode", "all", "--sizes", "4K,2M",
+                              "-n", "3", "--verify", "--latency", "--latency-iters", "20"],
+                             capture_output=True, text=True, timeout=300, env=env)
+        assert run.returncode == 0, run.stderr[-4000:]
+        assert "ThreadSanitizer" not in run.stderr
+        assert "verification: OK" in run.stdout
