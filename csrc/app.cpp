@@ -1,6 +1,7 @@
 #include "app.hpp"
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -205,6 +206,33 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
       *exit_code = 1;
       return false;
     };
+    // Numeric values are read whole and range-checked: a typo or a negative
+    // count fails at the command line instead of running something else.
+    bool bad = false;
+    auto int_arg = [&](long lo) -> int {
+      const std::string v = next();
+      char* end = nullptr;
+      long x = std::strtol(v.c_str(), &end, 10);
+      if (v.empty() || *end || x < lo || x > INT_MAX) {
+        if (!missing) std::fprintf(stderr, "p2p_matrix: %s needs a whole number >= %ld, got '%s'\n", a.c_str(), lo, v.c_str());
+        bad = true;
+        return 0;
+      }
+      return static_cast<int>(x);
+    };
+    auto num_arg = [&](double lo, bool strict) -> double {
+      const std::string v = next();
+      char* end = nullptr;
+      double x = std::strtod(v.c_str(), &end);
+      if (v.empty() || *end || !(strict ? x > lo : x >= lo)) {
+        if (!missing)
+          std::fprintf(stderr, "p2p_matrix: %s needs a number %s %g, got '%s'\n", a.c_str(), strict ? ">" : ">=", lo,
+                       v.c_str());
+        bad = true;
+        return 0;
+      }
+      return x;
+    };
     // Options taking a value check it before use.
     static const char* kValued[] = {"-m", "--mode", "-d", "--dir", "-b", "--size", "--sizes", "-n", "--iters", "-w",
                                     "--warmup", "--timing", "--latency-size", "--latency-iters", "--latency-preposted", "--verify-impl",
@@ -240,11 +268,18 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
       if (v == "auto") {
         cfg->iters_auto = true;
       } else {
-        cfg->run.iters = std::atoi(v.c_str());
+        char* end = nullptr;
+        long x = std::strtol(v.c_str(), &end, 10);
+        if (v.empty() || *end || x < 1 || x > INT_MAX) {
+          std::fprintf(stderr, "p2p_matrix: --iters must be >= 1 (or auto), got '%s'\n", v.c_str());
+          *exit_code = 1;
+          return false;
+        }
+        cfg->run.iters = static_cast<int>(x);
         cfg->iters_auto = false;
       }
     } else if (a == "-w" || a == "--warmup") {
-      cfg->run.warmup = std::atoi(next().c_str());
+      cfg->run.warmup = int_arg(0);
     } else if (a == "--timing") {
       cfg->run.timing = parse_timing(next());
     } else if (a == "--reference") {
@@ -257,7 +292,7 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
     } else if (a == "--two-streams") {
       cfg->two_streams = true;
     } else if (a == "--comms") {
-      cfg->comms = std::atoi(next().c_str());
+      cfg->comms = int_arg(1);
     } else if (a == "--no-warm") {
       cfg->warm_connections = false;
     } else if (a == "-l" || a == "--latency") {
@@ -265,22 +300,17 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
     } else if (a == "--device-latency") {
       cfg->device_latency = true;
     } else if (a == "--latency-preposted") {
-      cfg->latency_preposted = std::atoi(next().c_str());
+      cfg->latency_preposted = int_arg(0);
       cfg->latency = true;
     } else if (a == "--fuzz") {
-      cfg->fuzz_rounds = std::atoi(next().c_str());
+      cfg->fuzz_rounds = int_arg(0);
     } else if (a == "--repeat") {
-      cfg->repeat = std::atoi(next().c_str());
-      if (cfg->repeat < 1) {
-        std::fprintf(stderr, "p2p_matrix: --repeat needs a count >= 1\n");
-        *exit_code = 1;
-        return false;
-      }
+      cfg->repeat = int_arg(1);
     } else if (a == "--latency-size") {
       cfg->latency_bytes = parse_size(next());
       cfg->latency = true;
     } else if (a == "--latency-iters") {
-      cfg->latency_iters = std::atoi(next().c_str());
+      cfg->latency_iters = int_arg(1);
       cfg->latency = true;
     } else if (a == "-c" || a == "--verify") {
       cfg->run.verify = true;
@@ -302,11 +332,11 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
     } else if (a == "--bootstrap") {
       cfg->bootstrap = next();
     } else if (a == "--device") {
-      cfg->device = std::atoi(next().c_str());
+      cfg->device = int_arg(-1);
     } else if (a == "--min-gbs") {
-      cfg->min_gbs = std::atof(next().c_str());
+      cfg->min_gbs = num_arg(0, false);
     } else if (a == "--timeout") {
-      cfg->timeout_s = std::atof(next().c_str());
+      cfg->timeout_s = num_arg(0, true);
     } else if (a == "--json") {
       cfg->json_path = next();
     } else if (a == "--csv") {
@@ -345,6 +375,10 @@ bool parse_cli(int argc, char** argv, AppConfig* cfg, int* exit_code, FILE* out)
       cfg->verbose++;
     } else {
       std::fprintf(stderr, "p2p_matrix: unknown option '%s' (see --help)\n", argv[i]);
+      *exit_code = 1;
+      return false;
+    }
+    if (bad) {
       *exit_code = 1;
       return false;
     }

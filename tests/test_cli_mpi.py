@@ -331,4 +331,45 @@ def test_repeat_runs_summarised(mpirun, host_build, tmp_path):
         x = reps[d]
         assert len(x["runs"]) == 3 and x["min"] <= x["median"] <= x["max"] and x["median"] == sorted(x["runs"])[1]
     bad = run(mpirun, exe, 1, ["--transport", "host", "--repeat", "0"])
-    assert bad.returncode != 0 and "--repeat needs a count >= 1" in bad.stderr
+    assert bad.returncode != 0 and "--repeat needs a whole number >= 1" in bad.stderr
+
+
+@pytest.mark.parametrize("args,msg", [
+    (["-n", "0"], "--iters must be >= 1"),
+    (["-n", "5x"], "--iters must be >= 1"),
+    (["--comms", "0"], "--comms needs a whole number >= 1"),
+    (["-w", "-1"], "-w needs a whole number >= 0"),
+    (["--warmup=two"], "--warmup needs a whole number >= 0"),
+    (["--latency-iters", "0"], "--latency-iters needs a whole number >= 1"),
+    (["--fuzz", "-2"], "--fuzz needs a whole number >= 0"),
+    (["--timeout", "0"], "--timeout needs a number > 0"),
+    (["--device", "-2"], "--device needs a whole number >= -1"),
+    (["--min-gbs", "fast"], "--min-gbs needs a number >= 0"),
+    (["--iters"], "option --iters needs a value"),
+])
+def test_cli_rejects_bad_numbers(host_build, args, msg):
+    """Numeric options are read whole and range-checked: a typo or a negative
+    count exits 1 at the command line with a message naming the option,
+    instead of running with an atoi() zero (the reference takes no options)."""
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    out = subprocess.run([exe, "--transport", "host", "--mode", "self", "--size", "4K"] + args,
+                         capture_output=True, text=True, timeout=60)
+    assert out.returncode == 1, out.stdout + out.stderr
+    assert msg in out.stderr, out.stderr
+    assert "verification" not in out.stdout
+
+
+def test_cli_small_flags(host_build, tmp_path):
+    """--version, -v / --verbose, --bootstrap local, --no-warm, --two-streams
+    (ignored by the CPU transport) and --key=value spellings."""
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    v = subprocess.run([exe, "--version"], capture_output=True, text=True, timeout=60)
+    assert v.returncode == 0 and v.stdout.startswith("p2p_matrix (MI355X / gfx950, RCCL)")
+    js = tmp_path / "r.json"
+    out = subprocess.run([exe, "--transport=host", "--bootstrap=local", "--mode=self", "--size=8K", "--iters=3",
+                          "--warmup=0", "--no-warm", "--two-streams", "-v", "--timeout=2.5", "--json", str(js)],
+                         capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    assert "bootstrap local" in out.stdout and "verification: OK" in out.stdout
+    run_rec = [json.loads(l) for l in js.read_text().splitlines() if '"type":"run"' in l]
+    assert len(run_rec) == 1 and run_rec[0]["iters"] == 3 and run_rec[0]["warmup"] == 0

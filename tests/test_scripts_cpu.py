@@ -104,7 +104,8 @@ def emulated_tests():
 def measured_single_gpu_tier_s():
     """Duration of the single-GPU tier on a multi-GPU node, from the runs on
     one-GPU MI355X boxes: the final line of every profiles/r<k>*/pytest_gpu*.log
-    of the latest round k that has one (a whole tier, not a failed run), less
+    of the latest round k that has one (a whole tier, not a failed run, run
+    with --durations), less
     the `emulated` tests' durations its --durations table lists (skipped on a
     node), worst case."""
     import glob
@@ -117,7 +118,10 @@ def measured_single_gpu_tier_s():
         with open(path) as f:
             lines = [l for l in f.read().splitlines() if l.strip()]
         m = re.search(r"(\d+) passed.* in ([\d.]+)s", lines[-1] if lines else "")
-        if rnd and m and "failed" not in lines[-1]:
+        # Only a log with pytest's --durations table can have the emulated
+        # tests taken out; one without it (a plain -q run) is not comparable.
+        has_durations = any("slowest" in l and "durations" in l for l in lines)
+        if rnd and m and "failed" not in lines[-1] and has_durations:
             skipped_on_node = sum(float(d.group(1)) for d in (re.match(r"([\d.]+)s call\s+\S+::(\w+)", l) for l in lines)
                                   if d and d.group(2) in emulated)
             runs.append((int(rnd.group(1)), float(m.group(2)) - skipped_on_node, path))
