@@ -84,7 +84,7 @@ def set_hw_queues(argv) -> None:
         qn = int(q)
     except ValueError:  # argparse reports a bad --hw-queues; a bad P2P_BENCH_HW_QUEUES falls back
         qn = 8
-    if qn > 0:
+    if 0 < qn <= 32:  # more is refused by parse_args
         os.environ["GPU_MAX_HW_QUEUES"] = str(qn)
 
 
@@ -230,7 +230,25 @@ def parse_args(argv=None):
     ap.add_argument("--ref-stock", type=int, default=1,
                     help="1: also run the reference's methodology in a child with the stock RCCL / HIP settings "
                          "(RCCL's own unroll, the environment's HW queues, no INFO log): reference_semantics_stock")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    # Counts out of range fail here, before any rank starts, naming the option.
+    at_least = {"gpus": 1, "steps": 1, "warmup": 0, "msgs": 1, "latency_iters": 1, "latency_preposted": 0,
+                "tune_laps": 0, "tune_passes": 1, "ref_iters": 0, "ref_runs": 1, "hw_queues": 0}
+    for name, lo in at_least.items():
+        if getattr(args, name) < lo:
+            ap.error("--%s must be >= %d, got %d" % (name.replace("_", "-"), lo, getattr(args, name)))
+    if args.hw_queues > 32:
+        ap.error("--hw-queues must be <= 32, got %d" % args.hw_queues)
+    if args.comms == 0 or args.comms < -1:
+        ap.error("--comms must be -1 (tuned) or >= 1, got %d" % args.comms)
+    if args.batch not in (-1, 0, 1):
+        ap.error("--batch must be -1, 0 or 1, got %d" % args.batch)
+    for name in ("timeout", "deadline", "child_timeout"):
+        if not getattr(args, name) > 0:
+            ap.error("--%s must be > 0, got %g" % (name.replace("_", "-"), getattr(args, name)))
+    if args.untimed_budget < 0:
+        ap.error("--untimed-budget must be >= 0, got %g" % args.untimed_budget)
+    return args
 
 
 class BenchRun(HeadlineMixin, SectionsMixin):

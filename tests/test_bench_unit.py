@@ -2,6 +2,8 @@
 import os
 import sys
 
+import pytest
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import bench  # noqa: E402
@@ -71,6 +73,22 @@ def test_bench_help_lists_transports():
     assert args.transport == "rccl" and args.comms == -1 and args.isolate == 1 and args.deadline == 300.0
     for t in ("ipc:relay", "shm"):
         assert bench.parse_args(["--transport", t]).transport == t
+
+
+@pytest.mark.parametrize("argv,msg", [
+    (["--steps", "0"], "--steps must be >= 1"), (["--warmup", "-1"], "--warmup must be >= 0"),
+    (["--gpus", "0"], "--gpus must be >= 1"), (["--msgs", "0"], "--msgs must be >= 1"),
+    (["--comms", "0"], "--comms must be -1 (tuned) or >= 1"), (["--batch", "2"], "--batch must be -1, 0 or 1"),
+    (["--tune-passes", "0"], "--tune-passes must be >= 1"), (["--ref-runs", "0"], "--ref-runs must be >= 1"),
+    (["--hw-queues", "64"], "--hw-queues must be <= 32"), (["--deadline", "0"], "--deadline must be > 0"),
+    (["--timeout", "-3"], "--timeout must be > 0"), (["--untimed-budget", "-1"], "--untimed-budget must be >= 0"),
+])
+def test_bench_rejects_out_of_range_counts(argv, msg, capsys):
+    """Counts out of range stop bench.py at argument parsing, naming the
+    option (before any rank, GPU or rendezvous starts)."""
+    with pytest.raises(SystemExit) as e:
+        bench.parse_args(argv)
+    assert e.value.code == 2 and msg in capsys.readouterr().err
 
 
 def test_default_device_wraps_to_the_visible_gpus(monkeypatch):
