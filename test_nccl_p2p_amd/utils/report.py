@@ -297,6 +297,14 @@ def pair_sweep_lines(r: dict) -> List[str]:
     return out
 
 
+def repeat_line(r: dict) -> str:
+    """One p2p_matrix --repeat summary record: the median of the runs' mean
+    cells, their range and the spread ((max - min) / median)."""
+    spread = (r["max"] - r["min"]) / r["median"] if r["median"] else 0.0
+    return "%-10s %-3s %10d B, %d runs: GB/s median %.2f (min %.2f, max %.2f, spread %.1f%%)" % (
+        r["mode"], r["dir"], r["bytes"], len(r["runs"]), r["median"], r["min"], r["max"], 100.0 * spread)
+
+
 def bench_compat_text(r: dict, key: str = "reference_semantics") -> str:
     """The reference's two printed matrices for a bench.py line, from its
     config-3 matrices (`reference_semantics`: the reference's own method, or
@@ -394,8 +402,12 @@ def main(argv=None) -> int:
                         print("-- %s, %d GPUs, in the reference's format:" % (key, r["n_gpus"]))
                         print(txt, end="")
         for r in runs:
-            print("%-10s %-3s %10d B x %4d: GB/s min %.2f mean %.2f max %.2f"
-                  % (r["mode"], r["dir"], r["bytes"], r["iters"], r["gbs_min"], r["gbs_mean"], r["gbs_max"]))
+            print("%-10s %-3s %10d B x %4d: GB/s min %.2f mean %.2f max %.2f%s"
+                  % (r["mode"], r["dir"], r["bytes"], r["iters"], r["gbs_min"], r["gbs_mean"], r["gbs_max"],
+                     "  (run %d)" % r["repeat"] if r.get("repeat") else ""))
+        for r in recs:
+            if r.get("type") == "repeats":  # p2p_matrix --repeat R
+                print(repeat_line(r))
         if UNI_TITLE in text or BI_TITLE in text:
             print(summarize_compat(text))
     if len({r["n_gpus"] for r in all_bench}) > 1:  # one line per GPU count across files: the scaling curve

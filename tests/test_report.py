@@ -158,3 +158,22 @@ def test_scaling_table_never_mixes_value_kinds():
     # Lines from before the field are classed from n_gpus and headline_fallback.
     assert value_kind({"n_gpus": 1}) == SELF_COPY and value_kind({"n_gpus": 8}) == XGMI_LINK
     assert value_kind({"n_gpus": 8, "headline_fallback": {"from": "rccl"}}) == FALLBACK
+
+
+def test_report_cli_reads_repeat_records(tmp_path, capsys):
+    """p2p_matrix --repeat --json: the report tool lists each run with its
+    index and one summary line per repeats record."""
+    import json
+
+    from test_nccl_p2p_amd.utils.report import main, repeat_line
+
+    run = {"type": "run", "mode": "self", "dir": "uni", "bytes": 1 << 25, "iters": 128, "gbs_min": 500.0,
+           "gbs_mean": 500.0, "gbs_max": 500.0}
+    rep = {"type": "repeats", "mode": "self", "dir": "uni", "bytes": 1 << 25, "runs": [400.0, 500.0, 520.0],
+           "median": 500.0, "min": 400.0, "max": 520.0}
+    assert repeat_line(rep).endswith("3 runs: GB/s median 500.00 (min 400.00, max 520.00, spread 24.0%)")
+    p = tmp_path / "r.json"
+    p.write_text("\n".join(json.dumps(x) for x in (dict(run, repeat=0), dict(run, repeat=1), rep)) + "\n")
+    assert main([str(p)]) == 0
+    out = capsys.readouterr().out
+    assert "(run 1)" in out and "(run 0)" not in out and "spread 24.0%" in out
