@@ -208,3 +208,20 @@ def test_every_top_level_script_is_referenced():
         name = os.path.basename(path)
         refs = [p for p, t in texts.items() if p != path and "scripts/" + name in t]
         assert refs, "scripts/%s is referenced nowhere: move it to scripts/probes/" % name
+
+
+def test_busy_fraction_union_and_gaps(tmp_path):
+    """scripts/busy_fraction.py: overlapping kernels count once, the span runs
+    from the first start to the last end, and the idle gaps are the holes
+    between busy stretches."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import busy_fraction
+
+    st = busy_fraction.busy_stats([(0, 10_000), (5_000, 20_000), (30_000, 40_000), (60_000, 70_000)])
+    assert st["span_us"] == 70.0 and st["busy_us"] == 40.0 and st["busy_fraction"] == round(40 / 70, 4)
+    assert st["kernels"] == 4 and st["idle_gaps"] == 2 and st["idle_gap_p50_us"] == 15.0
+    p = tmp_path / "t_kernel_trace.csv"
+    p.write_text("Kernel_Name,Start_Timestamp,End_Timestamp\nrcclGenericKernel<4>,100,300\nfill,300,900\n"
+                 "rcclGenericKernel<4>,400,500\n")
+    assert busy_fraction.read_trace(str(p), "rccl") == [(100, 300), (400, 500)]
+    assert busy_fraction.main([str(p), "--json", str(tmp_path / "o.json")]) == 0
