@@ -7,7 +7,7 @@ stretches.  It shows where a method's time goes: the reference's method
 (p2p_matrix.cc:153-176, a host sync after every message) leaves the GPU idle
 between messages, ours posts them back to back.
 
-    python scripts/busy_fraction.py gpurun_out/x/ref_kernel_trace.csv [--match rcclGenericKernel] [--json out.json]
+    python scripts/busy_fraction.py gpurun_out/x/ref_kernel_trace.csv [--match rcclGenericKernel] [--last 128] [--json out.json]
 """
 import argparse
 import csv
@@ -42,20 +42,26 @@ def busy_stats(intervals):
     }
 
 
-def read_trace(path, match):
+def read_trace(path, match, last=0):
+    """The matching kernels' (start, end), in start order; the last `last`
+    of them (the timed iterations) when last > 0."""
     with open(path) as f:
-        return [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(f) if match in r["Kernel_Name"]]
+        iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(f)
+                    if match in r["Kernel_Name"])
+    return iv[-last:] if last > 0 else iv
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("traces", nargs="+")
     ap.add_argument("--match", default="rcclGenericKernel", help="substring of the kernel name")
+    ap.add_argument("--last", type=int, default=0,
+                    help="only the last N matching kernels (the timed iterations; 0: all)")
     ap.add_argument("--json", default=None, help="also write the results here")
     a = ap.parse_args(argv)
     out = {}
     for path in a.traces:
-        st = busy_stats(read_trace(path, a.match))
+        st = busy_stats(read_trace(path, a.match, a.last))
         out[path] = st
         if st is None:
             print("%s: no kernel matches %r" % (path, a.match))
