@@ -255,8 +255,12 @@ class SectionsMixin:
             out = matrices(h.ref_sess or h.sess, "wallclock", 0, False, 4.0)
             uni = (out.get("uni") or {}).get("median")
             return dict(out, size=self.size, comms=1,
+                        # One stream for both directions: the reference's bi loop
+                        # receives on a second stream (p2p_matrix.cc:214-225),
+                        # which cost ~35% on the self cell (profiles/r6_cli_ab2/),
+                        # so its bi cells read high here if anything.
                         method="reference semantics: serial ordered pairs, wall clock, stream sync per message, no "
-                               "warmup" + ("" if n > 1 else " (applied to the self cell)"),
+                               "warmup, one stream" + ("" if n > 1 else " (applied to the self cell)"),
                         # Kept from round 2: the headline cell over the
                         # reference's uni cell (schedule and method together).
                         value_ratio=round(h.value / uni, 3) if uni else None)
