@@ -75,7 +75,8 @@ timing
                          methodology on a stock RCCL setup, p2p_matrix.cc:141-267; and its
                          buffers: one send and one receive region reused by every
                          iteration (:124-130), so --verify checks the last delivery
-      --two-streams      RCCL: receives on a second stream, like the reference's s_1
+      --two-streams      RCCL: a receive posted in a group with a send goes on a second
+                         stream, like the reference's bi loop (s_1); alone it stays on the first (its uni loop)
       --comms K          RCCL: K communicators per rank on K streams; the i-th message
                          of >= 1 MiB from a to b uses communicator (i + a + b) mod K on both
                          ends, smaller messages stay on the first (P2P_RCCL_SPLIT_MIN)  [1]

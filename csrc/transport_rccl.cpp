@@ -251,6 +251,7 @@ class RcclTransport final : public Transport {
     check_live("group_begin");
     nccl_ok(ncclGroupStart(), "ncclGroupStart");
     in_group_ = true;
+    sent_in_group_ = false;
     if (cstreams_.size() > 1) {
       std::fill(used_.begin(), used_.end(), false);
       used_.resize(cstreams_.size(), false);
@@ -267,6 +268,7 @@ class RcclTransport final : public Transport {
     check_live("send");
     const int j = pick(&send_seq_, peer, bytes);
     touched_[static_cast<size_t>(peer)] = 1;
+    sent_in_group_ = true;
     const char* c = static_cast<const char*>(p);
     do {
       size_t n = chunk_of(bytes, peer);
@@ -279,7 +281,11 @@ class RcclTransport final : public Transport {
     check_live("recv");
     const int j = pick(&recv_seq_, peer, bytes);
     touched_[static_cast<size_t>(peer)] = 1;
-    hipStream_t s = j == 0 && recv_stream_ ? recv_stream_ : cstreams_[static_cast<size_t>(j)];
+    // Reference two-stream layout: the bi loop receives on s_1 next to its
+    // send on s_0 (p2p_matrix.cc:214-225, sends are posted first), the uni
+    // loop receives alone on s_0 (:163-168).
+    const bool side = j == 0 && recv_stream_ && sent_in_group_;
+    hipStream_t s = side ? recv_stream_ : cstreams_[static_cast<size_t>(j)];
     // Injected skip fault: the receive completes into a private sink.
     char* c = static_cast<char*>(discarding() ? discard_sink(bytes) : p);
     do {
@@ -288,7 +294,7 @@ class RcclTransport final : public Transport {
       c += n;
       bytes -= n;
     } while (bytes);
-    recv_on_side_ = recv_stream_ != nullptr;
+    recv_on_side_ = recv_on_side_ || side;
   }
   void group_end() override {
     in_group_ = false;
@@ -930,6 +936,7 @@ class RcclTransport final : public Transport {
   hipStream_t recv_stream_ = nullptr;  // two-stream (reference) layout only
   hipEvent_t join_ = nullptr;
   bool recv_on_side_ = false;
+  bool sent_in_group_ = false;  // this group posted a send (two-stream layout)
   // Message chunking (see send()): at most kRcclBytesPerChannel per p2p
   // channel of the peer (derive_op_limits), capped by set_chunk_cap().
   std::vector<size_t> peer_limit_;       // per peer; 0 = unsplit

@@ -118,8 +118,9 @@ def test_topology_probe(exe):
 
 
 def test_reference_methodology_two_streams(exe):
-    # --reference: wall clock, sync per message, no warmup, receives on a
-    # second stream (the reference's s_1); self path so one GPU suffices.
+    # --reference: wall clock, sync per message, no warmup; a receive in a
+    # group with a send goes on a second stream (the reference's bi loop,
+    # s_1): the self cell's does.  Self path so one GPU suffices.
     out = subprocess.run([exe, "--mode", "self", "--size", "32M", "-n", "16", "--reference", "--verify", "--no-compat"],
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr

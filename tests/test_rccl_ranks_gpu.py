@@ -147,8 +147,9 @@ def test_bench_deadline_aborts_rccl_inside_and_outside_the_engine(tmp_path):
 @pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
 def test_cli_four_rccl_ranks_reference_method(exe):
     """The reference's own methodology through RCCL across ranks: serial
-    ordered pairs, host clock, a stream sync per message, sends on s_0 and
-    receives on s_1 (p2p_matrix.cc:141-267), compat matrices on stdout."""
+    ordered pairs, host clock, a stream sync per message; uni receives on s_0,
+    bi sends on s_0 and receives on s_1 (p2p_matrix.cc:141-267), compat
+    matrices on stdout."""
     out = subprocess.run([MPIRUN, "-n", "4", exe, "--device", "0", "--reference", "--size", "4M", "-n", "8", "--verify",
                           "--timeout", "60"], capture_output=True, text=True, timeout=300, env=ENV)
     assert out.returncode == 0, out.stderr[-3000:]
