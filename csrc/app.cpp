@@ -119,7 +119,8 @@ transport / launch
                          X GB/s (use with the message size the check is for)
 output
       --json FILE        JSON lines, one object per run, appended + flushed as each run ends
-      --resume           skip the runs already in the --json file (restart a killed sweep)
+      --resume           skip the runs already in the --json file (restart a killed sweep;
+                         with --repeat R, run only the repeats it is missing)
       --trace FILE       Chrome/Perfetto trace of every rank's timed phases
                          (P2P_ROCTX=1 also emits roctx ranges for rocprofv3 --marker-trace)
       --csv FILE         per-flow CSV
@@ -460,8 +461,9 @@ std::unique_ptr<Transport> open_transport(const AppConfig& cfg, Bootstrap& boot,
 
 // Checkpoint / resume: every finished run is appended to the JSON-lines file
 // and flushed at once, so a killed sweep keeps what it measured; --resume
-// skips the (mode, dir, size) runs already present in that file.  Returns the
-// skip mask (collective: rank 0 reads the file, every rank gets the mask).
+// skips the (mode, dir, size) runs already present in that file (all R of
+// them with --repeat R).  Returns how many each has (collective: rank 0 reads
+// the file, every rank gets the counts).
 std::vector<uint8_t> open_results(const AppConfig& cfg, Bootstrap& boot, const std::vector<Schedule>& scheds,
                                   const std::string& provenance, std::ofstream* js) {
   std::vector<uint8_t> skip(scheds.size() * cfg.sizes.size(), 0);
@@ -473,10 +475,13 @@ std::vector<uint8_t> open_results(const AppConfig& cfg, Bootstrap& boot, const s
         std::string k = run_key_from_json(line);
         if (!k.empty()) done.push_back(k);
       }
+      // How many runs of each (mode, dir, size) the file holds (with
+      // --repeat R, a killed job resumes at the first missing repeat).
       for (size_t i = 0; i < scheds.size(); ++i)
-        for (size_t j = 0; j < cfg.sizes.size(); ++j)
-          skip[i * cfg.sizes.size() + j] = std::find(done.begin(), done.end(),
-                                                     run_key(scheds[i].mode, scheds[i].dir, cfg.sizes[j])) != done.end();
+        for (size_t j = 0; j < cfg.sizes.size(); ++j) {
+          const auto c = std::count(done.begin(), done.end(), run_key(scheds[i].mode, scheds[i].dir, cfg.sizes[j]));
+          skip[i * cfg.sizes.size() + j] = static_cast<uint8_t>(std::min<long>(c, 255));
+        }
     }
     js->open(cfg.json_path, cfg.resume ? std::ios::app : std::ios::trunc);
     P2P_CHECK(js->good(), "cannot write " + cfg.json_path);
@@ -497,11 +502,12 @@ void run_all(const AppConfig& cfg, Transport& t, Bootstrap& boot, const std::vec
   for (size_t sj = 0; sj < scheds.size(); ++sj) {
     const Schedule& s = scheds[sj];
     for (size_t si = 0; si < cfg.sizes.size(); ++si) {
-      if (skip[sj * cfg.sizes.size() + si]) {
+      const int done = skip[sj * cfg.sizes.size() + si];
+      if (done >= std::max(1, cfg.repeat)) {
         if (root) P2P_INFO("resume: skipping %s", run_key(s.mode, s.dir, cfg.sizes[si]).c_str());
         continue;
       }
-      for (int rep = 0; rep < std::max(1, cfg.repeat); ++rep) {
+      for (int rep = done; rep < std::max(1, cfg.repeat); ++rep) {
         RunRecord rec;
         rec.mode = s.mode;
         rec.dir = s.dir;

@@ -373,3 +373,24 @@ def test_cli_small_flags(host_build, tmp_path):
     assert "bootstrap local" in out.stdout and "verification: OK" in out.stdout
     run_rec = [json.loads(l) for l in js.read_text().splitlines() if '"type":"run"' in l]
     assert len(run_rec) == 1 and run_rec[0]["iters"] == 3 and run_rec[0]["warmup"] == 0
+
+
+def test_resume_completes_missing_repeats(mpirun, host_build, tmp_path):
+    """--resume with --repeat R: a configuration the file holds fewer than R
+    runs of runs only the missing repeats (numbered on from the last), one
+    with all R is skipped."""
+    exe = os.path.join(host_build, "p2p_matrix_host")
+    js = tmp_path / "r.json"
+    base = ["--transport", "host", "--mode", "self", "--sizes", "4K,64K", "-n", "2", "--no-compat", "--json", str(js)]
+    first = run(mpirun, exe, 1, base + ["--repeat", "2"])
+    assert first.returncode == 0, first.stderr
+
+    def runs():
+        return [(r["bytes"], r["repeat"]) for r in map(json.loads, js.read_text().splitlines()) if r["type"] == "run"]
+
+    assert sorted(runs()) == [(4096, 0), (4096, 1), (65536, 0), (65536, 1)]
+    again = run(mpirun, exe, 1, base + ["--repeat", "3", "--resume", "-v"])
+    assert again.returncode == 0, again.stderr
+    assert sorted(runs()) == [(4096, i) for i in range(3)] + [(65536, i) for i in range(3)]
+    done = run(mpirun, exe, 1, base + ["--repeat", "3", "--resume", "-v"])
+    assert done.returncode == 0 and done.stderr.count("resume: skipping") == 2 and len(runs()) == 6
